@@ -1,0 +1,99 @@
+#!/usr/bin/env python3
+"""Headline benchmark: images/sec (whole node) of ResNet-50 async-SGD (Downpour) through
+the mpit_amd parameter server on 1/2/4/8 MI355X (BASELINE.json).
+
+    python bench.py --gpus 1 --steps 20 --warmup 5
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+        --master-port 29500 bench.py --gpus 8 --steps 20 --warmup 5
+
+One process per GPU. Every rank trains a ResNet-50 replica on a synthetic ImageNet batch
+(random bf16 images, random labels, random-init weights) AND serves one shard of the
+flat parameter vector (co-located sharded parameter servers). Each step: forward +
+backward (bf16 autocast, channels_last), fused Downpour scale into the push window, push
+of every gradient shard to its server + pull of every refreshed shard (one fused HIP
+kernel per shard reading / writing the worker's HBM over xGMI), wait. Weak scaling: the
+per-GPU batch is fixed. The timed region is exactly `--steps` full steps bracketed by a
+barrier + device synchronize on both sides; the reported time is the max over ranks.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+METRIC = "images/sec (whole node) ResNet-50 async-SGD at 1/2/4/8 MI355X"
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--optimizer", default="downpour", choices=["downpour", "eamsgd", "easgd", "msgd", "allreduce"])
+    ap.add_argument("--topology", default="colocated", choices=["colocated", "dedicated"])
+    ap.add_argument("--servers", type=int, default=1)
+    ap.add_argument("--su", type=int, default=1)
+    ap.add_argument("--lr", type=float, default=0.05)
+    ap.add_argument("--datapath", type=int, default=0)
+    ap.add_argument("--no-amp", action="store_true")
+    ap.add_argument("--no-channels-last", action="store_true")
+    a = ap.parse_args(argv)
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}; launch N>1 with torch.distributed.run",
+              file=sys.stderr)
+        return 2
+
+    import torch
+
+    torch.backends.cudnn.benchmark = True
+    import mpit_amd as mp
+    from mpit_amd.train import TrainConfig, Trainer, timed_steps
+
+    mp.Init()
+    mva = 0.9 / max(1, a.gpus) if a.optimizer in ("eamsgd", "easgd") else 0.0
+    cfg = TrainConfig(model=a.model, batch=a.batch, optimizer=a.optimizer, topology=a.topology, servers=a.servers,
+                      su=a.su, lr=a.lr, mva=mva, mom=0.0, amp=not a.no_amp, channels_last=not a.no_channels_last,
+                      datapath=a.datapath)
+    tr = Trainer(cfg)
+    secs, loss = timed_steps(tr, a.steps, a.warmup)
+    nworkers = len(tr.cranks)
+    images = a.steps * a.batch * nworkers
+    value = images / secs
+    lossv = float(loss.float().item()) if loss is not None else None
+    tr.stop()
+    if tr.rank == 0:
+        par = {"downpour": "async-ps", "eamsgd": "easgd-ps", "easgd": "easgd-ps", "msgd": "local",
+               "allreduce": "dp"}[a.optimizer]
+        if a.optimizer != "allreduce" and a.optimizer != "msgd":
+            par += f"-{a.topology}-{len(tr.sranks)}srv-{nworkers}wrk"
+        else:
+            par += str(a.gpus)
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "images/sec",
+            "n_gpus": a.gpus,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1000.0 * secs / a.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16" if not a.no_amp else "fp32",
+            "data": "synthetic (random bf16 images 3x224x224, random labels, random-init weights)",
+            "config": {"model": a.model, "global_batch": a.batch * nworkers, "seq_len": None, "image_size": 224,
+                       "parallelism": par, "optimizer": a.optimizer, "su": a.su, "per_gpu_batch": a.batch,
+                       "master_weights": "fp32", "loss_last": lossv},
+        }
+        print(json.dumps(out), flush=True)
+    mp.Finalize()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

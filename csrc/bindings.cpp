@@ -1,0 +1,212 @@
+// Python bindings of the mpit native runtime + kernels (module mpit_amd._mpit).
+// Tensors cross the boundary as (data_ptr, numel, flags); streams as hipStream_t values
+// (torch.cuda.current_stream().cuda_stream). Every blocking call releases the GIL.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "core/engine.h"
+#include "core/ps.h"
+#include "core/window.h"
+#include "kernels/kernels.h"
+
+namespace py = pybind11;
+using namespace mpit;
+
+namespace {
+hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+py::tuple st_tuple(const Status& s) { return py::make_tuple(s.source, s.tag, s.error, s.count, s.cancelled); }
+}  // namespace
+
+PYBIND11_MODULE(_mpit, m) {
+  m.doc() = "mpit_amd native runtime: shm control plane, IPC windows, parameter server, CDNA4 kernels";
+  m.attr("ANY_SOURCE") = kAnySource;
+  m.attr("ANY_TAG") = kAnyTag;
+  m.attr("NORM_WS_FLOATS") = kNormWsFloats;
+
+  py::module_ k = m.def_submodule("rule");
+  k.attr("APPLY") = int(kApply);
+  k.attr("APPLY_SUM") = int(kApplySum);
+  k.attr("RMSPROP") = int(kRMSProp);
+  k.attr("ADAM") = int(kAdam);
+  k.attr("ADAMAX") = int(kAdamax);
+  k.attr("ADAGRAD") = int(kAdagrad);
+  k.attr("ADADELTA") = int(kAdadelta);
+  k.attr("NESTEROV_PRE") = int(kNesterovPre);
+  k.attr("NESTEROV_POST") = int(kNesterovPost);
+  k.attr("DOWNPOUR") = int(kDownpour);
+  k.attr("ELASTIC") = int(kElastic);
+  k.attr("REGCLIP") = int(kRegClip);
+  k.attr("SCALE") = int(kScale);
+  k.attr("COPY") = int(kCopy);
+  k.attr("FILL") = int(kFill);
+  k.attr("AXPBY") = int(kAxpby);
+  k.attr("OUT") = int(kOut);
+  k.attr("ADD") = int(kAdd);
+  k.attr("VT") = int(kVt);
+  k.attr("SUG") = int(kSug);
+
+  m.def(
+      "ew_update",
+      [](int rule, int variant, int dev, uintptr_t stream, int64_t n, std::vector<uintptr_t> ptrs, uint32_t bf,
+         std::vector<float> sc) { ew_update(rule, variant, dev, S(stream), n, ptrs, bf, sc); },
+      py::arg("rule"), py::arg("variant"), py::arg("dev"), py::arg("stream"), py::arg("n"), py::arg("ptrs"),
+      py::arg("bf"), py::arg("scalars"));
+  m.def("norms", [](int dev, uintptr_t stream, uintptr_t x, bool bf16, int64_t n, uintptr_t out, uintptr_t ws) {
+    norms(dev, S(stream), reinterpret_cast<const void*>(x), bf16, n, reinterpret_cast<float*>(out),
+          reinterpret_cast<float*>(ws));
+  });
+  m.def("dot", [](int dev, uintptr_t stream, uintptr_t x, uintptr_t y, bool bf16, int64_t n, uintptr_t out,
+                  uintptr_t ws) {
+    dot(dev, S(stream), reinterpret_cast<const void*>(x), reinterpret_cast<const void*>(y), bf16, n,
+        reinterpret_cast<float*>(out), reinterpret_cast<float*>(ws));
+  });
+  m.def("multi_copy", [](int dev, uintptr_t stream, uintptr_t table, int64_t nchunks, float scale) {
+    multi_copy(dev, S(stream), reinterpret_cast<const CopyChunk*>(table), nchunks, scale);
+  });
+  m.attr("COPY_CHUNK_BYTES") = int(sizeof(CopyChunk));
+
+  py::class_<Engine>(m, "Engine")
+      .def(py::init<const std::string&, int, int, bool, int, int64_t>(), py::arg("name"), py::arg("world"),
+           py::arg("rank"), py::arg("create"), py::arg("device"), py::arg("bulk_bytes"),
+           py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("rank", &Engine::rank)
+      .def_property_readonly("world", &Engine::world)
+      .def_property_readonly("device", &Engine::device)
+      .def("isend",
+           [](Engine& e, uintptr_t buf, int64_t n, bool dev, int dst, int tag, int ctx, bool sync) {
+             return e.isend(reinterpret_cast<const void*>(buf), n, dev, dst, tag, ctx, sync);
+           })
+      .def("irecv",
+           [](Engine& e, uintptr_t buf, int64_t cap, bool dev, int src, int tag, int ctx) {
+             return e.irecv(reinterpret_cast<void*>(buf), cap, dev, src, tag, ctx);
+           })
+      .def("test",
+           [](Engine& e, int64_t id, bool keep) -> py::object {
+             Status st;
+             if (!e.test(id, &st, keep)) return py::none();
+             return st_tuple(st);
+           },
+           py::arg("id"), py::arg("keep") = false)
+      .def("wait",
+           [](Engine& e, int64_t id) {
+             Status st;
+             {
+               py::gil_scoped_release r;
+               e.wait(id, &st);
+             }
+             return st_tuple(st);
+           })
+      .def("cancel", &Engine::cancel)
+      .def("free_request", &Engine::free_request)
+      .def("iprobe",
+           [](Engine& e, int src, int tag, int ctx) -> py::object {
+             Status st;
+             if (!e.iprobe(src, tag, ctx, &st)) return py::none();
+             return st_tuple(st);
+           })
+      .def("probe",
+           [](Engine& e, int src, int tag, int ctx) {
+             Status st;
+             {
+               py::gil_scoped_release r;
+               e.probe(src, tag, ctx, &st);
+             }
+             return st_tuple(st);
+           })
+      .def("barrier", &Engine::barrier, py::call_guard<py::gil_scoped_release>())
+      .def("allgather_small",
+           [](Engine& e, py::bytes blob) {
+             std::string s = blob;
+             std::vector<std::string> out;
+             {
+               py::gil_scoped_release r;
+               out = e.allgather_small(s);
+             }
+             py::list l;
+             for (auto& x : out) l.append(py::bytes(x));
+             return l;
+           })
+      .def("abort", &Engine::abort)
+      .def("shutdown", &Engine::shutdown, py::call_guard<py::gil_scoped_release>())
+      .def("unlink", [](Engine& e) { e.seg().unlink(); })
+      .def("comm_stream", [](Engine& e) { return reinterpret_cast<uintptr_t>(e.comm_stream()); })
+      .def("stats", [](Engine& e) {
+        return py::dict(py::arg("bytes_sent") = e.bytes_sent(), py::arg("bytes_recv") = e.bytes_recv(),
+                        py::arg("msgs_sent") = e.msgs_sent());
+      });
+
+  py::class_<Window>(m, "Window")
+      .def(py::init([](Engine& e, int64_t id, uintptr_t local, int64_t bytes, bool device) {
+             return new Window(e, id, local, bytes, device);
+           }),
+           py::keep_alive<1, 2>())
+      .def("blob", [](Window& w) { return py::bytes(w.blob()); })
+      .def("connect",
+           [](Window& w, std::vector<py::bytes> blobs, std::vector<int> ranks) {
+             std::vector<std::string> b;
+             for (auto& x : blobs) b.push_back(std::string(x));
+             py::gil_scoped_release r;
+             w.connect(b, ranks);
+           })
+      .def("unlink_names", &Window::unlink_names)
+      .def_property_readonly("local_ptr", &Window::local_ptr)
+      .def_property_readonly("bytes", &Window::bytes)
+      .def_property_readonly("device", &Window::device)
+      .def("remote_ptr", &Window::remote_ptr)
+      .def("remote_bytes", &Window::remote_bytes)
+      .def("remote_device", &Window::remote_device)
+      .def("put", [](Window& w, int m, int64_t off, uintptr_t src, int64_t n, uintptr_t s) { w.put(m, off, src, n, S(s)); },
+           py::call_guard<py::gil_scoped_release>())
+      .def("get", [](Window& w, uintptr_t dst, int m, int64_t off, int64_t n, uintptr_t s) { w.get(dst, m, off, n, S(s)); },
+           py::call_guard<py::gil_scoped_release>())
+      .def("accumulate",
+           [](Window& w, int m, int64_t off, uintptr_t src, bool src_dev, int64_t nelem, bool bf16, float a, float b,
+              uintptr_t s) { w.accumulate(m, off, src, src_dev, nelem, bf16, a, b, S(s)); },
+           py::call_guard<py::gil_scoped_release>())
+      .def("lock", &Window::lock, py::call_guard<py::gil_scoped_release>())
+      .def("try_lock", &Window::try_lock)
+      .def("unlock", &Window::unlock)
+      .def("flush", [](Window& w, uintptr_t s) { w.flush(S(s)); }, py::call_guard<py::gil_scoped_release>());
+
+  py::class_<ServerRule>(m, "ServerRule")
+      .def(py::init<>())
+      .def_readwrite("kind", &ServerRule::kind)
+      .def_readwrite("a", &ServerRule::a)
+      .def_readwrite("lr", &ServerRule::lr)
+      .def_readwrite("decay", &ServerRule::decay)
+      .def_readwrite("mom", &ServerRule::mom)
+      .def_readwrite("eps", &ServerRule::eps)
+      .def_readwrite("b1", &ServerRule::b1)
+      .def_readwrite("b2", &ServerRule::b2)
+      .def_readwrite("rho", &ServerRule::rho)
+      .def_readwrite("lrd", &ServerRule::lrd)
+      .def_readwrite("step_div", &ServerRule::step_div);
+
+  py::class_<PSServer>(m, "PSServer")
+      .def(py::init<Engine&, int, Window&, Window&, std::vector<int>, std::vector<int>, int64_t, int64_t, bool, uintptr_t,
+                    std::vector<uintptr_t>, uintptr_t, ServerRule, int, int64_t, bool, int>(),
+           py::keep_alive<1, 2>(), py::keep_alive<1, 4>(), py::keep_alive<1, 5>())
+      .def("start", &PSServer::start)
+      .def("done", &PSServer::done)
+      .def("wait_done", &PSServer::wait_done, py::call_guard<py::gil_scoped_release>())
+      .def("version", &PSServer::version)
+      .def("set_lr", &PSServer::set_lr)
+      .def("sync", &PSServer::sync, py::call_guard<py::gil_scoped_release>())
+      .def("stats", [](PSServer& s) {
+        auto st = s.stats();
+        return py::dict(py::arg("grads") = st.grads, py::arg("pulls") = st.pulls,
+                        py::arg("param_pushes") = st.param_pushes, py::arg("deferred") = st.deferred);
+      });
+
+  py::class_<PSClient>(m, "PSClient")
+      .def(py::init<Engine&, int, std::vector<int>, std::vector<int64_t>, std::vector<int64_t>>(), py::keep_alive<1, 2>())
+      .def("start", &PSClient::start)
+      .def("send_grad", [](PSClient& c, uintptr_t s, bool pull) { c.send_grad(S(s), pull); })
+      .def("recv_param", [](PSClient& c, uintptr_t s) { c.recv_param(S(s)); })
+      .def("send_param", [](PSClient& c, uintptr_t s) { c.send_param(S(s)); })
+      .def("stop", &PSClient::stop, py::call_guard<py::gil_scoped_release>())
+      .def("wait", &PSClient::wait, py::call_guard<py::gil_scoped_release>())
+      .def("test", &PSClient::test)
+      .def("pending", &PSClient::pending)
+      .def("replies", &PSClient::replies);
+}

@@ -1,0 +1,156 @@
+// Native parameter server and client (SURVEY §2.3 P1–P5), MI355X-first.
+//
+// Reference behaviour kept: the eight-tag protocol (asyncsgd/init.lua:3-10), contiguous
+// even sharding with the remainder on the last shard (asyncsgd/pclient.lua:116-128, here
+// 0-based), parameter init pushed by the first client (asyncsgd/pclient.lua:130-133,
+// asyncsgd/pserver.lua:152-158), gradient push + ack, parameter pull on request, stop
+// counting (asyncsgd/pserver.lua:125-139), server-side update rules including the
+// BiCNN adaptive family (BiCNN/pserver.lua:115-205).
+//
+// What changed and why (MI355X):
+//  * Data never travels inside messages. Every client exposes two IPC windows in HBM
+//    (rx: where pulled shards land, normally the model's own flat parameters; tx: the
+//    pushed gradient / parameter vector). A server reads tx and writes rx directly over
+//    xGMI; only 128-B control messages go through the shm rings.
+//  * A push is ONE fused kernel on the server's high-priority HIP stream: it reads the
+//    client's gradient shard from the peer's HBM, applies the update rule to the
+//    resident shard + optimizer state, and (for push+pull) stores the fresh shard
+//    straight into the client's rx window (datapath 0). Datapath 1 instead moves data
+//    with hipMemcpyAsync (SDMA engines, no CUs) around a local fused kernel.
+//  * All updates of a shard are serialised on that one stream, so a pull always copies a
+//    consistent snapshot (the reference sends p while recvgrad mutates it,
+//    asyncsgd/pserver.lua:81).
+//  * Optional bounded staleness (SSP): a pull by a client more than `staleness`
+//    pushes ahead of the slowest client is deferred (BASELINE config 4).
+//  * Clients gate their push on a HIP event of the producing stream, so Python never
+//    blocks to send; replies are counted and wait() sleeps with the GIL released.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <mutex>
+#include <vector>
+
+#include "engine.h"
+#include "window.h"
+
+namespace mpit {
+
+enum PsTag : int {
+  kTagInit = 1,
+  kTagGrad = 2,
+  kTagSendParam = 3,
+  kTagParam = 4,
+  kTagHeader = 5,
+  kTagStop = 6,
+  kTagParamTail = 7,
+  kTagGradTail = 8,
+};
+enum PsFlags : int64_t { kPsWithPull = 1 };
+
+inline int ps_am_id(int ps_id, int tag) { return 4096 + ps_id * 16 + tag; }
+
+// Server-side rule (BiCNN/plaunch.lua optimisation flags). kind: 0 = p += a*g (Downpour /
+// EASGD / local-mode pushes), 1 rmsprop, 2 adam, 3 adamax, 4 adagrad, 5 adadelta.
+struct ServerRule {
+  int kind = 0;
+  float a = 1.f;
+  float lr = 0.f, decay = 0.9f, mom = 0.f, eps = 1e-8f;
+  float b1 = 0.9f, b2 = 0.999f, rho = 0.95f, lrd = 0.f;
+  int64_t step_div = 1;
+};
+
+struct ServerStats {
+  int64_t grads = 0, pulls = 0, param_pushes = 0, deferred = 0;
+};
+
+class PSServer {
+ public:
+  // members: world ranks of the window members, in window member order; clients: the
+  // world ranks of this server's clients. p / state / inbox are caller-owned memory
+  // (device when device=true). state = rule-specific buffers, each shard_len fp32.
+  PSServer(Engine& eng, int ps_id, Window& rx, Window& tx, std::vector<int> members, std::vector<int> clients,
+           int64_t shard_off, int64_t shard_len, bool device, uintptr_t p, std::vector<uintptr_t> state,
+           uintptr_t inbox, ServerRule rule, int datapath, int64_t staleness, bool grad_bf16, int init_rank);
+  ~PSServer();
+  void start();
+  bool done() const { return stopped_.load() >= int(clients_.size()); }
+  void wait_done();
+  ServerStats stats() const;
+  int64_t version() const { return version_.load(); }
+  void set_lr(float lr);
+  void sync();  // wait for all queued server work
+
+ private:
+  void on_msg(const Msg& m);
+  void do_param(int c);
+  void do_grad(int c, bool pull);
+  void do_pull(int c);
+  void apply_rule(const void* g, void* out);
+  void copy_out(int c);
+  void reply(int c, int tag);
+  void finish(std::function<void()> then);
+  void release_deferred();
+  int member_of(int world_rank) const;
+  int client_index(int world_rank) const;
+
+  Engine& eng_;
+  int ps_id_;
+  Window& rx_;
+  Window& tx_;
+  std::vector<int> members_, clients_;
+  int64_t off_, len_;
+  bool device_;
+  void* p_;
+  std::vector<void*> st_;
+  void* inbox_;
+  ServerRule rule_;
+  int datapath_;
+  int64_t staleness_;
+  bool grad_bf16_;
+  hipStream_t stream_ = nullptr;
+  std::atomic<int> stopped_{0};
+  std::atomic<int64_t> version_{0};
+  int init_rank_;                 // client whose parameter push initialises the shard (-1: ready)
+  std::vector<Msg> backlog_;      // grads / pulls that arrived before that push
+  int64_t t_ = 0;  // rule step counter (adam / adamax / adagrad / adadelta)
+  std::vector<int64_t> clock_;  // pushes received per client (SSP)
+  std::deque<int> deferred_;     // clients whose pull waits for stragglers
+  mutable std::mutex mu_;
+  std::condition_variable cv_;
+  ServerStats stats_;
+};
+
+class PSClient {
+ public:
+  PSClient(Engine& eng, int ps_id, std::vector<int> servers, std::vector<int64_t> offs, std::vector<int64_t> lens);
+  ~PSClient();
+  void start();            // register reply handlers, send shard info (tag 1)
+  void send_grad(hipStream_t s, bool with_pull);  // gated on the work queued on s
+  void recv_param(hipStream_t s);  // tag 5 header -> tag 3 once the shard landed in rx;
+                                   // gated on s when rx is still being read there
+  void send_param(hipStream_t s);
+  void stop();
+  void wait();             // until every outstanding reply arrived (GIL released)
+  bool test() const { return pending_.load() == 0; }
+  int64_t pending() const { return pending_.load(); }
+  int64_t replies() const { return replies_.load(); }
+
+ private:
+  struct GateQueue;
+  void gate(hipStream_t s, std::function<void()> send);
+  void on_reply(const Msg& m);
+  Engine& eng_;
+  std::shared_ptr<GateQueue> gq_;
+  int hook_ = -1;
+  int ps_id_;
+  std::vector<int> servers_;
+  std::vector<int64_t> offs_, lens_;
+  std::atomic<int64_t> pending_{0};
+  std::atomic<int64_t> replies_{0};
+};
+
+}  // namespace mpit

@@ -1,0 +1,59 @@
+// Public C++ interface of the mpit HIP kernels (gfx950) and their host twins.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <vector>
+
+namespace mpit {
+
+// ---- fused elementwise update rules (updates.hip) --------------------------------
+enum Rule : int {
+  kApply = 0,        // K1   [p, g, (out)]                     sc: a
+  kApplySum = 1,     // K1   [p, g0..g{NG-1}, (out)]           sc: a          variant |= NG << 8
+  kRMSProp = 2,      // K2   [p, g, ga, gs, u, (out)]          sc: decay lr mom eps
+  kAdam = 3,         // K3   [p, g, m, v, (out)]               sc: b1 b2 eps lr_t
+  kAdamax = 4,       // K4   [p, g, m, u, (out)]               sc: b1 b2 eps lr_t
+  kAdagrad = 5,      // K5   [p, g, var, (out)]                sc: eps clr
+  kAdadelta = 6,     // K6   [p, g, var, acc, (out)]           sc: rho eps lr
+  kNesterovPre = 7,  // K7   [vt, w]                           sc: mom
+  kNesterovPost = 8, // K8   [w, g, vt, sug]                   sc: gscale l2wd clr
+  kDownpour = 9,     // K9   [g, w, acc]                       sc: lr gscale l2wd  variant = mode
+  kElastic = 10,     // K10  [w, c, sug]                       sc: mva
+  kRegClip = 11,     // K11  [g, p]                            sc: gscale l1 l2 clip
+  kScale = 12,       // K14  [x]                               sc: a
+  kCopy = 13,        //      [dst, src]                        sc: a
+  kFill = 14,        //      [dst]                             sc: v
+  kAxpby = 15,       //      [y, x]                            sc: a b
+};
+enum Variant : int {
+  kOut = 1 << 2,  // server rules: also write the new p to the last operand
+  kAdd = 1 << 3,  // RMSProp: add u into p (global mode); otherwise produce u only (local)
+  kVt = 1 << 4,   // Nesterov post: momentum buffer present
+  kSug = 1 << 5,  // Nesterov post: fused EASGD "w -= sug"
+};
+
+// dev < 0 → host; else launch on `s` (device `dev`). bf = bitmask of bf16 operands.
+void ew_update(int rule, int variant, int dev, hipStream_t s, int64_t n, const std::vector<uintptr_t>& ptrs,
+               uint32_t bf, const std::vector<float>& sc);
+
+// ---- reductions (reduce.hip) ------------------------------------------------------
+// out[0] = Σ|x|, out[1] = Σx², out[2] = max|x|  (deterministic two-pass; `ws` holds
+// kNormWsFloats floats of device scratch; ignored on host).
+constexpr int kNormMaxBlocks = 1024;
+constexpr int kNormWsFloats = 3 * kNormMaxBlocks;
+void norms(int dev, hipStream_t s, const void* x, bool bf16, int64_t n, float* out, float* ws);
+// out[0] = Σ x*y (fp32 accumulate), deterministic
+void dot(int dev, hipStream_t s, const void* x, const void* y, bool bf16, int64_t n, float* out, float* ws);
+
+// ---- multi-tensor pack / unpack with cast (multi_copy.hip) ------------------------
+struct CopyChunk {
+  uint64_t src;    // byte address of the first element
+  uint64_t dst;
+  int64_t n;       // elements
+  int32_t flags;   // bit0 src bf16, bit1 dst bf16
+  int32_t pad;
+};
+// `table` = device (or host when dev < 0) array of `nchunks` CopyChunk. dst = scale*src.
+void multi_copy(int dev, hipStream_t s, const CopyChunk* table, int64_t nchunks, float scale);
+
+}  // namespace mpit

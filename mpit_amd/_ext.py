@@ -1,0 +1,38 @@
+"""Loads the native module (``mpit_amd/_mpit*.so``), building it in-tree if missing.
+
+There is no Python fallback for any op: if the extension cannot be loaded the import
+fails loudly, so a GPU run can never silently measure an eager/PyTorch path.
+"""
+from __future__ import annotations
+
+import importlib
+import os
+import threading
+
+_lock = threading.Lock()
+_mod = None
+
+
+def native():
+    """Return the ``_mpit`` extension module (build it first if it is absent)."""
+    global _mod
+    if _mod is not None:
+        return _mod
+    with _lock:
+        if _mod is not None:
+            return _mod
+        try:
+            _mod = importlib.import_module("mpit_amd._mpit")
+        except ImportError:
+            if os.environ.get("MPIT_NO_AUTOBUILD"):
+                raise
+            from . import _build
+
+            _build.build()
+            importlib.invalidate_caches()
+            _mod = importlib.import_module("mpit_amd._mpit")
+    return _mod
+
+
+def native_path() -> str:
+    return native().__file__

@@ -1,0 +1,215 @@
+"""Data-parallel training driver shared by bench.py, the launchers and the tests.
+
+Roles (mirroring asyncsgd/mlaunch.lua and BiCNN/plaunch.lua, re-designed for one process
+per MI355X):
+* ``colocated`` (default): every rank is a worker AND the server of one shard — N shards
+  over N GPUs, each worker's push/pull fans out over all 7 xGMI links at once;
+* ``dedicated``: the first ``servers`` ranks only serve (the reference's server ranks,
+  BASELINE config "1 pserver + 7 workers"), the rest train;
+* ``allreduce``: synchronous DP, gradients all-reduced with RCCL in buckets overlapped
+  with backward (BASELINE config 3), no parameter server.
+
+Optimizers: ``downpour`` (async SGD), ``eamsgd`` / ``easgd`` (elastic averaging),
+``msgd`` (local Nesterov), plus the adaptive server rules via ``server_rule``.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from . import ops
+from . import runtime as _rt
+from .comm import COMM_WORLD, MAX
+from .models import get_model
+from .models.cnn import INPUT_SHAPES
+from .optim import distributed as dopt
+from .parallel.ps import PClient, PServer, ServerOpt
+from .utils.flat import FlatParams
+
+
+@dataclass
+class TrainConfig:
+    model: str = "resnet50"
+    batch: int = 256  # per worker
+    num_classes: int = 1000
+    optimizer: str = "downpour"  # downpour | eamsgd | easgd | msgd | allreduce
+    topology: str = "colocated"  # colocated | dedicated
+    servers: int = 1  # dedicated topology: ranks [0, servers) serve
+    lr: float = 0.05
+    su: int = 1
+    mva: float = 0.0
+    mom: float = 0.0
+    l2wd: float = 0.0
+    amp: bool = True  # bf16 autocast on GPU
+    channels_last: bool = True
+    datapath: int = 0
+    staleness: int = -1
+    server_rule: Optional[ServerOpt] = None
+    seed: int = 1234
+    bucket_mb: float = 64.0  # allreduce bucket size
+    extra: dict = field(default_factory=dict)
+
+
+class Trainer:
+    def __init__(self, cfg: TrainConfig):
+        if not _rt.Initialized():
+            _rt.Init()
+        self.cfg = cfg
+        st = _rt.state()
+        self.rank, self.world = st.rank, st.world
+        self.device = st.device if st.device is not None else torch.device("cpu")
+        self.on_gpu = self.device.type == "cuda"
+        # identical initial weights on every rank (per-rank seeds for data only)
+        torch.manual_seed(cfg.seed)
+        model = get_model(cfg.model, num_classes=cfg.num_classes)
+        if self.on_gpu and cfg.channels_last:
+            model = model.to(memory_format=torch.channels_last)
+        model = model.to(self.device)
+        self.model = model
+        self.flat = FlatParams(model, channels_last=self.on_gpu and cfg.channels_last)
+        self.plong = self.flat.numel
+        torch.manual_seed(cfg.seed + 7919 * self.rank)
+        self._roles()
+        self._data()
+        self.state = {}
+        self.ps_server = None
+        self.pc = None
+        self.ddp = None
+        if cfg.optimizer == "allreduce":
+            from .parallel.ddp import BucketedAllreduce
+
+            self.ddp = BucketedAllreduce(self.model, self.flat, bucket_mb=cfg.bucket_mb)
+        else:
+            self._start_ps()
+        self.steps = 0
+
+    # ------------------------------------------------------------------ setup
+    def _roles(self):
+        c = self.cfg
+        if c.optimizer in ("allreduce",) or self.world == 1 and c.topology == "dedicated":
+            self.sranks, self.cranks = [], list(range(self.world))
+        elif c.topology == "colocated":
+            self.sranks = list(range(self.world))
+            self.cranks = list(range(self.world))
+        elif c.topology == "dedicated":
+            ns = max(1, min(c.servers, self.world - 1))
+            self.sranks = list(range(ns))
+            self.cranks = list(range(ns, self.world))
+        else:
+            raise ValueError(f"unknown topology {c.topology!r}")
+        self.is_server = self.rank in self.sranks
+        self.is_worker = self.rank in self.cranks
+
+    def _data(self):
+        shape = INPUT_SHAPES.get(self.cfg.model, (3, 224, 224))
+        dt = torch.bfloat16 if (self.on_gpu and self.cfg.amp) else torch.float32
+        x = torch.randn((self.cfg.batch,) + tuple(shape), device=self.device, dtype=dt)
+        if self.on_gpu and self.cfg.channels_last and len(shape) == 3:
+            x = x.contiguous(memory_format=torch.channels_last)
+        self.x = x
+        self.y = torch.randint(0, self.cfg.num_classes, (self.cfg.batch,), device=self.device)
+
+    def _start_ps(self):
+        c = self.cfg
+        rule = c.server_rule or ServerOpt("sum", a=1.0)
+        conf = dict(rank=self.rank, sranks=self.sranks, cranks=self.cranks, plong=self.plong, opt=rule,
+                    datapath=c.datapath, staleness=c.staleness)
+        if self.is_server:
+            self.ps_server = PServer(conf)
+            self.ps_server.start(block=False)
+        if self.is_worker:
+            self.pc = PClient(conf)
+            if c.optimizer in ("eamsgd", "easgd"):
+                self.suw = torch.zeros(self.plong, device=self.device)
+                self.sug = torch.zeros(self.plong, device=self.device)
+                self.pc.start(self.suw, self.sug, init=self.flat.flat)
+            else:
+                tx = torch.zeros(self.plong, device=self.device)
+                self.pc.start(self.flat.flat, tx)
+                if self.pc.rx.data_ptr() != self.flat.flat.data_ptr():  # host shm window
+                    self.flat.rebind(self.pc.rx)
+            self.opt_config = dict(lr=c.lr, su=c.su, mva=c.mva, mom=c.mom, l2wd=c.l2wd, pclient=self.pc)
+            if c.optimizer == "downpour" and c.su == 0:
+                self.opt_config["su"] = 1
+        elif self.is_server and self.world > 1:
+            pass  # dedicated server rank: serve until the workers stop (see run_server)
+
+    # ------------------------------------------------------------------ step
+    def _feval(self, w):
+        self.flat.zero_grad()
+        if self.on_gpu and self.cfg.amp:
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                out = self.model(self.x)
+            loss = F.cross_entropy(out.float(), self.y)
+        else:
+            out = self.model(self.x)
+            loss = F.nll_loss(out, self.y) if self.cfg.model in ("cnn7", "lenet") else F.cross_entropy(out, self.y)
+        loss.backward()
+        return loss.detach(), self.flat.grad
+
+    def step(self):
+        """One training step of this worker; returns the loss tensor (not synced)."""
+        c = self.cfg
+        w = self.flat.flat
+        if c.optimizer == "allreduce":
+            loss, g = self._feval(w)
+            self.ddp.finish()
+            ops.nesterov_post_(w, g, None, None, clr=c.lr, gscale=1.0 / self.world, l2wd=c.l2wd)
+            fx = loss
+        elif c.optimizer == "downpour":
+            _, (fx,) = dopt.downpour(self._feval, w, self.opt_config, self.state)
+        elif c.optimizer in ("eamsgd", "easgd"):
+            _, (fx,) = dopt.eamsgd(self._feval, w, self.opt_config, self.state)
+        elif c.optimizer == "msgd":
+            _, (fx,) = dopt.msgd(self._feval, w, dict(lr=c.lr, mom=c.mom, l2wd=c.l2wd), self.state)
+        else:
+            raise ValueError(f"unknown optimizer {c.optimizer!r}")
+        self.steps += 1
+        return fx
+
+    def run_server(self):
+        """Block a dedicated server rank until all workers sent stop."""
+        if self.ps_server is not None and not self.is_worker:
+            self.ps_server.wait_done()
+
+    def stop(self):
+        if self.pc is not None:
+            self.pc.stop()
+        if self.ps_server is not None:
+            self.ps_server.wait_done()
+
+    def sync(self):
+        if self.on_gpu:
+            torch.cuda.synchronize()
+
+    def barrier(self):
+        COMM_WORLD().Barrier()
+
+    def max_over_ranks(self, v: float) -> float:
+        t = torch.tensor([v], dtype=torch.float64)
+        out = torch.zeros(1, dtype=torch.float64)
+        COMM_WORLD().Allreduce(t, out, MAX)
+        return float(out.item())
+
+
+def timed_steps(tr: Trainer, steps: int, warmup: int):
+    """Warm up, then time exactly `steps` steps bracketed by barrier + device sync on both
+    sides. Returns (max seconds over ranks, last loss)."""
+    loss = None
+    if tr.is_worker:
+        for _ in range(warmup):
+            loss = tr.step()
+    tr.sync()
+    tr.barrier()
+    t0 = time.perf_counter()
+    if tr.is_worker:
+        for _ in range(steps):
+            loss = tr.step()
+    tr.sync()
+    tr.barrier()
+    dt = time.perf_counter() - t0
+    return tr.max_over_ranks(dt), loss

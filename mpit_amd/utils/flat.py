@@ -1,0 +1,74 @@
+"""Flat parameter / gradient storage for a module (the reference's ``getParameters``,
+asyncsgd/goot.lua:41, BiCNN/bicnn.lua:255).
+
+Every parameter becomes a view into one contiguous fp32 buffer (which can be a PS or
+all-reduce window: the parameter server then writes pulled shards straight into the
+model), and every ``.grad`` a view into one contiguous gradient buffer that autograd
+accumulates into in place. 4-D conv weights may be laid out channels_last inside the
+flat buffer (the view carries NHWC strides), so MIOpen's NHWC kernels read them directly.
+Shared (tied) parameters are stored once, as ``getParameters`` does.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+
+
+class FlatParams:
+    def __init__(self, module: torch.nn.Module, param_buffer: Optional[torch.Tensor] = None,
+                 grad_buffer: Optional[torch.Tensor] = None, channels_last: bool = False,
+                 grad_dtype: torch.dtype = torch.float32, align: int = 64):
+        params: List[torch.nn.Parameter] = []
+        seen = set()
+        for p in module.parameters():
+            if id(p) in seen:
+                continue
+            seen.add(id(p))
+            params.append(p)
+        self.params = params
+        self.channels_last = channels_last
+        # offsets aligned to `align` elements so every view starts 16-B aligned
+        offs, o = [], 0
+        for p in params:
+            offs.append(o)
+            o += (p.numel() + align - 1) // align * align
+        self.offsets = offs
+        self.numel = o
+        dev = params[0].device if params else torch.device("cpu")
+        if param_buffer is None:
+            param_buffer = torch.zeros(self.numel, dtype=torch.float32, device=dev)
+        if param_buffer.numel() < self.numel:
+            raise ValueError(f"param buffer too small: {param_buffer.numel()} < {self.numel}")
+        self.flat = param_buffer.reshape(-1)
+        if grad_buffer is None:
+            grad_buffer = torch.zeros(self.numel, dtype=grad_dtype, device=self.flat.device)
+        self.grad = grad_buffer.reshape(-1)
+        with torch.no_grad():
+            for p, off in zip(params, offs):
+                pv = self._view(self.flat, p, off)
+                pv.copy_(p.data.to(self.flat.device))
+                p.data = pv
+                p.grad = self._view(self.grad, p, off)
+
+    def _view(self, buf: torch.Tensor, p: torch.Tensor, off: int) -> torch.Tensor:
+        n = p.numel()
+        seg = buf[off: off + n]
+        if self.channels_last and p.dim() == 4:
+            o, i, h, w = p.shape
+            return seg.view(o, h, w, i).permute(0, 3, 1, 2)
+        return seg.view(p.shape)
+
+    def rebind(self, param_buffer: torch.Tensor):
+        """Move the parameters into another flat buffer (e.g. a host shm window)."""
+        with torch.no_grad():
+            param_buffer.reshape(-1)[: self.numel].copy_(self.flat[: self.numel])
+            self.flat = param_buffer.reshape(-1)
+            for p, off in zip(self.params, self.offsets):
+                p.data = self._view(self.flat, p, off)
+
+    def zero_grad(self):
+        self.grad.zero_()
+
+    def __len__(self):
+        return self.numel

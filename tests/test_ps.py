@@ -1,0 +1,45 @@
+"""Parameter-server end to end: multi-process (gloo/CPU here; HBM + IPC on a GPU box)."""
+import re
+
+import pytest
+
+from mp_util import run_ranks
+
+
+def _result(out):
+    m = re.search(r"RESULT (.*)", out)
+    assert m, out
+    return m.group(1)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3])
+def test_downpour_colocated_cpu(n):
+    r = _result(run_ranks("ps_train.py", n, {"MPIT_CPU_ONLY": "1"}))
+    cs = eval(re.search(r"checksums=(\[.*?\])", r).group(1))
+    # after the final synchronous pull every worker holds the server parameters
+    assert max(cs) - min(cs) < 1e-6 * max(1.0, abs(cs[0])), cs
+
+
+def test_downpour_dedicated_cpu():
+    r = _result(run_ranks("ps_train.py", 3, {"MPIT_CPU_ONLY": "1", "T_TOPO": "dedicated"}))
+    assert "grads" in r
+
+
+@pytest.mark.parametrize("opt", ["eamsgd", "msgd"])
+def test_other_optimizers_cpu(opt):
+    r = _result(run_ranks("ps_train.py", 2, {"MPIT_CPU_ONLY": "1", "T_OPT": opt}))
+    assert "loss=" in r
+
+
+def test_downpour_su2_cpu():
+    r = _result(run_ranks("ps_train.py", 2, {"MPIT_CPU_ONLY": "1", "T_SU": "2"}))
+    assert "loss=" in r
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dp", [0, 1])
+def test_downpour_colocated_gpu_two_ranks_one_device(dp):
+    # two ranks share the box's single GPU: exercises HIP IPC windows + fused remote kernels
+    r = _result(run_ranks("ps_train.py", 2, {"T_MODEL": "cnn7", "T_DATAPATH": str(dp)}))
+    cs = eval(re.search(r"checksums=(\[.*?\])", r).group(1))
+    assert max(cs) - min(cs) < 1e-6 * max(1.0, abs(cs[0])), cs

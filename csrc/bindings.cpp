@@ -64,6 +64,20 @@ PYBIND11_MODULE(_mpit, m) {
     multi_copy(dev, S(stream), reinterpret_cast<const CopyChunk*>(table), nchunks, scale);
   });
   m.attr("COPY_CHUNK_BYTES") = int(sizeof(CopyChunk));
+  m.def("bn_workspace_floats", &bn_workspace_floats);
+  m.def("bn_act_fwd",
+        [](int dev, uintptr_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C, uintptr_t gamma,
+           uintptr_t beta, uintptr_t rmean, uintptr_t rvar, uintptr_t save_mean, uintptr_t save_rstd, uintptr_t ws,
+           float momentum, float eps, bool relu) {
+          bn_act_fwd(dev, S(s), bf16, x, res, y, M, C, gamma, beta, rmean, rvar, save_mean, save_rstd, ws, momentum, eps,
+                     relu);
+        });
+  m.def("bn_act_apply", [](int dev, uintptr_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C,
+                           uintptr_t coef, bool relu) { bn_act_apply(dev, S(s), bf16, x, res, y, M, C, coef, relu); });
+  m.def("bn_act_bwd",
+        [](int dev, uintptr_t s, bool bf16, uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t dx, uintptr_t dres, int64_t M,
+           int C, uintptr_t gamma, uintptr_t mean, uintptr_t rstd, uintptr_t dgamma, uintptr_t dbeta, uintptr_t ws,
+           bool relu) { bn_act_bwd(dev, S(s), bf16, dy, y, x, dx, dres, M, C, gamma, mean, rstd, dgamma, dbeta, ws, relu); });
 
   py::class_<Engine>(m, "Engine")
       .def(py::init<const std::string&, int, int, bool, int, int64_t>(), py::arg("name"), py::arg("world"),

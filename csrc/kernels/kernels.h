@@ -56,4 +56,17 @@ struct CopyChunk {
 // `table` = device (or host when dev < 0) array of `nchunks` CopyChunk. dst = scale*src.
 void multi_copy(int dev, hipStream_t s, const CopyChunk* table, int64_t nchunks, float scale);
 
+// ---- fused BatchNorm (+residual) (+ReLU), NHWC, training (bn_act.hip) -------------
+// x / res / y / dy / dx / dres: [M, C] row-major (channels_last), bf16 or fp32.
+int64_t bn_workspace_floats(int C);
+void bn_act_fwd(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C,
+                uintptr_t gamma, uintptr_t beta, uintptr_t rmean, uintptr_t rvar, uintptr_t save_mean,
+                uintptr_t save_rstd, uintptr_t ws, float momentum, float eps, bool relu);
+// y = act(x*coef[c] + coef[C+c] (+res))  — eval mode / precomputed coefficients
+void bn_act_apply(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C,
+                  uintptr_t coef, bool relu);
+void bn_act_bwd(int dev, hipStream_t s, bool bf16, uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t dx, uintptr_t dres,
+                int64_t M, int C, uintptr_t gamma, uintptr_t mean, uintptr_t rstd, uintptr_t dgamma, uintptr_t dbeta,
+                uintptr_t ws, bool relu);
+
 }  // namespace mpit

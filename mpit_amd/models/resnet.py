@@ -13,6 +13,16 @@ from typing import List, Type, Union
 import torch
 import torch.nn as nn
 
+from ..ops.bn import BatchNormAct2d
+
+# Fused BN(+add)(+ReLU) HIP kernels on MI355X (mpit_amd/ops/bn.py); same parameters and
+# state dict as nn.BatchNorm2d, and plain PyTorch math on CPU tensors.
+FUSED_BN = True
+
+
+def _bn(c, act):
+    return BatchNormAct2d(c, act=act) if FUSED_BN else nn.BatchNorm2d(c)
+
 
 def conv3x3(i, o, stride=1):
     return nn.Conv2d(i, o, 3, stride=stride, padding=1, bias=False)
@@ -28,14 +38,17 @@ class BasicBlock(nn.Module):
     def __init__(self, inp, planes, stride=1, downsample=None):
         super().__init__()
         self.conv1 = conv3x3(inp, planes, stride)
-        self.bn1 = nn.BatchNorm2d(planes)
+        self.bn1 = _bn(planes, True)
         self.relu = nn.ReLU(inplace=True)
         self.conv2 = conv3x3(planes, planes)
-        self.bn2 = nn.BatchNorm2d(planes)
+        self.bn2 = _bn(planes, True)
         self.downsample = downsample
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
+        if isinstance(self.bn1, BatchNormAct2d):
+            out = self.bn1(self.conv1(x))
+            return self.bn2(self.conv2(out), idt)
         out = self.relu(self.bn1(self.conv1(x)))
         out = self.bn2(self.conv2(out))
         return self.relu(out + idt)
@@ -47,16 +60,20 @@ class Bottleneck(nn.Module):
     def __init__(self, inp, planes, stride=1, downsample=None):
         super().__init__()
         self.conv1 = conv1x1(inp, planes)
-        self.bn1 = nn.BatchNorm2d(planes)
+        self.bn1 = _bn(planes, True)
         self.conv2 = conv3x3(planes, planes, stride)
-        self.bn2 = nn.BatchNorm2d(planes)
+        self.bn2 = _bn(planes, True)
         self.conv3 = conv1x1(planes, planes * 4)
-        self.bn3 = nn.BatchNorm2d(planes * 4)
+        self.bn3 = _bn(planes * 4, True)
         self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
+        if isinstance(self.bn1, BatchNormAct2d):
+            out = self.bn1(self.conv1(x))
+            out = self.bn2(self.conv2(out))
+            return self.bn3(self.conv3(out), idt)
         out = self.relu(self.bn1(self.conv1(x)))
         out = self.relu(self.bn2(self.conv2(out)))
         out = self.bn3(self.conv3(out))
@@ -69,7 +86,7 @@ class ResNet(nn.Module):
         super().__init__()
         self.inplanes = 64
         self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
-        self.bn1 = nn.BatchNorm2d(64)
+        self.bn1 = _bn(64, True)
         self.relu = nn.ReLU(inplace=True)
         self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
         self.layer1 = self._make(block, 64, layers[0])
@@ -81,7 +98,7 @@ class ResNet(nn.Module):
         for m in self.modules():
             if isinstance(m, nn.Conv2d):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
-            elif isinstance(m, nn.BatchNorm2d):
+            elif isinstance(m, nn.BatchNorm2d):  # includes BatchNormAct2d
                 nn.init.ones_(m.weight)
                 nn.init.zeros_(m.bias)
         if zero_init_residual:
@@ -95,7 +112,7 @@ class ResNet(nn.Module):
         down = None
         if stride != 1 or self.inplanes != planes * block.expansion:
             down = nn.Sequential(conv1x1(self.inplanes, planes * block.expansion, stride),
-                                 nn.BatchNorm2d(planes * block.expansion))
+                                 _bn(planes * block.expansion, False))
         layers = [block(self.inplanes, planes, stride, down)]
         self.inplanes = planes * block.expansion
         for _ in range(1, blocks):
@@ -103,7 +120,10 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        if isinstance(self.bn1, BatchNormAct2d):
+            x = self.maxpool(self.bn1(self.conv1(x)))
+        else:
+            x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)

@@ -1,0 +1,126 @@
+"""Fused BatchNorm2d (+ residual add) (+ ReLU) for channels_last activations on MI355X.
+
+Forward training = 2 HBM passes (statistics; normalise+add+ReLU), backward = 2 passes
+(reductions; dx [+ residual grad]) — csrc/kernels/bn_act.hip. Replaces
+BatchNorm -> add -> ReLU chains of 3 library/elementwise kernels each way.
+
+:class:`BatchNormAct2d` is an ``nn.BatchNorm2d`` (same parameters, buffers, state dict)
+whose forward takes an optional residual and applies ReLU when ``act=True``. On CPU
+tensors (tests, gloo plumbing) it computes the same function with PyTorch ops.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .._ext import native
+
+
+def _rows(x: torch.Tensor):
+    n, c, h, w = x.shape
+    return n * h * w, c
+
+
+def _cl(x: torch.Tensor) -> torch.Tensor:
+    return x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
+
+
+class _BNActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu):
+        x = _cl(x)
+        if residual is not None:
+            residual = _cl(residual).to(x.dtype)
+        M, C = _rows(x)
+        m = native()
+        dev = x.device.index
+        stream = torch.cuda.current_stream(x.device).cuda_stream
+        y = torch.empty_like(x, memory_format=torch.channels_last)
+        mean = torch.empty(C, dtype=torch.float32, device=x.device)
+        rstd = torch.empty(C, dtype=torch.float32, device=x.device)
+        ws = torch.empty(m.bn_workspace_floats(C), dtype=torch.float32, device=x.device)
+        w = weight.float().contiguous() if weight is not None else None
+        b = bias.float().contiguous() if bias is not None else None
+        m.bn_act_fwd(dev, stream, x.dtype == torch.bfloat16, x.data_ptr(),
+                     residual.data_ptr() if residual is not None else 0, y.data_ptr(), M, C,
+                     w.data_ptr() if w is not None else 0, b.data_ptr() if b is not None else 0,
+                     running_mean.data_ptr() if running_mean is not None else 0,
+                     running_var.data_ptr() if running_var is not None else 0,
+                     mean.data_ptr(), rstd.data_ptr(), ws.data_ptr(), float(momentum), float(eps), bool(relu))
+        ctx.save_for_backward(x, y, w, mean, rstd)
+        ctx.relu = relu
+        ctx.has_res = residual is not None
+        ctx.has_w = weight is not None
+        ctx.has_b = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, w, mean, rstd = ctx.saved_tensors
+        dy = _cl(dy).to(x.dtype)
+        M, C = _rows(x)
+        m = native()
+        dev = x.device.index
+        stream = torch.cuda.current_stream(x.device).cuda_stream
+        dx = torch.empty_like(x, memory_format=torch.channels_last)
+        dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
+        dgamma = torch.empty(C, dtype=torch.float32, device=x.device) if ctx.has_w else None
+        dbeta = torch.empty(C, dtype=torch.float32, device=x.device) if ctx.has_b else None
+        ws = torch.empty(m.bn_workspace_floats(C), dtype=torch.float32, device=x.device)
+        m.bn_act_bwd(dev, stream, x.dtype == torch.bfloat16, dy.data_ptr(), y.data_ptr(), x.data_ptr(), dx.data_ptr(),
+                     dres.data_ptr() if dres is not None else 0, M, C, w.data_ptr() if w is not None else 0,
+                     mean.data_ptr(), rstd.data_ptr(), dgamma.data_ptr() if dgamma is not None else 0,
+                     dbeta.data_ptr() if dbeta is not None else 0, ws.data_ptr(), bool(ctx.relu))
+        return dx, dgamma, dbeta, None, None, dres, None, None, None
+
+
+def bn_act_eval(x, weight, bias, running_mean, running_var, eps, residual=None, relu=True):
+    """Inference: coefficients from running statistics, one fused pass."""
+    x = _cl(x)
+    M, C = _rows(x)
+    rstd = torch.rsqrt(running_var.float() + eps)
+    sc = rstd * (weight.float() if weight is not None else 1.0)
+    sh = (bias.float() if bias is not None else 0.0) - running_mean.float() * sc
+    coef = torch.cat([sc.reshape(-1), sh.reshape(-1)]).contiguous()
+    y = torch.empty_like(x, memory_format=torch.channels_last)
+    if residual is not None:
+        residual = _cl(residual).to(x.dtype)
+    native().bn_act_apply(x.device.index, torch.cuda.current_stream(x.device).cuda_stream, x.dtype == torch.bfloat16,
+                          x.data_ptr(), residual.data_ptr() if residual is not None else 0, y.data_ptr(), M, C,
+                          coef.data_ptr(), bool(relu))
+    return y
+
+
+def _supported(x: torch.Tensor) -> bool:
+    if not x.is_cuda or x.dim() != 4 or x.dtype not in (torch.bfloat16, torch.float32):
+        return False
+    v = 8 if x.dtype == torch.bfloat16 else 4
+    return x.shape[1] % v == 0
+
+
+class BatchNormAct2d(nn.BatchNorm2d):
+    """``act(bn(x) + residual)`` with ReLU act; a drop-in ``nn.BatchNorm2d`` subclass."""
+
+    def __init__(self, num_features, eps=1e-5, momentum=0.1, affine=True, track_running_stats=True, act=True):
+        super().__init__(num_features, eps, momentum, affine, track_running_stats)
+        self.act = act
+
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+        if not _supported(x):
+            y = super().forward(x)
+            if residual is not None:
+                y = y + residual
+            return F.relu(y) if self.act else y
+        if self.training or not self.track_running_stats:
+            momentum = self.momentum
+            if self.training and self.track_running_stats:
+                self.num_batches_tracked.add_(1)
+                if momentum is None:
+                    momentum = 1.0 / float(self.num_batches_tracked)
+            rm = self.running_mean if (self.training and self.track_running_stats) else None
+            rv = self.running_var if (self.training and self.track_running_stats) else None
+            return _BNActFn.apply(x, self.weight, self.bias, rm, rv, residual, momentum or 0.0, self.eps, self.act)
+        return bn_act_eval(x, self.weight, self.bias, self.running_mean, self.running_var, self.eps, residual, self.act)

@@ -26,7 +26,9 @@
 namespace mpit {
 namespace {
 
-constexpr int kMaxStatBlocks = 1024;
+constexpr int kMaxStatBlocks = 512;
+constexpr int kFinCh = 64;   // channels per finalize block
+constexpr int kFinK = 4;     // partial-lanes per channel in the finalize block
 
 template <typename T>
 struct Vec;
@@ -123,19 +125,41 @@ __global__ __launch_bounds__(1024) void bn_stats_kernel(const T* __restrict__ x,
   }
 }
 
-template <typename T>
-__global__ void bn_finalize_fwd_kernel(const float* __restrict__ part, int nb, int C, int64_t M, const T* __restrict__ x,
-                                       const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
-                                       float momentum, float* __restrict__ rmean, float* __restrict__ rvar,
-                                       float* __restrict__ save_mean, float* __restrict__ save_rstd,
-                                       float* __restrict__ coef /*[2][C] scale, shift*/) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double a = 0, b = 0;
-  for (int k = 0; k < nb; ++k) {
-    a += part[(size_t(k) * 2 + 0) * C + c];
-    b += part[(size_t(k) * 2 + 1) * C + c];
+// Cross-block combine: a block owns kFinCh channels; kFinK lanes per channel stride over
+// the partials (coalesced 256-B rows, independent loads in flight), then combine in LDS.
+__device__ __forceinline__ bool fin_combine(const float* __restrict__ part, int nb, int C, double& a, double& b) {
+  __shared__ double sa[kFinK][kFinCh], sb[kFinK][kFinCh];
+  const int cl = threadIdx.x % kFinCh, kl = threadIdx.x / kFinCh;
+  const int c = blockIdx.x * kFinCh + cl;
+  double x = 0, y = 0;
+  if (c < C) {
+#pragma unroll 4
+    for (int k = kl; k < nb; k += kFinK) {
+      x += part[(size_t(k) * 2 + 0) * C + c];
+      y += part[(size_t(k) * 2 + 1) * C + c];
+    }
   }
+  sa[kl][cl] = x;
+  sb[kl][cl] = y;
+  __syncthreads();
+  if (kl != 0 || c >= C) return false;
+  a = 0;
+  b = 0;
+  for (int k = 0; k < kFinK; ++k) {
+    a += sa[k][cl];
+    b += sb[k][cl];
+  }
+  return true;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kFinCh * kFinK) void bn_finalize_fwd_kernel(
+    const float* __restrict__ part, int nb, int C, int64_t M, const T* __restrict__ x, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float eps, float momentum, float* __restrict__ rmean, float* __restrict__ rvar,
+    float* __restrict__ save_mean, float* __restrict__ save_rstd, float* __restrict__ coef /*[2][C] scale, shift*/) {
+  double a, b;
+  if (!fin_combine(part, nb, C, a, b)) return;
+  const int c = blockIdx.x * kFinCh + int(threadIdx.x % kFinCh);
   float k0;
   if constexpr (sizeof(T) == 2) k0 = bf2f(reinterpret_cast<const uint16_t*>(x)[c]);
   else k0 = reinterpret_cast<const float*>(x)[c];
@@ -253,17 +277,13 @@ __global__ __launch_bounds__(1024) void bn_bwd_reduce_kernel(const T* __restrict
   }
 }
 
-__global__ void bn_finalize_bwd_kernel(const float* __restrict__ part, int nb, int C, int64_t M,
-                                       const float* __restrict__ gamma, const float* __restrict__ mean,
-                                       const float* __restrict__ rstd, float* __restrict__ dgamma,
-                                       float* __restrict__ dbeta, float* __restrict__ coef /*[3][C] a c b*/) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double a = 0, b = 0;
-  for (int k = 0; k < nb; ++k) {
-    a += part[(size_t(k) * 2 + 0) * C + c];
-    b += part[(size_t(k) * 2 + 1) * C + c];
-  }
+__global__ __launch_bounds__(kFinCh * kFinK) void bn_finalize_bwd_kernel(
+    const float* __restrict__ part, int nb, int C, int64_t M, const float* __restrict__ gamma,
+    const float* __restrict__ mean, const float* __restrict__ rstd, float* __restrict__ dgamma, float* __restrict__ dbeta,
+    float* __restrict__ coef /*[3][C] a c b*/) {
+  double a, b;
+  if (!fin_combine(part, nb, C, a, b)) return;
+  const int c = blockIdx.x * kFinCh + int(threadIdx.x % kFinCh);
   const float rs = rstd[c];
   if (dgamma) dgamma[c] = float(b) * rs;
   if (dbeta) dbeta[c] = float(a);
@@ -345,7 +365,7 @@ void fwd_impl(int dev, hipStream_t s, const T* x, const T* res, T* y, int64_t M,
     float* part = ws + 2 * C;
     const size_t shm = size_t(R) * 2 * C * sizeof(float);
     hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(nb), dim3(blk), shm, s, x, M, C, rpb, part);
-    hipLaunchKernelGGL(bn_finalize_fwd_kernel<T>, dim3((C + 255) / 256), dim3(256), 0, s, part, nb, C, M, x, gamma,
+    hipLaunchKernelGGL(bn_finalize_fwd_kernel<T>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinK), 0, s, part, nb, C, M, x, gamma,
                        beta, eps, momentum, rmean, rvar, save_mean, save_rstd, coef);
   } else {
     // eval: coefficients from the running statistics (computed on the device, tiny)
@@ -396,7 +416,7 @@ void bwd_impl(hipStream_t s, const T* dy, const T* y, const T* x, T* dx, T* dres
   const size_t shm = size_t(R) * 2 * C * sizeof(float);
   if (relu) hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true>), dim3(nb), dim3(blk), shm, s, dy, y, x, mean, M, C, rpb, part);
   else hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false>), dim3(nb), dim3(blk), shm, s, dy, y, x, mean, M, C, rpb, part);
-  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, nb, C, M, gamma, mean, rstd,
+  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinK), 0, s, part, nb, C, M, gamma, mean, rstd,
                      dgamma, dbeta, coef);
   const int64_t nvec = M * G;
   const int grid = apply_grid(nvec, blk);

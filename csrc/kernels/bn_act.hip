@@ -28,7 +28,7 @@ namespace {
 
 constexpr int kMaxStatBlocks = 512;
 constexpr int kFinCh = 64;   // channels per finalize block
-constexpr int kFinK = 4;     // partial-lanes per channel in the finalize block
+constexpr int kFinK = 16;    // partial-lanes per channel in the finalize block (1024 threads)
 
 template <typename T>
 struct Vec;
@@ -133,7 +133,7 @@ __device__ __forceinline__ bool fin_combine(const float* __restrict__ part, int 
   const int c = blockIdx.x * kFinCh + cl;
   double x = 0, y = 0;
   if (c < C) {
-#pragma unroll 4
+#pragma unroll 8
     for (int k = kl; k < nb; k += kFinK) {
       x += part[(size_t(k) * 2 + 0) * C + c];
       y += part[(size_t(k) * 2 + 1) * C + c];

@@ -1,0 +1,100 @@
+"""BiCNN / GESD question-answer model (BiCNN/bicnn.lua:30-121), custom layers
+(BiCNN/Normalize.lua, BiCNN/DivideConstant.lua) and the margin ranking objective.
+
+Tower (weights shared by the Q, Q2, A+ and A- towers, ``:set()`` tying in the reference):
+Embedding(V, 100) -> Linear(100, 200) -> Tanh -> Conv1d(200, 3000, k=2) -> max over time
+-> ReLU -> L2 normalise. GESD similarity: ``1/(1+||a-b||) * 1/(1+exp(-(a.b+1)))``.
+``mmode`` 1 compares Q with both answers; 2 uses a second question encoding for the
+negative (BiCNN/bicnn.lua:87-116 — with tied weights the two are identical functions of
+the same question, kept for parity).
+
+MI355X adaptation: the reference runs one (question, answer) pair at a time with
+data-dependent negative sampling; here a batch of padded sequences is encoded at once
+(max-over-time masks the padding) and the hardest of ``num_neg`` sampled negatives is
+used per question, which is the batched form of "sample until a margin violation"
+(BiCNN/bicnn.lua:279-420).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import register
+
+
+class Normalize(nn.Module):
+    """Lp normalisation over the last dim (BiCNN/Normalize.lua:1-86; autograd supplies
+    the analytic Jacobian the reference wrote by hand)."""
+
+    def __init__(self, p: float = 2.0, eps: float = 1e-10):
+        super().__init__()
+        self.p, self.eps = p, eps
+
+    def forward(self, x):
+        return x / x.norm(p=self.p, dim=-1, keepdim=True).clamp_min(self.eps)
+
+
+class DivideConstant(nn.Module):
+    """``y = c / x``, ``dx = -c g / x^2`` (BiCNN/DivideConstant.lua:4-25)."""
+
+    def __init__(self, c: float = 1.0):
+        super().__init__()
+        self.c = c
+
+    def forward(self, x):
+        return self.c / x
+
+
+def gesd(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """GESD similarity of row pairs (BiCNN/bicnn.lua:99-105)."""
+    l2 = (a - b).norm(dim=-1)
+    dot = (a * b).sum(-1)
+    return (1.0 / (1.0 + l2)) * (1.0 / (1.0 + torch.exp(-(dot + 1.0))))
+
+
+class BiCNN(nn.Module):
+    def __init__(self, vocab: int = 22354, emb_dim: int = 100, hidden: int = 200, filters: int = 3000,
+                 conv_width: int = 2, mmode: int = 1, pad_idx: int = 0):
+        super().__init__()
+        self.embed = nn.Embedding(vocab, emb_dim, padding_idx=pad_idx)
+        self.hidden = nn.Linear(emb_dim, hidden)
+        self.conv = nn.Conv1d(hidden, filters, conv_width)
+        self.norm = Normalize(2)
+        self.mmode = mmode
+        self.pad_idx = pad_idx
+
+    def encode(self, tok: torch.Tensor) -> torch.Tensor:
+        """tok: [B, T] word ids (pad_idx = padding) -> [B, filters] unit embeddings."""
+        h = torch.tanh(self.hidden(self.embed(tok)))  # [B, T, H]
+        c = self.conv(h.transpose(1, 2))  # [B, F, T-k+1]
+        k = self.conv.kernel_size[0]
+        valid = (tok != self.pad_idx)
+        # a window is valid when its first token is not padding (sentences are left-aligned)
+        vw = valid[:, : c.shape[-1]].unsqueeze(1)
+        c = c.masked_fill(~vw, float("-inf"))
+        m = c.max(dim=-1).values
+        m = torch.nan_to_num(m, neginf=0.0)
+        return self.norm(F.relu(m))
+
+    def forward(self, q, a_pos, a_neg):
+        eq = self.encode(q)
+        ep = self.encode(a_pos)
+        b, nneg, t = a_neg.shape
+        en = self.encode(a_neg.reshape(b * nneg, t)).reshape(b, nneg, -1)
+        eq2 = eq if self.mmode == 1 else self.encode(q)
+        s_pos = gesd(eq, ep)
+        s_neg = gesd(eq2.unsqueeze(1).expand_as(en), en)  # [B, nneg]
+        return s_pos, s_neg
+
+
+def margin_ranking_loss(s_pos, s_neg, margin: float = 0.009):
+    """nn.MarginRankingCriterion(margin) with the hardest sampled negative
+    (BiCNN/bicnn.lua:121, :279-420)."""
+    hard = s_neg.max(dim=-1).values
+    return F.relu(margin - s_pos + hard).mean()
+
+
+@register("bicnn")
+def bicnn(num_classes=None, **kw):
+    return BiCNN(**kw)

@@ -43,3 +43,10 @@ def test_downpour_colocated_gpu_two_ranks_one_device(dp):
     r = _result(run_ranks("ps_train.py", 2, {"T_MODEL": "cnn7", "T_DATAPATH": str(dp)}))
     cs = eval(re.search(r"checksums=(\[.*?\])", r).group(1))
     assert max(cs) - min(cs) < 1e-6 * max(1.0, abs(cs[0])), cs
+
+
+def test_sync_allreduce_dp_cpu():
+    r = _result(run_ranks("ps_train.py", 3, {"MPIT_CPU_ONLY": "1", "T_OPT": "allreduce"}))
+    cs = eval(re.search(r"checksums=(\[.*?\])", r).group(1))
+    # synchronous DP keeps every replica bit-identical
+    assert max(cs) == min(cs), cs

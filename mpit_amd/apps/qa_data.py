@@ -1,0 +1,124 @@
+"""QA data preparation for BiCNN (BiCNN/prepareData.lua:1-299).
+
+File formats (tab separated, as read by the reference):
+* embedding file: ``word<TAB>v1 v2 ... vD``
+* train file:     ``labels<TAB>(ignored)<TAB>question words<TAB>answer words``
+* valid / test:   ``labels<TAB>question words<TAB>pool of answer labels``
+* label2answer:   ``label<TAB>answer words``
+
+Sentences are padded with ``convWidth`` SENTBEGIN tokens in front and ``convWidth-1``
+SENTEND tokens behind (prepareData.lua:90,102); out-of-vocabulary words get uniform
+random embeddings. Index 0 is reserved for batch padding here (the reference had no
+batching), so SENTBEGIN=1 and SENTEND=2 as in the reference.
+
+:func:`synthetic_qa` builds a learnable stand-in with the same structure (the reference's
+data files are not in the repository: .MISSING_LARGE_BLOBS).
+"""
+from __future__ import annotations
+
+import random
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import torch
+
+PAD, SENTBEGIN, SENTEND = 0, 1, 2
+
+
+@dataclass
+class QAData:
+    word2idx: Dict[str, int] = field(default_factory=lambda: {"<pad>": PAD, "SENTBEGIN": SENTBEGIN, "SENTEND": SENTEND})
+    vectors: List[List[float]] = field(default_factory=list)
+    train: List[tuple] = field(default_factory=list)  # (labels, q_ids, a_ids)
+    valid: List[tuple] = field(default_factory=list)  # (labels, q_ids, pool)
+    tests: List[List[tuple]] = field(default_factory=list)
+    answers: Dict[int, List[int]] = field(default_factory=dict)  # label -> token ids
+    emb_dim: int = 100
+    conv_width: int = 2
+
+    def _id(self, w: str, rng: random.Random) -> int:
+        i = self.word2idx.get(w)
+        if i is None:
+            i = len(self.word2idx)
+            self.word2idx[w] = i
+            self.vectors.append([rng.random() for _ in range(self.emb_dim)])
+        return i
+
+    def encode(self, words: List[str], rng: random.Random) -> List[int]:
+        k = self.conv_width
+        return [SENTBEGIN] * k + [self._id(w, rng) for w in words] + [SENTEND] * (k - 1)
+
+    def embedding_matrix(self) -> torch.Tensor:
+        v = torch.zeros(len(self.word2idx), self.emb_dim)
+        base = len(self.word2idx) - len(self.vectors)
+        if self.vectors:
+            v[base:] = torch.tensor(self.vectors)
+        return v
+
+
+def pad_batch(seqs: List[List[int]], min_len: int = 2) -> torch.Tensor:
+    T = max(min_len, max(len(s) for s in seqs))
+    out = torch.full((len(seqs), T), PAD, dtype=torch.long)
+    for i, s in enumerate(seqs):
+        out[i, : len(s)] = torch.tensor(s, dtype=torch.long)
+    return out
+
+
+def load_files(embedding: str, train: str, label2answer: str, valid: Optional[str] = None, tests=(),
+               emb_dim: int = 100, conv_width: int = 2, seed: int = 1) -> QAData:
+    rng = random.Random(seed)
+    d = QAData(emb_dim=emb_dim, conv_width=conv_width)
+    with open(embedding) as f:
+        for line in f:
+            k, _, v = line.rstrip("\n").partition("\t")
+            d.word2idx[k] = len(d.word2idx)
+            d.vectors.append([float(x) for x in v.split()])
+    with open(label2answer) as f:
+        for line in f:
+            lab, _, txt = line.rstrip("\n").partition("\t")
+            d.answers[int(lab)] = d.encode(txt.split(), rng)
+    with open(train) as f:
+        for line in f:
+            parts = line.rstrip("\n").split("\t")
+            labels = [int(x) for x in parts[0].split()]
+            d.train.append((labels, d.encode(parts[2].split(), rng), d.encode(parts[3].split(), rng)))
+
+    def eval_file(p):
+        out = []
+        with open(p) as f:
+            for line in f:
+                parts = line.rstrip("\n").split("\t")
+                out.append(([int(x) for x in parts[0].split()], d.encode(parts[1].split(), rng),
+                            [int(x) for x in parts[2].split()]))
+        return out
+
+    if valid:
+        d.valid = eval_file(valid)
+    d.tests = [eval_file(t) for t in tests]
+    return d
+
+
+def synthetic_qa(n_answers: int = 200, n_train: int = 2000, n_valid: int = 200, vocab: int = 2000, pool: int = 20,
+                 emb_dim: int = 100, conv_width: int = 2, seed: int = 1) -> QAData:
+    """Answers are random word sequences; a question shares 3 "key" words with its answer
+    plus noise words, so GESD ranking is learnable."""
+    rng = random.Random(seed)
+    d = QAData(emb_dim=emb_dim, conv_width=conv_width)
+    words = [f"w{i}" for i in range(vocab)]
+    for lab in range(n_answers):
+        d.answers[lab] = d.encode(rng.sample(words, rng.randint(6, 12)), rng)
+    ans_words = {lab: [w for w in d.answers[lab][conv_width:-(conv_width - 1) or None]] for lab in d.answers}
+    idx2w = {i: w for w, i in d.word2idx.items()}
+
+    def question(lab):
+        keys = [idx2w[i] for i in rng.sample(ans_words[lab], 3)]
+        return keys + rng.sample(words, rng.randint(2, 6))
+
+    for _ in range(n_train):
+        lab = rng.randrange(n_answers)
+        d.train.append(([lab], d.encode(question(lab), rng), d.answers[lab]))
+    for _ in range(n_valid):
+        lab = rng.randrange(n_answers)
+        cands = list({lab} | set(rng.sample(range(n_answers), pool - 1)))
+        d.valid.append(([lab], d.encode(question(lab), rng), cands))
+    return d

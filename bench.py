@@ -42,7 +42,7 @@ def main(argv=None) -> int:
     ap.add_argument("--servers", type=int, default=1)
     ap.add_argument("--su", type=int, default=1)
     ap.add_argument("--lr", type=float, default=0.05)
-    ap.add_argument("--datapath", type=int, default=0)
+    ap.add_argument("--datapath", type=int, default=2)
     ap.add_argument("--no-amp", action="store_true")
     ap.add_argument("--no-channels-last", action="store_true")
     ap.add_argument("--miopen-find", action="store_true",

@@ -48,6 +48,20 @@ PSServer::PSServer(Engine& eng, int ps_id, Window& rx, Window& tx, std::vector<i
     int lo = 0, hi = 0;
     hipp(hipDeviceGetStreamPriorityRange(&lo, &hi), "priority range");
     hipp(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi), "server stream");
+    if (datapath_ == 2) {
+      const size_t nc = clients_.size();
+      cstream_.resize(nc);
+      ev_in_.resize(nc);
+      ev_up_.resize(nc);
+      ev_out_.resize(nc);
+      for (size_t i = 0; i < nc; ++i) {
+        hipp(hipStreamCreateWithPriority(&cstream_[i], hipStreamNonBlocking, hi), "link stream");
+        hipp(hipEventCreateWithFlags(&ev_in_[i], hipEventDisableTiming), "event");
+        hipp(hipEventCreateWithFlags(&ev_up_[i], hipEventDisableTiming), "event");
+        hipp(hipEventCreateWithFlags(&ev_out_[i], hipEventDisableTiming), "event");
+      }
+      if (nc && len_ > 0) hipp(hipMalloc(reinterpret_cast<void**>(&stage_), nc * size_t(len_) * 8), "hipMalloc(stage)");
+    }
   }
 }
 
@@ -55,9 +69,23 @@ PSServer::~PSServer() {
   for (int t = 1; t <= 8; ++t) eng_.register_am(ps_am_id(ps_id_, t), [](const Msg&) {});
   if (stream_) {
     hipSetDevice(eng_.device());
+    for (auto s : cstream_) {
+      hipStreamSynchronize(s);
+      hipStreamDestroy(s);
+    }
     hipStreamSynchronize(stream_);
     hipStreamDestroy(stream_);
+    for (auto* v : {&ev_in_, &ev_up_, &ev_out_})
+      for (auto e : *v) hipEventDestroy(e);
+    if (stage_) hipFree(stage_);
   }
+}
+
+void PSServer::finish_on(hipStream_t s, std::function<void()> then) {
+  hipEvent_t ev;
+  hipp(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+  hipp(hipEventRecord(ev, s), "hipEventRecord");
+  eng_.track_copy(ev, std::move(then));
 }
 
 void PSServer::start() {
@@ -223,6 +251,27 @@ void PSServer::copy_out(int c) {
 }
 
 void PSServer::do_pull(int c) {
+  const int ci = client_index(c);
+  if (pipelined(ci)) {
+    // snapshot the shard in update order on stream_, push it over the client's link
+    hipp(hipSetDevice(eng_.device()), "hipSetDevice");
+    hipStream_t cs = cstream_[size_t(ci)];
+    uint8_t* out = stage_ + size_t(ci) * size_t(len_) * 8 + size_t(len_) * 4;
+    uint8_t* dst = reinterpret_cast<uint8_t*>(rx_.remote_ptr(member_of(c))) + off_ * 4;
+    hipp(hipStreamWaitEvent(stream_, ev_out_[size_t(ci)], 0), "wait outbox free");
+    ew_update(kCopy, 0, eng_.device(), stream_, len_, {reinterpret_cast<uintptr_t>(out), reinterpret_cast<uintptr_t>(p_)},
+              0u, {1.f});
+    hipp(hipEventRecord(ev_up_[size_t(ci)], stream_), "record snapshot");
+    hipp(hipStreamWaitEvent(cs, ev_up_[size_t(ci)], 0), "link waits snapshot");
+    hipp(hipMemcpyAsync(dst, out, size_t(len_) * 4, hipMemcpyDefault, cs), "param push (link)");
+    hipp(hipEventRecord(ev_out_[size_t(ci)], cs), "record outbox sent");
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      ++stats_.pulls;
+    }
+    finish_on(cs, [this, c] { reply(c, kTagSendParam); });
+    return;
+  }
   copy_out(c);
   {
     std::lock_guard<std::mutex> g(mu_);
@@ -246,6 +295,43 @@ void PSServer::do_grad(int c, bool pull) {
     }
   }
   if (!device_ && tx_.remote_device(m)) throw std::runtime_error("mpit: host server cannot read a device tx window");
+  if (pipelined(ci)) {
+    // link stream: pull the gradient shard into this client's inbox; stream_: fused update
+    // (+ snapshot into the outbox when a pull is due); link stream: push the snapshot
+    hipp(hipSetDevice(eng_.device()), "hipSetDevice");
+    const size_t k = size_t(ci);
+    hipStream_t cs = cstream_[k];
+    uint8_t* in = stage_ + k * size_t(len_) * 8;
+    uint8_t* out = in + size_t(len_) * 4;
+    const bool push_back = pull && !defer_pull;
+    hipp(hipMemcpyAsync(in, g, size_t(len_ * es), hipMemcpyDefault, cs), "grad pull (link)");
+    hipp(hipEventRecord(ev_in_[k], cs), "record inbox full");
+    hipp(hipStreamWaitEvent(stream_, ev_in_[k], 0), "update waits inbox");
+    if (push_back) hipp(hipStreamWaitEvent(stream_, ev_out_[k], 0), "update waits outbox free");
+    apply_rule(in, push_back ? out : nullptr);
+    hipp(hipEventRecord(ev_up_[k], stream_), "record update");
+    hipp(hipStreamWaitEvent(cs, ev_up_[k], 0), "link waits update");  // inbox reusable after this
+    if (push_back) {
+      uint8_t* dst = reinterpret_cast<uint8_t*>(rx_.remote_ptr(m)) + off_ * 4;
+      hipp(hipMemcpyAsync(dst, out, size_t(len_) * 4, hipMemcpyDefault, cs), "param push (link)");
+      hipp(hipEventRecord(ev_out_[k], cs), "record outbox sent");
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      ++stats_.grads;
+      if (push_back) ++stats_.pulls;
+      if (defer_pull) {
+        deferred_.push_back(c);
+        ++stats_.deferred;
+      }
+    }
+    finish_on(cs, [this, c, push_back] {
+      reply(c, kTagGradTail);
+      if (push_back) reply(c, kTagSendParam);
+    });
+    release_deferred();
+    return;
+  }
   void* fused_out = nullptr;
   if (pull && !defer_pull && (datapath_ == 0 || !device_))
     fused_out = reinterpret_cast<uint8_t*>(rx_.remote_ptr(m)) + off_ * 4;

@@ -112,6 +112,15 @@ class PSServer {
   int64_t staleness_;
   bool grad_bf16_;
   hipStream_t stream_ = nullptr;
+  // datapath 2 (default on HBM): one "link" stream + staging pair per client, so the
+  // gradient pulls and parameter pushes of different clients run concurrently over
+  // their own xGMI links (SDMA copies) and only the local fused update is serialised on
+  // stream_. stage_ = [clients][inbox | outbox] of shard_len fp32 each.
+  std::vector<hipStream_t> cstream_;
+  std::vector<hipEvent_t> ev_in_, ev_up_, ev_out_;
+  uint8_t* stage_ = nullptr;
+  void finish_on(hipStream_t s, std::function<void()> then);
+  bool pipelined(int ci) const { return device_ && datapath_ == 2 && ci >= 0; }
   std::atomic<int> stopped_{0};
   std::atomic<int64_t> version_{0};
   int init_rank_;                 // client whose parameter push initialises the shard (-1: ready)

@@ -184,7 +184,7 @@ class PServer:
         if isinstance(opt, dict):
             opt = ServerOpt.from_bicnn_opt(opt)
         self.opt: ServerOpt = opt or ServerOpt()
-        self.datapath = int(_conf_get(conf, "datapath", 0))
+        self.datapath = int(_conf_get(conf, "datapath", 2))
         self.staleness = int(_conf_get(conf, "staleness", -1))
         self.grad_dtype = _conf_get(conf, "grad_dtype", torch.float32)
         self.state = state or {}

@@ -46,7 +46,7 @@ class TrainConfig:
     l2wd: float = 0.0
     amp: bool = True  # bf16 autocast on GPU
     channels_last: bool = True
-    datapath: int = 0
+    datapath: int = 2  # 0 fused remote kernel, 1 serial SDMA, 2 per-client link streams
     staleness: int = -1
     server_rule: Optional[ServerOpt] = None
     seed: int = 1234

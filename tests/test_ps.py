@@ -37,7 +37,7 @@ def test_downpour_su2_cpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dp", [0, 1])
+@pytest.mark.parametrize("dp", [0, 1, 2])
 def test_downpour_colocated_gpu_two_ranks_one_device(dp):
     # two ranks share the box's single GPU: exercises HIP IPC windows + fused remote kernels
     r = _result(run_ranks("ps_train.py", 2, {"T_MODEL": "cnn7", "T_DATAPATH": str(dp)}))

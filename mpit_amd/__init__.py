@@ -62,6 +62,8 @@ from .runtime import (
 )
 from .window import LOCK_EXCLUSIVE, LOCK_SHARED, Win
 
+from . import datatypes, misc, ops, optim, parallel, topology  # noqa: E402
+
 __version__ = "0.1.0"
 
 

@@ -3,6 +3,9 @@
 #include <unistd.h>
 #include <xmmintrin.h>
 
+#include <cerrno>
+#include <csignal>
+
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -47,6 +50,8 @@ Engine::~Engine() {
 
 void Engine::shutdown() {
   if (!running_.exchange(false)) return;
+  // a clean exit: peers must not take this rank's disappearance for a crash
+  seg_->hdr()->ranks[rank_].attached.store(2, std::memory_order_release);
   if (thread_.joinable()) thread_.join();
   if (device_ >= 0) {
     hipSetDevice(device_);
@@ -603,11 +608,47 @@ bool Engine::progress_once() {
   return did;
 }
 
+void Engine::check_peers() {
+  // Failure detector: every rank of the node publishes its pid in the segment; a peer
+  // that disappeared without Finalize (crash, OOM kill) would leave everybody blocked
+  // in waits forever, so the first rank to notice aborts the whole job.
+  Header* h = seg_->hdr();
+  for (int r = 0; r < world_; ++r) {
+    if (r == rank_) continue;
+    const RankInfo& ri = h->ranks[r];
+    if (ri.attached.load(std::memory_order_acquire) != 1 || ri.pid <= 0) continue;
+    bool dead = ::kill(ri.pid, 0) != 0 && errno == ESRCH;
+    if (!dead) {  // an exited but not yet reaped process is a zombie: dead as well
+      char path[64], buf[256] = {0};
+      std::snprintf(path, sizeof(path), "/proc/%d/stat", ri.pid);
+      if (FILE* f = std::fopen(path, "r")) {
+        const size_t n = std::fread(buf, 1, sizeof(buf) - 1, f);
+        std::fclose(f);
+        const char* rp = static_cast<const char*>(std::memchr(buf, ')', n));
+        if (rp && rp + 2 < buf + n && rp[2] == 'Z') dead = true;
+      }
+    }
+    if (dead) {
+      std::fprintf(stderr, "[mpit rank %d] peer rank %d (pid %d) died; aborting the job\n", rank_, r, ri.pid);
+      std::fflush(stderr);
+      h->abort_code = 70;
+      h->abort_flag.store(1, std::memory_order_release);
+      ::_exit(70);
+    }
+  }
+}
+
 void Engine::progress_loop() {
   if (device_ >= 0) hipSetDevice(device_);
   int idle = 0;
   uint64_t last_act = 0;
+  auto last_check = std::chrono::steady_clock::now();
   while (running_.load(std::memory_order_relaxed)) {
+    const auto now = std::chrono::steady_clock::now();
+    if (now - last_check > std::chrono::milliseconds(500)) {
+      last_check = now;
+      check_peers();
+    }
     bool did = false;
     try {
       did = progress_once();

@@ -140,6 +140,7 @@ class Engine {
 
  private:
   void progress_loop();
+  void check_peers();
   bool progress_once();
   bool progress_sends_locked();
   bool progress_recvs_locked();

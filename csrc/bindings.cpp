@@ -64,6 +64,9 @@ PYBIND11_MODULE(_mpit, m) {
     multi_copy(dev, S(stream), reinterpret_cast<const CopyChunk*>(table), nchunks, scale);
   });
   m.attr("COPY_CHUNK_BYTES") = int(sizeof(CopyChunk));
+  m.def("gather_scale", [](int dev, uintptr_t s, std::vector<uintptr_t> srcs, std::vector<int64_t> offs,
+                           std::vector<int64_t> ns, uintptr_t dst, uintptr_t aux, float a,
+                           float b) { gather_scale(dev, S(s), srcs, offs, ns, dst, aux, a, b); });
   m.def("bn_workspace_floats", &bn_workspace_floats);
   m.def("bn_act_fwd",
         [](int dev, uintptr_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C, uintptr_t gamma,

@@ -56,6 +56,13 @@ struct CopyChunk {
 // `table` = device (or host when dev < 0) array of `nchunks` CopyChunk. dst = scale*src.
 void multi_copy(int dev, hipStream_t s, const CopyChunk* table, int64_t nchunks, float scale);
 
+// ---- gradient gather + Downpour scale (gather.hip) ---------------------------------
+// dst[off_t + i] = a*src_t[i] + b*aux[off_t + i]  (fp32; aux optional), one launch per
+// kGatherMaxT tensors, table passed by value.
+constexpr int kGatherMaxT = 128;
+void gather_scale(int dev, hipStream_t s, const std::vector<uintptr_t>& srcs, const std::vector<int64_t>& offs,
+                  const std::vector<int64_t>& ns, uintptr_t dst, uintptr_t aux, float a, float b);
+
 // ---- fused BatchNorm (+residual) (+ReLU), NHWC, training (bn_act.hip) -------------
 // x / res / y / dy / dx / dres: [M, C] row-major (channels_last), bf16 or fp32.
 int64_t bn_workspace_floats(int C);

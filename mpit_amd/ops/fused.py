@@ -233,3 +233,18 @@ def dot(x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
     else:
         m.dot(-1, 0, x.data_ptr(), y.data_ptr(), x.dtype == torch.bfloat16, x.numel(), out.data_ptr(), 0)
     return out
+
+
+def gather_scale_(dst: torch.Tensor, srcs, offs, ns, a: float = 1.0, aux=None, b: float = 0.0):
+    """K12+K9: ``dst[off_t:off_t+n_t] = a*src_t + b*aux[off_t:...]`` for raw fp32 tensor
+    pointers ``srcs`` (one launch per 128 tensors)."""
+    if dst.dtype != torch.float32 or (aux is not None and aux.dtype != torch.float32):
+        raise TypeError("gather_scale_ works on float32")
+    m = native()
+    if dst.is_cuda:
+        dev, stream = dst.device.index, torch.cuda.current_stream(dst.device).cuda_stream
+    else:
+        dev, stream = -1, 0
+    m.gather_scale(dev, stream, list(srcs), list(offs), list(ns), dst.data_ptr(),
+                   aux.data_ptr() if aux is not None else 0, float(a), float(b))
+    return dst

@@ -67,6 +67,20 @@ def downpour(opfunc, w, config, state=None):
     if lrd != 0:
         lr = lr / (1 + pv * lrd)
     fx, dfdx = opfunc(w)
+    from ..utils.flat import StolenGrads
+
+    if isinstance(dfdx, StolenGrads):
+        if pc is not None and su == 1:
+            # K12+K9 fused: gather every parameter's gradient straight into the push
+            # window with the -lr scale (and weight decay) applied, one launch
+            dfdx.gather(pc.tx, -lr * gscale, w if l2wd else None, -lr * l2wd)
+            pc.async_send_grad(pull=True)
+            t0 = time.perf_counter()
+            pc.wait()
+            state["dusync"] += time.perf_counter() - t0
+            state["pversion"] = pv + 1
+            return w, [fx]
+        dfdx = dfdx.materialize()
     if pc is not None and su > 1:
         acc = pc.tx  # the push window doubles as the accumulator (reference: config.dfdx)
         if not config.get("_acc_init"):

@@ -85,6 +85,12 @@ class Trainer:
             self.ddp = BucketedAllreduce(self.model, self.flat, bucket_mb=cfg.bucket_mb)
         else:
             self._start_ps()
+        # Downpour su=1 on the GPU: let autograd hand over its gradient tensors and gather
+        # them into the push window in one fused kernel (utils/flat.py StolenGrads)
+        self.steal = (self.on_gpu and cfg.optimizer == "downpour" and cfg.su <= 1 and self.pc is not None
+                      and cfg.extra.get("steal_grads", True))
+        if self.steal:
+            self.flat.steal_grads()
         self.steps = 0
 
     # ------------------------------------------------------------------ setup
@@ -140,7 +146,8 @@ class Trainer:
 
     # ------------------------------------------------------------------ step
     def _feval(self, w):
-        self.flat.zero_grad()
+        if not getattr(self, "steal", False):
+            self.flat.zero_grad()
         if self.on_gpu and self.cfg.amp:
             with torch.autocast("cuda", dtype=torch.bfloat16):
                 out = self.model(self.x)
@@ -149,6 +156,8 @@ class Trainer:
             out = self.model(self.x)
             loss = F.nll_loss(out, self.y) if self.cfg.model in ("cnn7", "lenet") else F.cross_entropy(out, self.y)
         loss.backward()
+        if getattr(self, "steal", False):
+            return loss.detach(), self.flat.stolen()
         return loss.detach(), self.flat.grad
 
     def step(self):

@@ -59,6 +59,19 @@ class FlatParams:
             return seg.view(o, h, w, i).permute(0, 3, 1, 2)
         return seg.view(p.shape)
 
+    # ------------------------------------------------------------------ steal mode
+    def steal_grads(self):
+        """Switch to "steal" mode: ``.grad`` is left unset so autograd hands over its
+        own gradient tensors (no per-parameter ``grad += new`` kernels, no memset);
+        :meth:`stolen` then gathers them in one fused kernel (ops.gather_scale_)."""
+        for p in self.params:
+            p.grad = None
+        self._steal = True
+        return self
+
+    def stolen(self) -> "StolenGrads":
+        return StolenGrads(self)
+
     def rebind(self, param_buffer: torch.Tensor):
         """Move the parameters into another flat buffer (e.g. a host shm window)."""
         with torch.no_grad():
@@ -72,3 +85,44 @@ class FlatParams:
 
     def __len__(self):
         return self.numel
+
+
+class StolenGrads:
+    """The gradients autograd produced for a :class:`FlatParams` in steal mode.
+
+    ``gather(dst, a, aux, b)`` writes ``dst[off] = a*g + b*aux[off]`` for every parameter in
+    one launch (K12 bucketing fused with K9's scale); ``materialize()`` gathers into the
+    flat gradient buffer for rules that need it. Either call releases the tensors."""
+
+    def __init__(self, flat: FlatParams):
+        self.flat = flat
+
+    def _table(self):
+        srcs, offs, ns = [], [], []
+        for p, off in zip(self.flat.params, self.flat.offsets):
+            g = p.grad
+            if g is None:
+                continue
+            if not g.is_contiguous(memory_format=torch.channels_last if g.dim() == 4 and self.flat.channels_last
+                                   else torch.contiguous_format):
+                g = g.contiguous(memory_format=torch.channels_last) if (g.dim() == 4 and self.flat.channels_last) \
+                    else g.contiguous()
+                p.grad = g
+            srcs.append(g.data_ptr())
+            offs.append(off)
+            ns.append(g.numel())
+        return srcs, offs, ns
+
+    def gather(self, dst: torch.Tensor, a: float = 1.0, aux: torch.Tensor = None, b: float = 0.0):
+        from ..ops.fused import gather_scale_
+
+        srcs, offs, ns = self._table()
+        if len(srcs) < len(self.flat.params):
+            dst.zero_()
+        gather_scale_(dst, srcs, offs, ns, a, aux, b)
+        for p in self.flat.params:
+            p.grad = None
+        return dst
+
+    def materialize(self) -> torch.Tensor:
+        return self.gather(self.flat.grad, 1.0)

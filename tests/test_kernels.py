@@ -228,6 +228,35 @@ def test_norms_dot(d, n):
 
 
 @pytest.mark.parametrize("d", DEVICES)
+@pytest.mark.parametrize("l2wd", [0.0, 1e-2])
+def test_stolen_grads_gather_scale(d, l2wd):
+    """K12+K9: autograd's own gradient tensors gathered into the push buffer with the
+    Downpour scale in one launch, channels_last conv weights included."""
+    d = _dev(d)
+    from mpit_amd.utils.flat import FlatParams
+
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Conv2d(3, 8, 3), torch.nn.ReLU(), torch.nn.Flatten(),
+                            torch.nn.Linear(8 * 6 * 6, 5)).to(d)
+    cl = d.type == "cuda"
+    if cl:
+        m = m.to(memory_format=torch.channels_last)
+    fp = FlatParams(m, channels_last=cl)
+    x = torch.randn(4, 3, 8, 8, device=d)
+    # reference: accumulate into the flat gradient views
+    m(x).square().sum().backward()
+    ref = -0.1 * (fp.grad.clone() + l2wd / 1.0 * 0) - 0.1 * l2wd * fp.flat
+    fp.steal_grads()
+    m(x).square().sum().backward()
+    out = torch.full((fp.numel,), 7.0, device=d)
+    fp.stolen().gather(out, -0.1, fp.flat if l2wd else None, -0.1 * l2wd)
+    # padding between parameters is not written by the gather; compare parameter ranges
+    for p, off in zip(fp.params, fp.offsets):
+        close(out[off: off + p.numel()], ref[off: off + p.numel()], 1e-5)
+    assert all(p.grad is None for p in fp.params)
+
+
+@pytest.mark.parametrize("d", DEVICES)
 def test_pack_unpack(d):
     d = _dev(d)
     shapes = [(64, 3, 7, 7), (1000,), (3,), (256, 1024), (70001,)]

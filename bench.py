@@ -43,6 +43,8 @@ def main(argv=None) -> int:
     ap.add_argument("--su", type=int, default=1)
     ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--datapath", type=int, default=2)
+    ap.add_argument("--staleness", type=int, default=-1, help="bounded staleness (SSP); -1 = fully async")
+    ap.add_argument("--wire", default="fp32", choices=["fp32", "bf16"], help="EASGD elastic-difference dtype")
     ap.add_argument("--no-amp", action="store_true")
     ap.add_argument("--no-channels-last", action="store_true")
     ap.add_argument("--miopen-find", action="store_true",
@@ -66,10 +68,13 @@ def main(argv=None) -> int:
     mva = 0.9 / max(1, a.gpus) if a.optimizer in ("eamsgd", "easgd") else 0.0
     cfg = TrainConfig(model=a.model, batch=a.batch, optimizer=a.optimizer, topology=a.topology, servers=a.servers,
                       su=a.su, lr=a.lr, mva=mva, mom=0.0, amp=not a.no_amp, channels_last=not a.no_channels_last,
-                      datapath=a.datapath)
+                      datapath=a.datapath, staleness=a.staleness, wire_dtype=a.wire)
     tr = Trainer(cfg)
     secs, loss = timed_steps(tr, a.steps, a.warmup)
     nworkers = len(tr.cranks)
+    from mpit_amd.models.cnn import INPUT_SHAPES
+
+    shape = INPUT_SHAPES.get(a.model, (3, 224, 224))
     images = a.steps * a.batch * nworkers
     value = images / secs
     lossv = float(loss.float().item()) if loss is not None else None
@@ -82,7 +87,8 @@ def main(argv=None) -> int:
         else:
             par += str(a.gpus)
         out = {
-            "metric": METRIC,
+            "metric": METRIC if (a.model == "resnet50" and a.optimizer == "downpour") else
+                      f"images/sec (whole node) {a.model} {a.optimizer}",
             "value": round(value, 2),
             "unit": "images/sec",
             "n_gpus": a.gpus,
@@ -92,9 +98,9 @@ def main(argv=None) -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16" if not a.no_amp else "fp32",
-            "data": "synthetic (random bf16 images 3x224x224, random labels, random-init weights)",
-            "config": {"model": a.model, "global_batch": a.batch * nworkers, "seq_len": None, "image_size": 224,
+            "dtype": "bf16" if (tr.on_gpu and not a.no_amp) else "fp32",
+            "data": f"synthetic (random images {shape[0]}x{shape[1]}x{shape[2]}, random labels, random-init weights)",
+            "config": {"model": a.model, "global_batch": a.batch * nworkers, "seq_len": None, "image_size": shape[-1],
                        "parallelism": par, "optimizer": a.optimizer, "su": a.su, "per_gpu_batch": a.batch,
                        "master_weights": "fp32", "loss_last": lossv},
         }

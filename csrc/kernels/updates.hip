@@ -132,13 +132,13 @@ void ew_update(int rule, int variant, int dev, hipStream_t s, int64_t n, const s
       const bool vt = variant & kVt, sug = variant & kSug;
       // operands always [w, g, vt, sug]; unused ones are neither read nor written
       if (vt && sug)
-        run_masks<4, 0xfu, bit(0) | bit(2), NesterovPostF<true, true>, 0u, bit(1)>(
+        run_masks<4, 0xfu, bit(0) | bit(2), NesterovPostF<true, true>, 0u, bit(1), bit(3), bit(1) | bit(3)>(
             bf, mk<4>(ptrs), n, NesterovPostF<true, true>{gs, l2, clr}, dev, s);
       else if (vt)
         run_masks<4, 0x7u, bit(0) | bit(2), NesterovPostF<true, false>, 0u, bit(1)>(
             bf, mk<4>(ptrs), n, NesterovPostF<true, false>{gs, l2, clr}, dev, s);
       else if (sug)
-        run_masks<4, bit(0) | bit(1) | bit(3), bit(0), NesterovPostF<false, true>, 0u, bit(1)>(
+        run_masks<4, bit(0) | bit(1) | bit(3), bit(0), NesterovPostF<false, true>, 0u, bit(1), bit(3), bit(1) | bit(3)>(
             bf, mk<4>(ptrs), n, NesterovPostF<false, true>{gs, l2, clr}, dev, s);
       else
         run_masks<4, 0x3u, bit(0), NesterovPostF<false, false>, 0u, bit(1)>(
@@ -169,7 +169,7 @@ void ew_update(int rule, int variant, int dev, hipStream_t s, int64_t n, const s
       break;
     }
     case kElastic:
-      run_masks<3, bit(0) | bit(1), bit(2), ElasticF, 0u>(bf, mk<3>(ptrs), n, ElasticF{S(sc, 0)}, dev, s);
+      run_masks<3, bit(0) | bit(1), bit(2), ElasticF, 0u, bit(2)>(bf, mk<3>(ptrs), n, ElasticF{S(sc, 0)}, dev, s);
       break;
     case kRegClip:
       run_masks<2, 0x3u, bit(0), RegClipF, 0u, bit(0)>(bf, mk<2>(ptrs), n,

@@ -146,7 +146,7 @@ def nesterov_post_(w, g, vt=None, sug=None, clr=0.0, gscale=1.0, l2wd=0.0):
     (asyncsgd/optim-msgd.lua:31-39, optim-eamsgd.lua:36-44,70)."""
     R = _R()
     var = (R.VT if vt is not None else 0) | (R.SUG if sug is not None else 0)
-    _launch(R.NESTEROV_POST, var, [w, g, vt, sug], [gscale, l2wd, clr], bf_ok=(1,))
+    _launch(R.NESTEROV_POST, var, [w, g, vt, sug], [gscale, l2wd, clr], bf_ok=(1, 3))
     return w
 
 
@@ -159,7 +159,7 @@ def downpour_(g, w, acc, lr, mode: int = 0, gscale=1.0, l2wd=0.0):
 
 def elastic_(w, center, sug, mva):
     """K10a: ``sug = mva*(w - center)`` (asyncsgd/optim-eamsgd.lua:62-64)."""
-    _launch(_R().ELASTIC, 0, [w, center, sug], [mva])
+    _launch(_R().ELASTIC, 0, [w, center, sug], [mva], bf_ok=(2,))
     return sug
 
 

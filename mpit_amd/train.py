@@ -47,7 +47,8 @@ class TrainConfig:
     amp: bool = True  # bf16 autocast on GPU
     channels_last: bool = True
     datapath: int = 2  # 0 fused remote kernel, 1 serial SDMA, 2 per-client link streams
-    staleness: int = -1
+    staleness: int = -1  # bounded staleness (SSP) for the PS; -1 = fully asynchronous
+    wire_dtype: str = "fp32"  # "bf16": EASGD elastic differences cross xGMI in bf16
     server_rule: Optional[ServerOpt] = None
     seed: int = 1234
     bucket_mb: float = 64.0  # allreduce bucket size
@@ -122,8 +123,11 @@ class Trainer:
     def _start_ps(self):
         c = self.cfg
         rule = c.server_rule or ServerOpt("sum", a=1.0)
+        # EASGD can ship the elastic difference in bf16 (half the xGMI bytes); gradients
+        # pushed by Downpour stay fp32 (they are summed into the fp32 master shard)
+        wire = torch.bfloat16 if (c.wire_dtype == "bf16" and c.optimizer in ("eamsgd", "easgd")) else torch.float32
         conf = dict(rank=self.rank, sranks=self.sranks, cranks=self.cranks, plong=self.plong, opt=rule,
-                    datapath=c.datapath, staleness=c.staleness)
+                    datapath=c.datapath, staleness=c.staleness, grad_dtype=wire)
         if self.is_server:
             self.ps_server = PServer(conf)
             self.ps_server.start(block=False)
@@ -131,7 +135,7 @@ class Trainer:
             self.pc = PClient(conf)
             if c.optimizer in ("eamsgd", "easgd"):
                 self.suw = torch.zeros(self.plong, device=self.device)
-                self.sug = torch.zeros(self.plong, device=self.device)
+                self.sug = torch.zeros(self.plong, device=self.device, dtype=wire)
                 self.pc.start(self.suw, self.sug, init=self.flat.flat)
             else:
                 tx = torch.zeros(self.plong, device=self.device)

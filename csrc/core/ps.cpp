@@ -239,7 +239,7 @@ void PSServer::copy_out(int c) {
   uint8_t* dst = reinterpret_cast<uint8_t*>(rx_.remote_ptr(m)) + off_ * 4;
   if (device_) {
     hipp(hipSetDevice(eng_.device()), "hipSetDevice");
-    if (datapath_ == 0)
+    if (datapath_ != 1)
       ew_update(kCopy, 0, eng_.device(), stream_, len_, {reinterpret_cast<uintptr_t>(dst), reinterpret_cast<uintptr_t>(p_)},
                 0u, {1.f});
     else
@@ -252,7 +252,7 @@ void PSServer::copy_out(int c) {
 
 void PSServer::do_pull(int c) {
   const int ci = client_index(c);
-  if (pipelined(ci)) {
+  if (pipelined(ci, c)) {
     // snapshot the shard in update order on stream_, push it over the client's link
     hipp(hipSetDevice(eng_.device()), "hipSetDevice");
     hipStream_t cs = cstream_[size_t(ci)];
@@ -295,7 +295,7 @@ void PSServer::do_grad(int c, bool pull) {
     }
   }
   if (!device_ && tx_.remote_device(m)) throw std::runtime_error("mpit: host server cannot read a device tx window");
-  if (pipelined(ci)) {
+  if (pipelined(ci, c)) {
     // link stream: pull the gradient shard into this client's inbox; stream_: fused update
     // (+ snapshot into the outbox when a pull is due); link stream: push the snapshot
     hipp(hipSetDevice(eng_.device()), "hipSetDevice");
@@ -333,7 +333,7 @@ void PSServer::do_grad(int c, bool pull) {
     return;
   }
   void* fused_out = nullptr;
-  if (pull && !defer_pull && (datapath_ == 0 || !device_))
+  if (pull && !defer_pull && (datapath_ != 1 || !device_))
     fused_out = reinterpret_cast<uint8_t*>(rx_.remote_ptr(m)) + off_ * 4;
   if (device_) {
     hipp(hipSetDevice(eng_.device()), "hipSetDevice");

@@ -12,11 +12,14 @@
 //    (rx: where pulled shards land, normally the model's own flat parameters; tx: the
 //    pushed gradient / parameter vector). A server reads tx and writes rx directly over
 //    xGMI; only 128-B control messages go through the shm rings.
-//  * A push is ONE fused kernel on the server's high-priority HIP stream: it reads the
-//    client's gradient shard from the peer's HBM, applies the update rule to the
-//    resident shard + optimizer state, and (for push+pull) stores the fresh shard
-//    straight into the client's rx window (datapath 0). Datapath 1 instead moves data
-//    with hipMemcpyAsync (SDMA engines, no CUs) around a local fused kernel.
+//  * Datapath 2 (default on HBM): every remote client has its own high-priority "link"
+//    stream and inbox/outbox pair; its gradient shard is pulled (SDMA peer copy over its
+//    own xGMI link) while other clients' transfers proceed on theirs, the fused update
+//    rule runs on the server stream (and snapshots the shard into the outbox when a pull
+//    is due), and the snapshot is pushed back on the link stream. The worker on the
+//    server's own GPU is served by ONE fused kernel (read tx, update, write rx) with no
+//    copies. Datapath 0 does that fused kernel for every client, reading/writing peer
+//    HBM directly; datapath 1 uses serial SDMA copies around a local kernel.
 //  * All updates of a shard are serialised on that one stream, so a pull always copies a
 //    consistent snapshot (the reference sends p while recvgrad mutates it,
 //    asyncsgd/pserver.lua:81).
@@ -120,7 +123,8 @@ class PSServer {
   std::vector<hipEvent_t> ev_in_, ev_up_, ev_out_;
   uint8_t* stage_ = nullptr;
   void finish_on(hipStream_t s, std::function<void()> then);
-  bool pipelined(int ci) const { return device_ && datapath_ == 2 && ci >= 0; }
+  // the worker on this very GPU is served by the fused local kernel (no copies at all)
+  bool pipelined(int ci, int c) const { return device_ && datapath_ == 2 && ci >= 0 && c != eng_.rank(); }
   std::atomic<int> stopped_{0};
   std::atomic<int64_t> version_{0};
   int init_rank_;                 // client whose parameter push initialises the shard (-1: ready)

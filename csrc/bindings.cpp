@@ -81,6 +81,17 @@ PYBIND11_MODULE(_mpit, m) {
         [](int dev, uintptr_t s, bool bf16, uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t dx, uintptr_t dres, int64_t M,
            int C, uintptr_t gamma, uintptr_t mean, uintptr_t rstd, uintptr_t dgamma, uintptr_t dbeta, uintptr_t ws,
            bool relu) { bn_act_bwd(dev, S(s), bf16, dy, y, x, dx, dres, M, C, gamma, mean, rstd, dgamma, dbeta, ws, relu); });
+  m.def("gemm_nt_supported", &gemm_nt_supported);
+  m.def("gemm_nt_stats_floats", &gemm_nt_stats_floats);
+  m.def("gemm_nt", [](int dev, uintptr_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B, int64_t ldb,
+                      uintptr_t C, int64_t ldc, uintptr_t stats) { gemm_nt(dev, S(s), M, N, K, A, lda, B, ldb, C, ldc, stats); });
+  m.def("gemm_tn_supported", &gemm_tn_supported);
+  m.def("gemm_tn_ws_floats", &gemm_tn_ws_floats);
+  m.def("gemm_tn", [](int dev, uintptr_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X, int64_t ldx,
+                      uintptr_t out, uintptr_t ws, float beta) { gemm_tn(dev, S(s), M, N, K, Y, ldy, X, ldx, out, ws, beta); });
+  m.def("cast_transpose", [](int dev, uintptr_t s, uintptr_t w, int R, int Cc, uintptr_t wb, uintptr_t wt) {
+    cast_transpose(dev, S(s), w, R, Cc, wb, wt);
+  });
 
   py::class_<Engine>(m, "Engine")
       .def(py::init<const std::string&, int, int, bool, int, int64_t>(), py::arg("name"), py::arg("world"),

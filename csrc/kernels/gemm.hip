@@ -1,0 +1,556 @@
+// MFMA GEMMs for NHWC 1x1 convolutions (bf16 operands, fp32 accumulate), gfx950.
+//
+// A stride-1 1x1 convolution over a channels_last activation is a plain GEMM over the
+// [M = N*H*W, C] row-major matrix view:
+//   forward  Y[M,Co]  = X[M,Ci] . W[Co,Ci]^T        -> gemm_nt  (A = X,  B = W)
+//   dgrad    dX[M,Ci] = dY[M,Co] . W[Co,Ci]         -> gemm_nt  (A = dY, B = W^T)
+//   wgrad    dW[Co,Ci] = dY[M,Co]^T . X[M,Ci]       -> gemm_tn  (reduction over M, split-K)
+// The ResNet-50 shapes are tall and skinny (M up to 802816, Ci/Co 64..2048), so most of
+// them are HBM-bound: the kernels below stream A once, keep the weight tile resident in
+// LDS/L2, and (forward) can emit the per-channel batch-norm statistics of the output
+// from the accumulators, which saves the separate statistics pass over Y.
+//
+// gemm_nt: C[M,N] = A[M,K] . B[N,K]^T, both operands K-contiguous. 256 threads = 4 waves
+// in a 2x2 arrangement; each wave owns a (BM/2)x(BN/2) sub-tile built from 32x32x16 bf16
+// MFMAs. Tiles of BK=64 are staged global->VGPR->LDS with 16-byte loads, double buffered
+// (one barrier per k-tile; the loads of tile k+1 are in flight during the MFMAs of tile
+// k). LDS rows are 128 B with the 16-byte chunk XOR-swizzled by (row>>1)&7, so the
+// ds_read_b128 fragment reads of any 16 consecutive rows hit 64 distinct banks. The MFMA
+// is issued with the operands swapped (D = B.A^T) so each lane ends up holding 4
+// consecutive output channels of one row: the epilogue packs them into 8-byte stores
+// without an LDS round trip. Block -> tile mapping is XCD-aware: the blocks that share
+// an A row-panel are dispatched to the same XCD so the panel is fetched into one L2.
+//
+// gemm_tn (wgrad): both operands are M-major, the reduction runs over rows. Tiles of 64
+// rows x 128 (or 64) columns are staged row-major in LDS (row stride padded by 64 B) and
+// the MFMA fragments (8 consecutive rows of one column) are read with the gfx950
+// transposing LDS read ds_read_b64_tr_b16. M is split over blocks; each split writes an
+// fp32 partial tile and a vectorised reduce sums the splits (deterministic, no atomics).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <stdexcept>
+#include <string>
+
+#include "ew.h"
+#include "kernels.h"
+
+namespace mpit {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int kBK = 32;  // k-depth of one staged tile (gemm_nt): 64-B LDS rows
+
+// 16-B chunk swizzle of a 64-B LDS row: any 16 consecutive rows read at one logical chunk
+// hit 16 distinct (row%4, chunk) bank groups = all 64 banks.
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+// 16-byte global -> LDS DMA; the LDS address must be wave-uniform (lane data lands at
+// lds + 16*lane).
+__device__ __forceinline__ void glds16(const void* src, void* lds) {
+  __builtin_amdgcn_global_load_lds(src, (lds_void*)lds, 16, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Map a linear block id to a tile id so that consecutive tile ids (which share the A
+// row-panel) land on one XCD: blocks are dispatched round-robin over the 8 XCDs.
+__device__ __forceinline__ int xcd_tile(int bid, int nb) {
+  if (nb % 8) return bid;
+  return (bid % 8) * (nb / 8) + bid / 8;
+}
+
+// ------------------------------------------------------------------------------ NT GEMM
+// EPI bit 0: accumulate per-column sum / sum of squares of the (bf16-rounded) output
+// into stats[blockRow][2][N] (fp32 partials, one row per M-tile; reduced by the caller).
+//
+// Staging: global_load_lds (16-B LDS DMA, no VGPRs) into a ring of STAGES buffers with
+// STAGES-1 k-tiles in flight; a counted s_waitcnt vmcnt + raw s_barrier retires exactly
+// the tile about to be used (a __syncthreads() would drain the whole ring). The LDS image
+// is lane-linear per wave instruction (16 rows x 64 B); the swizzle is applied on the
+// global source address.
+template <int BM, int BN, int STAGES, bool STATS>
+__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda,
+                                                         const uint16_t* __restrict__ B, int64_t ldb,
+                                                         uint16_t* __restrict__ C, int64_t ldc, int64_t M, int N, int K,
+                                                         int ntn, float* __restrict__ stats) {
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int TM = WM / 32, TN = WN / 32;
+  constexpr int IA = BM / 16 / 4, IB = BN / 16 / 4;  // glds instructions per wave per tile
+  constexpr int NI = IA + IB;
+  constexpr int TILE = (BM + BN) * kBK;  // elements per stage
+  static_assert(IA >= 1 && IB >= 1, "tile too small");
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int mt = tile / ntn, nt = tile % ntn;
+  const int64_t m0 = int64_t(mt) * BM;
+  const int n0 = nt * BN;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w >> 1, wn = w & 1;
+
+  // source of this lane for each of the wave's glds instructions (k offset added per tile)
+  const uint16_t* pa[IA];
+  const uint16_t* pb[IB];
+#pragma unroll
+  for (int i = 0; i < IA; ++i) {
+    const int row = (w * IA + i) * 16 + (lane >> 2), c = swz(row, lane & 3);
+    const int64_t gm = min(m0 + row, M - 1);  // clamp: tail rows compute garbage, never stored
+    pa[i] = A + gm * lda + c * 8;
+  }
+#pragma unroll
+  for (int i = 0; i < IB; ++i) {
+    const int row = (w * IB + i) * 16 + (lane >> 2), c = swz(row, lane & 3);
+    pb[i] = B + int64_t(n0 + row) * ldb + c * 8;
+  }
+  auto issue = [&](int kt, int buf) {
+    uint16_t* As = smem + buf * TILE;
+    uint16_t* Bs = As + BM * kBK;
+#pragma unroll
+    for (int i = 0; i < IA; ++i)
+      glds16(pa[i] + kt * kBK, As + (w * IA + i) * 16 * kBK);
+#pragma unroll
+    for (int i = 0; i < IB; ++i)
+      glds16(pb[i] + kt * kBK, Bs + (w * IB + i) * 16 * kBK);
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
+
+  const int nk = K / kBK;
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) issue(s, s);
+  const int fr = lane & 31, fh = lane >> 5;
+  for (int kt = 0; kt < nk; ++kt) {
+    // tiles issued after kt that may stay in flight
+    const int after = min(nk, kt + STAGES - 1) - (kt + 1);
+    if (STAGES >= 4 && after >= 2) wait_vmcnt<2 * NI>();
+    else if (STAGES >= 3 && after >= 1) wait_vmcnt<NI>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
+    const uint16_t* As = smem + (kt % STAGES) * TILE;
+    const uint16_t* Bs = As + BM * kBK;
+#pragma unroll
+    for (int kk = 0; kk < kBK / 16; ++kk) {
+      bf16x8 af[TM], bfg[TN];
+      const int c = 2 * kk + fh;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int r = wm * WM + i * 32 + fr;
+        af[i] = *reinterpret_cast<const bf16x8*>(As + r * kBK + swz(r, c) * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int r = wn * WN + j * 32 + fr;
+        bfg[j] = *reinterpret_cast<const bf16x8*>(Bs + r * kBK + swz(r, c) * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfg[j], af[i], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  // epilogue: lane holds D[n][m] with m = lane&31, n = (v&3) + 8*(v>>2) + 4*(lane>>5)
+  float s1[TN][16], s2[TN][16];
+  if constexpr (STATS) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) s1[j][v] = s2[j][v] = 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int64_t m = m0 + wm * WM + i * 32 + fr;
+    const bool ok = m < M;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = n0 + wn * WN + j * 32 + 8 * g + 4 * fh;
+        uint16_t h[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          h[e] = f2bf(acc[i][j][4 * g + e]);
+          if constexpr (STATS) {
+            const float y = ok ? bf2f(h[e]) : 0.f;
+            s1[j][4 * g + e] += y;
+            s2[j][4 * g + e] = fmaf(y, y, s2[j][4 * g + e]);
+          }
+        }
+        if (ok) {
+          uint2 pk;
+          pk.x = uint32_t(h[0]) | (uint32_t(h[1]) << 16);
+          pk.y = uint32_t(h[2]) | (uint32_t(h[3]) << 16);
+          *reinterpret_cast<uint2*>(C + m * ldc + n) = pk;
+        }
+      }
+    }
+  }
+  if constexpr (STATS) {
+    // reduce over the 32 lanes that share a column set (lane&31 varies = rows), then
+    // over the two row-halves of the block (wm) through LDS.
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        float a = s1[j][v], b = s2[j][v];
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) {
+          a += __shfl_xor(a, o);
+          b += __shfl_xor(b, o);
+        }
+        s1[j][v] = a;
+        s2[j][v] = b;
+      }
+    __syncthreads();  // the ring may still be read by other waves
+    float* red = reinterpret_cast<float*>(smem);  // [2 (wm)][2][BN]
+    if (fr == 0) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+          const int n = wn * WN + j * 32 + (v & 3) + 8 * (v >> 2) + 4 * fh;
+          red[(wm * 2 + 0) * BN + n] = s1[j][v];
+          red[(wm * 2 + 1) * BN + n] = s2[j][v];
+        }
+    }
+    __syncthreads();
+    for (int n = t; n < BN; n += 256) {
+      stats[(int64_t(mt) * 2 + 0) * N + n0 + n] = red[0 * BN + n] + red[2 * BN + n];
+      stats[(int64_t(mt) * 2 + 1) * N + n0 + n] = red[1 * BN + n] + red[3 * BN + n];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ TN GEMM
+// part[split][N][K] = sum over rows m of this split of dY[m][n] * X[m][k]
+constexpr int kRows = 64;  // rows (reduction) per staged step
+
+template <int TBN, int TBK>
+__global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const uint16_t* __restrict__ Y, int64_t ldy,
+                                                         const uint16_t* __restrict__ X, int64_t ldx,
+                                                         float* __restrict__ part, int64_t M, int N, int K,
+                                                         int64_t rows_per_split, int ntk, int ntiles) {
+  constexpr int SY = TBN + 32, SX = TBK + 32;  // padded LDS row strides (elements)
+  constexpr int WN = TBN / 2, WK = TBK / 2;
+  constexpr int TM = WN / 32, TN = WK / 32;
+  constexpr int YC = kRows * TBN / 8 / 256, XC = kRows * TBK / 8 / 256;
+  constexpr int CPY = TBN / 8, CPX = TBK / 8;  // 16-B chunks per row
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+
+  const int id = xcd_tile(blockIdx.x, gridDim.x);
+  const int tile = id % ntiles, split = id / ntiles;
+  const int n0 = (tile / ntk) * TBN, k0 = (tile % ntk) * TBK;
+  const int64_t r0 = int64_t(split) * rows_per_split;
+  const int64_t r1 = min(M, r0 + rows_per_split);
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, wn = w >> 1, wk = w & 1;
+
+  int ry[YC], cy[YC], rx[XC], cx[XC];
+#pragma unroll
+  for (int i = 0; i < YC; ++i) {
+    const int q = t + 256 * i;
+    ry[i] = q / CPY;
+    cy[i] = q % CPY;
+  }
+#pragma unroll
+  for (int i = 0; i < XC; ++i) {
+    const int q = t + 256 * i;
+    rx[i] = q / CPX;
+    cx[i] = q % CPX;
+  }
+  uint4 vy[YC], vx[XC];
+  auto gload = [&](int64_t rb) {
+#pragma unroll
+    for (int i = 0; i < YC; ++i) {
+      const int64_t r = rb + ry[i];
+      vy[i] = r < r1 ? *reinterpret_cast<const uint4*>(Y + r * ldy + n0 + cy[i] * 8) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < XC; ++i) {
+      const int64_t r = rb + rx[i];
+      vx[i] = r < r1 ? *reinterpret_cast<const uint4*>(X + r * ldx + k0 + cx[i] * 8) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto sstore = [&](int buf) {
+    uint16_t* Ys = smem + buf * kRows * (SY + SX);
+    uint16_t* Xs = Ys + kRows * SY;
+#pragma unroll
+    for (int i = 0; i < YC; ++i) *reinterpret_cast<uint4*>(Ys + ry[i] * SY + cy[i] * 8) = vy[i];
+#pragma unroll
+    for (int i = 0; i < XC; ++i) *reinterpret_cast<uint4*>(Xs + rx[i] * SX + cx[i] * 8) = vx[i];
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
+
+  // transposed-read lane geometry: 16-lane group g, lane i = 4q + p of the group
+  const int g = lane >> 4, gi = lane & 15, q = gi >> 2, p = gi & 3;
+  const int h = g >> 1, cb = 16 * (g & 1) + 4 * p;  // fragment rows 8h.., column block start
+
+  const int64_t nsteps = r1 > r0 ? (r1 - r0 + kRows - 1) / kRows : 0;
+  if (nsteps > 0) {
+    gload(r0);
+    sstore(0);
+  }
+  __syncthreads();
+  for (int64_t s = 0; s < nsteps; ++s) {
+    const int cur = int(s & 1);
+    if (s + 1 < nsteps) gload(r0 + (s + 1) * kRows);
+    const uint16_t* Ys = smem + cur * kRows * (SY + SX);
+    const uint16_t* Xs = Ys + kRows * SY;
+#pragma unroll
+    for (int kk = 0; kk < kRows / 16; ++kk) {
+      const int rr = 16 * kk + 8 * h + q;  // row of the first 4-row block
+      bf16x8 af[TM], bfg[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const uint16_t* base = Ys + rr * SY + wn * WN + i * 32 + cb;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + 4 * SY));
+        af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const uint16_t* base = Xs + rr * SX + wk * WK + j * 32 + cb;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + 4 * SX));
+        bfg[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
+    }
+    if (s + 1 < nsteps) sstore(cur ^ 1);
+    __syncthreads();
+  }
+  // D[n][k]: column k = lane&31, row n = (v&3) + 8*(v>>2) + 4*(lane>>5)
+  float* out = part + int64_t(split) * N * K;
+  const int fr = lane & 31, fh = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int n = n0 + wn * WN + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fh;
+        const int k = k0 + wk * WK + j * 32 + fr;
+        out[int64_t(n) * K + k] = acc[i][j][v];
+      }
+}
+
+// out[i] = beta*out[i] + sum_s part[s][i]   (float4 lanes)
+__global__ __launch_bounds__(256) void split_reduce_kernel(const float4* __restrict__ part, int nsplit, int64_t n4,
+                                                           float4* __restrict__ out, float beta) {
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n4; i += int64_t(gridDim.x) * blockDim.x) {
+    float4 a = part[i];
+    for (int s = 1; s < nsplit; ++s) {
+      const float4 b = part[int64_t(s) * n4 + i];
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    if (beta != 0.f) {
+      const float4 o = out[i];
+      a.x += beta * o.x; a.y += beta * o.y; a.z += beta * o.z; a.w += beta * o.w;
+    }
+    out[i] = a;
+  }
+}
+
+// fp32 [R][Cc] -> bf16 copy [R][Cc] and bf16 transpose [Cc][R]
+__global__ __launch_bounds__(256) void cast_transpose_kernel(const float* __restrict__ w, int R, int Cc,
+                                                             uint16_t* __restrict__ wb, uint16_t* __restrict__ wt) {
+  __shared__ uint16_t tile[32][33];
+  const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 8 rows per pass
+  for (int y = ty; y < 32; y += 8) {
+    const int r = r0 + y, c = c0 + tx;
+    if (r < R && c < Cc) {
+      const uint16_t b = f2bf(w[int64_t(r) * Cc + c]);
+      if (wb) wb[int64_t(r) * Cc + c] = b;
+      tile[y][tx] = b;
+    }
+  }
+  __syncthreads();
+  if (!wt) return;
+  for (int y = ty; y < 32; y += 8) {
+    const int c = c0 + y, r = r0 + tx;
+    if (r < R && c < Cc) wt[int64_t(c) * R + r] = tile[tx][y];
+  }
+}
+
+void check_ptr(uintptr_t p, const char* what) {
+  if (p % 16) throw std::invalid_argument(std::string("gemm: ") + what + " must be 16-byte aligned");
+}
+
+int cu_count(int dev) {
+  static int cached[64] = {0};
+  if (dev < 0 || dev >= 64) return 256;
+  if (!cached[dev]) {
+    int v = 0;
+    hip_check(hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev), "hipDeviceGetAttribute");
+    cached[dev] = v > 0 ? v : 256;
+  }
+  return cached[dev];
+}
+
+}  // namespace
+
+bool gemm_nt_supported(int64_t M, int N, int K) { return M > 0 && N > 0 && K > 0 && N % 64 == 0 && K % kBK == 0; }
+
+int64_t gemm_nt_stats_floats(int64_t M, int N) { return ((M + 127) / 128) * 2 * int64_t(N); }
+
+void gemm_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B, int64_t ldb,
+             uintptr_t C, int64_t ldc, uintptr_t stats) {
+  if (!gemm_nt_supported(M, N, K))
+    throw std::invalid_argument("gemm_nt: need N % 64 == 0 and K % 64 == 0 (M=" + std::to_string(M) +
+                                " N=" + std::to_string(N) + " K=" + std::to_string(K) + ")");
+  check_ptr(A, "A");
+  check_ptr(B, "B");
+  check_ptr(C, "C");
+  if (lda % 8 || ldb % 8 || ldc % 4 || lda < K || ldb < K || ldc < N)
+    throw std::invalid_argument("gemm_nt: bad leading dimensions");
+  hip_check(hipSetDevice(dev), "hipSetDevice");
+  const auto* a = reinterpret_cast<const uint16_t*>(A);
+  const auto* b = reinterpret_cast<const uint16_t*>(B);
+  auto* c = reinterpret_cast<uint16_t*>(C);
+  auto* st = reinterpret_cast<float*>(stats);
+  constexpr int BM = 128;
+  const int64_t mtn = (M + BM - 1) / BM;
+  const int nk = K / kBK;
+  const int stages = nk >= 4 ? 4 : (nk == 3 ? 3 : 2);
+  // (kernel templates are named at a non-template call site so their host stubs are emitted)
+#define MPIT_NT_LAUNCH(BN, ST)                                                                                  \
+  do {                                                                                                          \
+    const int ntn = N / BN;                                                                                     \
+    const int64_t nb = mtn * ntn;                                                                               \
+    if (nb > INT32_MAX) throw std::invalid_argument("gemm_nt: too many tiles");                                 \
+    const size_t shm = size_t(ST) * (BM + BN) * kBK * sizeof(uint16_t);                                         \
+    if (st)                                                                                                     \
+      hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, ST, true>), dim3(unsigned(nb)), dim3(256), shm, s, a, lda, b,  \
+                         ldb, c, ldc, M, N, K, ntn, st);                                                        \
+    else                                                                                                        \
+      hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, ST, false>), dim3(unsigned(nb)), dim3(256), shm, s, a, lda, b, \
+                         ldb, c, ldc, M, N, K, ntn, st);                                                        \
+  } while (0)
+  if (N % 128 == 0) {
+    if (stages == 4) MPIT_NT_LAUNCH(128, 4);
+    else if (stages == 3) MPIT_NT_LAUNCH(128, 3);
+    else MPIT_NT_LAUNCH(128, 2);
+  } else {
+    if (stages == 4) MPIT_NT_LAUNCH(64, 4);
+    else if (stages == 3) MPIT_NT_LAUNCH(64, 3);
+    else MPIT_NT_LAUNCH(64, 2);
+  }
+#undef MPIT_NT_LAUNCH
+  hip_check(hipGetLastError(), "gemm_nt launch");
+}
+
+bool gemm_tn_supported(int64_t M, int N, int K) { return M > 0 && N % 64 == 0 && K % 64 == 0 && N > 0 && K > 0; }
+
+// split-K plan: returns the number of splits and rows per split
+static int tn_plan(int dev, int64_t M, int N, int K, int64_t* rows_per_split, int* tbn, int* tbk) {
+  *tbn = N % 128 == 0 ? 128 : 64;
+  *tbk = K % 128 == 0 ? 128 : 64;
+  const int64_t ntiles = int64_t(N / *tbn) * (K / *tbk);
+  const int64_t target = 2 * int64_t(cu_count(dev));  // ~2 resident blocks per CU
+  int64_t ns = std::max<int64_t>(1, (target + ntiles - 1) / ntiles);
+  const int64_t min_rows = 8 * kRows;  // keep >= 8 staged steps per block
+  ns = std::min<int64_t>(ns, std::max<int64_t>(1, M / min_rows));
+  int64_t rps = (M + ns - 1) / ns;
+  rps = (rps + kRows - 1) / kRows * kRows;
+  ns = (M + rps - 1) / rps;
+  *rows_per_split = rps;
+  return int(ns);
+}
+
+int64_t gemm_tn_ws_floats(int dev, int64_t M, int N, int K) {
+  int64_t rps;
+  int tbn, tbk;
+  const int ns = tn_plan(dev, M, N, K, &rps, &tbn, &tbk);
+  return ns > 1 ? int64_t(ns) * N * K : 0;
+}
+
+void gemm_tn(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X, int64_t ldx,
+             uintptr_t out, uintptr_t ws, float beta) {
+  if (!gemm_tn_supported(M, N, K))
+    throw std::invalid_argument("gemm_tn: need N % 64 == 0 and K % 64 == 0");
+  check_ptr(Y, "Y");
+  check_ptr(X, "X");
+  check_ptr(out, "out");
+  if (ldy % 8 || ldx % 8 || ldy < N || ldx < K) throw std::invalid_argument("gemm_tn: bad leading dimensions");
+  hip_check(hipSetDevice(dev), "hipSetDevice");
+  int64_t rps;
+  int tbn, tbk;
+  const int ns = tn_plan(dev, M, N, K, &rps, &tbn, &tbk);
+  const int ntk = K / tbk;
+  const int ntiles = (N / tbn) * ntk;
+  const bool direct = ns == 1 && beta == 0.f;
+  if (!direct && ws == 0) throw std::invalid_argument("gemm_tn: workspace required");
+  if (!direct) check_ptr(ws, "ws");
+  float* part = reinterpret_cast<float*>(direct ? out : (ns > 1 ? ws : ws));
+  const auto* y = reinterpret_cast<const uint16_t*>(Y);
+  const auto* x = reinterpret_cast<const uint16_t*>(X);
+  const dim3 grid(unsigned(int64_t(ntiles) * ns));
+  const size_t shm = 2 * size_t(kRows) * ((tbn + 32) + (tbk + 32)) * sizeof(uint16_t);
+  static bool lds_attr_set = false;  // > 64 KiB of dynamic LDS must be opted into
+  if (!lds_attr_set) {
+    hip_check(hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_kernel<128, 128>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kRows * (160 + 160) * 2),
+              "hipFuncSetAttribute");
+    hip_check(hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_kernel<128, 64>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kRows * (160 + 96) * 2),
+              "hipFuncSetAttribute");
+    hip_check(hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_kernel<64, 128>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kRows * (96 + 160) * 2),
+              "hipFuncSetAttribute");
+    lds_attr_set = true;
+  }
+  if (tbn == 128 && tbk == 128)
+    hipLaunchKernelGGL((gemm_tn_kernel<128, 128>), grid, dim3(256), shm, s, y, ldy, x, ldx, part, M, N, K, rps, ntk, ntiles);
+  else if (tbn == 128)
+    hipLaunchKernelGGL((gemm_tn_kernel<128, 64>), grid, dim3(256), shm, s, y, ldy, x, ldx, part, M, N, K, rps, ntk, ntiles);
+  else if (tbk == 128)
+    hipLaunchKernelGGL((gemm_tn_kernel<64, 128>), grid, dim3(256), shm, s, y, ldy, x, ldx, part, M, N, K, rps, ntk, ntiles);
+  else
+    hipLaunchKernelGGL((gemm_tn_kernel<64, 64>), grid, dim3(256), shm, s, y, ldy, x, ldx, part, M, N, K, rps, ntk, ntiles);
+  hip_check(hipGetLastError(), "gemm_tn launch");
+  if (!direct) {
+    const int64_t n4 = int64_t(N) * K / 4;
+    const int g = int(std::min<int64_t>((n4 + 255) / 256, 2048));
+    hipLaunchKernelGGL(split_reduce_kernel, dim3(g), dim3(256), 0, s, reinterpret_cast<const float4*>(part), ns, n4,
+                       reinterpret_cast<float4*>(out), beta);
+    hip_check(hipGetLastError(), "gemm_tn reduce launch");
+  }
+}
+
+void cast_transpose(int dev, hipStream_t s, uintptr_t w, int R, int Cc, uintptr_t wb, uintptr_t wt) {
+  hip_check(hipSetDevice(dev), "hipSetDevice");
+  const dim3 grid((Cc + 31) / 32, (R + 31) / 32);
+  hipLaunchKernelGGL(cast_transpose_kernel, grid, dim3(256), 0, s, reinterpret_cast<const float*>(w), R, Cc,
+                     reinterpret_cast<uint16_t*>(wb), reinterpret_cast<uint16_t*>(wt));
+  hip_check(hipGetLastError(), "cast_transpose launch");
+}
+
+}  // namespace mpit

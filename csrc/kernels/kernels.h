@@ -76,4 +76,19 @@ void bn_act_bwd(int dev, hipStream_t s, bool bf16, uintptr_t dy, uintptr_t y, ui
                 int64_t M, int C, uintptr_t gamma, uintptr_t mean, uintptr_t rstd, uintptr_t dgamma, uintptr_t dbeta,
                 uintptr_t ws, bool relu);
 
+// ---- MFMA GEMMs for NHWC 1x1 convolutions (gemm.hip), bf16 operands, fp32 accumulate --
+// C[M,N] (bf16) = A[M,K] . B[N,K]^T; optional per-column {sum, sumsq} partials of C per
+// 128-row tile into stats[ceil(M/128)][2][N] (gemm_nt_stats_floats).
+bool gemm_nt_supported(int64_t M, int N, int K);
+int64_t gemm_nt_stats_floats(int64_t M, int N);
+void gemm_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B, int64_t ldb,
+             uintptr_t C, int64_t ldc, uintptr_t stats);
+// out[N,K] (fp32) = beta*out + Y[M,N]^T . X[M,K]  (split over M; ws: gemm_tn_ws_floats)
+bool gemm_tn_supported(int64_t M, int N, int K);
+int64_t gemm_tn_ws_floats(int dev, int64_t M, int N, int K);
+void gemm_tn(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X, int64_t ldx,
+             uintptr_t out, uintptr_t ws, float beta);
+// fp32 w[R][Cc] -> bf16 wb[R][Cc] (optional) and bf16 wt[Cc][R] (optional)
+void cast_transpose(int dev, hipStream_t s, uintptr_t w, int R, int Cc, uintptr_t wb, uintptr_t wt);
+
 }  // namespace mpit

@@ -3,17 +3,21 @@ workload "ResNet-50 synthetic ImageNet". Written from the architecture definitio
 (torchvision is not available in this image); parameter count 25,557,032 for
 ResNet-50 / 1000 classes, the standard figure.
 
-Runs channels_last + bf16 autocast on MI355X, so convolutions go to MIOpen's NHWC
-kernels and the batch-norm / ReLU / add chains to PyTorch-ROCm's fused NHWC kernels.
+Runs channels_last + bf16 autocast on MI355X: stride-1 1x1 convolutions on the
+hand-written MFMA GEMMs (mpit_amd/ops/conv.py), the 3x3 / 7x7 / strided ones on MIOpen's
+NHWC kernels, and every BatchNorm(+add)(+ReLU) on the fused HIP kernels (ops/bn.py).
 """
 from __future__ import annotations
 
 from typing import List, Type, Union
 
+import os
+
 import torch
 import torch.nn as nn
 
 from ..ops.bn import BatchNormAct2d
+from ..ops.conv import Conv1x1
 
 # Fused BN(+add)(+ReLU) HIP kernels on MI355X (mpit_amd/ops/bn.py); same parameters and
 # state dict as nn.BatchNorm2d, and plain PyTorch math on CPU tensors.
@@ -28,7 +32,14 @@ def conv3x3(i, o, stride=1):
     return nn.Conv2d(i, o, 3, stride=stride, padding=1, bias=False)
 
 
+# 1x1 convolutions as MFMA GEMMs (falls back to F.conv2d for strides / CPU / odd shapes);
+# MPIT_MFMA_CONV=0 routes them to MIOpen instead (A/B measurements).
+MFMA_CONV = os.environ.get("MPIT_MFMA_CONV", "1") != "0"
+
+
 def conv1x1(i, o, stride=1):
+    if MFMA_CONV:
+        return Conv1x1(i, o, stride=stride)
     return nn.Conv2d(i, o, 1, stride=stride, bias=False)
 
 

@@ -1,0 +1,158 @@
+"""1x1 convolutions on the hand-written MFMA GEMMs (csrc/kernels/gemm.hip).
+
+A stride-1 1x1 convolution over a channels_last activation is a GEMM over its [N*H*W, C]
+row-major view. Measured on MI355X (benchmarks/conv_vs_gemm.py, ResNet-50 at batch 256)
+MIOpen runs these at 100-450 TFLOP/s, and every backward-weight call also costs a zero
+fill + an fp32->bf16 cast of MIOpen's own. Here:
+
+* forward: ``Y = X . W^T`` (``gemm_nt``, bf16 out), optionally emitting the per-channel
+  batch-norm statistics of ``Y`` from the accumulators;
+* backward-data: ``dX = dY . W`` (``gemm_nt`` with a transposed bf16 copy of ``W`` made in
+  the forward by ``cast_transpose``);
+* backward-weight: ``dW = dY^T . X`` in fp32 straight from the accumulators (``gemm_tn``,
+  split over M, deterministic reduce) — the fp32 master weight gets an fp32 gradient with
+  no bf16 rounding and no cast kernel.
+
+:class:`Conv1x1` is a drop-in ``nn.Conv2d`` that takes this path on the GPU for bf16
+(autocast) channels_last inputs whose channel counts are multiples of 64, and falls
+back to ``F.conv2d`` otherwise (CPU tests, odd shapes, strides).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .._ext import native
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _cl(x: torch.Tensor) -> torch.Tensor:
+    return x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
+
+
+def gemm_nt(a: torch.Tensor, b: torch.Tensor, stats: bool = False):
+    """``a[M,K] . b[N,K]^T`` in bf16 (fp32 accumulate). With ``stats`` also returns the
+    per-column ``[sum, sum of squares]`` of the bf16 result as a [2, N] fp32 tensor."""
+    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
+        raise TypeError("gemm_nt takes bf16 operands")
+    if a.dim() != 2 or b.dim() != 2 or a.shape[1] != b.shape[1] or a.stride(1) != 1 or b.stride(1) != 1:
+        raise ValueError("gemm_nt: a[M,K], b[N,K] with unit column stride")
+    M, K = a.shape
+    N = b.shape[0]
+    c = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    m = native()
+    st = torch.empty(m.gemm_nt_stats_floats(M, N), dtype=torch.float32, device=a.device) if stats else None
+    m.gemm_nt(a.device.index, _stream(a), M, N, K, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(),
+              N, st.data_ptr() if st is not None else 0)
+    if stats:
+        return c, st.view(-1, 2, N).sum(0)
+    return c
+
+
+def gemm_tn(y: torch.Tensor, x: torch.Tensor, out: torch.Tensor = None, beta: float = 0.0) -> torch.Tensor:
+    """``out[N,K] = beta*out + y[M,N]^T . x[M,K]`` in fp32 from bf16 operands."""
+    if y.dtype != torch.bfloat16 or x.dtype != torch.bfloat16:
+        raise TypeError("gemm_tn takes bf16 operands")
+    M, N = y.shape
+    K = x.shape[1]
+    if x.shape[0] != M or y.stride(1) != 1 or x.stride(1) != 1:
+        raise ValueError("gemm_tn: y[M,N], x[M,K] with unit column stride")
+    if out is None:
+        out = torch.empty((N, K), dtype=torch.float32, device=y.device)
+        beta = 0.0
+    m = native()
+    dev = y.device.index
+    # split partials; with a single split and beta != 0 the one partial goes through the reduce
+    nws = m.gemm_tn_ws_floats(dev, M, N, K) or (N * K if beta != 0.0 else 0)
+    ws = torch.empty(nws, dtype=torch.float32, device=y.device) if nws else None
+    m.gemm_tn(dev, _stream(y), M, N, K, y.data_ptr(), y.stride(0), x.data_ptr(), x.stride(0), out.data_ptr(),
+              ws.data_ptr() if ws is not None else 0, float(beta))
+    return out
+
+
+def cast_transpose(w: torch.Tensor):
+    """fp32 ``w[R, C]`` -> (bf16 copy [R, C], bf16 transpose [C, R]) in one launch."""
+    w2 = w.reshape(w.shape[0], -1)
+    if w2.dtype != torch.float32 or not w2.is_contiguous():
+        w2 = w2.float().contiguous()
+    R, C = w2.shape
+    wb = torch.empty((R, C), dtype=torch.bfloat16, device=w.device)
+    wt = torch.empty((C, R), dtype=torch.bfloat16, device=w.device)
+    native().cast_transpose(w.device.index, _stream(w), w2.data_ptr(), R, C, wb.data_ptr(), wt.data_ptr())
+    return wb, wt
+
+
+class _Conv1x1Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight):
+        x = _cl(x)
+        if x.dtype != torch.bfloat16:
+            x = x.to(torch.bfloat16)
+        n, ci, h, w = x.shape
+        co = weight.shape[0]
+        M = n * h * w
+        wb, wt = cast_transpose(weight)
+        y = torch.empty((n, co, h, w), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+        m = native()
+        m.gemm_nt(x.device.index, _stream(x), M, co, ci, x.data_ptr(), ci, wb.data_ptr(), ci, y.data_ptr(), co, 0)
+        ctx.save_for_backward(x, wt)
+        ctx.wshape = weight.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wt = ctx.saved_tensors
+        dy = _cl(dy)
+        if dy.dtype != torch.bfloat16:
+            dy = dy.to(torch.bfloat16)
+        n, ci, h, w = x.shape
+        co = dy.shape[1]
+        M = n * h * w
+        m = native()
+        dev, s = x.device.index, _stream(x)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x, memory_format=torch.channels_last)
+            m.gemm_nt(dev, s, M, ci, co, dy.data_ptr(), co, wt.data_ptr(), co, dx.data_ptr(), ci, 0)
+        if ctx.needs_input_grad[1]:
+            dw = torch.empty(ctx.wshape, dtype=torch.float32, device=x.device)
+            nws = m.gemm_tn_ws_floats(dev, M, co, ci)
+            ws = torch.empty(nws, dtype=torch.float32, device=x.device) if nws else None
+            m.gemm_tn(dev, s, M, co, ci, dy.data_ptr(), co, x.data_ptr(), ci, dw.data_ptr(),
+                      ws.data_ptr() if ws is not None else 0, 0.0)
+        return dx, dw
+
+
+def conv1x1_supported(x: torch.Tensor, weight: torch.Tensor) -> bool:
+    if not x.is_cuda or x.dim() != 4:
+        return False
+    bf16 = x.dtype == torch.bfloat16 or (torch.is_autocast_enabled("cuda")
+                                         and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+    if not bf16:
+        return False
+    co, ci = weight.shape[0], weight.shape[1]
+    return ci % 64 == 0 and co % 64 == 0 and x.shape[1] == ci
+
+
+def conv1x1(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """Stride-1, unpadded, bias-free 1x1 convolution (MFMA GEMM path when supported)."""
+    if conv1x1_supported(x, weight):
+        return _Conv1x1Fn.apply(x, weight)
+    return F.conv2d(x, weight)
+
+
+class Conv1x1(nn.Conv2d):
+    """``nn.Conv2d(i, o, 1, bias=False)`` whose stride-1 forward/backward run on the MFMA
+    GEMMs on MI355X (see module docstring)."""
+
+    def __init__(self, in_channels: int, out_channels: int, stride: int = 1):
+        super().__init__(in_channels, out_channels, 1, stride=stride, bias=False)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.stride == (1, 1) and conv1x1_supported(x, self.weight):
+            return _Conv1x1Fn.apply(x, self.weight)
+        return super().forward(x)

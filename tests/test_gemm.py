@@ -1,0 +1,96 @@
+"""MFMA GEMM kernels (csrc/kernels/gemm.hip) and the 1x1-conv op built on them, against
+plain PyTorch fp32 references of the same math."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from mpit_amd.ops import conv as C
+
+
+def test_conv1x1_cpu_fallback_matches_conv2d():
+    torch.manual_seed(0)
+    m = C.Conv1x1(64, 128)
+    x = torch.randn(2, 64, 5, 5)
+    assert torch.allclose(m(x), F.conv2d(x, m.weight), atol=1e-6)
+    assert not C.conv1x1_supported(x, m.weight)
+
+
+gpu = pytest.mark.gpu
+
+
+def _bf(*shape, scale=1.0):
+    return (torch.randn(*shape, device="cuda") * scale).to(torch.bfloat16)
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
+
+@gpu
+@pytest.mark.parametrize("M,N,K", [(128, 64, 64), (256, 128, 64), (1000, 192, 128), (4096, 256, 512),
+                                   (333, 64, 1024), (12544, 2048, 512), (50176, 256, 1024)])
+def test_gemm_nt(M, N, K):
+    torch.manual_seed(M + N + K)
+    a, b = _bf(M, K), _bf(N, K, scale=0.05)
+    ref = a.float() @ b.float().t()
+    c = C.gemm_nt(a, b)
+    assert c.shape == (M, N) and c.dtype == torch.bfloat16
+    assert _rel(c, ref) < 8e-3
+
+
+@gpu
+@pytest.mark.parametrize("M,N,K", [(256, 64, 64), (1000, 128, 192), (4096, 256, 256)])
+def test_gemm_nt_stats(M, N, K):
+    torch.manual_seed(1)
+    a, b = _bf(M, K), _bf(N, K, scale=0.05)
+    c, st = C.gemm_nt(a, b, stats=True)
+    cf = c.float()
+    assert torch.allclose(st[0], cf.sum(0), rtol=1e-3, atol=1e-2)
+    assert torch.allclose(st[1], (cf * cf).sum(0), rtol=1e-3, atol=1e-2)
+
+
+@gpu
+@pytest.mark.parametrize("M,N,K", [(64, 64, 64), (1000, 64, 128), (4096, 128, 128), (802816, 256, 64),
+                                   (12544, 512, 2048), (5000, 192, 320)])
+def test_gemm_tn(M, N, K):
+    torch.manual_seed(M % 97 + N + K)
+    y, x = _bf(M, N), _bf(M, K)
+    ref = y.float().t() @ x.float()
+    out = C.gemm_tn(y, x)
+    assert out.dtype == torch.float32 and out.shape == (N, K)
+    assert _rel(out, ref) < 1e-4
+    # beta accumulate
+    base = torch.randn(N, K, device="cuda")
+    out2 = C.gemm_tn(y, x, out=base.clone(), beta=1.0)
+    assert _rel(out2, ref + base) < 1e-4
+
+
+@gpu
+def test_cast_transpose():
+    w = torch.randn(192, 320, device="cuda")
+    wb, wt = C.cast_transpose(w)
+    assert torch.equal(wb, w.to(torch.bfloat16))
+    assert torch.equal(wt, w.t().contiguous().to(torch.bfloat16))
+
+
+@gpu
+@pytest.mark.parametrize("n,ci,co,hw", [(4, 64, 256, 14), (2, 256, 64, 9), (3, 128, 128, 7)])
+def test_conv1x1_fwd_bwd(n, ci, co, hw):
+    torch.manual_seed(n * ci + co)
+    mod = C.Conv1x1(ci, co).cuda().to(memory_format=torch.channels_last)
+    ref = torch.nn.Conv2d(ci, co, 1, bias=False).cuda()
+    ref.weight.data.copy_(mod.weight.data)
+    x = torch.randn(n, ci, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x1 = x.clone().requires_grad_(True)
+    x2 = x.float().clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y1 = mod(x1)
+    y2 = ref(x2)
+    assert y1.dtype == torch.bfloat16
+    assert _rel(y1, y2) < 8e-3
+    g = torch.randn_like(y2)
+    y1.backward(g.to(torch.bfloat16))
+    y2.backward(g)
+    assert _rel(x1.grad, x2.grad) < 1e-2
+    assert mod.weight.grad.dtype == torch.float32
+    assert _rel(mod.weight.grad, ref.weight.grad) < 1e-2

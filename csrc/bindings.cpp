@@ -68,23 +68,30 @@ PYBIND11_MODULE(_mpit, m) {
                            std::vector<int64_t> ns, uintptr_t dst, uintptr_t aux, float a,
                            float b) { gather_scale(dev, S(s), srcs, offs, ns, dst, aux, a, b); });
   m.def("bn_workspace_floats", &bn_workspace_floats);
+  m.def("bn_mask_bytes", &bn_mask_bytes);
   m.def("bn_act_fwd",
         [](int dev, uintptr_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C, uintptr_t gamma,
            uintptr_t beta, uintptr_t rmean, uintptr_t rvar, uintptr_t save_mean, uintptr_t save_rstd, uintptr_t ws,
-           float momentum, float eps, bool relu) {
+           float momentum, float eps, bool relu, uintptr_t mask) {
           bn_act_fwd(dev, S(s), bf16, x, res, y, M, C, gamma, beta, rmean, rvar, save_mean, save_rstd, ws, momentum, eps,
-                     relu);
+                     relu, mask);
         });
   m.def("bn_act_apply", [](int dev, uintptr_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C,
                            uintptr_t coef, bool relu) { bn_act_apply(dev, S(s), bf16, x, res, y, M, C, coef, relu); });
   m.def("bn_act_bwd",
-        [](int dev, uintptr_t s, bool bf16, uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t dx, uintptr_t dres, int64_t M,
-           int C, uintptr_t gamma, uintptr_t mean, uintptr_t rstd, uintptr_t dgamma, uintptr_t dbeta, uintptr_t ws,
-           bool relu) { bn_act_bwd(dev, S(s), bf16, dy, y, x, dx, dres, M, C, gamma, mean, rstd, dgamma, dbeta, ws, relu); });
+        [](int dev, uintptr_t s, bool bf16, uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t dx, uintptr_t dres,
+           int64_t M, int C, uintptr_t gamma, uintptr_t mean, uintptr_t rstd, uintptr_t dgamma, uintptr_t dbeta,
+           uintptr_t ws, bool relu) {
+          bn_act_bwd(dev, S(s), bf16, dy, mask, x, dx, dres, M, C, gamma, mean, rstd, dgamma, dbeta, ws, relu);
+        });
   m.def("gemm_nt_supported", &gemm_nt_supported);
   m.def("gemm_nt_stats_floats", &gemm_nt_stats_floats);
-  m.def("gemm_nt", [](int dev, uintptr_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B, int64_t ldb,
-                      uintptr_t C, int64_t ldc, uintptr_t stats) { gemm_nt(dev, S(s), M, N, K, A, lda, B, ldb, C, ldc, stats); });
+  m.def(
+      "gemm_nt",
+      [](int dev, uintptr_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B, int64_t ldb, uintptr_t C,
+         int64_t ldc, uintptr_t stats, uintptr_t cin) { gemm_nt(dev, S(s), M, N, K, A, lda, B, ldb, C, ldc, stats, cin); },
+      py::arg("dev"), py::arg("stream"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("A"), py::arg("lda"),
+      py::arg("B"), py::arg("ldb"), py::arg("C"), py::arg("ldc"), py::arg("stats") = 0, py::arg("cin") = 0);
   m.def("gemm_tn_supported", &gemm_tn_supported);
   m.def("gemm_tn_ws_floats", &gemm_tn_ws_floats);
   m.def("gemm_tn", [](int dev, uintptr_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X, int64_t ldx,

@@ -5,8 +5,10 @@
 // ~6.6 ms more in separate PyTorch add / ReLU / ReLU-backward passes (profiles/
 // resnet50_n1_steady_kernels.md): 8 full passes over every activation in forward and 8 in
 // backward, at ~2.8 TB/s. Memory-bound work belongs in as few HBM passes as possible:
-//   forward : stats pass (read x) + apply pass (read x [, residual], write y)
-//   backward: reduce pass (read dy, y, x) + apply pass (read dy, y, x, write dx [, dres])
+//   forward : stats pass (read x) + apply pass (read x [, residual], write y [, ReLU bit mask])
+//   backward: reduce pass (read dy, mask, x) + apply pass (read dy, mask, x, write dx [, dres])
+// The ReLU mask is one bit per element (1/16 of a bf16 tensor), so the backward never
+// re-reads the forward output y.
 // Layout: the activation is a row-major [M = N*H*W, C] matrix. A thread owns VEC
 // consecutive channels (16 B: 8 bf16 or 4 fp32) and walks rows; since every block size
 // and grid stride is a multiple of G = C/VEC, a thread keeps the same channel group for
@@ -178,10 +180,12 @@ __global__ __launch_bounds__(kFinCh * kFinK) void bn_finalize_fwd_kernel(
 }
 
 // ---------------------------------------------------------------- forward: apply
-template <typename T, bool RES, bool RELU>
+// MASK: also store the ReLU mask, one byte per vector (bit v = element v of the vector is
+// positive), so the backward never re-reads y (1/16 of its bytes for bf16).
+template <typename T, bool RES, bool RELU, bool MASK>
 __global__ __launch_bounds__(1024) void bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res,
                                                         T* __restrict__ y, const float* __restrict__ coef, int64_t nvec,
-                                                        int C) {
+                                                        int C, uint8_t* __restrict__ mask) {
   constexpr int V = Vec<T>::N;
   const int G = C / V;
   int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -197,6 +201,7 @@ __global__ __launch_bounds__(1024) void bn_apply_kernel(const T* __restrict__ x,
     float a[V], rr[V];
     Vec<T>::load(x + i * V, a);
     if constexpr (RES) Vec<T>::load(res + i * V, rr);
+    uint32_t bits = 0;
 #pragma unroll
     for (int v = 0; v < V; ++v) {
       float t = fmaf(a[v], sc[v], sh[v]);
@@ -205,12 +210,18 @@ __global__ __launch_bounds__(1024) void bn_apply_kernel(const T* __restrict__ x,
       a[v] = t;
     }
     Vec<T>::store(y + i * V, a);
+    if constexpr (MASK) {  // (rounding to bf16 never flips the sign of a normal number)
+#pragma unroll
+      for (int v = 0; v < V; ++v) bits |= uint32_t(a[v] > 0.f) << v;
+      mask[i] = uint8_t(bits);
+    }
   }
 }
 
 // ---------------------------------------------------------------- backward: reduce
+// dz = dy (RELU: masked by the forward's bit mask); sums of dz and dz*(x - mean)
 template <typename T, bool RELU>
-__global__ __launch_bounds__(1024) void bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ y,
+__global__ __launch_bounds__(1024) void bn_bwd_reduce_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ mask,
                                                              const T* __restrict__ x, const float* __restrict__ mean,
                                                              int64_t M, int C, int64_t rows_per_block,
                                                              float* __restrict__ part) {
@@ -228,34 +239,36 @@ __global__ __launch_bounds__(1024) void bn_bwd_reduce_kernel(const T* __restrict
   const int64_t r1 = min(M, r0 + rows_per_block);
   int64_t r = r0 + rs;
   for (; r + R < r1; r += 2 * R) {
-    float d[2][V], xx[2][V], yy[2][V];
+    float d[2][V], xx[2][V];
+    uint32_t mb[2] = {0xffu, 0xffu};
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int64_t o = (r + u * R) * C + g * V;
       Vec<T>::load(dy + o, d[u]);
       Vec<T>::load(x + o, xx[u]);
-      if constexpr (RELU) Vec<T>::load(y + o, yy[u]);
+      if constexpr (RELU) mb[u] = mask[(r + u * R) * G + g];
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         float dz = d[u][v];
-        if constexpr (RELU) dz = yy[u][v] > 0.f ? dz : 0.f;
+        if constexpr (RELU) dz = (mb[u] >> v) & 1u ? dz : 0.f;
         s1[v] += dz;
         s2[v] = fmaf(dz, xx[u][v] - mu[v], s2[v]);
       }
   }
   for (; r < r1; r += R) {
-    float d[V], xx[V], yy[V];
+    float d[V], xx[V];
     const int64_t o = r * C + g * V;
     Vec<T>::load(dy + o, d);
     Vec<T>::load(x + o, xx);
-    if constexpr (RELU) Vec<T>::load(y + o, yy);
+    uint32_t mb = 0xffu;
+    if constexpr (RELU) mb = mask[r * G + g];
 #pragma unroll
     for (int v = 0; v < V; ++v) {
       float dz = d[v];
-      if constexpr (RELU) dz = yy[v] > 0.f ? dz : 0.f;
+      if constexpr (RELU) dz = (mb >> v) & 1u ? dz : 0.f;
       s1[v] += dz;
       s2[v] = fmaf(dz, xx[v] - mu[v], s2[v]);
     }
@@ -296,7 +309,7 @@ __global__ __launch_bounds__(kFinCh * kFinK) void bn_finalize_bwd_kernel(
 }
 
 template <typename T, bool RELU, bool RESGRAD>
-__global__ __launch_bounds__(1024) void bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ y,
+__global__ __launch_bounds__(1024) void bn_bwd_apply_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ mask,
                                                             const T* __restrict__ x, const float* __restrict__ coef,
                                                             T* __restrict__ dx, T* __restrict__ dres, int64_t nvec,
                                                             int C) {
@@ -313,14 +326,15 @@ __global__ __launch_bounds__(1024) void bn_bwd_apply_kernel(const T* __restrict_
     B[v] = coef[2 * C + g * V + v];
   }
   for (; i < nvec; i += stride) {
-    float d[V], xx[V], yy[V];
+    float d[V], xx[V];
     Vec<T>::load(dy + i * V, d);
     Vec<T>::load(x + i * V, xx);
-    if constexpr (RELU) Vec<T>::load(y + i * V, yy);
+    uint32_t mb = 0xffu;
+    if constexpr (RELU) mb = mask[i];
 #pragma unroll
     for (int v = 0; v < V; ++v) {
       float dz = d[v];
-      if constexpr (RELU) dz = yy[v] > 0.f ? dz : 0.f;
+      if constexpr (RELU) dz = (mb >> v) & 1u ? dz : 0.f;
       d[v] = dz;
       xx[v] = fmaf(A[v], dz, fmaf(Cc[v], xx[v], B[v]));
     }
@@ -350,62 +364,54 @@ int apply_grid(int64_t nvec, int block) {
 }
 
 template <typename T>
+void launch_apply(hipStream_t s, const T* x, const T* res, T* y, int64_t M, int C, const float* coef, bool relu,
+                  uint8_t* mask) {
+  constexpr int V = Vec<T>::N;
+  const int G = C / V;
+  const int blk = block_for(G);
+  const int64_t nvec = M * G;
+  const int grid = apply_grid(nvec, blk);
+  const dim3 g(grid), b(blk);
+  if (relu && mask) {
+    if (res) hipLaunchKernelGGL((bn_apply_kernel<T, true, true, true>), g, b, 0, s, x, res, y, coef, nvec, C, mask);
+    else hipLaunchKernelGGL((bn_apply_kernel<T, false, true, true>), g, b, 0, s, x, res, y, coef, nvec, C, mask);
+  } else if (relu) {
+    if (res) hipLaunchKernelGGL((bn_apply_kernel<T, true, true, false>), g, b, 0, s, x, res, y, coef, nvec, C, mask);
+    else hipLaunchKernelGGL((bn_apply_kernel<T, false, true, false>), g, b, 0, s, x, res, y, coef, nvec, C, mask);
+  } else {
+    if (res) hipLaunchKernelGGL((bn_apply_kernel<T, true, false, false>), g, b, 0, s, x, res, y, coef, nvec, C, mask);
+    else hipLaunchKernelGGL((bn_apply_kernel<T, false, false, false>), g, b, 0, s, x, res, y, coef, nvec, C, mask);
+  }
+}
+
+template <typename T>
 void fwd_impl(int dev, hipStream_t s, const T* x, const T* res, T* y, int64_t M, int C, const float* gamma,
               const float* beta, float* rmean, float* rvar, float* save_mean, float* save_rstd, float* ws,
-              float momentum, float eps, bool relu, bool training) {
+              float momentum, float eps, bool relu, uint8_t* mask) {
   constexpr int V = Vec<T>::N;
   check_shape(M, C, V, reinterpret_cast<uintptr_t>(x));
   const int G = C / V;
   const int blk = block_for(G);
   float* coef = ws;  // [2][C]
-  if (training) {
-    const int R = blk / G;
-    int64_t rpb;
-    const int nb = stat_blocks(M, R, &rpb);
-    float* part = ws + 2 * C;
-    const size_t shm = size_t(R) * 2 * C * sizeof(float);
-    hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(nb), dim3(blk), shm, s, x, M, C, rpb, part);
-    hipLaunchKernelGGL(bn_finalize_fwd_kernel<T>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinK), 0, s, part, nb, C, M, x, gamma,
-                       beta, eps, momentum, rmean, rvar, save_mean, save_rstd, coef);
-  } else {
-    // eval: coefficients from the running statistics (computed on the device, tiny)
-    throw std::invalid_argument("bn_act: eval mode coefficients are computed by the caller");
-  }
-  const int64_t nvec = M * G;
-  const int grid = apply_grid(nvec, blk);
-  if (res) {
-    if (relu) hipLaunchKernelGGL((bn_apply_kernel<T, true, true>), dim3(grid), dim3(blk), 0, s, x, res, y, coef, nvec, C);
-    else hipLaunchKernelGGL((bn_apply_kernel<T, true, false>), dim3(grid), dim3(blk), 0, s, x, res, y, coef, nvec, C);
-  } else {
-    if (relu) hipLaunchKernelGGL((bn_apply_kernel<T, false, true>), dim3(grid), dim3(blk), 0, s, x, res, y, coef, nvec, C);
-    else hipLaunchKernelGGL((bn_apply_kernel<T, false, false>), dim3(grid), dim3(blk), 0, s, x, res, y, coef, nvec, C);
-  }
+  const int R = blk / G;
+  int64_t rpb;
+  const int nb = stat_blocks(M, R, &rpb);
+  float* part = ws + 2 * C;
+  const size_t shm = size_t(R) * 2 * C * sizeof(float);
+  hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(nb), dim3(blk), shm, s, x, M, C, rpb, part);
+  hipLaunchKernelGGL(bn_finalize_fwd_kernel<T>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinK), 0, s, part, nb,
+                     C, M, x, gamma, beta, eps, momentum, rmean, rvar, save_mean, save_rstd, coef);
+  launch_apply<T>(s, x, res, y, M, C, coef, relu, mask);
   hip_check(hipGetLastError(), "bn_act forward launch");
 }
 
 template <typename T>
-void apply_impl(hipStream_t s, const T* x, const T* res, T* y, int64_t M, int C, const float* coef, bool relu) {
+void bwd_impl(hipStream_t s, const T* dy, const uint8_t* mask, const T* x, T* dx, T* dres, int64_t M, int C,
+              const float* gamma, const float* mean, const float* rstd, float* dgamma, float* dbeta, float* ws,
+              bool relu) {
   constexpr int V = Vec<T>::N;
   check_shape(M, C, V, reinterpret_cast<uintptr_t>(x));
-  const int G = C / V;
-  const int blk = block_for(G);
-  const int64_t nvec = M * G;
-  const int grid = apply_grid(nvec, blk);
-  if (res) {
-    if (relu) hipLaunchKernelGGL((bn_apply_kernel<T, true, true>), dim3(grid), dim3(blk), 0, s, x, res, y, coef, nvec, C);
-    else hipLaunchKernelGGL((bn_apply_kernel<T, true, false>), dim3(grid), dim3(blk), 0, s, x, res, y, coef, nvec, C);
-  } else {
-    if (relu) hipLaunchKernelGGL((bn_apply_kernel<T, false, true>), dim3(grid), dim3(blk), 0, s, x, res, y, coef, nvec, C);
-    else hipLaunchKernelGGL((bn_apply_kernel<T, false, false>), dim3(grid), dim3(blk), 0, s, x, res, y, coef, nvec, C);
-  }
-  hip_check(hipGetLastError(), "bn_act apply launch");
-}
-
-template <typename T>
-void bwd_impl(hipStream_t s, const T* dy, const T* y, const T* x, T* dx, T* dres, int64_t M, int C, const float* gamma,
-              const float* mean, const float* rstd, float* dgamma, float* dbeta, float* ws, bool relu) {
-  constexpr int V = Vec<T>::N;
-  check_shape(M, C, V, reinterpret_cast<uintptr_t>(x));
+  if (relu && !mask) throw std::invalid_argument("bn_act backward: ReLU needs the forward mask");
   const int G = C / V;
   const int blk = block_for(G);
   const int R = blk / G;
@@ -414,18 +420,20 @@ void bwd_impl(hipStream_t s, const T* dy, const T* y, const T* x, T* dx, T* dres
   float* coef = ws;  // [3][C]
   float* part = ws + 3 * C;
   const size_t shm = size_t(R) * 2 * C * sizeof(float);
-  if (relu) hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true>), dim3(nb), dim3(blk), shm, s, dy, y, x, mean, M, C, rpb, part);
-  else hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false>), dim3(nb), dim3(blk), shm, s, dy, y, x, mean, M, C, rpb, part);
-  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinK), 0, s, part, nb, C, M, gamma, mean, rstd,
-                     dgamma, dbeta, coef);
+  if (relu)
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true>), dim3(nb), dim3(blk), shm, s, dy, mask, x, mean, M, C, rpb, part);
+  else
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false>), dim3(nb), dim3(blk), shm, s, dy, mask, x, mean, M, C, rpb, part);
+  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinK), 0, s, part, nb, C, M,
+                     gamma, mean, rstd, dgamma, dbeta, coef);
   const int64_t nvec = M * G;
-  const int grid = apply_grid(nvec, blk);
+  const dim3 g(apply_grid(nvec, blk)), b(blk);
   if (relu) {
-    if (dres) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, true>), dim3(grid), dim3(blk), 0, s, dy, y, x, coef, dx, dres, nvec, C);
-    else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, false>), dim3(grid), dim3(blk), 0, s, dy, y, x, coef, dx, dres, nvec, C);
+    if (dres) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, true>), g, b, 0, s, dy, mask, x, coef, dx, dres, nvec, C);
+    else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, false>), g, b, 0, s, dy, mask, x, coef, dx, dres, nvec, C);
   } else {
-    if (dres) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false, true>), dim3(grid), dim3(blk), 0, s, dy, y, x, coef, dx, dres, nvec, C);
-    else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false, false>), dim3(grid), dim3(blk), 0, s, dy, y, x, coef, dx, dres, nvec, C);
+    if (dres) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false, true>), g, b, 0, s, dy, mask, x, coef, dx, dres, nvec, C);
+    else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false, false>), g, b, 0, s, dy, mask, x, coef, dx, dres, nvec, C);
   }
   hip_check(hipGetLastError(), "bn_act backward launch");
 }
@@ -434,46 +442,53 @@ void bwd_impl(hipStream_t s, const T* dy, const T* y, const T* x, T* dx, T* dres
 
 int64_t bn_workspace_floats(int C) { return int64_t(3) * C + int64_t(2) * kMaxStatBlocks * C; }
 
+int64_t bn_mask_bytes(bool bf16, int64_t M, int C) { return M * (C / (bf16 ? 8 : 4)); }
+
 void bn_act_fwd(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C,
                 uintptr_t gamma, uintptr_t beta, uintptr_t rmean, uintptr_t rvar, uintptr_t save_mean,
-                uintptr_t save_rstd, uintptr_t ws, float momentum, float eps, bool relu) {
+                uintptr_t save_rstd, uintptr_t ws, float momentum, float eps, bool relu, uintptr_t mask) {
   hip_check(hipSetDevice(dev), "hipSetDevice");
   auto F = [](uintptr_t p) { return reinterpret_cast<float*>(p); };
+  auto* mk = reinterpret_cast<uint8_t*>(mask);
   if (bf16)
     fwd_impl<uint16_t>(dev, s, reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(res),
                        reinterpret_cast<uint16_t*>(y), M, C, F(gamma), F(beta), F(rmean), F(rvar), F(save_mean),
-                       F(save_rstd), F(ws), momentum, eps, relu, true);
+                       F(save_rstd), F(ws), momentum, eps, relu, mk);
   else
     fwd_impl<float>(dev, s, reinterpret_cast<const float*>(x), reinterpret_cast<const float*>(res),
                     reinterpret_cast<float*>(y), M, C, F(gamma), F(beta), F(rmean), F(rvar), F(save_mean), F(save_rstd),
-                    F(ws), momentum, eps, relu, true);
+                    F(ws), momentum, eps, relu, mk);
 }
 
 void bn_act_apply(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C,
                   uintptr_t coef, bool relu) {
   hip_check(hipSetDevice(dev), "hipSetDevice");
-  if (bf16)
-    apply_impl<uint16_t>(s, reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(res),
-                         reinterpret_cast<uint16_t*>(y), M, C, reinterpret_cast<const float*>(coef), relu);
-  else
-    apply_impl<float>(s, reinterpret_cast<const float*>(x), reinterpret_cast<const float*>(res),
-                      reinterpret_cast<float*>(y), M, C, reinterpret_cast<const float*>(coef), relu);
+  if (bf16) {
+    check_shape(M, C, 8, x);
+    launch_apply<uint16_t>(s, reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(res),
+                           reinterpret_cast<uint16_t*>(y), M, C, reinterpret_cast<const float*>(coef), relu, nullptr);
+  } else {
+    check_shape(M, C, 4, x);
+    launch_apply<float>(s, reinterpret_cast<const float*>(x), reinterpret_cast<const float*>(res),
+                        reinterpret_cast<float*>(y), M, C, reinterpret_cast<const float*>(coef), relu, nullptr);
+  }
+  hip_check(hipGetLastError(), "bn_act apply launch");
 }
 
-void bn_act_bwd(int dev, hipStream_t s, bool bf16, uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t dx, uintptr_t dres,
-                int64_t M, int C, uintptr_t gamma, uintptr_t mean, uintptr_t rstd, uintptr_t dgamma, uintptr_t dbeta,
-                uintptr_t ws, bool relu) {
+void bn_act_bwd(int dev, hipStream_t s, bool bf16, uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t dx,
+                uintptr_t dres, int64_t M, int C, uintptr_t gamma, uintptr_t mean, uintptr_t rstd, uintptr_t dgamma,
+                uintptr_t dbeta, uintptr_t ws, bool relu) {
   hip_check(hipSetDevice(dev), "hipSetDevice");
   auto F = [](uintptr_t p) { return reinterpret_cast<float*>(p); };
+  const auto* mk = reinterpret_cast<const uint8_t*>(mask);
   if (bf16)
-    bwd_impl<uint16_t>(s, reinterpret_cast<const uint16_t*>(dy), reinterpret_cast<const uint16_t*>(y),
-                       reinterpret_cast<const uint16_t*>(x), reinterpret_cast<uint16_t*>(dx),
-                       reinterpret_cast<uint16_t*>(dres), M, C, F(gamma), F(mean), F(rstd), F(dgamma), F(dbeta), F(ws),
-                       relu);
+    bwd_impl<uint16_t>(s, reinterpret_cast<const uint16_t*>(dy), mk, reinterpret_cast<const uint16_t*>(x),
+                       reinterpret_cast<uint16_t*>(dx), reinterpret_cast<uint16_t*>(dres), M, C, F(gamma), F(mean),
+                       F(rstd), F(dgamma), F(dbeta), F(ws), relu);
   else
-    bwd_impl<float>(s, reinterpret_cast<const float*>(dy), reinterpret_cast<const float*>(y),
-                    reinterpret_cast<const float*>(x), reinterpret_cast<float*>(dx), reinterpret_cast<float*>(dres), M, C,
-                    F(gamma), F(mean), F(rstd), F(dgamma), F(dbeta), F(ws), relu);
+    bwd_impl<float>(s, reinterpret_cast<const float*>(dy), mk, reinterpret_cast<const float*>(x),
+                    reinterpret_cast<float*>(dx), reinterpret_cast<float*>(dres), M, C, F(gamma), F(mean), F(rstd),
+                    F(dgamma), F(dbeta), F(ws), relu);
 }
 
 }  // namespace mpit

@@ -57,6 +57,22 @@ __device__ __forceinline__ void glds16(const void* src, void* lds) {
   __builtin_amdgcn_global_load_lds(src, (lds_void*)lds, 16, 0, 0);
 }
 
+// ds_read_b64_tr_b16 (T10): lane 4q+p of each 16-lane group addresses row q, columns
+// 4p..4p+3 of a 4x16 block; lane i receives column i.
+__device__ __forceinline__ s16x4 ds_tr16(const uint16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p);
+}
+
+// The same LDS DMA issued from inline asm. hipcc treats a builtin LDS DMA as aliasing
+// every later ds_read_b64_tr_b16 and drains it (vmcnt(0)) before each transposed read,
+// which serialises the ring; issued from asm it is invisible to that tracking and the
+// kernel's own counted vmcnt waits order it. m0 carries the wave-uniform LDS base; no
+// other instruction of the kernels using this helper reads m0.
+__device__ __forceinline__ void glds16_asm(const void* src, void* lds) {
+  const uint32_t l = __builtin_amdgcn_readfirstlane(uint32_t(reinterpret_cast<uintptr_t>((lds_void*)lds)));
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(l), "v"(src) : "memory");
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -81,8 +97,8 @@ __device__ __forceinline__ int xcd_tile(int bid, int nb) {
 template <int BM, int BN, int STAGES, bool STATS>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda,
                                                          const uint16_t* __restrict__ B, int64_t ldb,
-                                                         uint16_t* __restrict__ C, int64_t ldc, int64_t M, int N, int K,
-                                                         int ntn, float* __restrict__ stats) {
+                                                         uint16_t* C, int64_t ldc, int64_t M, int N, int K,
+                                                         int ntn, float* __restrict__ stats, const uint16_t* Cin) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 32, TN = WN / 32;
   constexpr int IA = BM / 16 / 4, IB = BN / 16 / 4;  // glds instructions per wave per tile
@@ -184,6 +200,13 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const uint16_t* __restr
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int n = n0 + wn * WN + j * 32 + 8 * g + 4 * fh;
+        if (Cin != nullptr && ok) {  // C = A.B^T + Cin (Cin may alias C: same thread, read first)
+          const uint2 ci = *reinterpret_cast<const uint2*>(Cin + m * ldc + n);
+          acc[i][j][4 * g + 0] += bf2f(uint16_t(ci.x & 0xffff));
+          acc[i][j][4 * g + 1] += bf2f(uint16_t(ci.x >> 16));
+          acc[i][j][4 * g + 2] += bf2f(uint16_t(ci.y & 0xffff));
+          acc[i][j][4 * g + 3] += bf2f(uint16_t(ci.y >> 16));
+        }
         uint16_t h[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -241,18 +264,34 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const uint16_t* __restr
 
 // ------------------------------------------------------------------------------ TN GEMM
 // part[split][N][K] = sum over rows m of this split of dY[m][n] * X[m][k]
-constexpr int kRows = 64;  // rows (reduction) per staged step
+//
+// Staging: global_load_lds into a ring of STAGES tiles of kRows rows (same counted-vmcnt
+// scheme as gemm_nt). LDS rows are the plain data rows (128 B or 256 B) with a 16-B chunk
+// XOR swizzle chosen so the ds_read_b64_tr_b16 fragment reads of a 32-lane half (4 rows x
+// 32 columns) hit 64 distinct banks; glds is lane-linear, so the swizzle is applied to the
+// global source address. A partial last step (M % kRows) is zero-filled in LDS.
+constexpr int kRows = 32;  // rows (reduction) per staged step
 
-template <int TBN, int TBK>
+// 16-B chunk swizzle of a row of CPR chunks (CPR = 16: 256-B rows, 8: 128-B rows)
+template <int CPR>
+__device__ __forceinline__ int tswz(int row, int ch) {
+  if constexpr (CPR == 16) return ch ^ (((row & 3) << 2) | ((row >> 2) & 3));
+  else return ch ^ (((row >> 1) & 1) << 2);
+}
+
+template <int TBN, int TBK, int STAGES>
 __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const uint16_t* __restrict__ Y, int64_t ldy,
                                                          const uint16_t* __restrict__ X, int64_t ldx,
                                                          float* __restrict__ part, int64_t M, int N, int K,
                                                          int64_t rows_per_split, int ntk, int ntiles) {
-  constexpr int SY = TBN + 32, SX = TBK + 32;  // padded LDS row strides (elements)
   constexpr int WN = TBN / 2, WK = TBK / 2;
   constexpr int TM = WN / 32, TN = WK / 32;
-  constexpr int YC = kRows * TBN / 8 / 256, XC = kRows * TBK / 8 / 256;
-  constexpr int CPY = TBN / 8, CPX = TBK / 8;  // 16-B chunks per row
+  constexpr int CY = TBN / 8, CX = TBK / 8;           // 16-B chunks per row
+  constexpr int RY = 64 / CY, RX = 64 / CX;           // rows per glds wave-instruction
+  constexpr int IY = kRows / RY / 4, IX = kRows / RX / 4;  // glds per wave per tile
+  constexpr int NI = IY + IX;
+  constexpr int TILE = kRows * (TBN + TBK);
+  static_assert(IY >= 1 && IX >= 1, "tile too small");
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
 
   const int id = xcd_tile(blockIdx.x, gridDim.x);
@@ -262,39 +301,33 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const uint16_t* __restr
   const int64_t r1 = min(M, r0 + rows_per_split);
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, wn = w >> 1, wk = w & 1;
 
-  int ry[YC], cy[YC], rx[XC], cx[XC];
+  // per-lane source offsets (row within the tile, element column) of each glds
+  int ry[IY], oy[IY], rx[IX], ox[IX];
 #pragma unroll
-  for (int i = 0; i < YC; ++i) {
-    const int q = t + 256 * i;
-    ry[i] = q / CPY;
-    cy[i] = q % CPY;
+  for (int i = 0; i < IY; ++i) {
+    ry[i] = (w * IY + i) * RY + lane / CY;
+    oy[i] = n0 + tswz<CY>(ry[i], lane % CY) * 8;
   }
 #pragma unroll
-  for (int i = 0; i < XC; ++i) {
-    const int q = t + 256 * i;
-    rx[i] = q / CPX;
-    cx[i] = q % CPX;
+  for (int i = 0; i < IX; ++i) {
+    rx[i] = (w * IX + i) * RX + lane / CX;
+    ox[i] = k0 + tswz<CX>(rx[i], lane % CX) * 8;
   }
-  uint4 vy[YC], vx[XC];
-  auto gload = [&](int64_t rb) {
+  const int64_t nsteps = r1 > r0 ? (r1 - r0 + kRows - 1) / kRows : 0;
+  auto issue = [&](int64_t st, int buf) {
+    uint16_t* Ys = smem + buf * TILE;
+    uint16_t* Xs = Ys + kRows * TBN;
+    const int64_t rb = r0 + st * kRows;
 #pragma unroll
-    for (int i = 0; i < YC; ++i) {
-      const int64_t r = rb + ry[i];
-      vy[i] = r < r1 ? *reinterpret_cast<const uint4*>(Y + r * ldy + n0 + cy[i] * 8) : make_uint4(0, 0, 0, 0);
+    for (int i = 0; i < IY; ++i) {
+      const int64_t r = min(rb + ry[i], r1 - 1);  // clamp; rows >= r1 are zeroed in LDS
+      glds16_asm(Y + r * ldy + oy[i], Ys + (w * IY + i) * RY * TBN);
     }
 #pragma unroll
-    for (int i = 0; i < XC; ++i) {
-      const int64_t r = rb + rx[i];
-      vx[i] = r < r1 ? *reinterpret_cast<const uint4*>(X + r * ldx + k0 + cx[i] * 8) : make_uint4(0, 0, 0, 0);
+    for (int i = 0; i < IX; ++i) {
+      const int64_t r = min(rb + rx[i], r1 - 1);
+      glds16_asm(X + r * ldx + ox[i], Xs + (w * IX + i) * RX * TBK);
     }
-  };
-  auto sstore = [&](int buf) {
-    uint16_t* Ys = smem + buf * kRows * (SY + SX);
-    uint16_t* Xs = Ys + kRows * SY;
-#pragma unroll
-    for (int i = 0; i < YC; ++i) *reinterpret_cast<uint4*>(Ys + ry[i] * SY + cy[i] * 8) = vy[i];
-#pragma unroll
-    for (int i = 0; i < XC; ++i) *reinterpret_cast<uint4*>(Xs + rx[i] * SX + cx[i] * 8) = vx[i];
   };
 
   f32x16 acc[TM][TN];
@@ -307,35 +340,51 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const uint16_t* __restr
 
   // transposed-read lane geometry: 16-lane group g, lane i = 4q + p of the group
   const int g = lane >> 4, gi = lane & 15, q = gi >> 2, p = gi & 3;
-  const int h = g >> 1, cb = 16 * (g & 1) + 4 * p;  // fragment rows 8h.., column block start
+  const int h = g >> 1;
+  const int cbase = 2 * (g & 1) + (p >> 1), cbyte = 4 * (p & 1);  // chunk / element offset in it
 
-  const int64_t nsteps = r1 > r0 ? (r1 - r0 + kRows - 1) / kRows : 0;
-  if (nsteps > 0) {
-    gload(r0);
-    sstore(0);
-  }
-  __syncthreads();
-  for (int64_t s = 0; s < nsteps; ++s) {
-    const int cur = int(s & 1);
-    if (s + 1 < nsteps) gload(r0 + (s + 1) * kRows);
-    const uint16_t* Ys = smem + cur * kRows * (SY + SX);
-    const uint16_t* Xs = Ys + kRows * SY;
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nsteps) issue(s, s);
+  for (int64_t st = 0; st < nsteps; ++st) {
+    const int64_t after = min(nsteps, st + STAGES - 1) - (st + 1);
+    if (STAGES >= 4 && after >= 2) wait_vmcnt<2 * NI>();
+    else if (STAGES >= 3 && after >= 1) wait_vmcnt<NI>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int buf = int(st % STAGES);
+    uint16_t* Ys = smem + buf * TILE;
+    uint16_t* Xs = Ys + kRows * TBN;
+    const int64_t valid = r1 - (r0 + st * kRows);
+    if (valid < kRows) {  // last, partial step of this split (nothing else in flight)
+      for (int e = t; e < kRows * (TBN + TBK) / 8; e += 256) {
+        const int ey = e < kRows * CY;
+        const int row = ey ? e / CY : (e - kRows * CY) / CX;
+        if (row >= valid) {
+          uint4* dst = ey ? reinterpret_cast<uint4*>(Ys) + e : reinterpret_cast<uint4*>(Xs) + (e - kRows * CY);
+          *dst = make_uint4(0, 0, 0, 0);
+        }
+      }
+      __syncthreads();
+    }
+    if (st + STAGES - 1 < nsteps) issue(st + STAGES - 1, int((st + STAGES - 1) % STAGES));
 #pragma unroll
     for (int kk = 0; kk < kRows / 16; ++kk) {
-      const int rr = 16 * kk + 8 * h + q;  // row of the first 4-row block
+      const int rr = 16 * kk + 8 * h + q;  // row of this lane in the first 4-row block
       bf16x8 af[TM], bfg[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const uint16_t* base = Ys + rr * SY + wn * WN + i * 32 + cb;
-        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base));
-        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + 4 * SY));
+        const int ch = (wn * WN + i * 32) / 8 + cbase;
+        const s16x4 lo = ds_tr16(Ys + rr * TBN + tswz<CY>(rr, ch) * 8 + cbyte);
+        const s16x4 hi = ds_tr16(Ys + (rr + 4) * TBN + tswz<CY>(rr + 4, ch) * 8 + cbyte);
         af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const uint16_t* base = Xs + rr * SX + wk * WK + j * 32 + cb;
-        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base));
-        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(base + 4 * SX));
+        const int ch = (wk * WK + j * 32) / 8 + cbase;
+        const s16x4 lo = ds_tr16(Xs + rr * TBK + tswz<CX>(rr, ch) * 8 + cbyte);
+        const s16x4 hi = ds_tr16(Xs + (rr + 4) * TBK + tswz<CX>(rr + 4, ch) * 8 + cbyte);
         bfg[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
       }
 #pragma unroll
@@ -343,8 +392,6 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const uint16_t* __restr
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
     }
-    if (s + 1 < nsteps) sstore(cur ^ 1);
-    __syncthreads();
   }
   // D[n][k]: column k = lane&31, row n = (v&3) + 8*(v>>2) + 4*(lane>>5)
   float* out = part + int64_t(split) * N * K;
@@ -361,21 +408,29 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const uint16_t* __restr
       }
 }
 
-// out[i] = beta*out[i] + sum_s part[s][i]   (float4 lanes)
+// Split reduction, one level: block (x, y) sums splits [y*G, y*G+G) of its float4
+// lanes into out2[y] (or, when gridDim.y == 1, into out with out = beta*out + sum).
+constexpr int kReduceGroup = 32;
 __global__ __launch_bounds__(256) void split_reduce_kernel(const float4* __restrict__ part, int nsplit, int64_t n4,
                                                            float4* __restrict__ out, float beta) {
-  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n4; i += int64_t(gridDim.x) * blockDim.x) {
-    float4 a = part[i];
-    for (int s = 1; s < nsplit; ++s) {
-      const float4 b = part[int64_t(s) * n4 + i];
-      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
-    }
-    if (beta != 0.f) {
-      const float4 o = out[i];
-      a.x += beta * o.x; a.y += beta * o.y; a.z += beta * o.z; a.w += beta * o.w;
-    }
-    out[i] = a;
+  const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  const int s0 = blockIdx.y * kReduceGroup, s1 = min(nsplit, s0 + kReduceGroup);
+  float4 a = part[int64_t(s0) * n4 + i];
+#pragma unroll 8
+  for (int s = s0 + 1; s < s1; ++s) {
+    const float4 b = part[int64_t(s) * n4 + i];
+    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
   }
+  if (gridDim.y > 1) {
+    out[int64_t(blockIdx.y) * n4 + i] = a;
+    return;
+  }
+  if (beta != 0.f) {
+    const float4 o = out[i];
+    a.x += beta * o.x; a.y += beta * o.y; a.z += beta * o.z; a.w += beta * o.w;
+  }
+  out[i] = a;
 }
 
 // fp32 [R][Cc] -> bf16 copy [R][Cc] and bf16 transpose [Cc][R]
@@ -422,7 +477,7 @@ bool gemm_nt_supported(int64_t M, int N, int K) { return M > 0 && N > 0 && K > 0
 int64_t gemm_nt_stats_floats(int64_t M, int N) { return ((M + 127) / 128) * 2 * int64_t(N); }
 
 void gemm_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B, int64_t ldb,
-             uintptr_t C, int64_t ldc, uintptr_t stats) {
+             uintptr_t C, int64_t ldc, uintptr_t stats, uintptr_t cin) {
   if (!gemm_nt_supported(M, N, K))
     throw std::invalid_argument("gemm_nt: need N % 64 == 0 and K % 64 == 0 (M=" + std::to_string(M) +
                                 " N=" + std::to_string(N) + " K=" + std::to_string(K) + ")");
@@ -436,6 +491,8 @@ void gemm_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64
   const auto* b = reinterpret_cast<const uint16_t*>(B);
   auto* c = reinterpret_cast<uint16_t*>(C);
   auto* st = reinterpret_cast<float*>(stats);
+  const auto* ci = reinterpret_cast<const uint16_t*>(cin);
+  if (cin) check_ptr(cin, "Cin");
   constexpr int BM = 128;
   const int64_t mtn = (M + BM - 1) / BM;
   const int nk = K / kBK;
@@ -449,10 +506,10 @@ void gemm_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64
     const size_t shm = size_t(ST) * (BM + BN) * kBK * sizeof(uint16_t);                                         \
     if (st)                                                                                                     \
       hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, ST, true>), dim3(unsigned(nb)), dim3(256), shm, s, a, lda, b,  \
-                         ldb, c, ldc, M, N, K, ntn, st);                                                        \
+                         ldb, c, ldc, M, N, K, ntn, st, ci);                                                    \
     else                                                                                                        \
       hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, ST, false>), dim3(unsigned(nb)), dim3(256), shm, s, a, lda, b, \
-                         ldb, c, ldc, M, N, K, ntn, st);                                                        \
+                         ldb, c, ldc, M, N, K, ntn, st, ci);                                                    \
   } while (0)
   if (N % 128 == 0) {
     if (stages == 4) MPIT_NT_LAUNCH(128, 4);
@@ -469,15 +526,18 @@ void gemm_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64
 
 bool gemm_tn_supported(int64_t M, int N, int K) { return M > 0 && N % 64 == 0 && K % 64 == 0 && N > 0 && K > 0; }
 
-// split-K plan: returns the number of splits and rows per split
+// split-K plan: number of splits over M and rows per split, sized so the grid holds
+// about as many blocks as can be resident (4-stage ring: 64 KiB of LDS per 128x128 tile)
 static int tn_plan(int dev, int64_t M, int N, int K, int64_t* rows_per_split, int* tbn, int* tbk) {
   *tbn = N % 128 == 0 ? 128 : 64;
   *tbk = K % 128 == 0 ? 128 : 64;
   const int64_t ntiles = int64_t(N / *tbn) * (K / *tbk);
-  const int64_t target = 2 * int64_t(cu_count(dev));  // ~2 resident blocks per CU
+  const int per_cu = 2 * (128 / *tbn) * (128 / *tbk);
+  const int64_t target = int64_t(per_cu) * cu_count(dev);
   int64_t ns = std::max<int64_t>(1, (target + ntiles - 1) / ntiles);
   const int64_t min_rows = 8 * kRows;  // keep >= 8 staged steps per block
   ns = std::min<int64_t>(ns, std::max<int64_t>(1, M / min_rows));
+  ns = std::min<int64_t>(ns, int64_t(kReduceGroup) * kReduceGroup);  // two reduce levels at most
   int64_t rps = (M + ns - 1) / ns;
   rps = (rps + kRows - 1) / kRows * kRows;
   ns = (M + rps - 1) / rps;
@@ -485,11 +545,13 @@ static int tn_plan(int dev, int64_t M, int N, int K, int64_t* rows_per_split, in
   return int(ns);
 }
 
+static int64_t tn_groups(int ns) { return ns > kReduceGroup ? (ns + kReduceGroup - 1) / kReduceGroup : 0; }
+
 int64_t gemm_tn_ws_floats(int dev, int64_t M, int N, int K) {
   int64_t rps;
   int tbn, tbk;
   const int ns = tn_plan(dev, M, N, K, &rps, &tbn, &tbk);
-  return ns > 1 ? int64_t(ns) * N * K : 0;
+  return ns > 1 ? (int64_t(ns) + tn_groups(ns)) * N * K : 0;
 }
 
 void gemm_tn(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X, int64_t ldx,
@@ -509,37 +571,39 @@ void gemm_tn(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t Y, int64
   const bool direct = ns == 1 && beta == 0.f;
   if (!direct && ws == 0) throw std::invalid_argument("gemm_tn: workspace required");
   if (!direct) check_ptr(ws, "ws");
-  float* part = reinterpret_cast<float*>(direct ? out : (ns > 1 ? ws : ws));
+  float* part = reinterpret_cast<float*>(direct ? out : ws);
   const auto* y = reinterpret_cast<const uint16_t*>(Y);
   const auto* x = reinterpret_cast<const uint16_t*>(X);
   const dim3 grid(unsigned(int64_t(ntiles) * ns));
-  const size_t shm = 2 * size_t(kRows) * ((tbn + 32) + (tbk + 32)) * sizeof(uint16_t);
-  static bool lds_attr_set = false;  // > 64 KiB of dynamic LDS must be opted into
-  if (!lds_attr_set) {
-    hip_check(hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_kernel<128, 128>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kRows * (160 + 160) * 2),
-              "hipFuncSetAttribute");
-    hip_check(hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_kernel<128, 64>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kRows * (160 + 96) * 2),
-              "hipFuncSetAttribute");
-    hip_check(hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_kernel<64, 128>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kRows * (96 + 160) * 2),
-              "hipFuncSetAttribute");
-    lds_attr_set = true;
-  }
+  constexpr int ST = 4;
+  const size_t shm = size_t(ST) * kRows * (tbn + tbk) * sizeof(uint16_t);
   if (tbn == 128 && tbk == 128)
-    hipLaunchKernelGGL((gemm_tn_kernel<128, 128>), grid, dim3(256), shm, s, y, ldy, x, ldx, part, M, N, K, rps, ntk, ntiles);
+    hipLaunchKernelGGL((gemm_tn_kernel<128, 128, ST>), grid, dim3(256), shm, s, y, ldy, x, ldx, part, M, N, K, rps, ntk,
+                       ntiles);
   else if (tbn == 128)
-    hipLaunchKernelGGL((gemm_tn_kernel<128, 64>), grid, dim3(256), shm, s, y, ldy, x, ldx, part, M, N, K, rps, ntk, ntiles);
+    hipLaunchKernelGGL((gemm_tn_kernel<128, 64, ST>), grid, dim3(256), shm, s, y, ldy, x, ldx, part, M, N, K, rps, ntk,
+                       ntiles);
   else if (tbk == 128)
-    hipLaunchKernelGGL((gemm_tn_kernel<64, 128>), grid, dim3(256), shm, s, y, ldy, x, ldx, part, M, N, K, rps, ntk, ntiles);
+    hipLaunchKernelGGL((gemm_tn_kernel<64, 128, ST>), grid, dim3(256), shm, s, y, ldy, x, ldx, part, M, N, K, rps, ntk,
+                       ntiles);
   else
-    hipLaunchKernelGGL((gemm_tn_kernel<64, 64>), grid, dim3(256), shm, s, y, ldy, x, ldx, part, M, N, K, rps, ntk, ntiles);
+    hipLaunchKernelGGL((gemm_tn_kernel<64, 64, ST>), grid, dim3(256), shm, s, y, ldy, x, ldx, part, M, N, K, rps, ntk,
+                       ntiles);
   hip_check(hipGetLastError(), "gemm_tn launch");
   if (!direct) {
     const int64_t n4 = int64_t(N) * K / 4;
-    const int g = int(std::min<int64_t>((n4 + 255) / 256, 2048));
-    hipLaunchKernelGGL(split_reduce_kernel, dim3(g), dim3(256), 0, s, reinterpret_cast<const float4*>(part), ns, n4,
+    const unsigned gx = unsigned((n4 + 255) / 256);
+    const int64_t groups = tn_groups(ns);
+    const float4* src = reinterpret_cast<const float4*>(part);
+    int nsrc = ns;
+    if (groups) {  // level 1: groups of kReduceGroup splits -> ws tail
+      float4* mid = reinterpret_cast<float4*>(part + int64_t(ns) * N * K);
+      hipLaunchKernelGGL(split_reduce_kernel, dim3(gx, unsigned(groups)), dim3(256), 0, s, src, ns, n4, mid, beta);
+      hip_check(hipGetLastError(), "gemm_tn reduce launch");
+      src = mid;
+      nsrc = int(groups);
+    }
+    hipLaunchKernelGGL(split_reduce_kernel, dim3(gx, 1), dim3(256), 0, s, src, nsrc, n4,
                        reinterpret_cast<float4*>(out), beta);
     hip_check(hipGetLastError(), "gemm_tn reduce launch");
   }

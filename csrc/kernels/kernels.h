@@ -65,24 +65,27 @@ void gather_scale(int dev, hipStream_t s, const std::vector<uintptr_t>& srcs, co
 
 // ---- fused BatchNorm (+residual) (+ReLU), NHWC, training (bn_act.hip) -------------
 // x / res / y / dy / dx / dres: [M, C] row-major (channels_last), bf16 or fp32.
+// mask: ReLU bit mask written by the forward (bn_mask_bytes) and read by the backward.
 int64_t bn_workspace_floats(int C);
+int64_t bn_mask_bytes(bool bf16, int64_t M, int C);
 void bn_act_fwd(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C,
                 uintptr_t gamma, uintptr_t beta, uintptr_t rmean, uintptr_t rvar, uintptr_t save_mean,
-                uintptr_t save_rstd, uintptr_t ws, float momentum, float eps, bool relu);
+                uintptr_t save_rstd, uintptr_t ws, float momentum, float eps, bool relu, uintptr_t mask);
 // y = act(x*coef[c] + coef[C+c] (+res))  — eval mode / precomputed coefficients
 void bn_act_apply(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C,
                   uintptr_t coef, bool relu);
-void bn_act_bwd(int dev, hipStream_t s, bool bf16, uintptr_t dy, uintptr_t y, uintptr_t x, uintptr_t dx, uintptr_t dres,
-                int64_t M, int C, uintptr_t gamma, uintptr_t mean, uintptr_t rstd, uintptr_t dgamma, uintptr_t dbeta,
-                uintptr_t ws, bool relu);
+void bn_act_bwd(int dev, hipStream_t s, bool bf16, uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t dx,
+                uintptr_t dres, int64_t M, int C, uintptr_t gamma, uintptr_t mean, uintptr_t rstd, uintptr_t dgamma,
+                uintptr_t dbeta, uintptr_t ws, bool relu);
 
 // ---- MFMA GEMMs for NHWC 1x1 convolutions (gemm.hip), bf16 operands, fp32 accumulate --
 // C[M,N] (bf16) = A[M,K] . B[N,K]^T; optional per-column {sum, sumsq} partials of C per
-// 128-row tile into stats[ceil(M/128)][2][N] (gemm_nt_stats_floats).
+// 128-row tile into stats[ceil(M/128)][2][N] (gemm_nt_stats_floats); optional bf16 cin
+// [M, ldc] added to the product before rounding (may alias C).
 bool gemm_nt_supported(int64_t M, int N, int K);
 int64_t gemm_nt_stats_floats(int64_t M, int N);
 void gemm_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B, int64_t ldb,
-             uintptr_t C, int64_t ldc, uintptr_t stats);
+             uintptr_t C, int64_t ldc, uintptr_t stats, uintptr_t cin);
 // out[N,K] (fp32) = beta*out + Y[M,N]^T . X[M,K]  (split over M; ws: gemm_tn_ws_floats)
 bool gemm_tn_supported(int64_t M, int N, int K);
 int64_t gemm_tn_ws_floats(int dev, int64_t M, int N, int K);

@@ -17,7 +17,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.bn import BatchNormAct2d
-from ..ops.conv import Conv1x1
+from ..ops.conv import Conv1x1, GradSlot
 
 # Fused BN(+add)(+ReLU) HIP kernels on MI355X (mpit_amd/ops/bn.py); same parameters and
 # state dict as nn.BatchNorm2d, and plain PyTorch math on CPU tensors.
@@ -82,6 +82,14 @@ class Bottleneck(nn.Module):
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
         if isinstance(self.bn1, BatchNormAct2d):
+            if (self.downsample is None and isinstance(self.conv1, Conv1x1) and self.conv1.fused(x)
+                    and self.bn3.fused(x) and torch.is_grad_enabled()):
+                # identity shortcut: the shortcut gradient is added inside conv1's
+                # backward-data GEMM instead of by a separate autograd add (ops/conv.py)
+                slot = GradSlot()
+                out = self.bn1(self.conv1(x, slot))
+                out = self.bn2(self.conv2(out))
+                return self.bn3(self.conv3(out), idt, res_slot=slot)
             out = self.bn1(self.conv1(x))
             out = self.bn2(self.conv2(out))
             return self.bn3(self.conv3(out), idt)

@@ -30,7 +30,7 @@ def _cl(x: torch.Tensor) -> torch.Tensor:
 
 class _BNActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu):
+    def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu, res_slot=None):
         x = _cl(x)
         if residual is not None:
             residual = _cl(residual).to(x.dtype)
@@ -44,22 +44,27 @@ class _BNActFn(torch.autograd.Function):
         ws = torch.empty(m.bn_workspace_floats(C), dtype=torch.float32, device=x.device)
         w = weight.float().contiguous() if weight is not None else None
         b = bias.float().contiguous() if bias is not None else None
-        m.bn_act_fwd(dev, stream, x.dtype == torch.bfloat16, x.data_ptr(),
+        bf16 = x.dtype == torch.bfloat16
+        # ReLU: one mask bit per element replaces keeping / re-reading y in the backward
+        mask = torch.empty(m.bn_mask_bytes(bf16, M, C), dtype=torch.uint8, device=x.device) if relu else None
+        m.bn_act_fwd(dev, stream, bf16, x.data_ptr(),
                      residual.data_ptr() if residual is not None else 0, y.data_ptr(), M, C,
                      w.data_ptr() if w is not None else 0, b.data_ptr() if b is not None else 0,
                      running_mean.data_ptr() if running_mean is not None else 0,
                      running_var.data_ptr() if running_var is not None else 0,
-                     mean.data_ptr(), rstd.data_ptr(), ws.data_ptr(), float(momentum), float(eps), bool(relu))
-        ctx.save_for_backward(x, y, w, mean, rstd)
+                     mean.data_ptr(), rstd.data_ptr(), ws.data_ptr(), float(momentum), float(eps), bool(relu),
+                     mask.data_ptr() if mask is not None else 0)
+        ctx.save_for_backward(x, mask, w, mean, rstd)
         ctx.relu = relu
         ctx.has_res = residual is not None
+        ctx.res_slot = res_slot
         ctx.has_w = weight is not None
         ctx.has_b = bias is not None
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, w, mean, rstd = ctx.saved_tensors
+        x, mask, w, mean, rstd = ctx.saved_tensors
         dy = _cl(dy).to(x.dtype)
         M, C = _rows(x)
         m = native()
@@ -70,11 +75,15 @@ class _BNActFn(torch.autograd.Function):
         dgamma = torch.empty(C, dtype=torch.float32, device=x.device) if ctx.has_w else None
         dbeta = torch.empty(C, dtype=torch.float32, device=x.device) if ctx.has_b else None
         ws = torch.empty(m.bn_workspace_floats(C), dtype=torch.float32, device=x.device)
-        m.bn_act_bwd(dev, stream, x.dtype == torch.bfloat16, dy.data_ptr(), y.data_ptr(), x.data_ptr(), dx.data_ptr(),
+        m.bn_act_bwd(dev, stream, x.dtype == torch.bfloat16, dy.data_ptr(),
+                     mask.data_ptr() if mask is not None else 0, x.data_ptr(), dx.data_ptr(),
                      dres.data_ptr() if dres is not None else 0, M, C, w.data_ptr() if w is not None else 0,
                      mean.data_ptr(), rstd.data_ptr(), dgamma.data_ptr() if dgamma is not None else 0,
                      dbeta.data_ptr() if dbeta is not None else 0, ws.data_ptr(), bool(ctx.relu))
-        return dx, dgamma, dbeta, None, None, dres, None, None, None
+        if ctx.res_slot is not None:  # the shortcut's gradient is added by the block's first conv
+            ctx.res_slot.grad = dres
+            dres = None
+        return dx, dgamma, dbeta, None, None, dres, None, None, None, None
 
 
 def bn_act_eval(x, weight, bias, running_mean, running_var, eps, residual=None, relu=True):
@@ -108,7 +117,15 @@ class BatchNormAct2d(nn.BatchNorm2d):
         super().__init__(num_features, eps, momentum, affine, track_running_stats)
         self.act = act
 
-    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def fused(self, x: torch.Tensor) -> bool:
+        """True when a training forward of ``x`` runs the fused kernels (honours res_slot)."""
+        return _supported(x) and (self.training or not self.track_running_stats)
+
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None, res_slot=None) -> torch.Tensor:
+        """``res_slot``: a :class:`mpit_amd.ops.conv.GradSlot` that receives the residual's
+        gradient in the backward instead of autograd (fused path only)."""
+        if res_slot is not None and not self.fused(x):
+            raise RuntimeError("res_slot needs the fused training path (see BatchNormAct2d.fused)")
         if not _supported(x):
             y = super().forward(x)
             if residual is not None:
@@ -122,5 +139,6 @@ class BatchNormAct2d(nn.BatchNorm2d):
                     momentum = 1.0 / float(self.num_batches_tracked)
             rm = self.running_mean if (self.training and self.track_running_stats) else None
             rv = self.running_var if (self.training and self.track_running_stats) else None
-            return _BNActFn.apply(x, self.weight, self.bias, rm, rv, residual, momentum or 0.0, self.eps, self.act)
+            return _BNActFn.apply(x, self.weight, self.bias, rm, rv, residual, momentum or 0.0, self.eps, self.act,
+                                  res_slot)
         return bn_act_eval(x, self.weight, self.bias, self.running_mean, self.running_var, self.eps, residual, self.act)

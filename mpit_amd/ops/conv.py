@@ -86,9 +86,29 @@ def cast_transpose(w: torch.Tensor):
     return wb, wt
 
 
+class GradSlot:
+    """Hands a gradient from one backward to a later one outside autograd's accumulation.
+
+    A ResNet identity shortcut makes the block input feed both the first 1x1 convolution
+    and the last BN's residual add, so autograd would sum the two input gradients with a
+    separate add kernel (read 2, write 1 over the block input). Instead the BN backward
+    parks its residual gradient here and the convolution's backward-data GEMM adds it in
+    its epilogue (``C = dY.W + slot``). The BN backward always runs first: the
+    convolution's output feeds, through the block, the BN's input."""
+
+    __slots__ = ("grad",)
+
+    def __init__(self):
+        self.grad = None
+
+    def take(self):
+        g, self.grad = self.grad, None
+        return g
+
+
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight):
+    def forward(ctx, x, weight, slot=None):
         x = _cl(x)
         if x.dtype != torch.bfloat16:
             x = x.to(torch.bfloat16)
@@ -101,6 +121,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         m.gemm_nt(x.device.index, _stream(x), M, co, ci, x.data_ptr(), ci, wb.data_ptr(), ci, y.data_ptr(), co, 0)
         ctx.save_for_backward(x, wt)
         ctx.wshape = weight.shape
+        ctx.slot = slot
         return y
 
     @staticmethod
@@ -115,16 +136,25 @@ class _Conv1x1Fn(torch.autograd.Function):
         m = native()
         dev, s = x.device.index, _stream(x)
         dx = dw = None
+        extra = ctx.slot.take() if ctx.slot is not None else None
         if ctx.needs_input_grad[0]:
-            dx = torch.empty_like(x, memory_format=torch.channels_last)
-            m.gemm_nt(dev, s, M, ci, co, dy.data_ptr(), co, wt.data_ptr(), co, dx.data_ptr(), ci, 0)
+            if extra is not None:  # residual gradient parked by the block's last BN: add in place
+                extra = _cl(extra)
+                if extra.dtype != torch.bfloat16 or extra.shape != x.shape:
+                    raise RuntimeError("GradSlot gradient does not match the convolution input")
+                dx = extra
+                m.gemm_nt(dev, s, M, ci, co, dy.data_ptr(), co, wt.data_ptr(), co, dx.data_ptr(), ci, 0,
+                          dx.data_ptr())
+            else:
+                dx = torch.empty_like(x, memory_format=torch.channels_last)
+                m.gemm_nt(dev, s, M, ci, co, dy.data_ptr(), co, wt.data_ptr(), co, dx.data_ptr(), ci, 0)
         if ctx.needs_input_grad[1]:
             dw = torch.empty(ctx.wshape, dtype=torch.float32, device=x.device)
             nws = m.gemm_tn_ws_floats(dev, M, co, ci)
             ws = torch.empty(nws, dtype=torch.float32, device=x.device) if nws else None
             m.gemm_tn(dev, s, M, co, ci, dy.data_ptr(), co, x.data_ptr(), ci, dw.data_ptr(),
                       ws.data_ptr() if ws is not None else 0, 0.0)
-        return dx, dw
+        return dx, dw, None
 
 
 def conv1x1_supported(x: torch.Tensor, weight: torch.Tensor) -> bool:
@@ -152,7 +182,13 @@ class Conv1x1(nn.Conv2d):
     def __init__(self, in_channels: int, out_channels: int, stride: int = 1):
         super().__init__(in_channels, out_channels, 1, stride=stride, bias=False)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        if self.stride == (1, 1) and conv1x1_supported(x, self.weight):
-            return _Conv1x1Fn.apply(x, self.weight)
+    def fused(self, x: torch.Tensor) -> bool:
+        """True when ``forward(x)`` takes the MFMA path (and so honours a GradSlot)."""
+        return self.stride == (1, 1) and conv1x1_supported(x, self.weight)
+
+    def forward(self, x: torch.Tensor, slot: "GradSlot" = None) -> torch.Tensor:
+        if self.fused(x):
+            return _Conv1x1Fn.apply(x, self.weight, slot)
+        if slot is not None:
+            raise RuntimeError("GradSlot needs the MFMA path (see Conv1x1.fused)")
         return super().forward(x)

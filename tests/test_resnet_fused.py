@@ -61,10 +61,20 @@ def test_bottleneck_fused_matches_fp32(inp, planes, stride):
     grads1 = {n: p.grad.detach().clone() for n, p in blk.named_parameters()}
     blk.zero_grad(set_to_none=True)
 
+    # the same block through the plain library path in bf16 autocast: the bf16 error floor
+    x3 = x.clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y3 = _ref_block(blk, x3)
+    y3.backward(g.to(y3.dtype))
+    grads3 = {n: p.grad.detach().clone() for n, p in blk.named_parameters()}
+    blk.zero_grad(set_to_none=True)
+
     x2 = x.float().clone().requires_grad_(True)
     y2 = _ref_block(blk, x2)
     y2.backward(g)
-    assert _rel(y1, y2) < 2e-2
-    assert _rel(x1.grad, x2.grad) < 3e-2
+    errs = {"y": (_rel(y1, y2), _rel(y3, y2)), "x.grad": (_rel(x1.grad, x2.grad), _rel(x3.grad, x2.grad))}
     for n, p in blk.named_parameters():
-        assert _rel(grads1[n], p.grad) < 5e-2, n
+        errs[n] = (_rel(grads1[n], p.grad), _rel(grads3[n], p.grad))
+    print(errs)
+    for k, (fused, lib) in errs.items():
+        assert fused < 1.5 * lib + 1e-2, (k, fused, lib)

@@ -18,12 +18,21 @@ def _short(n, w=100):
     return n if len(n) <= w else n[: w - 3] + "..."
 
 
+def _traces(d):
+    """(path, [(start, end, name)]) per trace: rocprofv3 CSV or rocpd SQLite output."""
+    for t in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+        yield t, [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Kernel_Name", ""))
+                  for r in csv.DictReader(open(t))]
+    for t in glob.glob(os.path.join(d, "**", "*.db"), recursive=True):
+        import sqlite3
+
+        c = sqlite3.connect(t)
+        yield t, [(int(a), int(b), n) for a, b, n in c.execute("select start, end, name from kernels")]
+
+
 def summarise(d, out, marker="DownpourF", k=3, top=30):
     lines = []
-    for t in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
-        rows = []
-        for r in csv.DictReader(open(t)):
-            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Kernel_Name", "")))
+    for t, rows in _traces(d):
         rows.sort()
         marks = [s for (s, e, n) in rows if marker in n]
         if len(marks) < k + 1:
@@ -63,5 +72,6 @@ if __name__ == "__main__":
     ap.add_argument("out")
     ap.add_argument("--marker", default="DownpourF")
     ap.add_argument("-k", type=int, default=3)
+    ap.add_argument("--top", type=int, default=30)
     a = ap.parse_args()
-    print(summarise(a.dir, a.out, a.marker, a.k))
+    print(summarise(a.dir, a.out, a.marker, a.k, a.top))

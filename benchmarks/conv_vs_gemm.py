@@ -91,6 +91,42 @@ def main():
             tot.setdefault("miopen_1x1", 0.0)
             tot["mfma_1x1"] += mult * (k_f + k_d + k_w)
             tot["miopen_1x1"] += mult * (t_f + t_md + t_mw)
+        if k > 1 and cin % 64 == 0 and cout % 64 == 0:
+            from mpit_amd.ops import conv as MC
+            from mpit_amd._ext import native
+
+            nm = native()
+            wf = wt.float().contiguous(memory_format=torch.channels_last)
+            wb, wtt = MC.conv_weights(wf, dgrad=True)
+            dev_, st_ = x.device.index, torch.cuda.current_stream().cuda_stream
+            yk = torch.empty_like(y)
+            dxk = torch.empty_like(x)
+            ho = y.shape[2]
+            nws = nm.conv_wgrad_ws_floats(dev_, n, h, w, cin, cout, k, k, s, p)
+            ws = torch.empty(max(nws, 1), device=dev, dtype=torch.float32)
+            dwk = torch.empty(cout, k, k, cin, device=dev, dtype=torch.float32)
+            k_f = timeit(lambda: nm.conv_fwd(dev_, st_, n, h, w, cin, cout, k, k, s, p, x.data_ptr(), wb.data_ptr(),
+                                             yk.data_ptr(), 0, 0))
+            k_w = timeit(lambda: nm.conv_wgrad(dev_, st_, n, h, w, cin, cout, k, k, s, p, gy.data_ptr(), x.data_ptr(),
+                                               dwk.data_ptr(), ws.data_ptr(), 0.0))
+            t_md = timeit(lambda: torch.ops.aten.convolution_backward(gy, x, wt, None, [s, s], [p, p], [1, 1], False,
+                                                                       [0, 0], 1, [True, False, False]))
+            t_mw = timeit(lambda: torch.ops.aten.convolution_backward(gy, x, wt, None, [s, s], [p, p], [1, 1], False,
+                                                                       [0, 0], 1, [False, True, False]))
+            if s == 1:
+                k_d = timeit(lambda: nm.conv_fwd(dev_, st_, n, ho, ho, cout, cin, k, k, 1, k - 1 - p, gy.data_ptr(),
+                                                 wtt.data_ptr(), dxk.data_ptr(), 0, 0))
+            else:
+                k_d = t_md
+            rec.update(miopen_dgrad_ms=round(t_md, 4), miopen_wgrad_ms=round(t_mw, 4), mfma_fwd_ms=round(k_f, 4),
+                       mfma_dgrad_ms=round(k_d, 4), mfma_wgrad_ms=round(k_w, 4),
+                       mfma_fwd_tflops=round(fl / k_f / 1e9, 1), mfma_dgrad_tflops=round(fl / k_d / 1e9, 1),
+                       mfma_wgrad_tflops=round(fl / k_w / 1e9, 1))
+            tot.setdefault("mfma_kxk", 0.0)
+            tot.setdefault("miopen_kxk", 0.0)
+            tot["mfma_kxk"] += mult * (k_f + k_d + k_w)
+            tot["miopen_kxk"] += mult * (t_f + t_md + t_mw)
+            best = min(best, k_f + k_d + k_w)
         if k == 1:
             xin = x if s == 1 else x[:, :, ::s, ::s].contiguous(memory_format=torch.channels_last)
             X = xin.permute(0, 2, 3, 1).reshape(-1, cin)

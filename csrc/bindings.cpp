@@ -96,8 +96,26 @@ PYBIND11_MODULE(_mpit, m) {
   m.def("gemm_tn_ws_floats", &gemm_tn_ws_floats);
   m.def("gemm_tn", [](int dev, uintptr_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X, int64_t ldx,
                       uintptr_t out, uintptr_t ws, float beta) { gemm_tn(dev, S(s), M, N, K, Y, ldy, X, ldx, out, ws, beta); });
-  m.def("cast_transpose", [](int dev, uintptr_t s, uintptr_t w, int R, int Cc, uintptr_t wb, uintptr_t wt) {
-    cast_transpose(dev, S(s), w, R, Cc, wb, wt);
+  m.def(
+      "cast_transpose",
+      [](int dev, uintptr_t s, uintptr_t w, int R, int Cc, uintptr_t wb, uintptr_t wt, int taps) {
+        cast_transpose(dev, S(s), w, R, Cc, wb, wt, taps);
+      },
+      py::arg("dev"), py::arg("stream"), py::arg("w"), py::arg("R"), py::arg("Cc"), py::arg("wb"), py::arg("wt"),
+      py::arg("taps") = 1);
+  m.def("maxpool_fwd", [](int dev, uintptr_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t x,
+                          uintptr_t y, uintptr_t idx) { maxpool_fwd(dev, S(s), N, H, W, C, K, stride, pad, x, y, idx); });
+  m.def("maxpool_bwd", [](int dev, uintptr_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t dy,
+                          uintptr_t idx, uintptr_t dx) { maxpool_bwd(dev, S(s), N, H, W, C, K, stride, pad, dy, idx, dx); });
+  m.def("conv_supported", &conv_supported);
+  m.def("conv_fwd", [](int dev, uintptr_t s, int Nb, int H, int W, int C, int Co, int R, int S_, int stride, int pad,
+                       uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t cin) {
+    conv_fwd(dev, S(s), Nb, H, W, C, Co, R, S_, stride, pad, x, w, y, stats, cin);
+  });
+  m.def("conv_wgrad_ws_floats", &conv_wgrad_ws_floats);
+  m.def("conv_wgrad", [](int dev, uintptr_t s, int Nb, int H, int W, int C, int Co, int R, int S_, int stride, int pad,
+                         uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, float beta) {
+    conv_wgrad(dev, S(s), Nb, H, W, C, Co, R, S_, stride, pad, dy, x, dw, ws, beta);
   });
 
   py::class_<Engine>(m, "Engine")

@@ -26,6 +26,16 @@
 // the MFMA fragments (8 consecutive rows of one column) are read with the gfx950
 // transposing LDS read ds_read_b64_tr_b16. M is split over blocks; each split writes an
 // fp32 partial tile and a vectorised reduce sums the splits (deterministic, no atomics).
+//
+// RxS convolutions (3x3 in ResNet / VGG / AlexNet) run on the same two kernels as
+// implicit GEMMs over an NHWC input (template flag CONV, geometry in ConvGeo): the GEMM
+// K index is (tap, channel) with the weight stored [Co][R][S][C] (channels_last), so a
+// 32-wide k-tile of gemm_nt (or a TBK-wide column tile of gemm_tn) is one tap and a
+// contiguous run of channels of one input pixel. Each lane's LDS DMA source is that
+// pixel's row, or a zero line in global memory when the tap falls in the padding — the
+// im2col matrix is never materialised. forward = gemm_nt on (X, W); backward-data of a
+// stride-1 conv = gemm_nt on (dY, W flipped and transposed); backward-weight = gemm_tn on
+// (dY, implicit X) straight into the fp32 master-weight gradient.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -44,6 +54,17 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 constexpr int kBK = 32;  // k-depth of one staged tile (gemm_nt): 64-B LDS rows
+
+// NHWC convolution geometry for the implicit-GEMM (CONV) kernel variants
+struct ConvGeo {
+  int H, W, C;     // input image
+  int Ho, Wo;      // output image
+  int S;           // kernel width (taps are r*S + s)
+  int stride, pad;
+};
+
+// source line for padding taps: LDS DMA of zeros
+__device__ __attribute__((aligned(256))) uint16_t g_zero_line[128] = {};
 
 // 16-B chunk swizzle of a 64-B LDS row: any 16 consecutive rows read at one logical chunk
 // hit 16 distinct (row%4, chunk) bank groups = all 64 banks.
@@ -79,10 +100,12 @@ __device__ __forceinline__ void wait_vmcnt() {
 }
 
 // Map a linear block id to a tile id so that consecutive tile ids (which share the A
-// row-panel) land on one XCD: blocks are dispatched round-robin over the 8 XCDs.
+// row-panel, or the rows of a wgrad split) land on one XCD: blocks are dispatched
+// round-robin over the 8 XCDs, so XCD x runs blocks x, x+8, ...; it is given the x-th
+// contiguous range of tile ids (ranges differ in length by one when nb % 8 != 0).
 __device__ __forceinline__ int xcd_tile(int bid, int nb) {
-  if (nb % 8) return bid;
-  return (bid % 8) * (nb / 8) + bid / 8;
+  const int x = bid % 8, q = nb / 8, r = nb % 8;
+  return x * q + min(x, r) + bid / 8;
 }
 
 // ------------------------------------------------------------------------------ NT GEMM
@@ -94,11 +117,12 @@ __device__ __forceinline__ int xcd_tile(int bid, int nb) {
 // the tile about to be used (a __syncthreads() would drain the whole ring). The LDS image
 // is lane-linear per wave instruction (16 rows x 64 B); the swizzle is applied on the
 // global source address.
-template <int BM, int BN, int STAGES, bool STATS>
+template <int BM, int BN, int STAGES, bool STATS, bool CONV>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda,
                                                          const uint16_t* __restrict__ B, int64_t ldb,
                                                          uint16_t* C, int64_t ldc, int64_t M, int N, int K,
-                                                         int ntn, float* __restrict__ stats, const uint16_t* Cin) {
+                                                         int ntn, float* __restrict__ stats, const uint16_t* Cin,
+                                                         ConvGeo geo) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 32, TN = WN / 32;
   constexpr int IA = BM / 16 / 4, IB = BN / 16 / 4;  // glds instructions per wave per tile
@@ -113,15 +137,28 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const uint16_t* __restr
   const int n0 = nt * BN;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w >> 1, wn = w & 1;
 
-  // source of this lane for each of the wave's glds instructions (k offset added per tile)
+  // source of this lane for each of the wave's glds instructions (k offset added per tile);
+  // CONV: the output pixel of the row (first input pixel of its window) instead
   const uint16_t* pa[IA];
   const uint16_t* pb[IB];
+  int hi0[IA], wi0[IA], ca[IA], img[IA];
 #pragma unroll
   for (int i = 0; i < IA; ++i) {
     const int row = (w * IA + i) * 16 + (lane >> 2), c = swz(row, lane & 3);
     const int64_t gm = min(m0 + row, M - 1);  // clamp: tail rows compute garbage, never stored
-    pa[i] = A + gm * lda + c * 8;
+    if constexpr (CONV) {
+      const int hw = geo.Ho * geo.Wo;
+      const int64_t n = gm / hw;
+      const int rem = int(gm - n * hw), ho = rem / geo.Wo, wo = rem - ho * geo.Wo;
+      hi0[i] = ho * geo.stride - geo.pad;
+      wi0[i] = wo * geo.stride - geo.pad;
+      img[i] = int(n) * geo.H;
+      ca[i] = c * 8;
+    } else {
+      pa[i] = A + gm * lda + c * 8;
+    }
   }
+  int kc = 0, kr = 0, ks = 0;  // CONV: channel offset and tap of the next tile issued
 #pragma unroll
   for (int i = 0; i < IB; ++i) {
     const int row = (w * IB + i) * 16 + (lane >> 2), c = swz(row, lane & 3);
@@ -131,11 +168,29 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const uint16_t* __restr
     uint16_t* As = smem + buf * TILE;
     uint16_t* Bs = As + BM * kBK;
 #pragma unroll
-    for (int i = 0; i < IA; ++i)
-      glds16(pa[i] + kt * kBK, As + (w * IA + i) * 16 * kBK);
+    for (int i = 0; i < IA; ++i) {
+      if constexpr (CONV) {
+        const int hi = hi0[i] + kr, wi = wi0[i] + ks;
+        const bool ok = unsigned(hi) < unsigned(geo.H) && unsigned(wi) < unsigned(geo.W);
+        const uint16_t* src = ok ? A + (((img[i] + hi) * geo.W + wi) * geo.C + kc + ca[i]) : g_zero_line + ca[i];
+        glds16(src, As + (w * IA + i) * 16 * kBK);
+      } else {
+        glds16(pa[i] + kt * kBK, As + (w * IA + i) * 16 * kBK);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < IB; ++i)
       glds16(pb[i] + kt * kBK, Bs + (w * IB + i) * 16 * kBK);
+    if constexpr (CONV) {  // tiles are issued in k order: step to the next (tap, channel) slab
+      kc += kBK;
+      if (kc == geo.C) {
+        kc = 0;
+        if (++ks == geo.S) {
+          ks = 0;
+          ++kr;
+        }
+      }
+    }
   };
 
   f32x16 acc[TM][TN];
@@ -279,11 +334,11 @@ __device__ __forceinline__ int tswz(int row, int ch) {
   else return ch ^ (((row >> 1) & 1) << 2);
 }
 
-template <int TBN, int TBK, int STAGES>
+template <int TBN, int TBK, int STAGES, bool CONV>
 __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const uint16_t* __restrict__ Y, int64_t ldy,
                                                          const uint16_t* __restrict__ X, int64_t ldx,
                                                          float* __restrict__ part, int64_t M, int N, int K,
-                                                         int64_t rows_per_split, int ntk, int ntiles) {
+                                                         int64_t rows_per_split, int ntk, int ntiles, ConvGeo geo) {
   constexpr int WN = TBN / 2, WK = TBK / 2;
   constexpr int TM = WN / 32, TN = WK / 32;
   constexpr int CY = TBN / 8, CX = TBK / 8;           // 16-B chunks per row
@@ -301,32 +356,83 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const uint16_t* __restr
   const int64_t r1 = min(M, r0 + rows_per_split);
   const int t = threadIdx.x, lane = t & 63, w = t >> 6, wn = w >> 1, wk = w & 1;
 
-  // per-lane source offsets (row within the tile, element column) of each glds
-  int ry[IY], oy[IY], rx[IX], ox[IX];
+  // Per-lane sources of each glds. Addresses advance incrementally by one step of kRows
+  // rows (no per-step 64-bit multiplies: the VALU work between the MFMAs stays within
+  // their issue shadow); rows past the split's end read the split's last row (the LDS
+  // copy is zeroed before use). CONV: the column tile is channels [xc, xc + TBK) of tap
+  // (xr, xs) and each lane tracks the output pixel (pn, pho, pwo) of its rows, advanced
+  // by the step's (dn, dh, dw) decomposition of kRows with at most one carry per digit.
+  const int nrows = int(r1 - r0);
+  int ry[IY], rx[IX], ox[IX];
+  const uint16_t* py[IY];
+  const uint16_t* pyl[IY];
+  const uint16_t* px[IX];
+  const uint16_t* pxl[IX];
 #pragma unroll
   for (int i = 0; i < IY; ++i) {
     ry[i] = (w * IY + i) * RY + lane / CY;
-    oy[i] = n0 + tswz<CY>(ry[i], lane % CY) * 8;
+    const int oy = n0 + tswz<CY>(ry[i], lane % CY) * 8;
+    py[i] = Y + (r0 + ry[i]) * ldy + oy;
+    pyl[i] = Y + (r1 - 1) * ldy + oy;
   }
 #pragma unroll
   for (int i = 0; i < IX; ++i) {
     rx[i] = (w * IX + i) * RX + lane / CX;
-    ox[i] = k0 + tswz<CX>(rx[i], lane % CX) * 8;
+    ox[i] = tswz<CX>(rx[i], lane % CX) * 8;  // channel offset inside the tile
+    if constexpr (!CONV) {
+      px[i] = X + (r0 + rx[i]) * ldx + k0 + ox[i];
+      pxl[i] = X + (r1 - 1) * ldx + k0 + ox[i];
+    }
+  }
+  const int64_t ystep = int64_t(kRows) * ldy, xstep = int64_t(kRows) * ldx;
+  int xr = 0, xs = 0, xc = 0, dn = 0, dh = 0, dw = 0;
+  int pn[IX], pho[IX], pwo[IX];
+  if constexpr (CONV) {
+    const int tap = k0 / geo.C;
+    xc = k0 - tap * geo.C;
+    xr = tap / geo.S;
+    xs = tap - xr * geo.S;
+    const int hw = geo.Ho * geo.Wo;
+    dn = kRows / hw;
+    dh = (kRows - dn * hw) / geo.Wo;
+    dw = kRows - dn * hw - dh * geo.Wo;
+#pragma unroll
+    for (int i = 0; i < IX; ++i) {
+      const int64_t m = r0 + rx[i];
+      pn[i] = int(m / hw);
+      const int rem = int(m - int64_t(pn[i]) * hw);
+      pho[i] = rem / geo.Wo;
+      pwo[i] = rem - pho[i] * geo.Wo;
+    }
   }
   const int64_t nsteps = r1 > r0 ? (r1 - r0 + kRows - 1) / kRows : 0;
   auto issue = [&](int64_t st, int buf) {
     uint16_t* Ys = smem + buf * TILE;
     uint16_t* Xs = Ys + kRows * TBN;
-    const int64_t rb = r0 + st * kRows;
+    const int rs = int(st) * kRows;  // first row of the step, relative to r0
 #pragma unroll
     for (int i = 0; i < IY; ++i) {
-      const int64_t r = min(rb + ry[i], r1 - 1);  // clamp; rows >= r1 are zeroed in LDS
-      glds16_asm(Y + r * ldy + oy[i], Ys + (w * IY + i) * RY * TBN);
+      glds16_asm(rs + ry[i] < nrows ? py[i] : pyl[i], Ys + (w * IY + i) * RY * TBN);
+      py[i] += ystep;
     }
 #pragma unroll
     for (int i = 0; i < IX; ++i) {
-      const int64_t r = min(rb + rx[i], r1 - 1);
-      glds16_asm(X + r * ldx + ox[i], Xs + (w * IX + i) * RX * TBK);
+      if constexpr (CONV) {
+        const int hi = pho[i] * geo.stride - geo.pad + xr, wi = pwo[i] * geo.stride - geo.pad + xs;
+        const bool ok = rs + rx[i] < nrows && unsigned(hi) < unsigned(geo.H) && unsigned(wi) < unsigned(geo.W);
+        const int off = ((pn[i] * geo.H + hi) * geo.W + wi) * geo.C + xc + ox[i];  // < 2^31 (host-checked)
+        glds16_asm(ok ? X + off : g_zero_line + (ox[i] & 63), Xs + (w * IX + i) * RX * TBK);
+        pwo[i] += dw;  // next step's rows (issued strictly in order)
+        const int cw = pwo[i] >= geo.Wo;
+        pwo[i] -= cw ? geo.Wo : 0;
+        pho[i] += dh + cw;
+        const int ch = pho[i] >= geo.Ho;
+        pho[i] -= ch ? geo.Ho : 0;
+        pn[i] += dn + ch;
+      } else {
+        glds16_asm(rs + rx[i] < nrows ? px[i] : pxl[i], Xs + (w * IX + i) * RX * TBK);
+        px[i] += xstep;
+      }
     }
   };
 
@@ -433,17 +539,20 @@ __global__ __launch_bounds__(256) void split_reduce_kernel(const float4* __restr
   out[i] = a;
 }
 
-// fp32 [R][Cc] -> bf16 copy [R][Cc] and bf16 transpose [Cc][R]
-__global__ __launch_bounds__(256) void cast_transpose_kernel(const float* __restrict__ w, int R, int Cc,
+// fp32 w[R][T][Cc] -> bf16 copy wb[R][T][Cc] and bf16 tap-flipped transpose
+// wt[Cc][T-1-t][R] (T = 1: the plain transpose; T = taps of a conv: the dgrad weight).
+// Tap t = blockIdx.z.
+__global__ __launch_bounds__(256) void cast_transpose_kernel(const float* __restrict__ w, int R, int Cc, int T,
                                                              uint16_t* __restrict__ wb, uint16_t* __restrict__ wt) {
   __shared__ uint16_t tile[32][33];
-  const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+  const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32, tap = blockIdx.z;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 8 rows per pass
   for (int y = ty; y < 32; y += 8) {
     const int r = r0 + y, c = c0 + tx;
     if (r < R && c < Cc) {
-      const uint16_t b = f2bf(w[int64_t(r) * Cc + c]);
-      if (wb) wb[int64_t(r) * Cc + c] = b;
+      const int64_t i = (int64_t(r) * T + tap) * Cc + c;
+      const uint16_t b = f2bf(w[i]);
+      if (wb) wb[i] = b;
       tile[y][tx] = b;
     }
   }
@@ -451,7 +560,7 @@ __global__ __launch_bounds__(256) void cast_transpose_kernel(const float* __rest
   if (!wt) return;
   for (int y = ty; y < 32; y += 8) {
     const int c = c0 + y, r = r0 + tx;
-    if (r < R && c < Cc) wt[int64_t(c) * R + r] = tile[tx][y];
+    if (r < R && c < Cc) wt[(int64_t(c) * T + (T - 1 - tap)) * R + r] = tile[tx][y];
   }
 }
 
@@ -476,15 +585,15 @@ bool gemm_nt_supported(int64_t M, int N, int K) { return M > 0 && N > 0 && K > 0
 
 int64_t gemm_nt_stats_floats(int64_t M, int N) { return ((M + 127) / 128) * 2 * int64_t(N); }
 
-void gemm_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B, int64_t ldb,
-             uintptr_t C, int64_t ldc, uintptr_t stats, uintptr_t cin) {
+static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B,
+                      int64_t ldb, uintptr_t C, int64_t ldc, uintptr_t stats, uintptr_t cin, const ConvGeo* geo) {
   if (!gemm_nt_supported(M, N, K))
-    throw std::invalid_argument("gemm_nt: need N % 64 == 0 and K % 64 == 0 (M=" + std::to_string(M) +
+    throw std::invalid_argument("gemm_nt: need N % 64 == 0 and K % 32 == 0 (M=" + std::to_string(M) +
                                 " N=" + std::to_string(N) + " K=" + std::to_string(K) + ")");
   check_ptr(A, "A");
   check_ptr(B, "B");
   check_ptr(C, "C");
-  if (lda % 8 || ldb % 8 || ldc % 4 || lda < K || ldb < K || ldc < N)
+  if (lda % 8 || ldb % 8 || ldc % 4 || (!geo && lda < K) || ldb < K || ldc < N)
     throw std::invalid_argument("gemm_nt: bad leading dimensions");
   hip_check(hipSetDevice(dev), "hipSetDevice");
   const auto* a = reinterpret_cast<const uint16_t*>(A);
@@ -493,23 +602,28 @@ void gemm_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64
   auto* st = reinterpret_cast<float*>(stats);
   const auto* ci = reinterpret_cast<const uint16_t*>(cin);
   if (cin) check_ptr(cin, "Cin");
+  const ConvGeo g = geo ? *geo : ConvGeo{};
   constexpr int BM = 128;
   const int64_t mtn = (M + BM - 1) / BM;
   const int nk = K / kBK;
   const int stages = nk >= 4 ? 4 : (nk == 3 ? 3 : 2);
   // (kernel templates are named at a non-template call site so their host stubs are emitted)
-#define MPIT_NT_LAUNCH(BN, ST)                                                                                  \
-  do {                                                                                                          \
-    const int ntn = N / BN;                                                                                     \
-    const int64_t nb = mtn * ntn;                                                                               \
-    if (nb > INT32_MAX) throw std::invalid_argument("gemm_nt: too many tiles");                                 \
-    const size_t shm = size_t(ST) * (BM + BN) * kBK * sizeof(uint16_t);                                         \
-    if (st)                                                                                                     \
-      hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, ST, true>), dim3(unsigned(nb)), dim3(256), shm, s, a, lda, b,  \
-                         ldb, c, ldc, M, N, K, ntn, st, ci);                                                    \
-    else                                                                                                        \
-      hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, ST, false>), dim3(unsigned(nb)), dim3(256), shm, s, a, lda, b, \
-                         ldb, c, ldc, M, N, K, ntn, st, ci);                                                    \
+#define MPIT_NT_LAUNCH1(BN, ST, STATS, CONV)                                                                   \
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, ST, STATS, CONV>), dim3(unsigned(nb)), dim3(256), shm, s, a, lda, b, \
+                     ldb, c, ldc, M, N, K, ntn, st, ci, g)
+#define MPIT_NT_LAUNCH(BN, ST)                                                   \
+  do {                                                                           \
+    const int ntn = N / BN;                                                      \
+    const int64_t nb = mtn * ntn;                                                \
+    if (nb > INT32_MAX) throw std::invalid_argument("gemm_nt: too many tiles");  \
+    const size_t shm = size_t(ST) * (BM + BN) * kBK * sizeof(uint16_t);          \
+    if (geo) {                                                                   \
+      if (st) MPIT_NT_LAUNCH1(BN, ST, true, true);                               \
+      else MPIT_NT_LAUNCH1(BN, ST, false, true);                                 \
+    } else {                                                                     \
+      if (st) MPIT_NT_LAUNCH1(BN, ST, true, false);                              \
+      else MPIT_NT_LAUNCH1(BN, ST, false, false);                                \
+    }                                                                            \
   } while (0)
   if (N % 128 == 0) {
     if (stages == 4) MPIT_NT_LAUNCH(128, 4);
@@ -521,20 +635,27 @@ void gemm_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64
     else MPIT_NT_LAUNCH(64, 2);
   }
 #undef MPIT_NT_LAUNCH
+#undef MPIT_NT_LAUNCH1
   hip_check(hipGetLastError(), "gemm_nt launch");
+}
+
+void gemm_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B, int64_t ldb,
+             uintptr_t C, int64_t ldc, uintptr_t stats, uintptr_t cin) {
+  launch_nt(dev, s, M, N, K, A, lda, B, ldb, C, ldc, stats, cin, nullptr);
 }
 
 bool gemm_tn_supported(int64_t M, int N, int K) { return M > 0 && N % 64 == 0 && K % 64 == 0 && N > 0 && K > 0; }
 
 // split-K plan: number of splits over M and rows per split, sized so the grid holds
 // about as many blocks as can be resident (4-stage ring: 64 KiB of LDS per 128x128 tile)
-static int tn_plan(int dev, int64_t M, int N, int K, int64_t* rows_per_split, int* tbn, int* tbk) {
+static int tn_plan(int dev, int64_t M, int N, int K, int64_t* rows_per_split, int* tbn, int* tbk, int cin = 0) {
   *tbn = N % 128 == 0 ? 128 : 64;
-  *tbk = K % 128 == 0 ? 128 : 64;
+  *tbk = (cin ? cin : K) % 128 == 0 ? 128 : 64;  // conv: a column tile never straddles two taps
   const int64_t ntiles = int64_t(N / *tbn) * (K / *tbk);
   const int per_cu = 2 * (128 / *tbn) * (128 / *tbk);
   const int64_t target = int64_t(per_cu) * cu_count(dev);
-  int64_t ns = std::max<int64_t>(1, (target + ntiles - 1) / ntiles);
+  // floor: one more block than there are slots would run as a whole second round
+  int64_t ns = std::max<int64_t>(1, target / ntiles);
   const int64_t min_rows = 8 * kRows;  // keep >= 8 staged steps per block
   ns = std::min<int64_t>(ns, std::max<int64_t>(1, M / min_rows));
   ns = std::min<int64_t>(ns, int64_t(kReduceGroup) * kReduceGroup);  // two reduce levels at most
@@ -554,18 +675,18 @@ int64_t gemm_tn_ws_floats(int dev, int64_t M, int N, int K) {
   return ns > 1 ? (int64_t(ns) + tn_groups(ns)) * N * K : 0;
 }
 
-void gemm_tn(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X, int64_t ldx,
-             uintptr_t out, uintptr_t ws, float beta) {
+static void launch_tn(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X,
+                      int64_t ldx, uintptr_t out, uintptr_t ws, float beta, const ConvGeo* geo) {
   if (!gemm_tn_supported(M, N, K))
     throw std::invalid_argument("gemm_tn: need N % 64 == 0 and K % 64 == 0");
   check_ptr(Y, "Y");
   check_ptr(X, "X");
   check_ptr(out, "out");
-  if (ldy % 8 || ldx % 8 || ldy < N || ldx < K) throw std::invalid_argument("gemm_tn: bad leading dimensions");
+  if (ldy % 8 || ldx % 8 || ldy < N || (!geo && ldx < K)) throw std::invalid_argument("gemm_tn: bad leading dimensions");
   hip_check(hipSetDevice(dev), "hipSetDevice");
   int64_t rps;
   int tbn, tbk;
-  const int ns = tn_plan(dev, M, N, K, &rps, &tbn, &tbk);
+  const int ns = tn_plan(dev, M, N, K, &rps, &tbn, &tbk, geo ? geo->C : 0);
   const int ntk = K / tbk;
   const int ntiles = (N / tbn) * ntk;
   const bool direct = ns == 1 && beta == 0.f;
@@ -574,21 +695,24 @@ void gemm_tn(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t Y, int64
   float* part = reinterpret_cast<float*>(direct ? out : ws);
   const auto* y = reinterpret_cast<const uint16_t*>(Y);
   const auto* x = reinterpret_cast<const uint16_t*>(X);
+  const ConvGeo g = geo ? *geo : ConvGeo{};
   const dim3 grid(unsigned(int64_t(ntiles) * ns));
   constexpr int ST = 4;
   const size_t shm = size_t(ST) * kRows * (tbn + tbk) * sizeof(uint16_t);
-  if (tbn == 128 && tbk == 128)
-    hipLaunchKernelGGL((gemm_tn_kernel<128, 128, ST>), grid, dim3(256), shm, s, y, ldy, x, ldx, part, M, N, K, rps, ntk,
-                       ntiles);
-  else if (tbn == 128)
-    hipLaunchKernelGGL((gemm_tn_kernel<128, 64, ST>), grid, dim3(256), shm, s, y, ldy, x, ldx, part, M, N, K, rps, ntk,
-                       ntiles);
-  else if (tbk == 128)
-    hipLaunchKernelGGL((gemm_tn_kernel<64, 128, ST>), grid, dim3(256), shm, s, y, ldy, x, ldx, part, M, N, K, rps, ntk,
-                       ntiles);
-  else
-    hipLaunchKernelGGL((gemm_tn_kernel<64, 64, ST>), grid, dim3(256), shm, s, y, ldy, x, ldx, part, M, N, K, rps, ntk,
-                       ntiles);
+#define MPIT_TN_LAUNCH(A, B)                                                                                       \
+  do {                                                                                                             \
+    if (geo)                                                                                                       \
+      hipLaunchKernelGGL((gemm_tn_kernel<A, B, ST, true>), grid, dim3(256), shm, s, y, ldy, x, ldx, part, M, N, K, \
+                         rps, ntk, ntiles, g);                                                                     \
+    else                                                                                                           \
+      hipLaunchKernelGGL((gemm_tn_kernel<A, B, ST, false>), grid, dim3(256), shm, s, y, ldy, x, ldx, part, M, N,  \
+                         K, rps, ntk, ntiles, g);                                                                  \
+  } while (0)
+  if (tbn == 128 && tbk == 128) MPIT_TN_LAUNCH(128, 128);
+  else if (tbn == 128) MPIT_TN_LAUNCH(128, 64);
+  else if (tbk == 128) MPIT_TN_LAUNCH(64, 128);
+  else MPIT_TN_LAUNCH(64, 64);
+#undef MPIT_TN_LAUNCH
   hip_check(hipGetLastError(), "gemm_tn launch");
   if (!direct) {
     const int64_t n4 = int64_t(N) * K / 4;
@@ -609,10 +733,59 @@ void gemm_tn(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t Y, int64
   }
 }
 
-void cast_transpose(int dev, hipStream_t s, uintptr_t w, int R, int Cc, uintptr_t wb, uintptr_t wt) {
+void gemm_tn(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X, int64_t ldx,
+             uintptr_t out, uintptr_t ws, float beta) {
+  launch_tn(dev, s, M, N, K, Y, ldy, X, ldx, out, ws, beta, nullptr);
+}
+
+// ------------------------------------------------------------------ convolutions
+static ConvGeo conv_geo(int H, int W, int C, int R, int S, int stride, int pad, int* Ho, int* Wo) {
+  if (H <= 0 || W <= 0 || C <= 0 || R <= 0 || S <= 0 || stride <= 0 || pad < 0)
+    throw std::invalid_argument("conv: bad geometry");
+  *Ho = (H + 2 * pad - R) / stride + 1;
+  *Wo = (W + 2 * pad - S) / stride + 1;
+  if (*Ho <= 0 || *Wo <= 0) throw std::invalid_argument("conv: empty output");
+  return ConvGeo{H, W, C, *Ho, *Wo, S, stride, pad};
+}
+
+bool conv_supported(int C, int Co) { return C % 32 == 0 && Co % 64 == 0; }
+
+void conv_fwd(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad,
+              uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t cin) {
+  if (!conv_supported(C, Co)) throw std::invalid_argument("conv_fwd: need C % 32 == 0 and Co % 64 == 0");
+  if (int64_t(Nb) * H * W * C >= (int64_t(1) << 31)) throw std::invalid_argument("conv_fwd: input too large");
+  int Ho, Wo;
+  const ConvGeo g = conv_geo(H, W, C, R, S, stride, pad, &Ho, &Wo);
+  const int64_t M = int64_t(Nb) * Ho * Wo;
+  launch_nt(dev, s, M, Co, R * S * C, x, C, w, int64_t(R) * S * C, y, Co, stats, cin, &g);
+}
+
+int64_t conv_wgrad_ws_floats(int dev, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad) {
+  int Ho, Wo;
+  conv_geo(H, W, C, R, S, stride, pad, &Ho, &Wo);
+  const int64_t M = int64_t(Nb) * Ho * Wo;
+  const int K = R * S * C;
+  int64_t rps;
+  int tbn, tbk;
+  const int ns = tn_plan(dev, M, Co, K, &rps, &tbn, &tbk, C);
+  return ns > 1 ? (int64_t(ns) + tn_groups(ns)) * Co * K : 0;
+}
+
+void conv_wgrad(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad,
+                uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, float beta) {
+  if (C % 64 || Co % 64) throw std::invalid_argument("conv_wgrad: need C % 64 == 0 and Co % 64 == 0");
+  if (int64_t(Nb) * H * W * C >= (int64_t(1) << 31)) throw std::invalid_argument("conv_wgrad: input too large");
+  int Ho, Wo;
+  const ConvGeo g = conv_geo(H, W, C, R, S, stride, pad, &Ho, &Wo);
+  const int64_t M = int64_t(Nb) * Ho * Wo;
+  launch_tn(dev, s, M, Co, R * S * C, dy, Co, x, C, dw, ws, beta, &g);
+}
+
+void cast_transpose(int dev, hipStream_t s, uintptr_t w, int R, int Cc, uintptr_t wb, uintptr_t wt, int taps) {
+  if (taps < 1) throw std::invalid_argument("cast_transpose: taps >= 1");
   hip_check(hipSetDevice(dev), "hipSetDevice");
-  const dim3 grid((Cc + 31) / 32, (R + 31) / 32);
-  hipLaunchKernelGGL(cast_transpose_kernel, grid, dim3(256), 0, s, reinterpret_cast<const float*>(w), R, Cc,
+  const dim3 grid((Cc + 31) / 32, (R + 31) / 32, taps);
+  hipLaunchKernelGGL(cast_transpose_kernel, grid, dim3(256), 0, s, reinterpret_cast<const float*>(w), R, Cc, taps,
                      reinterpret_cast<uint16_t*>(wb), reinterpret_cast<uint16_t*>(wt));
   hip_check(hipGetLastError(), "cast_transpose launch");
 }

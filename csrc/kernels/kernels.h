@@ -91,7 +91,27 @@ bool gemm_tn_supported(int64_t M, int N, int K);
 int64_t gemm_tn_ws_floats(int dev, int64_t M, int N, int K);
 void gemm_tn(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X, int64_t ldx,
              uintptr_t out, uintptr_t ws, float beta);
-// fp32 w[R][Cc] -> bf16 wb[R][Cc] (optional) and bf16 wt[Cc][R] (optional)
-void cast_transpose(int dev, hipStream_t s, uintptr_t w, int R, int Cc, uintptr_t wb, uintptr_t wt);
+// fp32 w[R][T][Cc] -> bf16 wb[R][T][Cc] (optional) and bf16 tap-flipped transpose
+// wt[Cc][T-1-t][R] (optional); T = 1 is the plain transpose
+void cast_transpose(int dev, hipStream_t s, uintptr_t w, int R, int Cc, uintptr_t wb, uintptr_t wt, int taps = 1);
+
+// ---- NHWC RxS convolutions as implicit GEMMs on the same MFMA kernels ----------------
+// x [Nb,H,W,C], w [Co,R,S,C] (bf16), y [Nb,Ho,Wo,Co] (bf16); stats / cin as gemm_nt.
+// Backward-data of a stride-1 conv = conv_fwd(dy, wt, pad' = R-1-pad) with wt the
+// tap-flipped transpose [C,R,S,Co] (cast_transpose taps = R*S).
+bool conv_supported(int C, int Co);
+void conv_fwd(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad,
+              uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t cin);
+// dw [Co,R,S,C] (fp32) = beta*dw + dY^T . im2col(x)   (C % 64 == 0, Co % 64 == 0)
+int64_t conv_wgrad_ws_floats(int dev, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad);
+void conv_wgrad(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad,
+                uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, float beta);
+
+// ---- NHWC bf16 max pooling with a uint8 argmax per output element (pool.hip) ---------
+// x [N,H,W,C] -> y, idx [N,Ho,Wo,C]; dx [N,H,W,C] gathered from dy + idx (no atomics).
+void maxpool_fwd(int dev, hipStream_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t x,
+                 uintptr_t y, uintptr_t idx);
+void maxpool_bwd(int dev, hipStream_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t dy,
+                 uintptr_t idx, uintptr_t dx);
 
 }  // namespace mpit

@@ -1,0 +1,151 @@
+// NHWC bf16 max pooling (ResNet stem: 3x3, stride 2, pad 1) with a one-byte argmax.
+//
+// Forward: one thread owns 8 channels (16 B) of one output pixel, reads its KxK window
+// (16-B loads, channels contiguous), writes the max and the window index of the max
+// (uint8, first maximum in scan order like PyTorch; a NaN wins and propagates).
+// Backward: one thread owns 8 channels of one INPUT pixel and gathers the gradients of
+// the (at most ceil(K/stride)^2) output windows that selected it — a gather, so no
+// atomics and no zero-fill pass: dx is written exactly once. PyTorch's NHWC
+// max_pool_backward walks the same windows but at ~6x the time (rocprof, profiles/).
+#include <hip/hip_runtime.h>
+
+#include <stdexcept>
+#include <string>
+
+#include "ew.h"
+#include "kernels.h"
+
+namespace mpit {
+namespace {
+
+struct PoolGeo {
+  int N, H, W, C, Ho, Wo, K, stride, pad;
+};
+
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                          uint8_t* __restrict__ idx, PoolGeo g) {
+  const int cv = g.C / 8;
+  const int64_t total = int64_t(g.N) * g.Ho * g.Wo * cv;
+  for (int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; t < total; t += int64_t(gridDim.x) * blockDim.x) {
+    const int c8 = int(t % cv);
+    const int64_t pix = t / cv;
+    const int wo = int(pix % g.Wo);
+    const int64_t r = pix / g.Wo;
+    const int ho = int(r % g.Ho);
+    const int64_t n = r / g.Ho;
+    float best[8];
+    uint8_t arg[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      best[e] = -__builtin_inff();
+      arg[e] = 0;
+    }
+    const int h0 = ho * g.stride - g.pad, w0 = wo * g.stride - g.pad;
+    for (int i = 0; i < g.K; ++i) {
+      const int h = h0 + i;
+      if (unsigned(h) >= unsigned(g.H)) continue;
+      for (int j = 0; j < g.K; ++j) {
+        const int w = w0 + j;
+        if (unsigned(w) >= unsigned(g.W)) continue;
+        const uint4 v = *reinterpret_cast<const uint4*>(x + ((n * g.H + h) * g.W + w) * g.C + c8 * 8);
+        const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+        const uint8_t k = uint8_t(i * g.K + j);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float f = bf2f(uint16_t((u[e >> 1] >> (16 * (e & 1))) & 0xffff));
+          if (f > best[e] || (f != f && best[e] == best[e])) {
+            best[e] = f;
+            arg[e] = k;
+          }
+        }
+      }
+    }
+    uint4 o;
+    uint32_t* op = &o.x;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) op[e] = uint32_t(f2bf(best[2 * e])) | (uint32_t(f2bf(best[2 * e + 1])) << 16);
+    *reinterpret_cast<uint4*>(y + pix * g.C + c8 * 8) = o;
+    uint2 a;
+    a.x = uint32_t(arg[0]) | (uint32_t(arg[1]) << 8) | (uint32_t(arg[2]) << 16) | (uint32_t(arg[3]) << 24);
+    a.y = uint32_t(arg[4]) | (uint32_t(arg[5]) << 8) | (uint32_t(arg[6]) << 16) | (uint32_t(arg[7]) << 24);
+    *reinterpret_cast<uint2*>(idx + pix * g.C + c8 * 8) = a;
+  }
+}
+
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const uint16_t* __restrict__ dy,
+                                                          const uint8_t* __restrict__ idx, uint16_t* __restrict__ dx,
+                                                          PoolGeo g) {
+  const int cv = g.C / 8;
+  const int64_t total = int64_t(g.N) * g.H * g.W * cv;
+  for (int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; t < total; t += int64_t(gridDim.x) * blockDim.x) {
+    const int c8 = int(t % cv);
+    const int64_t pix = t / cv;
+    const int w = int(pix % g.W);
+    const int64_t r = pix / g.W;
+    const int h = int(r % g.H);
+    const int64_t n = r / g.H;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    // output windows containing h: ho*stride - pad <= h <= ho*stride - pad + K - 1
+    const int hlo = max(0, (h + g.pad - g.K + g.stride) / g.stride), hhi = min(g.Ho - 1, (h + g.pad) / g.stride);
+    const int wlo = max(0, (w + g.pad - g.K + g.stride) / g.stride), whi = min(g.Wo - 1, (w + g.pad) / g.stride);
+    for (int ho = hlo; ho <= hhi; ++ho) {
+      const int i = h - (ho * g.stride - g.pad);
+      if (i < 0 || i >= g.K) continue;
+      for (int wo = wlo; wo <= whi; ++wo) {
+        const int j = w - (wo * g.stride - g.pad);
+        if (j < 0 || j >= g.K) continue;
+        const int64_t o = ((n * g.Ho + ho) * g.Wo + wo) * g.C + c8 * 8;
+        const uint2 a = *reinterpret_cast<const uint2*>(idx + o);
+        const uint4 v = *reinterpret_cast<const uint4*>(dy + o);
+        const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+        const uint8_t k = uint8_t(i * g.K + j);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint8_t ae = uint8_t(((e < 4 ? a.x : a.y) >> (8 * (e & 3))) & 0xff);
+          if (ae == k) acc[e] += bf2f(uint16_t((u[e >> 1] >> (16 * (e & 1))) & 0xffff));
+        }
+      }
+    }
+    uint4 o;
+    uint32_t* op = &o.x;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) op[e] = uint32_t(f2bf(acc[2 * e])) | (uint32_t(f2bf(acc[2 * e + 1])) << 16);
+    *reinterpret_cast<uint4*>(dx + pix * g.C + c8 * 8) = o;
+  }
+}
+
+PoolGeo pool_geo(int N, int H, int W, int C, int K, int stride, int pad) {
+  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 8 || K <= 0 || K > 15 || stride <= 0 || pad < 0 || 2 * pad > K)
+    throw std::invalid_argument("maxpool: unsupported geometry (C % 8 == 0, K <= 15, pad <= K/2)");
+  PoolGeo g{N, H, W, C, (H + 2 * pad - K) / stride + 1, (W + 2 * pad - K) / stride + 1, K, stride, pad};
+  if (g.Ho <= 0 || g.Wo <= 0) throw std::invalid_argument("maxpool: empty output");
+  return g;
+}
+
+unsigned grid_for(int64_t work) { return unsigned(std::min<int64_t>((work + 255) / 256, 8192)); }
+
+}  // namespace
+
+void maxpool_fwd(int dev, hipStream_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t x,
+                 uintptr_t y, uintptr_t idx) {
+  const PoolGeo g = pool_geo(N, H, W, C, K, stride, pad);
+  if ((x | y) % 16 || idx % 8) throw std::invalid_argument("maxpool_fwd: misaligned buffers");
+  hip_check(hipSetDevice(dev), "hipSetDevice");
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(int64_t(N) * g.Ho * g.Wo * (C / 8))), dim3(256), 0, s,
+                     reinterpret_cast<const uint16_t*>(x), reinterpret_cast<uint16_t*>(y),
+                     reinterpret_cast<uint8_t*>(idx), g);
+  hip_check(hipGetLastError(), "maxpool_fwd launch");
+}
+
+void maxpool_bwd(int dev, hipStream_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t dy,
+                 uintptr_t idx, uintptr_t dx) {
+  const PoolGeo g = pool_geo(N, H, W, C, K, stride, pad);
+  if ((dy | dx) % 16 || idx % 8) throw std::invalid_argument("maxpool_bwd: misaligned buffers");
+  hip_check(hipSetDevice(dev), "hipSetDevice");
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(int64_t(N) * H * W * (C / 8))), dim3(256), 0, s,
+                     reinterpret_cast<const uint16_t*>(dy), reinterpret_cast<const uint8_t*>(idx),
+                     reinterpret_cast<uint16_t*>(dx), g);
+  hip_check(hipGetLastError(), "maxpool_bwd launch");
+}
+
+}  // namespace mpit

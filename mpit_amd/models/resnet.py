@@ -4,8 +4,9 @@ workload "ResNet-50 synthetic ImageNet". Written from the architecture definitio
 ResNet-50 / 1000 classes, the standard figure.
 
 Runs channels_last + bf16 autocast on MI355X: stride-1 1x1 convolutions on the
-hand-written MFMA GEMMs (mpit_amd/ops/conv.py), the 3x3 / 7x7 / strided ones on MIOpen's
-NHWC kernels, and every BatchNorm(+add)(+ReLU) on the fused HIP kernels (ops/bn.py).
+hand-written MFMA GEMMs and the 3x3s on MFMA implicit GEMMs (mpit_amd/ops/conv.py), the
+7x7 stem, the strided 1x1 shortcuts and the strided 3x3 backward-data on MIOpen's NHWC
+kernels, and every BatchNorm(+add)(+ReLU) on the fused HIP kernels (ops/bn.py).
 """
 from __future__ import annotations
 
@@ -17,7 +18,8 @@ import torch
 import torch.nn as nn
 
 from ..ops.bn import BatchNormAct2d
-from ..ops.conv import Conv1x1, GradSlot
+from ..ops.conv import Conv1x1, ConvNHWC, GradSlot
+from ..ops.pool import MaxPool2dNHWC
 
 # Fused BN(+add)(+ReLU) HIP kernels on MI355X (mpit_amd/ops/bn.py); same parameters and
 # state dict as nn.BatchNorm2d, and plain PyTorch math on CPU tensors.
@@ -28,13 +30,17 @@ def _bn(c, act):
     return BatchNormAct2d(c, act=act) if FUSED_BN else nn.BatchNorm2d(c)
 
 
-def conv3x3(i, o, stride=1):
-    return nn.Conv2d(i, o, 3, stride=stride, padding=1, bias=False)
-
-
-# 1x1 convolutions as MFMA GEMMs (falls back to F.conv2d for strides / CPU / odd shapes);
-# MPIT_MFMA_CONV=0 routes them to MIOpen instead (A/B measurements).
+# 1x1 convolutions as MFMA GEMMs and 3x3 ones as MFMA implicit GEMMs (both fall back to
+# nn.Conv2d for CPU / odd shapes); MPIT_MFMA_CONV=0 routes them to MIOpen instead (A/B
+# measurements), MPIT_MFMA_CONV3=0 only the 3x3s.
 MFMA_CONV = os.environ.get("MPIT_MFMA_CONV", "1") != "0"
+MFMA_CONV3 = MFMA_CONV and os.environ.get("MPIT_MFMA_CONV3", "1") != "0"
+
+
+def conv3x3(i, o, stride=1):
+    if MFMA_CONV3:
+        return ConvNHWC(i, o, 3, stride=stride, padding=1)
+    return nn.Conv2d(i, o, 3, stride=stride, padding=1, bias=False)
 
 
 def conv1x1(i, o, stride=1):
@@ -107,7 +113,7 @@ class ResNet(nn.Module):
         self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
         self.bn1 = _bn(64, True)
         self.relu = nn.ReLU(inplace=True)
-        self.maxpool = nn.MaxPool2d(3, stride=2, padding=1)
+        self.maxpool = MaxPool2dNHWC(3, stride=2, padding=1) if MFMA_CONV else nn.MaxPool2d(3, stride=2, padding=1)
         self.layer1 = self._make(block, 64, layers[0])
         self.layer2 = self._make(block, 128, layers[1], 2)
         self.layer3 = self._make(block, 256, layers[2], 2)

@@ -1,4 +1,4 @@
-"""1x1 convolutions on the hand-written MFMA GEMMs (csrc/kernels/gemm.hip).
+"""Convolutions on the hand-written MFMA GEMMs (csrc/kernels/gemm.hip).
 
 A stride-1 1x1 convolution over a channels_last activation is a GEMM over its [N*H*W, C]
 row-major view. Measured on MI355X (benchmarks/conv_vs_gemm.py, ResNet-50 at batch 256)
@@ -16,6 +16,12 @@ fill + an fp32->bf16 cast of MIOpen's own. Here:
 :class:`Conv1x1` is a drop-in ``nn.Conv2d`` that takes this path on the GPU for bf16
 (autocast) channels_last inputs whose channel counts are multiples of 64, and falls
 back to ``F.conv2d`` otherwise (CPU tests, odd shapes, strides).
+
+:class:`ConvNHWC` does the same for RxS convolutions (ResNet's 3x3s, VGG, AlexNet) as
+implicit GEMMs: forward and stride-1 backward-data gather the im2col rows straight from
+the NHWC activation inside the kernel (padding taps read a zero line), backward-weight
+reduces into the fp32 master gradient directly. Only the backward-data of a strided conv
+stays on MIOpen.
 """
 from __future__ import annotations
 
@@ -191,4 +197,101 @@ class Conv1x1(nn.Conv2d):
             return _Conv1x1Fn.apply(x, self.weight, slot)
         if slot is not None:
             raise RuntimeError("GradSlot needs the MFMA path (see Conv1x1.fused)")
+        return super().forward(x)
+
+
+# ------------------------------------------------------------------ RxS convolutions
+
+def _weight_nhwc(weight: torch.Tensor) -> torch.Tensor:
+    """fp32 [Co, C, R, S] weight whose memory is [Co][R][S][C] (channels_last)."""
+    w = weight if weight.dtype == torch.float32 else weight.float()
+    return w if w.is_contiguous(memory_format=torch.channels_last) else w.contiguous(memory_format=torch.channels_last)
+
+
+def conv_weights(weight: torch.Tensor, dgrad: bool):
+    """(bf16 [Co][R][S][C], bf16 tap-flipped transpose [C][R][S][Co] or None), one launch."""
+    co, c, r, s = weight.shape
+    w = _weight_nhwc(weight)
+    wb = torch.empty((co, r, s, c), dtype=torch.bfloat16, device=w.device)
+    wt = torch.empty((c, r, s, co), dtype=torch.bfloat16, device=w.device) if dgrad else None
+    native().cast_transpose(w.device.index, _stream(w), w.data_ptr(), co, c, wb.data_ptr(),
+                            wt.data_ptr() if wt is not None else 0, r * s)
+    return wb, wt
+
+
+class _ConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, stride: int, pad: int):
+        x = _cl(x)
+        if x.dtype != torch.bfloat16:
+            x = x.to(torch.bfloat16)
+        nb, c, h, w = x.shape
+        co, _, r, s = weight.shape
+        ho, wo = (h + 2 * pad - r) // stride + 1, (w + 2 * pad - s) // stride + 1
+        need_dx = ctx.needs_input_grad[0]
+        wb, wt = conv_weights(weight, dgrad=need_dx and stride == 1)
+        y = torch.empty((nb, co, ho, wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+        native().conv_fwd(x.device.index, _stream(x), nb, h, w, c, co, r, s, stride, pad, x.data_ptr(), wb.data_ptr(),
+                          y.data_ptr(), 0, 0)
+        ctx.save_for_backward(x, wb, wt)
+        ctx.geo = (stride, pad)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wb, wt = ctx.saved_tensors
+        stride, pad = ctx.geo
+        dy = _cl(dy)
+        if dy.dtype != torch.bfloat16:
+            dy = dy.to(torch.bfloat16)
+        nb, c, h, w = x.shape
+        co, r, s, _ = wb.shape
+        ho, wo = dy.shape[2], dy.shape[3]
+        m = native()
+        dev, st = x.device.index, _stream(x)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            if stride == 1 and wt is not None:
+                # backward-data = forward conv of dy with the flipped, transposed weight
+                dx = torch.empty_like(x, memory_format=torch.channels_last)
+                m.conv_fwd(dev, st, nb, ho, wo, co, c, r, s, 1, r - 1 - pad, dy.data_ptr(), wt.data_ptr(),
+                           dx.data_ptr(), 0, 0)
+            else:  # strided: MIOpen's NHWC backward-data
+                wv = wb.permute(0, 3, 1, 2)  # [Co, C, R, S] view with channels_last strides
+                dx = torch.ops.aten.convolution_backward(dy, x, wv, None, [stride, stride], [pad, pad], [1, 1], False,
+                                                         [0, 0], 1, [True, False, False])[0]
+        if ctx.needs_input_grad[1]:
+            dw = torch.empty((co, c, r, s), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
+            nws = m.conv_wgrad_ws_floats(dev, nb, h, w, c, co, r, s, stride, pad)
+            ws = torch.empty(nws, dtype=torch.float32, device=x.device) if nws else None
+            m.conv_wgrad(dev, st, nb, h, w, c, co, r, s, stride, pad, dy.data_ptr(), x.data_ptr(), dw.data_ptr(),
+                         ws.data_ptr() if ws is not None else 0, 0.0)
+        return dx, dw, None, None
+
+
+def conv_supported(x: torch.Tensor, weight: torch.Tensor) -> bool:
+    """The MFMA implicit-GEMM path takes bf16 (autocast) NHWC-able inputs with channel
+    counts that are multiples of 64 (wgrad tiles are 64 wide)."""
+    if not x.is_cuda or x.dim() != 4 or weight.dim() != 4:
+        return False
+    bf16 = x.dtype == torch.bfloat16 or (torch.is_autocast_enabled("cuda")
+                                         and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+    co, ci = weight.shape[0], weight.shape[1]
+    return bf16 and ci % 64 == 0 and co % 64 == 0 and x.shape[1] == ci
+
+
+class ConvNHWC(nn.Conv2d):
+    """``nn.Conv2d(i, o, k, stride, padding, bias=False)`` (square kernel / stride /
+    padding, groups = dilation = 1) whose training forward/backward run as MFMA implicit
+    GEMMs on MI355X (see module docstring); falls back to ``nn.Conv2d`` otherwise."""
+
+    def __init__(self, in_channels: int, out_channels: int, kernel_size: int, stride: int = 1, padding: int = 0):
+        super().__init__(in_channels, out_channels, kernel_size, stride=stride, padding=padding, bias=False)
+
+    def fused(self, x: torch.Tensor) -> bool:
+        return conv_supported(x, self.weight)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.fused(x):
+            return _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0])
         return super().forward(x)

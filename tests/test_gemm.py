@@ -7,6 +7,14 @@ import torch.nn.functional as F
 from mpit_amd.ops import conv as C
 
 
+def test_convnhwc_cpu_fallback_matches_conv2d():
+    torch.manual_seed(0)
+    m = C.ConvNHWC(64, 64, 3, stride=2, padding=1)
+    x = torch.randn(2, 64, 9, 9)
+    assert torch.allclose(m(x), F.conv2d(x, m.weight, stride=2, padding=1), atol=1e-5)
+    assert not C.conv_supported(x, m.weight)
+
+
 def test_conv1x1_cpu_fallback_matches_conv2d():
     torch.manual_seed(0)
     m = C.Conv1x1(64, 128)
@@ -87,6 +95,42 @@ def test_conv1x1_fwd_bwd(n, ci, co, hw):
         y1 = mod(x1)
     y2 = ref(x2)
     assert y1.dtype == torch.bfloat16
+    assert _rel(y1, y2) < 8e-3
+    g = torch.randn_like(y2)
+    y1.backward(g.to(torch.bfloat16))
+    y2.backward(g)
+    assert _rel(x1.grad, x2.grad) < 1e-2
+    assert mod.weight.grad.dtype == torch.float32
+    assert _rel(mod.weight.grad, ref.weight.grad) < 1e-2
+
+
+@gpu
+def test_cast_transpose_taps():
+    w = torch.randn(128, 64, 3, 3, device="cuda").contiguous(memory_format=torch.channels_last)
+    wb, wt = C.conv_weights(w, dgrad=True)
+    ref = w.permute(0, 2, 3, 1).to(torch.bfloat16)  # [Co][R][S][C]
+    assert torch.equal(wb, ref)
+    assert torch.equal(wt, ref.flip(1, 2).permute(3, 1, 2, 0).contiguous())  # [C][R'][S'][Co]
+
+
+@gpu
+@pytest.mark.parametrize("n,ci,co,hw,k,stride", [(2, 64, 64, 56, 3, 1), (3, 128, 128, 28, 3, 2), (4, 256, 256, 14, 3, 1),
+                                                 (2, 512, 512, 7, 3, 1), (2, 64, 128, 9, 3, 2), (2, 128, 64, 13, 5, 1),
+                                                 (5, 64, 192, 11, 3, 1)])
+def test_conv_nhwc_fwd_bwd(n, ci, co, hw, k, stride):
+    """Implicit-GEMM conv (fwd, dgrad, wgrad) against fp32 PyTorch conv2d."""
+    torch.manual_seed(n * ci + co + k)
+    pad = k // 2
+    mod = C.ConvNHWC(ci, co, k, stride=stride, padding=pad).cuda().to(memory_format=torch.channels_last)
+    ref = torch.nn.Conv2d(ci, co, k, stride=stride, padding=pad, bias=False).cuda()
+    ref.weight.data.copy_(mod.weight.data)
+    x = torch.randn(n, ci, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x1 = x.clone().requires_grad_(True)
+    x2 = x.float().clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y1 = mod(x1)
+    y2 = ref(x2)
+    assert y1.dtype == torch.bfloat16 and y1.shape == y2.shape
     assert _rel(y1, y2) < 8e-3
     g = torch.randn_like(y2)
     y1.backward(g.to(torch.bfloat16))

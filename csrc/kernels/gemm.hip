@@ -252,6 +252,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const uint16_t* __restr
     const bool ok = m < M;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
+      uint32_t pk[4][2];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int n = n0 + wn * WN + j * 32 + 8 * g + 4 * fh;
@@ -272,42 +273,58 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const uint16_t* __restr
             s2[j][4 * g + e] = fmaf(y, y, s2[j][4 * g + e]);
           }
         }
+        pk[g][0] = uint32_t(h[0]) | (uint32_t(h[1]) << 16);
+        pk[g][1] = uint32_t(h[2]) | (uint32_t(h[3]) << 16);
+      }
+      // T21: a row's 8 consecutive columns of group g are split over lanes r and r+32;
+      // v_permlane32_swap pairs groups (g, g+1) so each lane stores 16 contiguous bytes
+      // (lanes < 32: columns 8g..8g+7, lanes >= 32: 8g+8..8g+15) — half the store
+      // instructions of 8-byte stores, same addresses.
+#pragma unroll
+      for (int gp = 0; gp < 4; gp += 2) {
+        const auto r0 = __builtin_amdgcn_permlane32_swap(pk[gp][0], pk[gp + 1][0], false, false);
+        const auto r1 = __builtin_amdgcn_permlane32_swap(pk[gp][1], pk[gp + 1][1], false, false);
         if (ok) {
-          uint2 pk;
-          pk.x = uint32_t(h[0]) | (uint32_t(h[1]) << 16);
-          pk.y = uint32_t(h[2]) | (uint32_t(h[3]) << 16);
-          *reinterpret_cast<uint2*>(C + m * ldc + n) = pk;
+          const int n = n0 + wn * WN + j * 32 + 8 * gp + 8 * fh;
+          *reinterpret_cast<uint4*>(C + m * ldc + n) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
         }
       }
     }
   }
   if constexpr (STATS) {
-    // reduce over the 32 lanes that share a column set (lane&31 varies = rows), then
-    // over the two row-halves of the block (wm) through LDS.
+    // Sum over the 32 lanes that share a column set (lane&31 = rows) by a transposing
+    // butterfly: at each lane bit the lane keeps half of its values and adds its
+    // partner's copy of that half (31 shuffles for 64 values instead of 5 per value).
+    // Afterwards lane r holds values [r*NV/32, (r+1)*NV/32) of the flattened
+    // [stat][j][v] array; the two row-halves of the block (wm) are combined in LDS.
+    constexpr int NV = 2 * TN * 16, NL = NV / 32;
+    float a[NV];
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
-        float a = s1[j][v], b = s2[j][v];
-#pragma unroll
-        for (int o = 1; o < 32; o <<= 1) {
-          a += __shfl_xor(a, o);
-          b += __shfl_xor(b, o);
-        }
-        s1[j][v] = a;
-        s2[j][v] = b;
+        a[j * 16 + v] = s1[j][v];
+        a[TN * 16 + j * 16 + v] = s2[j][v];
       }
+#pragma unroll
+    for (int b = 16, len = NV; b >= 1; b >>= 1, len >>= 1) {
+      const bool up = (fr & b) != 0;
+      const int half = len / 2;
+#pragma unroll
+      for (int q = 0; q < half; ++q) {
+        const float send = up ? a[q] : a[q + half];
+        const float keep = up ? a[q + half] : a[q];
+        a[q] = keep + __shfl_xor(send, b);
+      }
+    }
     __syncthreads();  // the ring may still be read by other waves
-    float* red = reinterpret_cast<float*>(smem);  // [2 (wm)][2][BN]
-    if (fr == 0) {
+    float* red = reinterpret_cast<float*>(smem);  // [2 (wm)][2 (stat)][BN]
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) {
-          const int n = wn * WN + j * 32 + (v & 3) + 8 * (v >> 2) + 4 * fh;
-          red[(wm * 2 + 0) * BN + n] = s1[j][v];
-          red[(wm * 2 + 1) * BN + n] = s2[j][v];
-        }
+    for (int q = 0; q < NL; ++q) {
+      const int k = fr * NL + q;
+      const int st = k / (TN * 16), j = (k / 16) % TN, v = k % 16;
+      const int n = wn * WN + j * 32 + (v & 3) + 8 * (v >> 2) + 4 * fh;
+      red[(wm * 2 + st) * BN + n] = a[q];
     }
     __syncthreads();
     for (int n = t; n < BN; n += 256) {
@@ -593,7 +610,7 @@ static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t
   check_ptr(A, "A");
   check_ptr(B, "B");
   check_ptr(C, "C");
-  if (lda % 8 || ldb % 8 || ldc % 4 || (!geo && lda < K) || ldb < K || ldc < N)
+  if (lda % 8 || ldb % 8 || ldc % 8 || (!geo && lda < K) || ldb < K || ldc < N)
     throw std::invalid_argument("gemm_nt: bad leading dimensions");
   hip_check(hipSetDevice(dev), "hipSetDevice");
   const auto* a = reinterpret_cast<const uint16_t*>(A);

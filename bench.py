@@ -41,7 +41,9 @@ def main(argv=None) -> int:
     ap.add_argument("--topology", default="colocated", choices=["colocated", "dedicated"])
     ap.add_argument("--servers", type=int, default=1)
     ap.add_argument("--su", type=int, default=1)
-    ap.add_argument("--lr", type=float, default=0.05)
+    ap.add_argument("--lr", type=float, default=0.05,
+                    help="learning rate; Downpour divides it by the number of workers (every worker's "
+                         "push is applied, so N pushes per round then add up to one step of this size)")
     ap.add_argument("--datapath", type=int, default=2)
     ap.add_argument("--staleness", type=int, default=-1, help="bounded staleness (SSP); -1 = fully async")
     ap.add_argument("--wire", default="fp32", choices=["fp32", "bf16"], help="EASGD elastic-difference dtype")
@@ -66,8 +68,10 @@ def main(argv=None) -> int:
 
     mp.Init()
     mva = 0.9 / max(1, a.gpus) if a.optimizer in ("eamsgd", "easgd") else 0.0
+    nw = a.gpus if a.topology == "colocated" else max(1, a.gpus - a.servers)
+    lr = a.lr / max(1, nw) if a.optimizer == "downpour" else a.lr
     cfg = TrainConfig(model=a.model, batch=a.batch, optimizer=a.optimizer, topology=a.topology, servers=a.servers,
-                      su=a.su, lr=a.lr, mva=mva, mom=0.0, amp=not a.no_amp, channels_last=not a.no_channels_last,
+                      su=a.su, lr=lr, mva=mva, mom=0.0, amp=not a.no_amp, channels_last=not a.no_channels_last,
                       datapath=a.datapath, staleness=a.staleness, wire_dtype=a.wire)
     tr = Trainer(cfg)
     secs, loss = timed_steps(tr, a.steps, a.warmup)
@@ -77,7 +81,11 @@ def main(argv=None) -> int:
     shape = INPUT_SHAPES.get(a.model, (3, 224, 224))
     images = a.steps * a.batch * nworkers
     value = images / secs
+    import math
+
     lossv = float(loss.float().item()) if loss is not None else None
+    if lossv is not None and not math.isfinite(lossv):
+        lossv = None  # keep the line strict JSON
     tr.stop()
     if tr.rank == 0:
         par = {"downpour": "async-ps", "eamsgd": "easgd-ps", "easgd": "easgd-ps", "msgd": "local",

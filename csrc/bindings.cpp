@@ -89,9 +89,10 @@ PYBIND11_MODULE(_mpit, m) {
   m.def(
       "gemm_nt",
       [](int dev, uintptr_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B, int64_t ldb, uintptr_t C,
-         int64_t ldc, uintptr_t stats, uintptr_t cin) { gemm_nt(dev, S(s), M, N, K, A, lda, B, ldb, C, ldc, stats, cin); },
+         int64_t ldc, uintptr_t stats, uintptr_t cin,
+         uintptr_t cmask) { gemm_nt(dev, S(s), M, N, K, A, lda, B, ldb, C, ldc, stats, cin, cmask); },
       py::arg("dev"), py::arg("stream"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("A"), py::arg("lda"),
-      py::arg("B"), py::arg("ldb"), py::arg("C"), py::arg("ldc"), py::arg("stats") = 0, py::arg("cin") = 0);
+      py::arg("B"), py::arg("ldb"), py::arg("C"), py::arg("ldc"), py::arg("stats") = 0, py::arg("cin") = 0, py::arg("cmask") = 0);
   m.def("gemm_tn_supported", &gemm_tn_supported);
   m.def("gemm_tn_ws_floats", &gemm_tn_ws_floats);
   m.def("gemm_tn", [](int dev, uintptr_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X, int64_t ldx,

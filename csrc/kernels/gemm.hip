@@ -122,7 +122,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const uint16_t* __restr
                                                          const uint16_t* __restrict__ B, int64_t ldb,
                                                          uint16_t* C, int64_t ldc, int64_t M, int N, int K,
                                                          int ntn, float* __restrict__ stats, const uint16_t* Cin,
-                                                         ConvGeo geo) {
+                                                         const uint8_t* __restrict__ Cmask, ConvGeo geo) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 32, TN = WN / 32;
   constexpr int IA = BM / 16 / 4, IB = BN / 16 / 4;  // glds instructions per wave per tile
@@ -258,10 +258,13 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const uint16_t* __restr
         const int n = n0 + wn * WN + j * 32 + 8 * g + 4 * fh;
         if (Cin != nullptr && ok) {  // C = A.B^T + Cin (Cin may alias C: same thread, read first)
           const uint2 ci = *reinterpret_cast<const uint2*>(Cin + m * ldc + n);
-          acc[i][j][4 * g + 0] += bf2f(uint16_t(ci.x & 0xffff));
-          acc[i][j][4 * g + 1] += bf2f(uint16_t(ci.x >> 16));
-          acc[i][j][4 * g + 2] += bf2f(uint16_t(ci.y & 0xffff));
-          acc[i][j][4 * g + 3] += bf2f(uint16_t(ci.y >> 16));
+          // Cmask: Cin is a ReLU'd gradient given as (dy, forward bit mask: one byte per 8
+          // channels, bit v = channel 8k+v positive) — dy*mask is never materialised
+          const uint32_t mb = Cmask ? uint32_t(Cmask[(m * ldc + n) >> 3]) >> (n & 7) : 0xfu;
+          acc[i][j][4 * g + 0] += (mb & 1u) ? bf2f(uint16_t(ci.x & 0xffff)) : 0.f;
+          acc[i][j][4 * g + 1] += (mb & 2u) ? bf2f(uint16_t(ci.x >> 16)) : 0.f;
+          acc[i][j][4 * g + 2] += (mb & 4u) ? bf2f(uint16_t(ci.y & 0xffff)) : 0.f;
+          acc[i][j][4 * g + 3] += (mb & 8u) ? bf2f(uint16_t(ci.y >> 16)) : 0.f;
         }
         uint16_t h[4];
 #pragma unroll
@@ -603,7 +606,8 @@ bool gemm_nt_supported(int64_t M, int N, int K) { return M > 0 && N > 0 && K > 0
 int64_t gemm_nt_stats_floats(int64_t M, int N) { return ((M + 127) / 128) * 2 * int64_t(N); }
 
 static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B,
-                      int64_t ldb, uintptr_t C, int64_t ldc, uintptr_t stats, uintptr_t cin, const ConvGeo* geo) {
+                      int64_t ldb, uintptr_t C, int64_t ldc, uintptr_t stats, uintptr_t cin, uintptr_t cmask,
+                      const ConvGeo* geo) {
   if (!gemm_nt_supported(M, N, K))
     throw std::invalid_argument("gemm_nt: need N % 64 == 0 and K % 32 == 0 (M=" + std::to_string(M) +
                                 " N=" + std::to_string(N) + " K=" + std::to_string(K) + ")");
@@ -619,6 +623,8 @@ static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t
   auto* st = reinterpret_cast<float*>(stats);
   const auto* ci = reinterpret_cast<const uint16_t*>(cin);
   if (cin) check_ptr(cin, "Cin");
+  if (cmask && (!cin || ldc != N)) throw std::invalid_argument("gemm_nt: cmask needs cin with ldc == N");
+  const auto* cm = reinterpret_cast<const uint8_t*>(cmask);
   const ConvGeo g = geo ? *geo : ConvGeo{};
   constexpr int BM = 128;
   const int64_t mtn = (M + BM - 1) / BM;
@@ -627,7 +633,7 @@ static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t
   // (kernel templates are named at a non-template call site so their host stubs are emitted)
 #define MPIT_NT_LAUNCH1(BN, ST, STATS, CONV)                                                                   \
   hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, ST, STATS, CONV>), dim3(unsigned(nb)), dim3(256), shm, s, a, lda, b, \
-                     ldb, c, ldc, M, N, K, ntn, st, ci, g)
+                     ldb, c, ldc, M, N, K, ntn, st, ci, cm, g)
 #define MPIT_NT_LAUNCH(BN, ST)                                                   \
   do {                                                                           \
     const int ntn = N / BN;                                                      \
@@ -657,8 +663,8 @@ static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t
 }
 
 void gemm_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B, int64_t ldb,
-             uintptr_t C, int64_t ldc, uintptr_t stats, uintptr_t cin) {
-  launch_nt(dev, s, M, N, K, A, lda, B, ldb, C, ldc, stats, cin, nullptr);
+             uintptr_t C, int64_t ldc, uintptr_t stats, uintptr_t cin, uintptr_t cmask) {
+  launch_nt(dev, s, M, N, K, A, lda, B, ldb, C, ldc, stats, cin, cmask, nullptr);
 }
 
 bool gemm_tn_supported(int64_t M, int N, int K) { return M > 0 && N % 64 == 0 && K % 64 == 0 && N > 0 && K > 0; }
@@ -774,7 +780,7 @@ void conv_fwd(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R
   int Ho, Wo;
   const ConvGeo g = conv_geo(H, W, C, R, S, stride, pad, &Ho, &Wo);
   const int64_t M = int64_t(Nb) * Ho * Wo;
-  launch_nt(dev, s, M, Co, R * S * C, x, C, w, int64_t(R) * S * C, y, Co, stats, cin, &g);
+  launch_nt(dev, s, M, Co, R * S * C, x, C, w, int64_t(R) * S * C, y, Co, stats, cin, 0, &g);
 }
 
 int64_t conv_wgrad_ws_floats(int dev, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad) {

@@ -81,11 +81,12 @@ void bn_act_bwd(int dev, hipStream_t s, bool bf16, uintptr_t dy, uintptr_t mask,
 // ---- MFMA GEMMs for NHWC 1x1 convolutions (gemm.hip), bf16 operands, fp32 accumulate --
 // C[M,N] (bf16) = A[M,K] . B[N,K]^T; optional per-column {sum, sumsq} partials of C per
 // 128-row tile into stats[ceil(M/128)][2][N] (gemm_nt_stats_floats); optional bf16 cin
-// [M, ldc] added to the product before rounding (may alias C).
+// [M, ldc] added to the product before rounding (may alias C); optional cmask (with cin,
+// ldc == N): the bn_act ReLU bit mask of cin (1 byte / 8 channels) — adds cin*mask.
 bool gemm_nt_supported(int64_t M, int N, int K);
 int64_t gemm_nt_stats_floats(int64_t M, int N);
 void gemm_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B, int64_t ldb,
-             uintptr_t C, int64_t ldc, uintptr_t stats, uintptr_t cin);
+             uintptr_t C, int64_t ldc, uintptr_t stats, uintptr_t cin, uintptr_t cmask = 0);
 // out[N,K] (fp32) = beta*out + Y[M,N]^T . X[M,K]  (split over M; ws: gemm_tn_ws_floats)
 bool gemm_tn_supported(int64_t M, int N, int K);
 int64_t gemm_tn_ws_floats(int dev, int64_t M, int N, int K);

@@ -18,7 +18,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.bn import BatchNormAct2d
-from ..ops.conv import Conv1x1, ConvNHWC, GradSlot
+from ..ops.conv import Conv1x1, ConvNHWC, GradSlot, park_grad
 from ..ops.pool import MaxPool2dNHWC
 
 # Fused BN(+add)(+ReLU) HIP kernels on MI355X (mpit_amd/ops/bn.py); same parameters and
@@ -45,7 +45,8 @@ def conv3x3(i, o, stride=1):
 
 def conv1x1(i, o, stride=1):
     if MFMA_CONV:
-        return Conv1x1(i, o, stride=stride)
+        # strided (downsample) 1x1: implicit GEMM over the strided pixels (fwd, wgrad)
+        return Conv1x1(i, o) if stride == 1 else ConvNHWC(i, o, 1, stride=stride)
     return nn.Conv2d(i, o, 1, stride=stride, bias=False)
 
 
@@ -86,19 +87,31 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
-        idt = x if self.downsample is None else self.downsample(x)
         if isinstance(self.bn1, BatchNormAct2d):
-            if (self.downsample is None and isinstance(self.conv1, Conv1x1) and self.conv1.fused(x)
-                    and self.bn3.fused(x) and torch.is_grad_enabled()):
-                # identity shortcut: the shortcut gradient is added inside conv1's
-                # backward-data GEMM instead of by a separate autograd add (ops/conv.py)
+            fused = (isinstance(self.conv1, Conv1x1) and self.conv1.fused(x) and self.bn3.fused(x)
+                     and torch.is_grad_enabled())
+            if fused and self.downsample is None:
+                # identity shortcut: the shortcut gradient (dy*mask of bn3) is added inside
+                # conv1's backward-data GEMM instead of by a separate autograd add
                 slot = GradSlot()
                 out = self.bn1(self.conv1(x, slot))
                 out = self.bn2(self.conv2(out))
-                return self.bn3(self.conv3(out), idt, res_slot=slot)
+                return self.bn3(self.conv3(out), x, res_slot=slot)
+            if fused:
+                # downsample shortcut, computed after the main branch so that its backward runs
+                # first: the shortcut conv's input gradient is parked and added in conv1's
+                # backward-data epilogue (no autograd add over the block input)
+                slot = GradSlot()
+                out = self.bn1(self.conv1(x, slot))
+                out = self.bn2(self.conv2(out))
+                out = self.conv3(out)
+                idt = self.downsample(park_grad(x, slot))
+                return self.bn3(out, idt)
+            idt = x if self.downsample is None else self.downsample(x)
             out = self.bn1(self.conv1(x))
             out = self.bn2(self.conv2(out))
             return self.bn3(self.conv3(out), idt)
+        idt = x if self.downsample is None else self.downsample(x)
         out = self.relu(self.bn1(self.conv1(x)))
         out = self.relu(self.bn2(self.conv2(out)))
         out = self.bn3(self.conv3(out))

@@ -71,7 +71,10 @@ class _BNActFn(torch.autograd.Function):
         dev = x.device.index
         stream = torch.cuda.current_stream(x.device).cuda_stream
         dx = torch.empty_like(x, memory_format=torch.channels_last)
-        dres = torch.empty_like(x, memory_format=torch.channels_last) if ctx.has_res else None
+        # residual gradient of act(bn(x) + res) = dy*mask: with a GradSlot consumer it is
+        # handed over as (dy, mask) and never written
+        park = ctx.has_res and ctx.res_slot is not None and ctx.relu and mask is not None and dy.dtype == torch.bfloat16
+        dres = torch.empty_like(x, memory_format=torch.channels_last) if (ctx.has_res and not park) else None
         dgamma = torch.empty(C, dtype=torch.float32, device=x.device) if ctx.has_w else None
         dbeta = torch.empty(C, dtype=torch.float32, device=x.device) if ctx.has_b else None
         ws = torch.empty(m.bn_workspace_floats(C), dtype=torch.float32, device=x.device)
@@ -81,7 +84,11 @@ class _BNActFn(torch.autograd.Function):
                      mean.data_ptr(), rstd.data_ptr(), dgamma.data_ptr() if dgamma is not None else 0,
                      dbeta.data_ptr() if dbeta is not None else 0, ws.data_ptr(), bool(ctx.relu))
         if ctx.res_slot is not None:  # the shortcut's gradient is added by the block's first conv
-            ctx.res_slot.grad = dres
+            if park:
+                if not ctx.res_slot.put(dy, mask):
+                    raise RuntimeError("GradSlot consumer ran before the BN backward")
+            elif not ctx.res_slot.put(dres):
+                raise RuntimeError("GradSlot consumer ran before the BN backward")
             dres = None
         return dx, dgamma, dbeta, None, None, dres, None, None, None, None
 

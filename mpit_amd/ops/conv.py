@@ -98,18 +98,54 @@ class GradSlot:
     A ResNet identity shortcut makes the block input feed both the first 1x1 convolution
     and the last BN's residual add, so autograd would sum the two input gradients with a
     separate add kernel (read 2, write 1 over the block input). Instead the BN backward
-    parks its residual gradient here and the convolution's backward-data GEMM adds it in
-    its epilogue (``C = dY.W + slot``). The BN backward always runs first: the
-    convolution's output feeds, through the block, the BN's input."""
+    parks its residual gradient here — as the pair (dy, ReLU bit mask), since the
+    residual gradient of act(bn(y) + res) is just dy*mask — and the convolution's
+    backward-data GEMM adds ``dy*mask`` in its epilogue (``C = dY.W + dy*mask``): the
+    residual gradient is never written. The BN backward always runs first: the
+    convolution's output feeds, through the block, the BN's input.
 
-    __slots__ = ("grad",)
+    A downsample block parks the shortcut convolution's input gradient the same way
+    (:class:`ParkGrad`), as a plain tensor. If the consumer's backward ran before the
+    producer's, the slot is closed and the producer returns its gradient to autograd."""
+
+    __slots__ = ("grad", "mask", "closed")
 
     def __init__(self):
         self.grad = None
+        self.mask = None
+        self.closed = False
+
+    def put(self, grad, mask=None) -> bool:
+        """Park ``grad`` (times ``mask`` when given); False if the consumer already ran."""
+        if self.closed:
+            return False
+        self.grad, self.mask = grad, mask
+        return True
 
     def take(self):
-        g, self.grad = self.grad, None
-        return g
+        g, m = self.grad, self.mask
+        self.grad = self.mask = None
+        self.closed = True
+        return g, m
+
+
+class _ParkGradFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, slot):
+        ctx.slot = slot
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        if ctx.slot.put(g):
+            return None, None
+        return g, None
+
+
+def park_grad(x: torch.Tensor, slot: GradSlot) -> torch.Tensor:
+    """Identity whose backward parks the incoming gradient in ``slot`` for a later
+    GEMM epilogue to add (see :class:`GradSlot`)."""
+    return _ParkGradFn.apply(x, slot)
 
 
 class _Conv1x1Fn(torch.autograd.Function):
@@ -142,15 +178,17 @@ class _Conv1x1Fn(torch.autograd.Function):
         m = native()
         dev, s = x.device.index, _stream(x)
         dx = dw = None
-        extra = ctx.slot.take() if ctx.slot is not None else None
+        extra, emask = ctx.slot.take() if ctx.slot is not None else (None, None)
         if ctx.needs_input_grad[0]:
-            if extra is not None:  # residual gradient parked by the block's last BN: add in place
+            if extra is not None:  # gradient parked by the block (GradSlot): added in the epilogue
                 extra = _cl(extra)
-                if extra.dtype != torch.bfloat16 or extra.shape != x.shape:
+                if extra.dtype != torch.bfloat16:
+                    extra = extra.to(torch.bfloat16)
+                if extra.shape != x.shape:
                     raise RuntimeError("GradSlot gradient does not match the convolution input")
-                dx = extra
+                dx = torch.empty_like(x, memory_format=torch.channels_last)
                 m.gemm_nt(dev, s, M, ci, co, dy.data_ptr(), co, wt.data_ptr(), co, dx.data_ptr(), ci, 0,
-                          dx.data_ptr())
+                          extra.data_ptr(), emask.data_ptr() if emask is not None else 0)
             else:
                 dx = torch.empty_like(x, memory_format=torch.channels_last)
                 m.gemm_nt(dev, s, M, ci, co, dy.data_ptr(), co, wt.data_ptr(), co, dx.data_ptr(), ci, 0)

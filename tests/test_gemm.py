@@ -138,3 +138,19 @@ def test_conv_nhwc_fwd_bwd(n, ci, co, hw, k, stride):
     assert _rel(x1.grad, x2.grad) < 1e-2
     assert mod.weight.grad.dtype == torch.float32
     assert _rel(mod.weight.grad, ref.weight.grad) < 1e-2
+
+
+def test_park_grad_slot_protocol():
+    # producer runs first: the gradient is parked, autograd gets none
+    slot = C.GradSlot()
+    x = torch.randn(3, 4, requires_grad=True)
+    (C.park_grad(x, slot) * 2).sum().backward()
+    assert x.grad is None
+    g, m = slot.take()
+    assert torch.equal(g, torch.full((3, 4), 2.0)) and m is None
+    # consumer already ran (slot closed): the gradient goes back to autograd
+    slot2 = C.GradSlot()
+    slot2.take()
+    x2 = torch.randn(3, 4, requires_grad=True)
+    (C.park_grad(x2, slot2) * 3).sum().backward()
+    assert torch.equal(x2.grad, torch.full((3, 4), 3.0))

@@ -109,10 +109,18 @@ PYBIND11_MODULE(_mpit, m) {
   m.def("maxpool_bwd", [](int dev, uintptr_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t dy,
                           uintptr_t idx, uintptr_t dx) { maxpool_bwd(dev, S(s), N, H, W, C, K, stride, pad, dy, idx, dx); });
   m.def("conv_supported", &conv_supported);
-  m.def("conv_fwd", [](int dev, uintptr_t s, int Nb, int H, int W, int C, int Co, int R, int S_, int stride, int pad,
-                       uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t cin) {
-    conv_fwd(dev, S(s), Nb, H, W, C, Co, R, S_, stride, pad, x, w, y, stats, cin);
-  });
+  m.def(
+      "conv_fwd",
+      [](int dev, uintptr_t s, int Nb, int H, int W, int C, int Co, int R, int S_, int stride, int pad, uintptr_t x,
+         uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t cin, uintptr_t bias, bool relu) {
+        conv_fwd(dev, S(s), Nb, H, W, C, Co, R, S_, stride, pad, x, w, y, stats, cin, bias, relu);
+      },
+      py::arg("dev"), py::arg("stream"), py::arg("Nb"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("Co"),
+      py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("x"), py::arg("w"), py::arg("y"),
+      py::arg("stats") = 0, py::arg("cin") = 0, py::arg("bias") = 0, py::arg("relu") = false);
+  m.def("relu_bias_bwd_ws_floats", &relu_bias_bwd_ws_floats);
+  m.def("relu_bias_bwd", [](int dev, uintptr_t s, int64_t M, int C, uintptr_t dy, uintptr_t y, uintptr_t dz, uintptr_t db,
+                            uintptr_t ws) { relu_bias_bwd(dev, S(s), M, C, dy, y, dz, db, ws); });
   m.def("conv_wgrad_ws_floats", &conv_wgrad_ws_floats);
   m.def("conv_wgrad", [](int dev, uintptr_t s, int Nb, int H, int W, int C, int Co, int R, int S_, int stride, int pad,
                          uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, float beta) {

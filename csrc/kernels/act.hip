@@ -1,0 +1,102 @@
+// ReLU + bias backward for the conv(+bias)(+ReLU) layers whose forward runs the bias and
+// the ReLU in the GEMM epilogue (VGG / AlexNet on the MFMA implicit-GEMM path):
+//   dz = dy * (y > 0)            (bf16 [M, C], y = the layer's saved output)
+//   db[c] = sum over rows of dz  (fp32, optional)
+// One pass over dy and y (the masked gradient is what the dgrad / wgrad GEMMs consume, so
+// it has to be written once anyway); the bias gradient rides along as a per-thread
+// channel-group accumulation, combined per block in LDS and across blocks by a second
+// tiny kernel in a fixed order (deterministic, no atomics).
+#include <hip/hip_runtime.h>
+
+#include <stdexcept>
+#include <string>
+
+#include "ew.h"
+#include "kernels.h"
+
+namespace mpit {
+namespace {
+
+constexpr int kMaxBlocks = 1024;
+
+__global__ __launch_bounds__(1024) void relu_bias_bwd_kernel(const uint16_t* __restrict__ dy,
+                                                             const uint16_t* __restrict__ y,
+                                                             uint16_t* __restrict__ dz, int64_t M, int C,
+                                                             int64_t rows_per_block, float* __restrict__ part) {
+  extern __shared__ float lds[];  // [R][C]
+  const int G = C / 8;
+  const int g = threadIdx.x % G, rs = threadIdx.x / G, R = blockDim.x / G;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int64_t r0 = int64_t(blockIdx.x) * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
+  for (int64_t r = r0 + rs; r < r1; r += R) {
+    const int64_t o = r * C + g * 8;
+    const uint4 a = *reinterpret_cast<const uint4*>(dy + o);
+    const uint4 b = *reinterpret_cast<const uint4*>(y + o);
+    const uint32_t av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+    uint32_t ov[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      uint32_t w = 0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint16_t yv = uint16_t(bv[k] >> (16 * h));
+        const uint16_t gv = uint16_t(av[k] >> (16 * h));
+        const bool pos = bf2f(yv) > 0.f;
+        const uint16_t z = pos ? gv : uint16_t(0);
+        acc[2 * k + h] += bf2f(z);
+        w |= uint32_t(z) << (16 * h);
+      }
+      ov[k] = w;
+    }
+    *reinterpret_cast<uint4*>(dz + o) = make_uint4(ov[0], ov[1], ov[2], ov[3]);
+  }
+  if (!part) return;
+#pragma unroll
+  for (int v = 0; v < 8; ++v) lds[rs * C + g * 8 + v] = acc[v];
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float s = 0.f;
+    for (int k = 0; k < R; ++k) s += lds[k * C + c];
+    part[int64_t(blockIdx.x) * C + c] = s;
+  }
+}
+
+__global__ __launch_bounds__(256) void sum_parts_kernel(const float* __restrict__ part, int nb, int C,
+                                                        float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int k = 0; k < nb; ++k) s += part[int64_t(k) * C + c];
+  out[c] = s;
+}
+
+}  // namespace
+
+int64_t relu_bias_bwd_ws_floats(int C) { return int64_t(kMaxBlocks) * C; }
+
+void relu_bias_bwd(int dev, hipStream_t s, int64_t M, int C, uintptr_t dy, uintptr_t y, uintptr_t dz, uintptr_t db,
+                   uintptr_t ws) {
+  if (M <= 0 || C <= 0 || C % 8 || C / 8 > 1024) throw std::invalid_argument("relu_bias_bwd: need C % 8 == 0, C <= 8192");
+  if ((dy | y | dz) % 16) throw std::invalid_argument("relu_bias_bwd: buffers must be 16-byte aligned");
+  if (db && !ws) throw std::invalid_argument("relu_bias_bwd: bias gradient needs the workspace");
+  hip_check(hipSetDevice(dev), "hipSetDevice");
+  const int G = C / 8;
+  const int blk = G >= 256 ? G : (256 / G) * G;
+  const int R = blk / G;
+  int64_t nb = std::min<int64_t>(kMaxBlocks, std::max<int64_t>(1, (M + R * 16 - 1) / (R * 16)));
+  int64_t rpb = (M + nb - 1) / nb;
+  nb = (M + rpb - 1) / rpb;
+  float* part = db ? reinterpret_cast<float*>(ws) : nullptr;
+  const size_t shm = db ? size_t(R) * C * sizeof(float) : 0;
+  hipLaunchKernelGGL(relu_bias_bwd_kernel, dim3(unsigned(nb)), dim3(blk), shm, s, reinterpret_cast<const uint16_t*>(dy),
+                     reinterpret_cast<const uint16_t*>(y), reinterpret_cast<uint16_t*>(dz), M, C, rpb, part);
+  hip_check(hipGetLastError(), "relu_bias_bwd launch");
+  if (db) {
+    hipLaunchKernelGGL(sum_parts_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, int(nb), C,
+                       reinterpret_cast<float*>(db));
+    hip_check(hipGetLastError(), "relu_bias_bwd sum launch");
+  }
+}
+
+}  // namespace mpit

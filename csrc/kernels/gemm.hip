@@ -122,7 +122,8 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const uint16_t* __restr
                                                          const uint16_t* __restrict__ B, int64_t ldb,
                                                          uint16_t* C, int64_t ldc, int64_t M, int N, int K,
                                                          int ntn, float* __restrict__ stats, const uint16_t* Cin,
-                                                         const uint8_t* __restrict__ Cmask, ConvGeo geo) {
+                                                         const uint8_t* __restrict__ Cmask,
+                                                         const float* __restrict__ bias, int relu, ConvGeo geo) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 32, TN = WN / 32;
   constexpr int IA = BM / 16 / 4, IB = BN / 16 / 4;  // glds instructions per wave per tile
@@ -265,6 +266,17 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const uint16_t* __restr
           acc[i][j][4 * g + 1] += (mb & 2u) ? bf2f(uint16_t(ci.x >> 16)) : 0.f;
           acc[i][j][4 * g + 2] += (mb & 4u) ? bf2f(uint16_t(ci.y & 0xffff)) : 0.f;
           acc[i][j][4 * g + 3] += (mb & 8u) ? bf2f(uint16_t(ci.y >> 16)) : 0.f;
+        }
+        if (bias != nullptr) {  // conv bias (+ ReLU) fused into the epilogue (VGG / AlexNet)
+          const float4 b4 = *reinterpret_cast<const float4*>(bias + n);
+          acc[i][j][4 * g + 0] += b4.x;
+          acc[i][j][4 * g + 1] += b4.y;
+          acc[i][j][4 * g + 2] += b4.z;
+          acc[i][j][4 * g + 3] += b4.w;
+        }
+        if (relu) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[i][j][4 * g + e] = fmaxf(acc[i][j][4 * g + e], 0.f);
         }
         uint16_t h[4];
 #pragma unroll
@@ -607,7 +619,7 @@ int64_t gemm_nt_stats_floats(int64_t M, int N) { return ((M + 127) / 128) * 2 * 
 
 static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B,
                       int64_t ldb, uintptr_t C, int64_t ldc, uintptr_t stats, uintptr_t cin, uintptr_t cmask,
-                      const ConvGeo* geo) {
+                      const ConvGeo* geo, uintptr_t bias = 0, bool relu = false) {
   if (!gemm_nt_supported(M, N, K))
     throw std::invalid_argument("gemm_nt: need N % 64 == 0 and K % 32 == 0 (M=" + std::to_string(M) +
                                 " N=" + std::to_string(N) + " K=" + std::to_string(K) + ")");
@@ -625,6 +637,9 @@ static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t
   if (cin) check_ptr(cin, "Cin");
   if (cmask && (!cin || ldc != N)) throw std::invalid_argument("gemm_nt: cmask needs cin with ldc == N");
   const auto* cm = reinterpret_cast<const uint8_t*>(cmask);
+  if (bias) check_ptr(bias, "bias");
+  const auto* bs = reinterpret_cast<const float*>(bias);
+  const int rl = relu ? 1 : 0;
   const ConvGeo g = geo ? *geo : ConvGeo{};
   constexpr int BM = 128;
   const int64_t mtn = (M + BM - 1) / BM;
@@ -633,7 +648,7 @@ static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t
   // (kernel templates are named at a non-template call site so their host stubs are emitted)
 #define MPIT_NT_LAUNCH1(BN, ST, STATS, CONV)                                                                   \
   hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, ST, STATS, CONV>), dim3(unsigned(nb)), dim3(256), shm, s, a, lda, b, \
-                     ldb, c, ldc, M, N, K, ntn, st, ci, cm, g)
+                     ldb, c, ldc, M, N, K, ntn, st, ci, cm, bs, rl, g)
 #define MPIT_NT_LAUNCH(BN, ST)                                                   \
   do {                                                                           \
     const int ntn = N / BN;                                                      \
@@ -774,13 +789,13 @@ static ConvGeo conv_geo(int H, int W, int C, int R, int S, int stride, int pad, 
 bool conv_supported(int C, int Co) { return C % 32 == 0 && Co % 64 == 0; }
 
 void conv_fwd(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad,
-              uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t cin) {
+              uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t cin, uintptr_t bias, bool relu) {
   if (!conv_supported(C, Co)) throw std::invalid_argument("conv_fwd: need C % 32 == 0 and Co % 64 == 0");
   if (int64_t(Nb) * H * W * C >= (int64_t(1) << 31)) throw std::invalid_argument("conv_fwd: input too large");
   int Ho, Wo;
   const ConvGeo g = conv_geo(H, W, C, R, S, stride, pad, &Ho, &Wo);
   const int64_t M = int64_t(Nb) * Ho * Wo;
-  launch_nt(dev, s, M, Co, R * S * C, x, C, w, int64_t(R) * S * C, y, Co, stats, cin, 0, &g);
+  launch_nt(dev, s, M, Co, R * S * C, x, C, w, int64_t(R) * S * C, y, Co, stats, cin, 0, &g, bias, relu);
 }
 
 int64_t conv_wgrad_ws_floats(int dev, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad) {

@@ -101,8 +101,15 @@ void cast_transpose(int dev, hipStream_t s, uintptr_t w, int R, int Cc, uintptr_
 // Backward-data of a stride-1 conv = conv_fwd(dy, wt, pad' = R-1-pad) with wt the
 // tap-flipped transpose [C,R,S,Co] (cast_transpose taps = R*S).
 bool conv_supported(int C, int Co);
+// bias (fp32 [Co], optional) and ReLU are applied in the epilogue.
 void conv_fwd(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad,
-              uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t cin);
+              uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t cin, uintptr_t bias = 0,
+              bool relu = false);
+// ReLU + bias backward: dz = dy * (y > 0) (bf16 [M, C]), db[c] = sum_m dz (fp32, optional,
+// deterministic); ws: relu_bias_bwd_ws_floats(C)
+int64_t relu_bias_bwd_ws_floats(int C);
+void relu_bias_bwd(int dev, hipStream_t s, int64_t M, int C, uintptr_t dy, uintptr_t y, uintptr_t dz, uintptr_t db,
+                   uintptr_t ws);
 // dw [Co,R,S,C] (fp32) = beta*dw + dY^T . im2col(x)   (C % 64 == 0, Co % 64 == 0)
 int64_t conv_wgrad_ws_floats(int dev, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad);
 void conv_wgrad(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad,

@@ -12,6 +12,8 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
+from ..ops.conv import ConvAct2d
+from ..ops.pool import MaxPool2dNHWC
 from . import register
 
 
@@ -49,14 +51,18 @@ class LeNet(nn.Module):
 
 
 class AlexNet(nn.Module):
+    """conv(+bias)+ReLU layers are :class:`ConvAct2d` (MFMA implicit GEMM with the bias and
+    ReLU in the epilogue on MI355X; the 3-channel 11x11 stem stays on MIOpen) and the pools
+    NHWC max-pool kernels."""
+
     def __init__(self, num_classes: int = 1000, dropout: float = 0.5):
         super().__init__()
         self.features = nn.Sequential(
-            nn.Conv2d(3, 64, 11, stride=4, padding=2), nn.ReLU(inplace=True), nn.MaxPool2d(3, 2),
-            nn.Conv2d(64, 192, 5, padding=2), nn.ReLU(inplace=True), nn.MaxPool2d(3, 2),
-            nn.Conv2d(192, 384, 3, padding=1), nn.ReLU(inplace=True),
-            nn.Conv2d(384, 256, 3, padding=1), nn.ReLU(inplace=True),
-            nn.Conv2d(256, 256, 3, padding=1), nn.ReLU(inplace=True), nn.MaxPool2d(3, 2),
+            ConvAct2d(3, 64, 11, stride=4, padding=2), MaxPool2dNHWC(3, 2),
+            ConvAct2d(64, 192, 5, padding=2), MaxPool2dNHWC(3, 2),
+            ConvAct2d(192, 384, 3, padding=1),
+            ConvAct2d(384, 256, 3, padding=1),
+            ConvAct2d(256, 256, 3, padding=1), MaxPool2dNHWC(3, 2),
         )
         self.avgpool = nn.AdaptiveAvgPool2d((6, 6))
         self.classifier = nn.Sequential(
@@ -72,17 +78,20 @@ _VGG16 = [64, 64, "M", 128, 128, "M", 256, 256, 256, "M", 512, 512, 512, "M", 51
 
 
 class VGG(nn.Module):
+    """Without batch norm every conv(+bias)+ReLU is one :class:`ConvAct2d` (bias and ReLU in
+    the MFMA GEMM epilogue on MI355X) and the pools are NHWC max-pool kernels."""
+
     def __init__(self, cfg=_VGG16, num_classes: int = 1000, dropout: float = 0.5, batch_norm: bool = False):
         super().__init__()
         layers, c = [], 3
         for v in cfg:
             if v == "M":
-                layers.append(nn.MaxPool2d(2, 2))
+                layers.append(MaxPool2dNHWC(2, 2))
+            elif batch_norm:
+                layers += [nn.Conv2d(c, v, 3, padding=1), nn.BatchNorm2d(v), nn.ReLU(inplace=True)]
+                c = v
             else:
-                layers.append(nn.Conv2d(c, v, 3, padding=1))
-                if batch_norm:
-                    layers.append(nn.BatchNorm2d(v))
-                layers.append(nn.ReLU(inplace=True))
+                layers.append(ConvAct2d(c, v, 3, padding=1))
                 c = v
         self.features = nn.Sequential(*layers)
         self.avgpool = nn.AdaptiveAvgPool2d((7, 7))

@@ -257,54 +257,81 @@ def conv_weights(weight: torch.Tensor, dgrad: bool):
     return wb, wt
 
 
+def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int):
+    """(dx, dw) of an NHWC implicit-GEMM conv from the gradient ``dz`` of its output."""
+    nb, c, h, w = x.shape
+    co, r, s, _ = wb.shape
+    ho, wo = dz.shape[2], dz.shape[3]
+    m = native()
+    dev, st = x.device.index, _stream(x)
+    dx = dw = None
+    if ctx.needs_input_grad[0]:
+        if stride == 1 and wt is not None:
+            # backward-data = forward conv of dz with the flipped, transposed weight
+            dx = torch.empty_like(x, memory_format=torch.channels_last)
+            m.conv_fwd(dev, st, nb, ho, wo, co, c, r, s, 1, r - 1 - pad, dz.data_ptr(), wt.data_ptr(), dx.data_ptr())
+        else:  # strided: MIOpen's NHWC backward-data
+            wv = wb.permute(0, 3, 1, 2)  # [Co, C, R, S] view with channels_last strides
+            dx = torch.ops.aten.convolution_backward(dz, x, wv, None, [stride, stride], [pad, pad], [1, 1], False,
+                                                     [0, 0], 1, [True, False, False])[0]
+    if ctx.needs_input_grad[1]:
+        dw = torch.empty((co, c, r, s), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
+        nws = m.conv_wgrad_ws_floats(dev, nb, h, w, c, co, r, s, stride, pad)
+        ws = torch.empty(nws, dtype=torch.float32, device=x.device) if nws else None
+        m.conv_wgrad(dev, st, nb, h, w, c, co, r, s, stride, pad, dz.data_ptr(), x.data_ptr(), dw.data_ptr(),
+                     ws.data_ptr() if ws is not None else 0, 0.0)
+    return dx, dw
+
+
+def _bf16_cl(t: torch.Tensor) -> torch.Tensor:
+    t = _cl(t)
+    return t if t.dtype == torch.bfloat16 else t.to(torch.bfloat16)
+
+
 class _ConvFn(torch.autograd.Function):
+    """conv (+ bias) (+ ReLU): the bias and the ReLU run in the GEMM epilogue; the backward
+    of the ReLU / bias is one pass over (dy, y) (csrc/kernels/act.hip)."""
+
     @staticmethod
-    def forward(ctx, x, weight, stride: int, pad: int):
-        x = _cl(x)
-        if x.dtype != torch.bfloat16:
-            x = x.to(torch.bfloat16)
+    def forward(ctx, x, weight, stride: int, pad: int, bias=None, relu: bool = False):
+        x = _bf16_cl(x)
         nb, c, h, w = x.shape
         co, _, r, s = weight.shape
         ho, wo = (h + 2 * pad - r) // stride + 1, (w + 2 * pad - s) // stride + 1
         need_dx = ctx.needs_input_grad[0]
         wb, wt = conv_weights(weight, dgrad=need_dx and stride == 1)
         y = torch.empty((nb, co, ho, wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+        b = None
+        if bias is not None:
+            b = bias if (bias.dtype == torch.float32 and bias.is_contiguous()) else bias.float().contiguous()
         native().conv_fwd(x.device.index, _stream(x), nb, h, w, c, co, r, s, stride, pad, x.data_ptr(), wb.data_ptr(),
-                          y.data_ptr(), 0, 0)
-        ctx.save_for_backward(x, wb, wt)
-        ctx.geo = (stride, pad)
+                          y.data_ptr(), bias=b.data_ptr() if b is not None else 0, relu=bool(relu))
+        ctx.save_for_backward(x, wb, wt, y if relu else None)
+        ctx.geo = (stride, pad, bias is not None, bool(relu))
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, wb, wt = ctx.saved_tensors
-        stride, pad = ctx.geo
-        dy = _cl(dy)
-        if dy.dtype != torch.bfloat16:
-            dy = dy.to(torch.bfloat16)
-        nb, c, h, w = x.shape
-        co, r, s, _ = wb.shape
-        ho, wo = dy.shape[2], dy.shape[3]
-        m = native()
-        dev, st = x.device.index, _stream(x)
-        dx = dw = None
-        if ctx.needs_input_grad[0]:
-            if stride == 1 and wt is not None:
-                # backward-data = forward conv of dy with the flipped, transposed weight
-                dx = torch.empty_like(x, memory_format=torch.channels_last)
-                m.conv_fwd(dev, st, nb, ho, wo, co, c, r, s, 1, r - 1 - pad, dy.data_ptr(), wt.data_ptr(),
-                           dx.data_ptr(), 0, 0)
-            else:  # strided: MIOpen's NHWC backward-data
-                wv = wb.permute(0, 3, 1, 2)  # [Co, C, R, S] view with channels_last strides
-                dx = torch.ops.aten.convolution_backward(dy, x, wv, None, [stride, stride], [pad, pad], [1, 1], False,
-                                                         [0, 0], 1, [True, False, False])[0]
-        if ctx.needs_input_grad[1]:
-            dw = torch.empty((co, c, r, s), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
-            nws = m.conv_wgrad_ws_floats(dev, nb, h, w, c, co, r, s, stride, pad)
-            ws = torch.empty(nws, dtype=torch.float32, device=x.device) if nws else None
-            m.conv_wgrad(dev, st, nb, h, w, c, co, r, s, stride, pad, dy.data_ptr(), x.data_ptr(), dw.data_ptr(),
-                         ws.data_ptr() if ws is not None else 0, 0.0)
-        return dx, dw, None, None
+        x, wb, wt, y = ctx.saved_tensors
+        stride, pad, has_bias, relu = ctx.geo
+        dy = _bf16_cl(dy)
+        db = None
+        if relu:
+            nb_, co, ho, wo = dy.shape
+            M = nb_ * ho * wo
+            dz = torch.empty_like(dy, memory_format=torch.channels_last)
+            m = native()
+            want_db = has_bias and ctx.needs_input_grad[4]
+            db = torch.empty(co, dtype=torch.float32, device=dy.device) if want_db else None
+            ws = torch.empty(m.relu_bias_bwd_ws_floats(co), dtype=torch.float32, device=dy.device) if want_db else None
+            m.relu_bias_bwd(dy.device.index, _stream(dy), M, co, dy.data_ptr(), y.data_ptr(), dz.data_ptr(),
+                            db.data_ptr() if db is not None else 0, ws.data_ptr() if ws is not None else 0)
+        else:
+            dz = dy
+            if has_bias and ctx.needs_input_grad[4]:
+                db = dy.float().sum(dim=(0, 2, 3))
+        dx, dw = _conv_backward(ctx, x, wb, wt, dz, stride, pad)
+        return dx, dw, None, None, db, None
 
 
 def conv_supported(x: torch.Tensor, weight: torch.Tensor) -> bool:
@@ -316,6 +343,26 @@ def conv_supported(x: torch.Tensor, weight: torch.Tensor) -> bool:
                                          and torch.get_autocast_dtype("cuda") == torch.bfloat16)
     co, ci = weight.shape[0], weight.shape[1]
     return bf16 and ci % 64 == 0 and co % 64 == 0 and x.shape[1] == ci
+
+
+class ConvAct2d(nn.Conv2d):
+    """``act(conv2d(x) + bias)`` with act = ReLU or identity (square kernel / stride /
+    padding, groups = dilation = 1): on the MFMA implicit-GEMM path the bias and the ReLU
+    are applied in the GEMM epilogue; otherwise ``nn.Conv2d`` followed by ``F.relu``."""
+
+    def __init__(self, in_channels: int, out_channels: int, kernel_size: int, stride: int = 1, padding: int = 0,
+                 bias: bool = True, act: bool = True):
+        super().__init__(in_channels, out_channels, kernel_size, stride=stride, padding=padding, bias=bias)
+        self.act = act
+
+    def fused(self, x: torch.Tensor) -> bool:
+        return conv_supported(x, self.weight)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.fused(x):
+            return _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0], self.bias, self.act)
+        y = super().forward(x)
+        return F.relu(y) if self.act else y
 
 
 class ConvNHWC(nn.Conv2d):
@@ -331,5 +378,5 @@ class ConvNHWC(nn.Conv2d):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.fused(x):
-            return _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0])
+            return _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0], None, False)
         return super().forward(x)

@@ -154,3 +154,40 @@ def test_park_grad_slot_protocol():
     x2 = torch.randn(3, 4, requires_grad=True)
     (C.park_grad(x2, slot2) * 3).sum().backward()
     assert torch.equal(x2.grad, torch.full((3, 4), 3.0))
+
+
+@gpu
+@pytest.mark.parametrize("n,ci,co,hw,k,relu", [(2, 64, 192, 13, 5, True), (3, 192, 384, 13, 3, True),
+                                               (2, 128, 64, 9, 3, False)])
+def test_conv_act_bias_relu(n, ci, co, hw, k, relu):
+    """conv + bias + ReLU with the bias / ReLU in the GEMM epilogue and the one-pass
+    ReLU/bias backward, against fp32 PyTorch; ReLU mask flips of near-zero outputs under
+    bf16 make the gradient error data dependent, so it is held to the error of the same
+    layer on the bf16 library path (MIOpen under autocast)."""
+    torch.manual_seed(ci + co)
+    pad = k // 2
+    mod = C.ConvAct2d(ci, co, k, padding=pad, act=relu).cuda().to(memory_format=torch.channels_last)
+    mod.bias.data.uniform_(-0.5, 0.5)
+    x = torch.randn(n, ci, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    g = torch.randn(n, co, hw, hw, device="cuda")
+
+    def ref(xx, dtype):
+        xx = xx.clone().to(dtype).requires_grad_(True)
+        ww = mod.weight.detach().clone().requires_grad_(True)
+        bb = mod.bias.detach().clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=dtype == torch.bfloat16):
+            y = F.conv2d(xx, ww, bb, padding=pad)
+            y = F.relu(y) if relu else y
+        y.backward(g.to(y.dtype))
+        return y, xx.grad, ww.grad, bb.grad
+
+    x1 = x.clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y1 = mod(x1)
+    y1.backward(g.to(torch.bfloat16))
+    got = (y1, x1.grad, mod.weight.grad, mod.bias.grad)
+    lib = ref(x, torch.bfloat16)
+    exact = ref(x, torch.float32)
+    for name, a, b, e in zip(("y", "dx", "dw", "db"), got, lib, exact):
+        err, floor = _rel(a, e), _rel(b, e)
+        assert err < 1.5 * floor + 5e-3, (name, err, floor)

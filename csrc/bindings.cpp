@@ -118,6 +118,15 @@ PYBIND11_MODULE(_mpit, m) {
       py::arg("dev"), py::arg("stream"), py::arg("Nb"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("Co"),
       py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("x"), py::arg("w"), py::arg("y"),
       py::arg("stats") = 0, py::arg("cin") = 0, py::arg("bias") = 0, py::arg("relu") = false);
+  m.def("conv_dgrad_strided_wfloats", &conv_dgrad_strided_wfloats);
+  m.def("conv_dgrad_strided_weights", [](int dev, uintptr_t s, uintptr_t w, int Co, int C, int R, int S_, int stride,
+                                         int pad, uintptr_t wb, uintptr_t wcls) {
+    conv_dgrad_strided_weights(dev, S(s), w, Co, C, R, S_, stride, pad, wb, wcls);
+  });
+  m.def("conv_dgrad_strided", [](int dev, uintptr_t s, int Nb, int H, int W, int C, int Co, int R, int S_, int stride,
+                                 int pad, uintptr_t dy, uintptr_t wcls, uintptr_t dx) {
+    conv_dgrad_strided(dev, S(s), Nb, H, W, C, Co, R, S_, stride, pad, dy, wcls, dx);
+  });
   m.def("relu_bias_bwd_ws_floats", &relu_bias_bwd_ws_floats);
   m.def("relu_bias_bwd", [](int dev, uintptr_t s, int64_t M, int C, uintptr_t dy, uintptr_t y, uintptr_t dz, uintptr_t db,
                             uintptr_t ws) { relu_bias_bwd(dev, S(s), M, C, dy, y, dz, db, ws); });

@@ -58,9 +58,13 @@ constexpr int kBK = 32;  // k-depth of one staged tile (gemm_nt): 64-B LDS rows
 // NHWC convolution geometry for the implicit-GEMM (CONV) kernel variants
 struct ConvGeo {
   int H, W, C;     // input image
-  int Ho, Wo;      // output image
+  int Ho, Wo;      // output (GEMM row) grid
   int S;           // kernel width (taps are r*S + s)
-  int stride, pad;
+  int stride, pad, padw;
+  // output row mapping (gemm_nt epilogue): ostr > 1 writes grid pixel (i, j) to pixel
+  // (i*ostr + oph, j*ostr + opw) of an OH x OW image (one parity class of a strided conv's
+  // backward-data); ozero also writes zeros to the other three parities (stride 2 only)
+  int ostr, oph, opw, OH, OW, ozero;
 };
 
 // source line for padding taps: LDS DMA of zeros
@@ -152,7 +156,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const uint16_t* __restr
       const int64_t n = gm / hw;
       const int rem = int(gm - n * hw), ho = rem / geo.Wo, wo = rem - ho * geo.Wo;
       hi0[i] = ho * geo.stride - geo.pad;
-      wi0[i] = wo * geo.stride - geo.pad;
+      wi0[i] = wo * geo.stride - geo.padw;
       img[i] = int(n) * geo.H;
       ca[i] = c * 8;
     } else {
@@ -251,6 +255,15 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const uint16_t* __restr
   for (int i = 0; i < TM; ++i) {
     const int64_t m = m0 + wm * WM + i * 32 + fr;
     const bool ok = m < M;
+    int64_t orow = m;  // output row (pixel) of GEMM row m
+    if constexpr (CONV) {
+      if (geo.ostr > 1) {
+        const int hw = geo.Ho * geo.Wo;
+        const int64_t nimg = m / hw;
+        const int rem = int(m - nimg * hw), gi = rem / geo.Wo, gj = rem - gi * geo.Wo;
+        orow = (nimg * geo.OH + gi * geo.ostr + geo.oph) * geo.OW + gj * geo.ostr + geo.opw;
+      }
+    }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       uint32_t pk[4][2];
@@ -301,7 +314,19 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const uint16_t* __restr
         const auto r1 = __builtin_amdgcn_permlane32_swap(pk[gp][1], pk[gp + 1][1], false, false);
         if (ok) {
           const int n = n0 + wn * WN + j * 32 + 8 * gp + 8 * fh;
-          *reinterpret_cast<uint4*>(C + m * ldc + n) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+          *reinterpret_cast<uint4*>(C + orow * ldc + n) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+          if constexpr (CONV) {
+            if (geo.ozero) {  // class (0,0) of a stride-2 conv whose other parities have no taps
+              const int64_t pix = orow % (int64_t(geo.OH) * geo.OW);
+              const int oh = int(pix / geo.OW), ow = int(pix % geo.OW);
+              const uint4 z = make_uint4(0, 0, 0, 0);
+              if (ow + 1 < geo.OW) *reinterpret_cast<uint4*>(C + (orow + 1) * ldc + n) = z;
+              if (oh + 1 < geo.OH) {
+                *reinterpret_cast<uint4*>(C + (orow + geo.OW) * ldc + n) = z;
+                if (ow + 1 < geo.OW) *reinterpret_cast<uint4*>(C + (orow + geo.OW + 1) * ldc + n) = z;
+              }
+            }
+          }
         }
       }
     }
@@ -450,7 +475,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const uint16_t* __restr
 #pragma unroll
     for (int i = 0; i < IX; ++i) {
       if constexpr (CONV) {
-        const int hi = pho[i] * geo.stride - geo.pad + xr, wi = pwo[i] * geo.stride - geo.pad + xs;
+        const int hi = pho[i] * geo.stride - geo.pad + xr, wi = pwo[i] * geo.stride - geo.padw + xs;
         const bool ok = rs + rx[i] < nrows && unsigned(hi) < unsigned(geo.H) && unsigned(wi) < unsigned(geo.W);
         const int off = ((pn[i] * geo.H + hi) * geo.W + wi) * geo.C + xc + ox[i];  // < 2^31 (host-checked)
         glds16_asm(ok ? X + off : g_zero_line + (ox[i] & 63), Xs + (w * IX + i) * RX * TBK);
@@ -571,11 +596,20 @@ __global__ __launch_bounds__(256) void split_reduce_kernel(const float4* __restr
   out[i] = a;
 }
 
-// fp32 w[R][T][Cc] -> bf16 copy wb[R][T][Cc] and bf16 tap-flipped transpose
-// wt[Cc][T-1-t][R] (T = 1: the plain transpose; T = taps of a conv: the dgrad weight).
+// fp32 w[R][T][Cc] -> bf16 copy wb[R][T][Cc] and a bf16 transpose wt with the taps
+// rearranged by `map`: tap t goes to wt[base[t] + (c*tc[t] + dt[t])*R + r]. The default
+// map (base 0, tc T, dt T-1-t) is the tap-flipped transpose [Cc][T][R] of a stride-1
+// backward-data; the parity classes of a strided one get one block each.
 // Tap t = blockIdx.z.
+constexpr int kMaxTaps = 49;
+struct TapMap {
+  int64_t base[kMaxTaps];
+  int16_t tc[kMaxTaps], dt[kMaxTaps];
+};
+
 __global__ __launch_bounds__(256) void cast_transpose_kernel(const float* __restrict__ w, int R, int Cc, int T,
-                                                             uint16_t* __restrict__ wb, uint16_t* __restrict__ wt) {
+                                                             uint16_t* __restrict__ wb, uint16_t* __restrict__ wt,
+                                                             TapMap map) {
   __shared__ uint16_t tile[32][33];
   const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32, tap = blockIdx.z;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 8 rows per pass
@@ -590,9 +624,11 @@ __global__ __launch_bounds__(256) void cast_transpose_kernel(const float* __rest
   }
   __syncthreads();
   if (!wt) return;
+  const int64_t base = map.base[tap];
+  const int tc = map.tc[tap], dt = map.dt[tap];
   for (int y = ty; y < 32; y += 8) {
     const int c = c0 + y, r = r0 + tx;
-    if (r < R && c < Cc) wt[(int64_t(c) * T + (T - 1 - tap)) * R + r] = tile[tx][y];
+    if (r < R && c < Cc) wt[base + (int64_t(c) * tc + dt) * R + r] = tile[tx][y];
   }
 }
 
@@ -783,7 +819,7 @@ static ConvGeo conv_geo(int H, int W, int C, int R, int S, int stride, int pad, 
   *Ho = (H + 2 * pad - R) / stride + 1;
   *Wo = (W + 2 * pad - S) / stride + 1;
   if (*Ho <= 0 || *Wo <= 0) throw std::invalid_argument("conv: empty output");
-  return ConvGeo{H, W, C, *Ho, *Wo, S, stride, pad};
+  return ConvGeo{H, W, C, *Ho, *Wo, S, stride, pad, pad, 1, 0, 0, *Ho, *Wo, 0};
 }
 
 bool conv_supported(int C, int Co) { return C % 32 == 0 && Co % 64 == 0; }
@@ -819,13 +855,105 @@ void conv_wgrad(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int
   launch_tn(dev, s, M, Co, R * S * C, dy, Co, x, C, dw, ws, beta, &g);
 }
 
-void cast_transpose(int dev, hipStream_t s, uintptr_t w, int R, int Cc, uintptr_t wb, uintptr_t wt, int taps) {
-  if (taps < 1) throw std::invalid_argument("cast_transpose: taps >= 1");
+static void launch_cast(int dev, hipStream_t s, uintptr_t w, int R, int Cc, uintptr_t wb, uintptr_t wt, int taps,
+                        const TapMap& map) {
+  if (taps < 1 || taps > kMaxTaps) throw std::invalid_argument("cast_transpose: 1 <= taps <= 49");
   hip_check(hipSetDevice(dev), "hipSetDevice");
   const dim3 grid((Cc + 31) / 32, (R + 31) / 32, taps);
   hipLaunchKernelGGL(cast_transpose_kernel, grid, dim3(256), 0, s, reinterpret_cast<const float*>(w), R, Cc, taps,
-                     reinterpret_cast<uint16_t*>(wb), reinterpret_cast<uint16_t*>(wt));
+                     reinterpret_cast<uint16_t*>(wb), reinterpret_cast<uint16_t*>(wt), map);
   hip_check(hipGetLastError(), "cast_transpose launch");
+}
+
+void cast_transpose(int dev, hipStream_t s, uintptr_t w, int R, int Cc, uintptr_t wb, uintptr_t wt, int taps) {
+  TapMap map{};
+  for (int t = 0; t < taps && t < kMaxTaps; ++t) {
+    map.base[t] = 0;
+    map.tc[t] = int16_t(taps);
+    map.dt[t] = int16_t(taps - 1 - t);
+  }
+  launch_cast(dev, s, w, R, Cc, wb, wt, taps, map);
+}
+
+// ---- backward-data of a strided conv as stride^2 parity classes ----------------------
+// Output pixel h = st*i + ph receives taps r with (ph + pad - r) % st == 0 from dY row
+// i + q(r), q(r) = (ph + pad - r) / st. Class (ph, pw) is a stride-1 implicit GEMM over dY
+// with the kernel {r} x {s} ordered by ascending q (window start = min q -> padding -min q)
+// whose epilogue writes pixel (st*i + ph, st*j + pw).
+struct StridedPlan {
+  int ncls = 0;
+  struct Cls {
+    int ph, pw, nr, ns, padh, padw, Hc, Wc;
+    int64_t base;  // element offset of the class weight [C][nr][ns][Co] in the packed buffer
+  } cls[16];
+  int64_t wfloats = 0;  // total bf16 elements of the packed class weights
+  bool any_empty = false;
+  TapMap map{};
+};
+
+static StridedPlan strided_plan(int H, int W, int C, int Co, int R, int S, int st, int pad) {
+  StridedPlan P;
+  if (st < 2 || st > 4 || R * S > kMaxTaps) throw std::invalid_argument("conv_dgrad_strided: bad geometry");
+  for (int ph = 0; ph < st; ++ph)
+    for (int pw = 0; pw < st; ++pw) {
+      int rl[16], sl[16], nr = 0, ns = 0;
+      for (int r = R - 1; r >= 0; --r)  // descending r = ascending q
+        if (((ph + pad - r) % st + st) % st == 0) rl[nr++] = r;
+      for (int c = S - 1; c >= 0; --c)
+        if (((pw + pad - c) % st + st) % st == 0) sl[ns++] = c;
+      // a class with no pixels (tiny image) keeps its weights in the layout; it is skipped
+      // at launch
+      const int Hc = std::max(0, (H - ph + st - 1) / st), Wc = std::max(0, (W - pw + st - 1) / st);
+      if (nr == 0 || ns == 0) {
+        if (Hc > 0 && Wc > 0) P.any_empty = true;
+        continue;
+      }
+      auto q = [&](int p, int r) { return (p + pad - r) / st; };  // exact: divisible
+      StridedPlan::Cls& k = P.cls[P.ncls++];
+      k = {ph, pw, nr, ns, -q(ph, rl[0]), -q(pw, sl[0]), Hc, Wc, P.wfloats};
+      for (int a = 0; a < nr; ++a)
+        for (int b = 0; b < ns; ++b) {
+          const int t = rl[a] * S + sl[b];
+          P.map.base[t] = k.base;
+          P.map.tc[t] = int16_t(nr * ns);
+          P.map.dt[t] = int16_t(a * ns + b);
+        }
+      P.wfloats += int64_t(C) * nr * ns * Co;
+    }
+  return P;
+}
+
+int64_t conv_dgrad_strided_wfloats(int C, int Co, int R, int S, int stride, int pad) {
+  return strided_plan(2 * stride, 2 * stride, C, Co, R, S, stride, pad).wfloats;
+}
+
+void conv_dgrad_strided_weights(int dev, hipStream_t s, uintptr_t w, int Co, int C, int R, int S, int stride, int pad,
+                                uintptr_t wb, uintptr_t wcls) {
+  const StridedPlan P = strided_plan(2 * stride, 2 * stride, C, Co, R, S, stride, pad);
+  launch_cast(dev, s, w, Co, C, wb, wcls, R * S, P.map);
+}
+
+void conv_dgrad_strided(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad,
+                        uintptr_t dy, uintptr_t wcls, uintptr_t dx) {
+  if (C % 64 || Co % 32) throw std::invalid_argument("conv_dgrad_strided: need C % 64 == 0 and Co % 32 == 0");
+  int Ho, Wo;
+  conv_geo(H, W, C, R, S, stride, pad, &Ho, &Wo);
+  if (int64_t(Nb) * Ho * Wo * Co >= (int64_t(1) << 31)) throw std::invalid_argument("conv_dgrad_strided: too large");
+  const StridedPlan P = strided_plan(H, W, C, Co, R, S, stride, pad);
+  // the only class with taps is (0,0) of a stride-2 conv: its epilogue zero-fills the rest
+  const bool ozero = P.any_empty && stride == 2 && P.ncls == 1 && P.cls[0].ph == 0 && P.cls[0].pw == 0;
+  if (P.any_empty && !ozero) {
+    hip_check(hipSetDevice(dev), "hipSetDevice");
+    hip_check(hipMemsetAsync(reinterpret_cast<void*>(dx), 0, size_t(Nb) * H * W * C * 2, s), "dgrad zero fill");
+  }
+  for (int k = 0; k < P.ncls; ++k) {
+    const auto& c = P.cls[k];
+    if (c.Hc == 0 || c.Wc == 0) continue;
+    ConvGeo g{Ho, Wo, Co, c.Hc, c.Wc, c.ns, 1, c.padh, c.padw, stride, c.ph, c.pw, H, W, ozero ? 1 : 0};
+    const int64_t M = int64_t(Nb) * c.Hc * c.Wc;
+    const int K = c.nr * c.ns * Co;
+    launch_nt(dev, s, M, C, K, dy, Co, wcls + uintptr_t(c.base) * 2, K, dx, C, 0, 0, 0, &g);
+  }
 }
 
 }  // namespace mpit

@@ -107,6 +107,14 @@ void conv_fwd(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R
               bool relu = false);
 // ReLU + bias backward: dz = dy * (y > 0) (bf16 [M, C]), db[c] = sum_m dz (fp32, optional,
 // deterministic); ws: relu_bias_bwd_ws_floats(C)
+// Backward-data of a strided conv (stride 2..4) as stride^2 parity-class implicit GEMMs
+// over dy; wcls = packed class weights (conv_dgrad_strided_wfloats bf16 elements) made by
+// conv_dgrad_strided_weights from the fp32 master (also writes wb like cast_transpose).
+int64_t conv_dgrad_strided_wfloats(int C, int Co, int R, int S, int stride, int pad);
+void conv_dgrad_strided_weights(int dev, hipStream_t s, uintptr_t w, int Co, int C, int R, int S, int stride, int pad,
+                                uintptr_t wb, uintptr_t wcls);
+void conv_dgrad_strided(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad,
+                        uintptr_t dy, uintptr_t wcls, uintptr_t dx);
 int64_t relu_bias_bwd_ws_floats(int C);
 void relu_bias_bwd(int dev, hipStream_t s, int64_t M, int C, uintptr_t dy, uintptr_t y, uintptr_t dz, uintptr_t db,
                    uintptr_t ws);

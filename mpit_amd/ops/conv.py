@@ -270,7 +270,13 @@ def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int):
             # backward-data = forward conv of dz with the flipped, transposed weight
             dx = torch.empty_like(x, memory_format=torch.channels_last)
             m.conv_fwd(dev, st, nb, ho, wo, co, c, r, s, 1, r - 1 - pad, dz.data_ptr(), wt.data_ptr(), dx.data_ptr())
-        else:  # strided: MIOpen's NHWC backward-data
+        elif wt is not None:
+            # strided: stride^2 parity classes, each a stride-1 implicit GEMM over dz whose
+            # epilogue writes its pixels of dx (wt = the packed class weights)
+            dx = torch.empty_like(x, memory_format=torch.channels_last)
+            m.conv_dgrad_strided(dev, st, nb, h, w, c, co, r, s, stride, pad, dz.data_ptr(), wt.data_ptr(),
+                                 dx.data_ptr())
+        else:  # MIOpen's NHWC backward-data
             wv = wb.permute(0, 3, 1, 2)  # [Co, C, R, S] view with channels_last strides
             dx = torch.ops.aten.convolution_backward(dz, x, wv, None, [stride, stride], [pad, pad], [1, 1], False,
                                                      [0, 0], 1, [True, False, False])[0]
@@ -288,6 +294,22 @@ def _bf16_cl(t: torch.Tensor) -> torch.Tensor:
     return t if t.dtype == torch.bfloat16 else t.to(torch.bfloat16)
 
 
+def strided_dgrad_supported(c: int, co: int, stride: int) -> bool:
+    return 2 <= stride <= 4 and c % 64 == 0 and co % 32 == 0
+
+
+def strided_dgrad_weights(weight: torch.Tensor, stride: int, pad: int):
+    """(bf16 [Co][R][S][C], packed parity-class backward-data weights), one launch."""
+    co, c, r, s = weight.shape
+    w = _weight_nhwc(weight)
+    m = native()
+    wb = torch.empty((co, r, s, c), dtype=torch.bfloat16, device=w.device)
+    wc = torch.empty(m.conv_dgrad_strided_wfloats(c, co, r, s, stride, pad), dtype=torch.bfloat16, device=w.device)
+    m.conv_dgrad_strided_weights(w.device.index, _stream(w), w.data_ptr(), co, c, r, s, stride, pad, wb.data_ptr(),
+                                 wc.data_ptr())
+    return wb, wc
+
+
 class _ConvFn(torch.autograd.Function):
     """conv (+ bias) (+ ReLU): the bias and the ReLU run in the GEMM epilogue; the backward
     of the ReLU / bias is one pass over (dy, y) (csrc/kernels/act.hip)."""
@@ -299,7 +321,10 @@ class _ConvFn(torch.autograd.Function):
         co, _, r, s = weight.shape
         ho, wo = (h + 2 * pad - r) // stride + 1, (w + 2 * pad - s) // stride + 1
         need_dx = ctx.needs_input_grad[0]
-        wb, wt = conv_weights(weight, dgrad=need_dx and stride == 1)
+        if need_dx and stride > 1 and strided_dgrad_supported(c, co, stride):
+            wb, wt = strided_dgrad_weights(weight, stride, pad)
+        else:
+            wb, wt = conv_weights(weight, dgrad=need_dx and stride == 1)
         y = torch.empty((nb, co, ho, wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
         b = None
         if bias is not None:

@@ -116,7 +116,8 @@ def test_cast_transpose_taps():
 @gpu
 @pytest.mark.parametrize("n,ci,co,hw,k,stride", [(2, 64, 64, 56, 3, 1), (3, 128, 128, 28, 3, 2), (4, 256, 256, 14, 3, 1),
                                                  (2, 512, 512, 7, 3, 1), (2, 64, 128, 9, 3, 2), (2, 128, 64, 13, 5, 1),
-                                                 (5, 64, 192, 11, 3, 1)])
+                                                 (5, 64, 192, 11, 3, 1), (2, 256, 512, 14, 1, 2), (2, 128, 256, 15, 1, 2),
+                                                 (2, 64, 64, 11, 5, 2), (2, 64, 64, 12, 3, 3)])
 def test_conv_nhwc_fwd_bwd(n, ci, co, hw, k, stride):
     """Implicit-GEMM conv (fwd, dgrad, wgrad) against fp32 PyTorch conv2d."""
     torch.manual_seed(n * ci + co + k)

@@ -179,6 +179,77 @@ __global__ __launch_bounds__(kFinCh * kFinK) void bn_finalize_fwd_kernel(
   if (rvar) rvar[c] = (1.f - momentum) * rvar[c] + momentum * float(var * double(M) / double(M > 1 ? M - 1 : 1));
 }
 
+// Partials emitted by a GEMM epilogue (gemm.hip), one row pair per 128-row tile — up to
+// thousands of rows, too many for one finalize block per 64 channels. Level 1 folds
+// groups of tile rows in parallel (grid: channel blocks x groups) into the [groups][2][C]
+// layout the finalize kernels take:
+//   CHAN (forward statistics): tile k holds (mean_k, M2_k) of n_k = min(128, M - 128k)
+//        rows; out = sum n_k d_k, sum M2_k + n_k d_k^2 with d_k = mean_k - x[0][c] — the
+//        shifted sums bn_finalize_fwd_kernel expects (shift = row 0 of x), fp64 inside;
+//   plain (backward reductions): tile sums are added.
+constexpr int kTileRows = 128;
+constexpr int kTileLanes = 4;  // row lanes per channel (64 channels x 4 = 256 threads)
+template <typename T, bool CHAN>
+__global__ __launch_bounds__(64 * kTileLanes) void bn_tiles_reduce_kernel(const float* __restrict__ part, int nt,
+                                                                          int C, int64_t M, const T* __restrict__ x,
+                                                                          int rows_per_group,
+                                                                          float* __restrict__ out) {
+  __shared__ double sa[kTileLanes][64], sb[kTileLanes][64];
+  const int cl = threadIdx.x % 64, kl = threadIdx.x / 64;
+  const int c = blockIdx.x * 64 + cl, grp = blockIdx.y;
+  double a = 0, b = 0;
+  if (c < C) {
+    double k0 = 0;
+    if constexpr (CHAN) {
+      if constexpr (sizeof(T) == 2) k0 = bf2f(reinterpret_cast<const uint16_t*>(x)[c]);
+      else k0 = reinterpret_cast<const float*>(x)[c];
+    }
+    const int r0 = grp * rows_per_group, r1 = min(nt, r0 + rows_per_group);
+#pragma unroll 4
+    for (int k = r0 + kl; k < r1; k += kTileLanes) {
+      const float p0 = part[(size_t(k) * 2 + 0) * C + c], p1 = part[(size_t(k) * 2 + 1) * C + c];
+      if constexpr (CHAN) {
+        const double n = double(min<int64_t>(kTileRows, M - int64_t(k) * kTileRows));
+        const double d = double(p0) - k0;
+        a = fma(n, d, a);
+        b += double(p1) + n * d * d;
+      } else {
+        a += p0;
+        b += p1;
+      }
+    }
+  }
+  sa[kl][cl] = a;
+  sb[kl][cl] = b;
+  __syncthreads();
+  if (kl != 0 || c >= C) return;
+#pragma unroll
+  for (int k = 1; k < kTileLanes; ++k) {
+    a += sa[k][cl];
+    b += sb[k][cl];
+  }
+  out[(size_t(grp) * 2 + 0) * C + c] = float(a);
+  out[(size_t(grp) * 2 + 1) * C + c] = float(b);
+}
+
+// groups for level 1: >= 16 tile rows each, at most kMaxStatBlocks (the finalize input)
+int tile_groups(int64_t nt, int* rows_per_group) {
+  int g = int(std::min<int64_t>(256, std::max<int64_t>(1, (nt + 15) / 16)));
+  *rows_per_group = int((nt + g - 1) / g);
+  g = int((nt + *rows_per_group - 1) / *rows_per_group);
+  return g;
+}
+
+template <typename T, bool CHAN>
+int launch_tiles_reduce(hipStream_t s, const float* part, int64_t nt, int C, int64_t M, const T* x, float* out) {
+  if (nt <= 0 || nt > INT32_MAX) throw std::invalid_argument("bn_act: bad partial count");
+  int rpg;
+  const int g = tile_groups(nt, &rpg);
+  hipLaunchKernelGGL((bn_tiles_reduce_kernel<T, CHAN>), dim3((C + 63) / 64, g), dim3(64 * kTileLanes), 0, s, part,
+                     int(nt), C, M, x, rpg, out);
+  return g;
+}
+
 // ---------------------------------------------------------------- forward: apply
 // MASK: also store the ReLU mask, one byte per vector (bit v = element v of the vector is
 // positive), so the backward never re-reads y (1/16 of its bytes for bf16).
@@ -387,12 +458,22 @@ void launch_apply(hipStream_t s, const T* x, const T* res, T* y, int64_t M, int 
 template <typename T>
 void fwd_impl(int dev, hipStream_t s, const T* x, const T* res, T* y, int64_t M, int C, const float* gamma,
               const float* beta, float* rmean, float* rvar, float* save_mean, float* save_rstd, float* ws,
-              float momentum, float eps, bool relu, uint8_t* mask) {
+              float momentum, float eps, bool relu, uint8_t* mask, const float* tstats, int64_t nstat) {
   constexpr int V = Vec<T>::N;
   check_shape(M, C, V, reinterpret_cast<uintptr_t>(x));
   const int G = C / V;
   const int blk = block_for(G);
   float* coef = ws;  // [2][C]
+  if (tstats) {  // statistics from the producing GEMM's epilogue: no pass over x
+    if (nstat != (M + kTileRows - 1) / kTileRows) throw std::invalid_argument("bn_act: stats tiles do not match M");
+    float* part = ws + 2 * C;
+    const int nb = launch_tiles_reduce<T, true>(s, tstats, nstat, C, M, x, part);
+    hipLaunchKernelGGL(bn_finalize_fwd_kernel<T>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinK), 0, s, part,
+                       nb, C, M, x, gamma, beta, eps, momentum, rmean, rvar, save_mean, save_rstd, coef);
+    launch_apply<T>(s, x, res, y, M, C, coef, relu, mask);
+    hip_check(hipGetLastError(), "bn_act forward launch");
+    return;
+  }
   const int R = blk / G;
   int64_t rpb;
   const int nb = stat_blocks(M, R, &rpb);
@@ -408,7 +489,7 @@ void fwd_impl(int dev, hipStream_t s, const T* x, const T* res, T* y, int64_t M,
 template <typename T>
 void bwd_impl(hipStream_t s, const T* dy, const uint8_t* mask, const T* x, T* dx, T* dres, int64_t M, int C,
               const float* gamma, const float* mean, const float* rstd, float* dgamma, float* dbeta, float* ws,
-              bool relu) {
+              bool relu, const float* gpart, int64_t npart) {
   constexpr int V = Vec<T>::N;
   check_shape(M, C, V, reinterpret_cast<uintptr_t>(x));
   if (relu && !mask) throw std::invalid_argument("bn_act backward: ReLU needs the forward mask");
@@ -420,12 +501,20 @@ void bwd_impl(hipStream_t s, const T* dy, const uint8_t* mask, const T* x, T* dx
   float* coef = ws;  // [3][C]
   float* part = ws + 3 * C;
   const size_t shm = size_t(R) * 2 * C * sizeof(float);
-  if (relu)
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true>), dim3(nb), dim3(blk), shm, s, dy, mask, x, mean, M, C, rpb, part);
-  else
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false>), dim3(nb), dim3(blk), shm, s, dy, mask, x, mean, M, C, rpb, part);
-  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinK), 0, s, part, nb, C, M,
-                     gamma, mean, rstd, dgamma, dbeta, coef);
+  if (gpart) {  // reductions already produced by the GEMM that wrote dy (gemm.hip EPI_BNRED)
+    const int ng = launch_tiles_reduce<T, false>(s, gpart, npart, C, M, x, part);
+    hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinK), 0, s, part, ng,
+                       C, M, gamma, mean, rstd, dgamma, dbeta, coef);
+  } else {
+    if (relu)
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true>), dim3(nb), dim3(blk), shm, s, dy, mask, x, mean, M, C, rpb,
+                         part);
+    else
+      hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false>), dim3(nb), dim3(blk), shm, s, dy, mask, x, mean, M, C, rpb,
+                         part);
+    hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinK), 0, s, part, nb,
+                       C, M, gamma, mean, rstd, dgamma, dbeta, coef);
+  }
   const int64_t nvec = M * G;
   const dim3 g(apply_grid(nvec, blk)), b(blk);
   if (relu) {
@@ -446,18 +535,19 @@ int64_t bn_mask_bytes(bool bf16, int64_t M, int C) { return M * (C / (bf16 ? 8 :
 
 void bn_act_fwd(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C,
                 uintptr_t gamma, uintptr_t beta, uintptr_t rmean, uintptr_t rvar, uintptr_t save_mean,
-                uintptr_t save_rstd, uintptr_t ws, float momentum, float eps, bool relu, uintptr_t mask) {
+                uintptr_t save_rstd, uintptr_t ws, float momentum, float eps, bool relu, uintptr_t mask,
+                uintptr_t stats, int64_t nstat) {
   hip_check(hipSetDevice(dev), "hipSetDevice");
   auto F = [](uintptr_t p) { return reinterpret_cast<float*>(p); };
   auto* mk = reinterpret_cast<uint8_t*>(mask);
   if (bf16)
     fwd_impl<uint16_t>(dev, s, reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(res),
                        reinterpret_cast<uint16_t*>(y), M, C, F(gamma), F(beta), F(rmean), F(rvar), F(save_mean),
-                       F(save_rstd), F(ws), momentum, eps, relu, mk);
+                       F(save_rstd), F(ws), momentum, eps, relu, mk, F(stats), nstat);
   else
     fwd_impl<float>(dev, s, reinterpret_cast<const float*>(x), reinterpret_cast<const float*>(res),
                     reinterpret_cast<float*>(y), M, C, F(gamma), F(beta), F(rmean), F(rvar), F(save_mean), F(save_rstd),
-                    F(ws), momentum, eps, relu, mk);
+                    F(ws), momentum, eps, relu, mk, F(stats), nstat);
 }
 
 void bn_act_apply(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C,
@@ -477,18 +567,18 @@ void bn_act_apply(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res,
 
 void bn_act_bwd(int dev, hipStream_t s, bool bf16, uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t dx,
                 uintptr_t dres, int64_t M, int C, uintptr_t gamma, uintptr_t mean, uintptr_t rstd, uintptr_t dgamma,
-                uintptr_t dbeta, uintptr_t ws, bool relu) {
+                uintptr_t dbeta, uintptr_t ws, bool relu, uintptr_t part, int64_t npart) {
   hip_check(hipSetDevice(dev), "hipSetDevice");
   auto F = [](uintptr_t p) { return reinterpret_cast<float*>(p); };
   const auto* mk = reinterpret_cast<const uint8_t*>(mask);
   if (bf16)
     bwd_impl<uint16_t>(s, reinterpret_cast<const uint16_t*>(dy), mk, reinterpret_cast<const uint16_t*>(x),
                        reinterpret_cast<uint16_t*>(dx), reinterpret_cast<uint16_t*>(dres), M, C, F(gamma), F(mean),
-                       F(rstd), F(dgamma), F(dbeta), F(ws), relu);
+                       F(rstd), F(dgamma), F(dbeta), F(ws), relu, F(part), npart);
   else
     bwd_impl<float>(s, reinterpret_cast<const float*>(dy), mk, reinterpret_cast<const float*>(x),
                     reinterpret_cast<float*>(dx), reinterpret_cast<float*>(dres), M, C, F(gamma), F(mean), F(rstd),
-                    F(dgamma), F(dbeta), F(ws), relu);
+                    F(dgamma), F(dbeta), F(ws), relu, F(part), npart);
 }
 
 }  // namespace mpit

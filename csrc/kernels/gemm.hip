@@ -67,6 +67,17 @@ struct ConvGeo {
   int ostr, oph, opw, OH, OW, ozero;
 };
 
+enum { EPI_NONE = 0, EPI_STATS = 1, EPI_BNRED = 2 };
+
+// column-reduction epilogue operands (see gemm_nt_kernel)
+struct EpiArgs {
+  float* part;                 // [row0 + tiles][2][N] fp32 partials
+  const uint16_t* x;           // EPI_BNRED: the BN's input, laid out like C (ldc == N)
+  const uint8_t* mask;         // EPI_BNRED: the BN's ReLU bit mask (1 byte / 8 channels) or null
+  const float* mean;           // EPI_BNRED: the BN's batch mean [N]
+  int64_t row0;                // first partial row of this launch
+};
+
 // source line for padding taps: LDS DMA of zeros
 __device__ __attribute__((aligned(256))) uint16_t g_zero_line[128] = {};
 
@@ -113,19 +124,28 @@ __device__ __forceinline__ int xcd_tile(int bid, int nb) {
 }
 
 // ------------------------------------------------------------------------------ NT GEMM
-// EPI bit 0: accumulate per-column sum / sum of squares of the (bf16-rounded) output
-// into stats[blockRow][2][N] (fp32 partials, one row per M-tile; reduced by the caller).
+// Column-reduction epilogues (EPI), one fp32 partial row pair per 128-row M-tile written to
+// ep.part[ep.row0 + mt][2][N] (deterministic, no atomics; reduced by the consumer):
+//   EPI_STATS  forward batch-norm statistics of the output: (mean, M2) of the tile's rows
+//              per column (Chan form: each 64-row half is summed shifted by its own first
+//              row, the halves are merged exactly), so no E[y^2]-E[y]^2 cancellation;
+//   EPI_BNRED  backward batch-norm reduction for the BN whose OUTPUT gradient this GEMM
+//              produces (a convolution's backward-data): dz = round(C) * relu_mask,
+//              (sum dz, sum dz*(x - mean)) per column with x the BN's input — the separate
+//              reduction pass over (dz, x) of the BN backward disappears.
+// Per element the reductions cost 3-5 VALU ops on values already in registers; the
+// per-column sums over the 32 rows a wave holds use one transposing butterfly.
 //
 // Staging: global_load_lds (16-B LDS DMA, no VGPRs) into a ring of STAGES buffers with
 // STAGES-1 k-tiles in flight; a counted s_waitcnt vmcnt + raw s_barrier retires exactly
 // the tile about to be used (a __syncthreads() would drain the whole ring). The LDS image
 // is lane-linear per wave instruction (16 rows x 64 B); the swizzle is applied on the
 // global source address.
-template <int BM, int BN, int STAGES, bool STATS, bool CONV>
+template <int BM, int BN, int STAGES, int EPI, bool CONV>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda,
                                                          const uint16_t* __restrict__ B, int64_t ldb,
                                                          uint16_t* C, int64_t ldc, int64_t M, int N, int K,
-                                                         int ntn, float* __restrict__ stats, const uint16_t* Cin,
+                                                         int ntn, EpiArgs ep, const uint16_t* Cin,
                                                          const uint8_t* __restrict__ Cmask,
                                                          const float* __restrict__ bias, int relu, ConvGeo geo) {
   constexpr int WM = BM / 2, WN = BN / 2;
@@ -206,11 +226,11 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const uint16_t* __restr
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
 
+  const int fr = lane & 31, fh = lane >> 5;
   const int nk = K / kBK;
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
     if (s < nk) issue(s, s);
-  const int fr = lane & 31, fh = lane >> 5;
   for (int kt = 0; kt < nk; ++kt) {
     // tiles issued after kt that may stay in flight
     const int after = min(nk, kt + STAGES - 1) - (kt + 1);
@@ -243,45 +263,21 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const uint16_t* __restr
     }
   }
 
-  // epilogue: lane holds D[n][m] with m = lane&31, n = (v&3) + 8*(v>>2) + 4*(lane>>5)
-  float s1[TN][16], s2[TN][16];
-  if constexpr (STATS) {
+  // ---- epilogue, phase A: accumulators (+ bias, ReLU) -> bf16 tile in LDS. Lane holds
+  // D[n][m] with m = lane&31, n = (v&3) + 8*(v>>2) + 4*(lane>>5): 4 consecutive columns of
+  // one row, one 8-B LDS store each.
+  constexpr int LDT = BN + 8;  // LDS row stride (elements): 16-B aligned rows
+  uint16_t* tl = smem;         // reuses the ring
+  __syncthreads();             // every wave is done reading the ring
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int v = 0; v < 16; ++v) s1[j][v] = s2[j][v] = 0.f;
-  }
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int64_t m = m0 + wm * WM + i * 32 + fr;
-    const bool ok = m < M;
-    int64_t orow = m;  // output row (pixel) of GEMM row m
-    if constexpr (CONV) {
-      if (geo.ostr > 1) {
-        const int hw = geo.Ho * geo.Wo;
-        const int64_t nimg = m / hw;
-        const int rem = int(m - nimg * hw), gi = rem / geo.Wo, gj = rem - gi * geo.Wo;
-        orow = (nimg * geo.OH + gi * geo.ostr + geo.oph) * geo.OW + gj * geo.ostr + geo.opw;
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      uint32_t pk[4][2];
-#pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int n = n0 + wn * WN + j * 32 + 8 * g + 4 * fh;
-        if (Cin != nullptr && ok) {  // C = A.B^T + Cin (Cin may alias C: same thread, read first)
-          const uint2 ci = *reinterpret_cast<const uint2*>(Cin + m * ldc + n);
-          // Cmask: Cin is a ReLU'd gradient given as (dy, forward bit mask: one byte per 8
-          // channels, bit v = channel 8k+v positive) — dy*mask is never materialised
-          const uint32_t mb = Cmask ? uint32_t(Cmask[(m * ldc + n) >> 3]) >> (n & 7) : 0xfu;
-          acc[i][j][4 * g + 0] += (mb & 1u) ? bf2f(uint16_t(ci.x & 0xffff)) : 0.f;
-          acc[i][j][4 * g + 1] += (mb & 2u) ? bf2f(uint16_t(ci.x >> 16)) : 0.f;
-          acc[i][j][4 * g + 2] += (mb & 4u) ? bf2f(uint16_t(ci.y & 0xffff)) : 0.f;
-          acc[i][j][4 * g + 3] += (mb & 8u) ? bf2f(uint16_t(ci.y >> 16)) : 0.f;
-        }
-        if (bias != nullptr) {  // conv bias (+ ReLU) fused into the epilogue (VGG / AlexNet)
-          const float4 b4 = *reinterpret_cast<const float4*>(bias + n);
+        const int nl = wn * WN + j * 32 + 8 * g + 4 * fh;
+        if (bias != nullptr) {  // conv bias (+ ReLU) (VGG / AlexNet)
+          const float4 b4 = *reinterpret_cast<const float4*>(bias + n0 + nl);
           acc[i][j][4 * g + 0] += b4.x;
           acc[i][j][4 * g + 1] += b4.y;
           acc[i][j][4 * g + 2] += b4.z;
@@ -291,85 +287,155 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const uint16_t* __restr
 #pragma unroll
           for (int e = 0; e < 4; ++e) acc[i][j][4 * g + e] = fmaxf(acc[i][j][4 * g + e], 0.f);
         }
-        uint16_t h[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          h[e] = f2bf(acc[i][j][4 * g + e]);
-          if constexpr (STATS) {
-            const float y = ok ? bf2f(h[e]) : 0.f;
-            s1[j][4 * g + e] += y;
-            s2[j][4 * g + e] = fmaf(y, y, s2[j][4 * g + e]);
-          }
-        }
-        pk[g][0] = uint32_t(h[0]) | (uint32_t(h[1]) << 16);
-        pk[g][1] = uint32_t(h[2]) | (uint32_t(h[3]) << 16);
+        const uint32_t lo = uint32_t(f2bf(acc[i][j][4 * g])) | (uint32_t(f2bf(acc[i][j][4 * g + 1])) << 16);
+        const uint32_t hi = uint32_t(f2bf(acc[i][j][4 * g + 2])) | (uint32_t(f2bf(acc[i][j][4 * g + 3])) << 16);
+        *reinterpret_cast<uint2*>(tl + (wm * WM + i * 32 + fr) * LDT + nl) = make_uint2(lo, hi);
       }
-      // T21: a row's 8 consecutive columns of group g are split over lanes r and r+32;
-      // v_permlane32_swap pairs groups (g, g+1) so each lane stores 16 contiguous bytes
-      // (lanes < 32: columns 8g..8g+7, lanes >= 32: 8g+8..8g+15) — half the store
-      // instructions of 8-byte stores, same addresses.
+  __syncthreads();
+
+  // ---- phase B: row-major. A thread owns one 16-B chunk (8 channels) of a row and walks
+  // the rows RPP apart, so every global access of a wave covers whole 256-B (BN = 128) row
+  // segments: the C store, the Cin / Cmask / BN x / BN mask loads.
+  constexpr int CPR = BN / 8, RPP = 256 / CPR, NP = BM / RPP;
+  const int ch = t % CPR, rr = t / CPR;
+  const int nc = n0 + ch * 8;  // first global column of this thread
+  float s1[8], s2[8], sf[8], mu[8];
+  int nv = 0;
 #pragma unroll
-      for (int gp = 0; gp < 4; gp += 2) {
-        const auto r0 = __builtin_amdgcn_permlane32_swap(pk[gp][0], pk[gp + 1][0], false, false);
-        const auto r1 = __builtin_amdgcn_permlane32_swap(pk[gp][1], pk[gp + 1][1], false, false);
-        if (ok) {
-          const int n = n0 + wn * WN + j * 32 + 8 * gp + 8 * fh;
-          *reinterpret_cast<uint4*>(C + orow * ldc + n) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
-          if constexpr (CONV) {
-            if (geo.ozero) {  // class (0,0) of a stride-2 conv whose other parities have no taps
-              const int64_t pix = orow % (int64_t(geo.OH) * geo.OW);
-              const int oh = int(pix / geo.OW), ow = int(pix % geo.OW);
-              const uint4 z = make_uint4(0, 0, 0, 0);
-              if (ow + 1 < geo.OW) *reinterpret_cast<uint4*>(C + (orow + 1) * ldc + n) = z;
-              if (oh + 1 < geo.OH) {
-                *reinterpret_cast<uint4*>(C + (orow + geo.OW) * ldc + n) = z;
-                if (ow + 1 < geo.OW) *reinterpret_cast<uint4*>(C + (orow + geo.OW + 1) * ldc + n) = z;
-              }
-            }
-          }
+  for (int e = 0; e < 8; ++e) s1[e] = s2[e] = sf[e] = mu[e] = 0.f;
+  if constexpr (EPI == EPI_BNRED) {
+    const float4 a0 = *reinterpret_cast<const float4*>(ep.mean + nc);
+    const float4 a1 = *reinterpret_cast<const float4*>(ep.mean + nc + 4);
+    mu[0] = a0.x; mu[1] = a0.y; mu[2] = a0.z; mu[3] = a0.w;
+    mu[4] = a1.x; mu[5] = a1.y; mu[6] = a1.z; mu[7] = a1.w;
+  }
+  // all loads of the thread's NP rows are issued before its first store (C may alias
+  // Cin, so the compiler would otherwise serialise load -> store per row)
+  int64_t orow[NP];
+  uint4 cv[NP], xq[NP];
+  uint32_t cmb[NP], xmb[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int64_t m = m0 + rr + p * RPP;
+    orow[p] = m;  // output row (pixel) of GEMM row m
+    if constexpr (CONV) {
+      if (geo.ostr > 1) {
+        const int hw = geo.Ho * geo.Wo;
+        const int64_t nimg = m / hw;
+        const int rem = int(m - nimg * hw), gi = rem / geo.Wo, gj = rem - gi * geo.Wo;
+        orow[p] = (nimg * geo.OH + gi * geo.ostr + geo.oph) * geo.OW + gj * geo.ostr + geo.opw;
+      }
+    }
+    const bool ok = m < M;
+    const int64_t o = orow[p] * ldc + nc;
+    if (Cin != nullptr) {
+      cv[p] = ok ? *reinterpret_cast<const uint4*>(Cin + o) : make_uint4(0, 0, 0, 0);
+      cmb[p] = Cmask ? (ok ? uint32_t(Cmask[o >> 3]) : 0u) : 0xffu;
+    }
+    if constexpr (EPI == EPI_BNRED) {
+      xq[p] = ok ? *reinterpret_cast<const uint4*>(ep.x + o) : make_uint4(0, 0, 0, 0);
+      xmb[p] = ok ? (ep.mask ? uint32_t(ep.mask[o >> 3]) : 0xffu) : 0u;
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int rl = rr + p * RPP;
+    if (m0 + rl >= M) continue;
+    const int64_t o = orow[p] * ldc + nc;
+    const uint4 hv = *reinterpret_cast<const uint4*>(tl + rl * LDT + ch * 8);
+    uint32_t hw4[4] = {hv.x, hv.y, hv.z, hv.w};
+    if (Cin != nullptr) {  // C = A.B^T + Cin
+      // Cmask: Cin is a ReLU'd gradient given as (dy, forward bit mask: one byte per 8
+      // channels, bit e = channel 8k+e positive) — dy*mask is never materialised
+      const uint32_t mb = cmb[p];
+      const uint32_t cw[4] = {cv[p].x, cv[p].y, cv[p].z, cv[p].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float v0 = bf2f(uint16_t(hw4[q] & 0xffff)) + ((mb >> (2 * q)) & 1u ? bf2f(uint16_t(cw[q] & 0xffff)) : 0.f);
+        const float v1 = bf2f(uint16_t(hw4[q] >> 16)) + ((mb >> (2 * q + 1)) & 1u ? bf2f(uint16_t(cw[q] >> 16)) : 0.f);
+        hw4[q] = uint32_t(f2bf(v0)) | (uint32_t(f2bf(v1)) << 16);
+      }
+    }
+    *reinterpret_cast<uint4*>(C + o) = make_uint4(hw4[0], hw4[1], hw4[2], hw4[3]);
+    if constexpr (CONV) {
+      if (geo.ozero) {  // class (0,0) of a stride-2 conv whose other parities have no taps
+        const int64_t pix = orow[p] % (int64_t(geo.OH) * geo.OW);
+        const int oh = int(pix / geo.OW), ow = int(pix % geo.OW);
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        if (ow + 1 < geo.OW) *reinterpret_cast<uint4*>(C + o + ldc) = z;
+        if (oh + 1 < geo.OH) {
+          *reinterpret_cast<uint4*>(C + o + int64_t(geo.OW) * ldc) = z;
+          if (ow + 1 < geo.OW) *reinterpret_cast<uint4*>(C + o + int64_t(geo.OW + 1) * ldc) = z;
         }
+      }
+    }
+    if constexpr (EPI == EPI_STATS) {  // shifted by this thread's first row
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float y = bf2f(uint16_t((e & 1) ? (hw4[e >> 1] >> 16) : (hw4[e >> 1] & 0xffff)));
+        if (nv == 0) sf[e] = y;
+        const float d = y - sf[e];
+        s1[e] += d;
+        s2[e] = fmaf(d, d, s2[e]);
+      }
+      ++nv;
+    } else if constexpr (EPI == EPI_BNRED) {  // dz = C * mask; (sum dz, sum dz (x - mean))
+      const uint32_t xb = xmb[p];
+      const uint32_t xw[4] = {xq[p].x, xq[p].y, xq[p].z, xq[p].w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint32_t hwd = hw4[e >> 1], xwd = xw[e >> 1];
+        const float dz = (xb >> e) & 1u ? bf2f(uint16_t((e & 1) ? (hwd >> 16) : (hwd & 0xffff))) : 0.f;
+        const float xe = bf2f(uint16_t((e & 1) ? (xwd >> 16) : (xwd & 0xffff)));
+        s1[e] += dz;
+        s2[e] = fmaf(dz, xe - mu[e], s2[e]);
       }
     }
   }
-  if constexpr (STATS) {
-    // Sum over the 32 lanes that share a column set (lane&31 = rows) by a transposing
-    // butterfly: at each lane bit the lane keeps half of its values and adds its
-    // partner's copy of that half (31 shuffles for 64 values instead of 5 per value).
-    // Afterwards lane r holds values [r*NV/32, (r+1)*NV/32) of the flattened
-    // [stat][j][v] array; the two row-halves of the block (wm) are combined in LDS.
-    constexpr int NV = 2 * TN * 16, NL = NV / 32;
-    float a[NV];
+  if constexpr (EPI != EPI_NONE) {
+    // combine the RPP threads of each chunk through LDS: [RPP][3][BN] floats
+    float* red = reinterpret_cast<float*>(smem);
+    __syncthreads();  // phase B is done reading the tile
+    if constexpr (EPI == EPI_STATS) {  // this thread's (n, mean, M2)
+      const float n = float(nv);
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        a[j * 16 + v] = s1[j][v];
-        a[TN * 16 + j * 16 + v] = s2[j][v];
+      for (int e = 0; e < 8; ++e) {
+        const float d = nv ? s1[e] / n : 0.f;
+        red[(rr * 3 + 0) * BN + ch * 8 + e] = n;
+        red[(rr * 3 + 1) * BN + ch * 8 + e] = nv ? sf[e] + d : 0.f;
+        red[(rr * 3 + 2) * BN + ch * 8 + e] = nv ? fmaxf(s2[e] - s1[e] * d, 0.f) : 0.f;
       }
+    } else {
 #pragma unroll
-    for (int b = 16, len = NV; b >= 1; b >>= 1, len >>= 1) {
-      const bool up = (fr & b) != 0;
-      const int half = len / 2;
-#pragma unroll
-      for (int q = 0; q < half; ++q) {
-        const float send = up ? a[q] : a[q + half];
-        const float keep = up ? a[q + half] : a[q];
-        a[q] = keep + __shfl_xor(send, b);
+      for (int e = 0; e < 8; ++e) {
+        red[(rr * 3 + 0) * BN + ch * 8 + e] = s1[e];
+        red[(rr * 3 + 1) * BN + ch * 8 + e] = s2[e];
       }
-    }
-    __syncthreads();  // the ring may still be read by other waves
-    float* red = reinterpret_cast<float*>(smem);  // [2 (wm)][2 (stat)][BN]
-#pragma unroll
-    for (int q = 0; q < NL; ++q) {
-      const int k = fr * NL + q;
-      const int st = k / (TN * 16), j = (k / 16) % TN, v = k % 16;
-      const int n = wn * WN + j * 32 + (v & 3) + 8 * (v >> 2) + 4 * fh;
-      red[(wm * 2 + st) * BN + n] = a[q];
     }
     __syncthreads();
+    float* prow = ep.part + (ep.row0 + mt) * 2 * int64_t(N) + n0;
     for (int n = t; n < BN; n += 256) {
-      stats[(int64_t(mt) * 2 + 0) * N + n0 + n] = red[0 * BN + n] + red[2 * BN + n];
-      stats[(int64_t(mt) * 2 + 1) * N + n0 + n] = red[1 * BN + n] + red[3 * BN + n];
+      if constexpr (EPI == EPI_STATS) {  // merge the RPP (n, mean, M2) triples (Chan et al.)
+        float na = 0.f, mean = 0.f, m2 = 0.f;
+        for (int k = 0; k < RPP; ++k) {
+          const float nb = red[(k * 3 + 0) * BN + n];
+          if (nb == 0.f) continue;
+          const float mb = red[(k * 3 + 1) * BN + n], tot = na + nb, d = mb - mean;
+          mean += d * (nb / tot);
+          m2 += red[(k * 3 + 2) * BN + n] + d * d * (na * nb / tot);
+          na = tot;
+        }
+        prow[n] = mean;
+        prow[N + n] = m2;
+      } else {
+        float a = 0.f, b = 0.f;
+        for (int k = 0; k < RPP; ++k) {
+          a += red[(k * 3 + 0) * BN + n];
+          b += red[(k * 3 + 1) * BN + n];
+        }
+        prow[n] = a;
+        prow[N + n] = b;
+      }
     }
   }
 }
@@ -651,11 +717,13 @@ int cu_count(int dev) {
 
 bool gemm_nt_supported(int64_t M, int N, int K) { return M > 0 && N > 0 && K > 0 && N % 64 == 0 && K % kBK == 0; }
 
-int64_t gemm_nt_stats_floats(int64_t M, int N) { return ((M + 127) / 128) * 2 * int64_t(N); }
+int64_t gemm_nt_stats_floats(int64_t M, int N) { return gemm_nt_tiles(M) * 2 * int64_t(N); }
+
+int64_t gemm_nt_tiles(int64_t M) { return (M + 127) / 128; }
 
 static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B,
-                      int64_t ldb, uintptr_t C, int64_t ldc, uintptr_t stats, uintptr_t cin, uintptr_t cmask,
-                      const ConvGeo* geo, uintptr_t bias = 0, bool relu = false) {
+                      int64_t ldb, uintptr_t C, int64_t ldc, uintptr_t cin, uintptr_t cmask, const ConvGeo* geo,
+                      const EpiArgs& ep, int epi, uintptr_t bias = 0, bool relu = false) {
   if (!gemm_nt_supported(M, N, K))
     throw std::invalid_argument("gemm_nt: need N % 64 == 0 and K % 32 == 0 (M=" + std::to_string(M) +
                                 " N=" + std::to_string(N) + " K=" + std::to_string(K) + ")");
@@ -664,11 +732,18 @@ static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t
   check_ptr(C, "C");
   if (lda % 8 || ldb % 8 || ldc % 8 || (!geo && lda < K) || ldb < K || ldc < N)
     throw std::invalid_argument("gemm_nt: bad leading dimensions");
+  if (epi != EPI_NONE) {
+    if (!ep.part) throw std::invalid_argument("gemm_nt: reduction epilogue needs a partials buffer");
+    if (epi == EPI_BNRED) {
+      if (!ep.x || !ep.mean || ldc != N) throw std::invalid_argument("gemm_nt: BN reduction needs x, mean, ldc == N");
+      check_ptr(reinterpret_cast<uintptr_t>(ep.x), "BN x");
+      check_ptr(reinterpret_cast<uintptr_t>(ep.mean), "BN mean");
+    }
+  }
   hip_check(hipSetDevice(dev), "hipSetDevice");
   const auto* a = reinterpret_cast<const uint16_t*>(A);
   const auto* b = reinterpret_cast<const uint16_t*>(B);
   auto* c = reinterpret_cast<uint16_t*>(C);
-  auto* st = reinterpret_cast<float*>(stats);
   const auto* ci = reinterpret_cast<const uint16_t*>(cin);
   if (cin) check_ptr(cin, "Cin");
   if (cmask && (!cin || ldc != N)) throw std::invalid_argument("gemm_nt: cmask needs cin with ldc == N");
@@ -682,22 +757,25 @@ static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t
   const int nk = K / kBK;
   const int stages = nk >= 4 ? 4 : (nk == 3 ? 3 : 2);
   // (kernel templates are named at a non-template call site so their host stubs are emitted)
-#define MPIT_NT_LAUNCH1(BN, ST, STATS, CONV)                                                                   \
-  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, ST, STATS, CONV>), dim3(unsigned(nb)), dim3(256), shm, s, a, lda, b, \
-                     ldb, c, ldc, M, N, K, ntn, st, ci, cm, bs, rl, g)
+#define MPIT_NT_LAUNCH1(BN, ST, EPI, CONV)                                                                   \
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, ST, EPI, CONV>), dim3(unsigned(nb)), dim3(256), shm, s, a, lda, b, \
+                     ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g)
+#define MPIT_NT_LAUNCH2(BN, ST, CONV)                                   \
+  do {                                                                  \
+    if (epi == EPI_STATS) MPIT_NT_LAUNCH1(BN, ST, EPI_STATS, CONV);     \
+    else if (epi == EPI_BNRED) MPIT_NT_LAUNCH1(BN, ST, EPI_BNRED, CONV); \
+    else MPIT_NT_LAUNCH1(BN, ST, EPI_NONE, CONV);                       \
+  } while (0)
 #define MPIT_NT_LAUNCH(BN, ST)                                                   \
   do {                                                                           \
     const int ntn = N / BN;                                                      \
     const int64_t nb = mtn * ntn;                                                \
     if (nb > INT32_MAX) throw std::invalid_argument("gemm_nt: too many tiles");  \
-    const size_t shm = size_t(ST) * (BM + BN) * kBK * sizeof(uint16_t);          \
-    if (geo) {                                                                   \
-      if (st) MPIT_NT_LAUNCH1(BN, ST, true, true);                               \
-      else MPIT_NT_LAUNCH1(BN, ST, false, true);                                 \
-    } else {                                                                     \
-      if (st) MPIT_NT_LAUNCH1(BN, ST, true, false);                              \
-      else MPIT_NT_LAUNCH1(BN, ST, false, false);                                \
-    }                                                                            \
+    /* LDS: the k-tile ring, reused by the epilogue's bf16 tile and reduction table */      \
+    const size_t shm = std::max({size_t(ST) * (BM + BN) * kBK * 2, size_t(BM) * (BN + 8) * 2,     \
+                                 size_t(256) * 8 * 3 * sizeof(float)});                          \
+    if (geo) MPIT_NT_LAUNCH2(BN, ST, true);                                      \
+    else MPIT_NT_LAUNCH2(BN, ST, false);                                         \
   } while (0)
   if (N % 128 == 0) {
     if (stages == 4) MPIT_NT_LAUNCH(128, 4);
@@ -709,13 +787,35 @@ static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t
     else MPIT_NT_LAUNCH(64, 2);
   }
 #undef MPIT_NT_LAUNCH
+#undef MPIT_NT_LAUNCH2
 #undef MPIT_NT_LAUNCH1
   hip_check(hipGetLastError(), "gemm_nt launch");
 }
 
+// the reduction epilogue selected by the (stats, BN reduction) operands
+static EpiArgs epi_args(uintptr_t stats, const BnRed* r, int* mode) {
+  EpiArgs ep{};
+  *mode = EPI_NONE;
+  if (stats && r && r->part) throw std::invalid_argument("gemm_nt: stats and BN reduction are exclusive");
+  if (stats) {
+    ep.part = reinterpret_cast<float*>(stats);
+    *mode = EPI_STATS;
+  } else if (r && r->part) {
+    ep.part = reinterpret_cast<float*>(r->part);
+    ep.x = reinterpret_cast<const uint16_t*>(r->x);
+    ep.mask = reinterpret_cast<const uint8_t*>(r->mask);
+    ep.mean = reinterpret_cast<const float*>(r->mean);
+    ep.row0 = r->row0;
+    *mode = EPI_BNRED;
+  }
+  return ep;
+}
+
 void gemm_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B, int64_t ldb,
-             uintptr_t C, int64_t ldc, uintptr_t stats, uintptr_t cin, uintptr_t cmask) {
-  launch_nt(dev, s, M, N, K, A, lda, B, ldb, C, ldc, stats, cin, cmask, nullptr);
+             uintptr_t C, int64_t ldc, uintptr_t stats, uintptr_t cin, uintptr_t cmask, const BnRed* red) {
+  int mode;
+  const EpiArgs ep = epi_args(stats, red, &mode);
+  launch_nt(dev, s, M, N, K, A, lda, B, ldb, C, ldc, cin, cmask, nullptr, ep, mode);
 }
 
 bool gemm_tn_supported(int64_t M, int N, int K) { return M > 0 && N % 64 == 0 && K % 64 == 0 && N > 0 && K > 0; }
@@ -825,13 +925,16 @@ static ConvGeo conv_geo(int H, int W, int C, int R, int S, int stride, int pad, 
 bool conv_supported(int C, int Co) { return C % 32 == 0 && Co % 64 == 0; }
 
 void conv_fwd(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad,
-              uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t cin, uintptr_t bias, bool relu) {
+              uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t cin, uintptr_t bias, bool relu,
+              const BnRed* red) {
   if (!conv_supported(C, Co)) throw std::invalid_argument("conv_fwd: need C % 32 == 0 and Co % 64 == 0");
   if (int64_t(Nb) * H * W * C >= (int64_t(1) << 31)) throw std::invalid_argument("conv_fwd: input too large");
   int Ho, Wo;
   const ConvGeo g = conv_geo(H, W, C, R, S, stride, pad, &Ho, &Wo);
   const int64_t M = int64_t(Nb) * Ho * Wo;
-  launch_nt(dev, s, M, Co, R * S * C, x, C, w, int64_t(R) * S * C, y, Co, stats, cin, 0, &g, bias, relu);
+  int mode;
+  const EpiArgs ep = epi_args(stats, red, &mode);
+  launch_nt(dev, s, M, Co, R * S * C, x, C, w, int64_t(R) * S * C, y, Co, cin, 0, &g, ep, mode, bias, relu);
 }
 
 int64_t conv_wgrad_ws_floats(int dev, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad) {
@@ -933,8 +1036,16 @@ void conv_dgrad_strided_weights(int dev, hipStream_t s, uintptr_t w, int Co, int
   launch_cast(dev, s, w, Co, C, wb, wcls, R * S, P.map);
 }
 
+int64_t conv_dgrad_strided_tiles(int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad) {
+  const StridedPlan P = strided_plan(H, W, C, Co, R, S, stride, pad);
+  int64_t t = 0;
+  for (int k = 0; k < P.ncls; ++k)
+    if (P.cls[k].Hc > 0 && P.cls[k].Wc > 0) t += gemm_nt_tiles(int64_t(Nb) * P.cls[k].Hc * P.cls[k].Wc);
+  return t;
+}
+
 void conv_dgrad_strided(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad,
-                        uintptr_t dy, uintptr_t wcls, uintptr_t dx) {
+                        uintptr_t dy, uintptr_t wcls, uintptr_t dx, const BnRed* red) {
   if (C % 64 || Co % 32) throw std::invalid_argument("conv_dgrad_strided: need C % 64 == 0 and Co % 32 == 0");
   int Ho, Wo;
   conv_geo(H, W, C, R, S, stride, pad, &Ho, &Wo);
@@ -946,13 +1057,20 @@ void conv_dgrad_strided(int dev, hipStream_t s, int Nb, int H, int W, int C, int
     hip_check(hipSetDevice(dev), "hipSetDevice");
     hip_check(hipMemsetAsync(reinterpret_cast<void*>(dx), 0, size_t(Nb) * H * W * C * 2, s), "dgrad zero fill");
   }
+  int64_t row0 = 0;
   for (int k = 0; k < P.ncls; ++k) {
     const auto& c = P.cls[k];
     if (c.Hc == 0 || c.Wc == 0) continue;
     ConvGeo g{Ho, Wo, Co, c.Hc, c.Wc, c.ns, 1, c.padh, c.padw, stride, c.ph, c.pw, H, W, ozero ? 1 : 0};
     const int64_t M = int64_t(Nb) * c.Hc * c.Wc;
     const int K = c.nr * c.ns * Co;
-    launch_nt(dev, s, M, C, K, dy, Co, wcls + uintptr_t(c.base) * 2, K, dx, C, 0, 0, 0, &g);
+    // BN reduction: each class writes its own run of partial rows (zero-filled pixels
+    // contribute nothing)
+    int mode;
+    EpiArgs ep = epi_args(0, red, &mode);
+    ep.row0 += row0;
+    row0 += gemm_nt_tiles(M);
+    launch_nt(dev, s, M, C, K, dy, Co, wcls + uintptr_t(c.base) * 2, K, dx, C, 0, 0, &g, ep, mode);
   }
 }
 

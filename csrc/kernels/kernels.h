@@ -68,25 +68,41 @@ void gather_scale(int dev, hipStream_t s, const std::vector<uintptr_t>& srcs, co
 // mask: ReLU bit mask written by the forward (bn_mask_bytes) and read by the backward.
 int64_t bn_workspace_floats(int C);
 int64_t bn_mask_bytes(bool bf16, int64_t M, int C);
+// stats / nstat (optional): the statistics of x as per-128-row-tile (mean, M2) partials
+// [nstat][2][C] emitted by the GEMM that produced x (EPI_STATS) — the statistics pass over
+// x is skipped.
 void bn_act_fwd(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C,
                 uintptr_t gamma, uintptr_t beta, uintptr_t rmean, uintptr_t rvar, uintptr_t save_mean,
-                uintptr_t save_rstd, uintptr_t ws, float momentum, float eps, bool relu, uintptr_t mask);
+                uintptr_t save_rstd, uintptr_t ws, float momentum, float eps, bool relu, uintptr_t mask,
+                uintptr_t stats = 0, int64_t nstat = 0);
 // y = act(x*coef[c] + coef[C+c] (+res))  — eval mode / precomputed coefficients
 void bn_act_apply(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C,
                   uintptr_t coef, bool relu);
+// part / npart (optional): (sum dz, sum dz*(x-mean)) partials [npart][2][C] already
+// produced by the GEMM that wrote dy (EPI_BNRED) — the reduction pass is skipped.
 void bn_act_bwd(int dev, hipStream_t s, bool bf16, uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t dx,
                 uintptr_t dres, int64_t M, int C, uintptr_t gamma, uintptr_t mean, uintptr_t rstd, uintptr_t dgamma,
-                uintptr_t dbeta, uintptr_t ws, bool relu);
+                uintptr_t dbeta, uintptr_t ws, bool relu, uintptr_t part = 0, int64_t npart = 0);
 
 // ---- MFMA GEMMs for NHWC 1x1 convolutions (gemm.hip), bf16 operands, fp32 accumulate --
-// C[M,N] (bf16) = A[M,K] . B[N,K]^T; optional per-column {sum, sumsq} partials of C per
+// C[M,N] (bf16) = A[M,K] . B[N,K]^T; optional per-column (mean, M2) partials of C per
 // 128-row tile into stats[ceil(M/128)][2][N] (gemm_nt_stats_floats); optional bf16 cin
 // [M, ldc] added to the product before rounding (may alias C); optional cmask (with cin,
 // ldc == N): the bn_act ReLU bit mask of cin (1 byte / 8 channels) — adds cin*mask.
+// Optional red: C is the output gradient of a bn_act layer (x, mask, mean its forward
+// input / ReLU mask / batch mean, [.., N] like C): the GEMM also writes that layer's
+// backward reduction partials (sum dz, sum dz*(x-mean)), dz = C*mask, one row pair per
+// 128-row tile at part[row0 + tile][2][N] — bn_act_bwd(part, npart) then skips its pass.
+struct BnRed {
+  uintptr_t part = 0, x = 0, mask = 0, mean = 0;
+  int64_t row0 = 0;
+};
 bool gemm_nt_supported(int64_t M, int N, int K);
+int64_t gemm_nt_tiles(int64_t M);
 int64_t gemm_nt_stats_floats(int64_t M, int N);
 void gemm_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B, int64_t ldb,
-             uintptr_t C, int64_t ldc, uintptr_t stats, uintptr_t cin, uintptr_t cmask = 0);
+             uintptr_t C, int64_t ldc, uintptr_t stats, uintptr_t cin, uintptr_t cmask = 0,
+             const BnRed* red = nullptr);
 // out[N,K] (fp32) = beta*out + Y[M,N]^T . X[M,K]  (split over M; ws: gemm_tn_ws_floats)
 bool gemm_tn_supported(int64_t M, int N, int K);
 int64_t gemm_tn_ws_floats(int dev, int64_t M, int N, int K);
@@ -104,7 +120,7 @@ bool conv_supported(int C, int Co);
 // bias (fp32 [Co], optional) and ReLU are applied in the epilogue.
 void conv_fwd(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad,
               uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t cin, uintptr_t bias = 0,
-              bool relu = false);
+              bool relu = false, const BnRed* red = nullptr);
 // ReLU + bias backward: dz = dy * (y > 0) (bf16 [M, C]), db[c] = sum_m dz (fp32, optional,
 // deterministic); ws: relu_bias_bwd_ws_floats(C)
 // Backward-data of a strided conv (stride 2..4) as stride^2 parity-class implicit GEMMs
@@ -113,8 +129,10 @@ void conv_fwd(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R
 int64_t conv_dgrad_strided_wfloats(int C, int Co, int R, int S, int stride, int pad);
 void conv_dgrad_strided_weights(int dev, hipStream_t s, uintptr_t w, int Co, int C, int R, int S, int stride, int pad,
                                 uintptr_t wb, uintptr_t wcls);
+// partial rows a BN reduction over the strided backward-data writes (all classes)
+int64_t conv_dgrad_strided_tiles(int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad);
 void conv_dgrad_strided(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad,
-                        uintptr_t dy, uintptr_t wcls, uintptr_t dx);
+                        uintptr_t dy, uintptr_t wcls, uintptr_t dx, const BnRed* red = nullptr);
 int64_t relu_bias_bwd_ws_floats(int C);
 void relu_bias_bwd(int dev, hipStream_t s, int64_t M, int C, uintptr_t dy, uintptr_t y, uintptr_t dz, uintptr_t db,
                    uintptr_t ws);

@@ -30,6 +30,17 @@ def _bn(c, act):
     return BatchNormAct2d(c, act=act) if FUSED_BN else nn.BatchNorm2d(c)
 
 
+def _feeds_bn(*convs):
+    """The MFMA convolutions whose outputs feed a fused BN emit its statistics from the
+    GEMM accumulators (ops/bn.py), so the BN forward is one pass. A ``(conv, BN)``
+    downsample Sequential may be passed as is."""
+    for c in convs:
+        if isinstance(c, nn.Sequential) and len(c) == 2 and isinstance(c[1], BatchNormAct2d):
+            c = c[0]
+        if FUSED_BN and hasattr(c, "emit_stats"):
+            c.emit_stats = True
+
+
 # 1x1 convolutions as MFMA GEMMs and 3x3 ones as MFMA implicit GEMMs (both fall back to
 # nn.Conv2d for CPU / odd shapes); MPIT_MFMA_CONV=0 routes them to MIOpen instead (A/B
 # measurements), MPIT_MFMA_CONV3=0 only the 3x3s.
@@ -61,6 +72,7 @@ class BasicBlock(nn.Module):
         self.conv2 = conv3x3(planes, planes)
         self.bn2 = _bn(planes, True)
         self.downsample = downsample
+        _feeds_bn(self.conv1, self.conv2, downsample)
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
@@ -85,6 +97,7 @@ class Bottleneck(nn.Module):
         self.bn3 = _bn(planes * 4, True)
         self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample
+        _feeds_bn(self.conv1, self.conv2, self.conv3, downsample)
 
     def forward(self, x):
         if isinstance(self.bn1, BatchNormAct2d):

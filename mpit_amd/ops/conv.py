@@ -40,9 +40,18 @@ def _cl(x: torch.Tensor) -> torch.Tensor:
     return x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
 
 
+def tile_stats_to_sums(part: torch.Tensor, M: int, N: int) -> torch.Tensor:
+    """Per-128-row-tile (mean, M2) partials ([tiles][2][N]) -> [2, N] (sum, sum of squares)."""
+    p = part.view(-1, 2, N).double()
+    n = (M - 128 * torch.arange(p.shape[0], device=p.device, dtype=torch.float64)).clamp(max=128)[:, None]
+    mean, m2 = p[:, 0], p[:, 1]
+    return torch.stack([(n * mean).sum(0), (m2 + n * mean * mean).sum(0)]).float()
+
+
 def gemm_nt(a: torch.Tensor, b: torch.Tensor, stats: bool = False):
     """``a[M,K] . b[N,K]^T`` in bf16 (fp32 accumulate). With ``stats`` also returns the
-    per-column ``[sum, sum of squares]`` of the bf16 result as a [2, N] fp32 tensor."""
+    per-column ``[sum, sum of squares]`` of the result as a [2, N] fp32 tensor (from the
+    epilogue's per-tile (mean, M2) partials)."""
     if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
         raise TypeError("gemm_nt takes bf16 operands")
     if a.dim() != 2 or b.dim() != 2 or a.shape[1] != b.shape[1] or a.stride(1) != 1 or b.stride(1) != 1:
@@ -55,7 +64,7 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, stats: bool = False):
     m.gemm_nt(a.device.index, _stream(a), M, N, K, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(),
               N, st.data_ptr() if st is not None else 0)
     if stats:
-        return c, st.view(-1, 2, N).sum(0)
+        return c, tile_stats_to_sums(st, M, N)
     return c
 
 
@@ -90,6 +99,32 @@ def cast_transpose(w: torch.Tensor):
     wt = torch.empty((C, R), dtype=torch.bfloat16, device=w.device)
     native().cast_transpose(w.device.index, _stream(w), w2.data_ptr(), R, C, wb.data_ptr(), wt.data_ptr())
     return wb, wt
+
+
+def _red_args(link, c: int, ntiles: int, device):
+    """(kernel keyword arguments, partials tensor) of a BN backward reduction folded into a
+    backward-data GEMM (see ops/bn.py BNLink)."""
+    part = torch.empty(ntiles * 2 * c, dtype=torch.float32, device=device)
+    return dict(red_part=part.data_ptr(), red_x=link.x.data_ptr(),
+                red_mask=link.mask.data_ptr() if link.mask is not None else 0,
+                red_mean=link.mean.data_ptr()), part
+
+
+def _link_of(x: torch.Tensor):
+    link = getattr(x, "_mpit_bnlink", None)
+    return link if (link is not None and link.ready(x)) else None
+
+
+def _tile_stats(co: int, M: int, device):
+    nt = native().gemm_nt_tiles(M)
+    return torch.empty(nt * 2 * co, dtype=torch.float32, device=device), nt
+
+
+def _attach_stats(y: torch.Tensor, hold: list) -> torch.Tensor:
+    if hold:
+        part, nt = hold[0]
+        y._mpit_tstats = (part, nt, y.data_ptr())
+    return y
 
 
 class GradSlot:
@@ -150,7 +185,7 @@ def park_grad(x: torch.Tensor, slot: GradSlot) -> torch.Tensor:
 
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, slot=None):
+    def forward(ctx, x, weight, slot=None, hold=None, link=None):
         x = _cl(x)
         if x.dtype != torch.bfloat16:
             x = x.to(torch.bfloat16)
@@ -160,10 +195,16 @@ class _Conv1x1Fn(torch.autograd.Function):
         wb, wt = cast_transpose(weight)
         y = torch.empty((n, co, h, w), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
         m = native()
-        m.gemm_nt(x.device.index, _stream(x), M, co, ci, x.data_ptr(), ci, wb.data_ptr(), ci, y.data_ptr(), co, 0)
+        st = None
+        if hold is not None:  # batch-norm statistics of y from the accumulators
+            st, nt = _tile_stats(co, M, x.device)
+            hold.append((st, nt))
+        m.gemm_nt(x.device.index, _stream(x), M, co, ci, x.data_ptr(), ci, wb.data_ptr(), ci, y.data_ptr(), co,
+                  st.data_ptr() if st is not None else 0)
         ctx.save_for_backward(x, wt)
         ctx.wshape = weight.shape
         ctx.slot = slot
+        ctx.link = link
         return y
 
     @staticmethod
@@ -180,25 +221,30 @@ class _Conv1x1Fn(torch.autograd.Function):
         dx = dw = None
         extra, emask = ctx.slot.take() if ctx.slot is not None else (None, None)
         if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x, memory_format=torch.channels_last)
+            kw, part = {}, None
+            if ctx.link is not None:  # the producing BN's backward reduction, in the epilogue
+                nt = m.gemm_nt_tiles(M)
+                kw, part = _red_args(ctx.link, ci, nt, x.device)
             if extra is not None:  # gradient parked by the block (GradSlot): added in the epilogue
                 extra = _cl(extra)
                 if extra.dtype != torch.bfloat16:
                     extra = extra.to(torch.bfloat16)
                 if extra.shape != x.shape:
                     raise RuntimeError("GradSlot gradient does not match the convolution input")
-                dx = torch.empty_like(x, memory_format=torch.channels_last)
                 m.gemm_nt(dev, s, M, ci, co, dy.data_ptr(), co, wt.data_ptr(), co, dx.data_ptr(), ci, 0,
-                          extra.data_ptr(), emask.data_ptr() if emask is not None else 0)
+                          extra.data_ptr(), emask.data_ptr() if emask is not None else 0, **kw)
             else:
-                dx = torch.empty_like(x, memory_format=torch.channels_last)
-                m.gemm_nt(dev, s, M, ci, co, dy.data_ptr(), co, wt.data_ptr(), co, dx.data_ptr(), ci, 0)
+                m.gemm_nt(dev, s, M, ci, co, dy.data_ptr(), co, wt.data_ptr(), co, dx.data_ptr(), ci, 0, **kw)
+            if part is not None:
+                ctx.link.publish(part, nt, dx)
         if ctx.needs_input_grad[1]:
             dw = torch.empty(ctx.wshape, dtype=torch.float32, device=x.device)
             nws = m.gemm_tn_ws_floats(dev, M, co, ci)
             ws = torch.empty(nws, dtype=torch.float32, device=x.device) if nws else None
             m.gemm_tn(dev, s, M, co, ci, dy.data_ptr(), co, x.data_ptr(), ci, dw.data_ptr(),
                       ws.data_ptr() if ws is not None else 0, 0.0)
-        return dx, dw, None
+        return dx, dw, None, None, None
 
 
 def conv1x1_supported(x: torch.Tensor, weight: torch.Tensor) -> bool:
@@ -215,7 +261,7 @@ def conv1x1_supported(x: torch.Tensor, weight: torch.Tensor) -> bool:
 def conv1x1(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     """Stride-1, unpadded, bias-free 1x1 convolution (MFMA GEMM path when supported)."""
     if conv1x1_supported(x, weight):
-        return _Conv1x1Fn.apply(x, weight)
+        return _Conv1x1Fn.apply(x, weight, None, None, None)
     return F.conv2d(x, weight)
 
 
@@ -225,6 +271,7 @@ class Conv1x1(nn.Conv2d):
 
     def __init__(self, in_channels: int, out_channels: int, stride: int = 1):
         super().__init__(in_channels, out_channels, 1, stride=stride, bias=False)
+        self.emit_stats = False  # output feeds a training BatchNormAct2d: emit its statistics
 
     def fused(self, x: torch.Tensor) -> bool:
         """True when ``forward(x)`` takes the MFMA path (and so honours a GradSlot)."""
@@ -232,7 +279,9 @@ class Conv1x1(nn.Conv2d):
 
     def forward(self, x: torch.Tensor, slot: "GradSlot" = None) -> torch.Tensor:
         if self.fused(x):
-            return _Conv1x1Fn.apply(x, self.weight, slot)
+            hold = [] if (self.emit_stats and self.training) else None
+            y = _Conv1x1Fn.apply(x, self.weight, slot, hold, _link_of(x) if torch.is_grad_enabled() else None)
+            return _attach_stats(y, hold)
         if slot is not None:
             raise RuntimeError("GradSlot needs the MFMA path (see Conv1x1.fused)")
         return super().forward(x)
@@ -257,8 +306,9 @@ def conv_weights(weight: torch.Tensor, dgrad: bool):
     return wb, wt
 
 
-def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int):
-    """(dx, dw) of an NHWC implicit-GEMM conv from the gradient ``dz`` of its output."""
+def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None):
+    """(dx, dw) of an NHWC implicit-GEMM conv from the gradient ``dz`` of its output; with a
+    BNLink the backward-data GEMM also produces the producing BN's backward reduction."""
     nb, c, h, w = x.shape
     co, r, s, _ = wb.shape
     ho, wo = dz.shape[2], dz.shape[3]
@@ -269,13 +319,26 @@ def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int):
         if stride == 1 and wt is not None:
             # backward-data = forward conv of dz with the flipped, transposed weight
             dx = torch.empty_like(x, memory_format=torch.channels_last)
-            m.conv_fwd(dev, st, nb, ho, wo, co, c, r, s, 1, r - 1 - pad, dz.data_ptr(), wt.data_ptr(), dx.data_ptr())
+            kw, part, nt = {}, None, 0
+            if link is not None:
+                nt = m.gemm_nt_tiles(nb * h * w)
+                kw, part = _red_args(link, c, nt, x.device)
+            m.conv_fwd(dev, st, nb, ho, wo, co, c, r, s, 1, r - 1 - pad, dz.data_ptr(), wt.data_ptr(), dx.data_ptr(),
+                       **kw)
+            if part is not None:
+                link.publish(part, nt, dx)
         elif wt is not None:
             # strided: stride^2 parity classes, each a stride-1 implicit GEMM over dz whose
             # epilogue writes its pixels of dx (wt = the packed class weights)
             dx = torch.empty_like(x, memory_format=torch.channels_last)
+            kw, part, nt = {}, None, 0
+            if link is not None:
+                nt = m.conv_dgrad_strided_tiles(nb, h, w, c, co, r, s, stride, pad)
+                kw, part = _red_args(link, c, nt, x.device)
             m.conv_dgrad_strided(dev, st, nb, h, w, c, co, r, s, stride, pad, dz.data_ptr(), wt.data_ptr(),
-                                 dx.data_ptr())
+                                 dx.data_ptr(), **kw)
+            if part is not None:
+                link.publish(part, nt, dx)
         else:  # MIOpen's NHWC backward-data
             wv = wb.permute(0, 3, 1, 2)  # [Co, C, R, S] view with channels_last strides
             dx = torch.ops.aten.convolution_backward(dz, x, wv, None, [stride, stride], [pad, pad], [1, 1], False,
@@ -315,7 +378,7 @@ class _ConvFn(torch.autograd.Function):
     of the ReLU / bias is one pass over (dy, y) (csrc/kernels/act.hip)."""
 
     @staticmethod
-    def forward(ctx, x, weight, stride: int, pad: int, bias=None, relu: bool = False):
+    def forward(ctx, x, weight, stride: int, pad: int, bias=None, relu: bool = False, hold=None, link=None):
         x = _bf16_cl(x)
         nb, c, h, w = x.shape
         co, _, r, s = weight.shape
@@ -329,10 +392,16 @@ class _ConvFn(torch.autograd.Function):
         b = None
         if bias is not None:
             b = bias if (bias.dtype == torch.float32 and bias.is_contiguous()) else bias.float().contiguous()
+        st = None
+        if hold is not None and not relu and b is None:  # batch-norm statistics of y
+            st, nt = _tile_stats(co, nb * ho * wo, x.device)
+            hold.append((st, nt))
         native().conv_fwd(x.device.index, _stream(x), nb, h, w, c, co, r, s, stride, pad, x.data_ptr(), wb.data_ptr(),
-                          y.data_ptr(), bias=b.data_ptr() if b is not None else 0, relu=bool(relu))
+                          y.data_ptr(), stats=st.data_ptr() if st is not None else 0,
+                          bias=b.data_ptr() if b is not None else 0, relu=bool(relu))
         ctx.save_for_backward(x, wb, wt, y if relu else None)
         ctx.geo = (stride, pad, bias is not None, bool(relu))
+        ctx.link = link
         return y
 
     @staticmethod
@@ -355,8 +424,8 @@ class _ConvFn(torch.autograd.Function):
             dz = dy
             if has_bias and ctx.needs_input_grad[4]:
                 db = dy.float().sum(dim=(0, 2, 3))
-        dx, dw = _conv_backward(ctx, x, wb, wt, dz, stride, pad)
-        return dx, dw, None, None, db, None
+        dx, dw = _conv_backward(ctx, x, wb, wt, dz, stride, pad, ctx.link)
+        return dx, dw, None, None, db, None, None, None
 
 
 def conv_supported(x: torch.Tensor, weight: torch.Tensor) -> bool:
@@ -385,7 +454,7 @@ class ConvAct2d(nn.Conv2d):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.fused(x):
-            return _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0], self.bias, self.act)
+            return _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0], self.bias, self.act, None, None)
         y = super().forward(x)
         return F.relu(y) if self.act else y
 
@@ -397,11 +466,15 @@ class ConvNHWC(nn.Conv2d):
 
     def __init__(self, in_channels: int, out_channels: int, kernel_size: int, stride: int = 1, padding: int = 0):
         super().__init__(in_channels, out_channels, kernel_size, stride=stride, padding=padding, bias=False)
+        self.emit_stats = False  # output feeds a training BatchNormAct2d: emit its statistics
 
     def fused(self, x: torch.Tensor) -> bool:
         return conv_supported(x, self.weight)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.fused(x):
-            return _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0], None, False)
+            hold = [] if (self.emit_stats and self.training) else None
+            y = _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0], None, False, hold,
+                              _link_of(x) if torch.is_grad_enabled() else None)
+            return _attach_stats(y, hold)
         return super().forward(x)

@@ -30,7 +30,7 @@ def _traces(d):
         yield t, [(int(a), int(b), n) for a, b, n in c.execute("select start, end, name from kernels")]
 
 
-def summarise(d, out, marker="DownpourF", k=3, top=30):
+def summarise(d, out, marker="ApplyF<true>", k=3, top=30):
     lines = []
     for t, rows in _traces(d):
         rows.sort()
@@ -70,7 +70,7 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("out")
-    ap.add_argument("--marker", default="DownpourF")
+    ap.add_argument("--marker", default="ApplyF<true>")
     ap.add_argument("-k", type=int, default=3)
     ap.add_argument("--top", type=int, default=30)
     a = ap.parse_args()

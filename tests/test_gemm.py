@@ -52,6 +52,7 @@ def test_gemm_nt_stats(M, N, K):
     torch.manual_seed(1)
     a, b = _bf(M, K), _bf(N, K, scale=0.05)
     c, st = C.gemm_nt(a, b, stats=True)
+    # the statistics are those of the stored (bf16) C
     cf = c.float()
     assert torch.allclose(st[0], cf.sum(0), rtol=1e-3, atol=1e-2)
     assert torch.allclose(st[1], (cf * cf).sum(0), rtol=1e-3, atol=1e-2)
@@ -192,3 +193,26 @@ def test_conv_act_bias_relu(n, ci, co, hw, k, relu):
     for name, a, b, e in zip(("y", "dx", "dw", "db"), got, lib, exact):
         err, floor = _rel(a, e), _rel(b, e)
         assert err < 1.5 * floor + 5e-3, (name, err, floor)
+
+
+@gpu
+@pytest.mark.parametrize("M", [1000, 70000])
+def test_gemm_nt_tile_stats_large_mean(M):
+    """Per-tile (mean, M2) statistics stay exact when |mean| >> std (no E[y^2]-E[y]^2
+    cancellation): C = A . I reproduces A's columns, offset by 300 with unit spread."""
+    torch.manual_seed(M)
+    N = K = 64
+    a = (torch.randn(M, K, device="cuda") + 300.0).to(torch.bfloat16)
+    b = torch.eye(N, K, device="cuda", dtype=torch.bfloat16)
+    m = C.native()
+    c = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    st = torch.empty(m.gemm_nt_stats_floats(M, N), dtype=torch.float32, device="cuda")
+    m.gemm_nt(0, torch.cuda.current_stream().cuda_stream, M, N, K, a.data_ptr(), K, b.data_ptr(), K, c.data_ptr(), N,
+              st.data_ptr())
+    p = st.view(-1, 2, N).double()
+    n = (M - 128 * torch.arange(p.shape[0], device="cuda", dtype=torch.float64)).clamp(max=128)[:, None]
+    mean = (n * p[:, 0]).sum(0) / M
+    var = (p[:, 1] + n * (p[:, 0] - mean) ** 2).sum(0) / M
+    cd = c.double()
+    torch.testing.assert_close(mean, cd.mean(0), rtol=1e-7, atol=1e-4)
+    torch.testing.assert_close(var, cd.var(0, unbiased=False), rtol=1e-4, atol=1e-5)

@@ -78,3 +78,60 @@ def test_bottleneck_fused_matches_fp32(inp, planes, stride):
     print(errs)
     for k, (fused, lib) in errs.items():
         assert fused < 1.5 * lib + 1e-2, (k, fused, lib)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stride", [1, 2])
+def test_chained_blocks_fold_bn_passes(stride):
+    """Two chained bottlenecks: every BN takes its statistics from the producing conv's
+    GEMM epilogue, and every BN whose output feeds a conv gets its backward reduction from
+    that conv's backward-data epilogue (bn1 -> 3x3 incl. the strided parity classes, bn2
+    -> 1x1, block-1 bn3 -> block-2 conv1 with the parked shortcut gradient). Checked
+    against fp32 and the bf16 library floor, and the fused hand-overs must have fired."""
+    from mpit_amd.ops import bn as bnmod
+
+    torch.manual_seed(7 + stride)
+    inp, planes = 256, 64 * stride
+    down = None
+    if stride != 1 or inp != planes * 4:
+        down = torch.nn.Sequential(conv1x1(inp, planes * 4, stride), BatchNormAct2d(planes * 4, act=False))
+    b1 = Bottleneck(inp, planes, stride, down)
+    b2 = Bottleneck(planes * 4, planes)
+    net = torch.nn.Sequential(b1, b2).cuda().to(memory_format=torch.channels_last)
+    for m in net.modules():
+        if isinstance(m, BatchNormAct2d):
+            m.weight.data.uniform_(0.5, 1.5)
+            m.bias.data.uniform_(-0.2, 0.2)
+    x = torch.randn(4, inp, 14, 14, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    c0 = dict(bnmod.COUNTERS)
+    x1 = x.clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y1 = net(x1)
+    g = torch.randn(y1.shape, device="cuda")
+    y1.backward(g.to(y1.dtype))
+    fired = {k: bnmod.COUNTERS[k] - c0[k] for k in c0}
+    nbn = sum(isinstance(m, BatchNormAct2d) for m in net.modules())
+    assert fired["fwd_tile_stats"] == nbn, fired
+    # bn1, bn2 of both blocks + bn3 of block 1 (block 2's bn3 output is the loss input)
+    assert fired["bwd_linked"] == 5, fired
+    grads1 = {n: p.grad.detach().clone() for n, p in net.named_parameters()}
+    net.zero_grad(set_to_none=True)
+
+    def ref(t):
+        return _ref_block(b2, _ref_block(b1, t))
+
+    x3 = x.clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y3 = ref(x3)
+    y3.backward(g.to(y3.dtype))
+    grads3 = {n: p.grad.detach().clone() for n, p in net.named_parameters()}
+    net.zero_grad(set_to_none=True)
+    x2 = x.float().clone().requires_grad_(True)
+    y2 = ref(x2)
+    y2.backward(g)
+    errs = {"y": (_rel(y1, y2), _rel(y3, y2)), "x.grad": (_rel(x1.grad, x2.grad), _rel(x3.grad, x2.grad))}
+    for n, p in net.named_parameters():
+        errs[n] = (_rel(grads1[n], p.grad), _rel(grads3[n], p.grad))
+    print(errs)
+    for k, (fused, lib) in errs.items():
+        assert fused < 1.5 * lib + 1e-2, (k, fused, lib)

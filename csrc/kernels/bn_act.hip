@@ -18,6 +18,7 @@
 // deterministic (no atomics) and free of the E[x^2]-E[x]^2 cancellation for |mean|>>std.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cmath>
 #include <stdexcept>
 #include <string>
@@ -155,13 +156,35 @@ __device__ __forceinline__ bool fin_combine(const float* __restrict__ part, int 
 }
 
 template <typename T>
+__device__ __forceinline__ void fin_fwd_channel(int c, double a, double b, int C, int64_t M, const T* __restrict__ x,
+                                                const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                float eps, float momentum, float* __restrict__ rmean,
+                                                float* __restrict__ rvar, float* __restrict__ save_mean,
+                                                float* __restrict__ save_rstd, float* __restrict__ coef);
+
+__device__ __forceinline__ void fin_bwd_channel(int c, double a, double b, int C, int64_t M,
+                                                const float* __restrict__ gamma, const float* __restrict__ mean,
+                                                const float* __restrict__ rstd, float* __restrict__ dgamma,
+                                                float* __restrict__ dbeta, float* __restrict__ coef);
+
+template <typename T>
 __global__ __launch_bounds__(kFinCh * kFinK) void bn_finalize_fwd_kernel(
     const float* __restrict__ part, int nb, int C, int64_t M, const T* __restrict__ x, const float* __restrict__ gamma,
     const float* __restrict__ beta, float eps, float momentum, float* __restrict__ rmean, float* __restrict__ rvar,
     float* __restrict__ save_mean, float* __restrict__ save_rstd, float* __restrict__ coef /*[2][C] scale, shift*/) {
   double a, b;
   if (!fin_combine(part, nb, C, a, b)) return;
-  const int c = blockIdx.x * kFinCh + int(threadIdx.x % kFinCh);
+  fin_fwd_channel(blockIdx.x * kFinCh + int(threadIdx.x % kFinCh), a, b, C, M, x, gamma, beta, eps, momentum, rmean,
+                  rvar, save_mean, save_rstd, coef);
+}
+
+// channel c of the forward finalize from the fp64 sums (a, b) of (x - x[0][c]) and its square
+template <typename T>
+__device__ __forceinline__ void fin_fwd_channel(int c, double a, double b, int C, int64_t M, const T* __restrict__ x,
+                                                const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                float eps, float momentum, float* __restrict__ rmean,
+                                                float* __restrict__ rvar, float* __restrict__ save_mean,
+                                                float* __restrict__ save_rstd, float* __restrict__ coef) {
   float k0;
   if constexpr (sizeof(T) == 2) k0 = bf2f(reinterpret_cast<const uint16_t*>(x)[c]);
   else k0 = reinterpret_cast<const float*>(x)[c];
@@ -188,13 +211,38 @@ __global__ __launch_bounds__(kFinCh * kFinK) void bn_finalize_fwd_kernel(
 //        shifted sums bn_finalize_fwd_kernel expects (shift = row 0 of x), fp64 inside;
 //   plain (backward reductions): tile sums are added.
 constexpr int kTileRows = 128;
-constexpr int kTileLanes = 4;  // row lanes per channel (64 channels x 4 = 256 threads)
+constexpr int kTileLanes = 4;     // row lanes per channel (64 channels x 4 = 256 threads)
+constexpr int kTicketSlots = 64;  // rotating ticket sets (one per launch in flight)
+constexpr int kMaxChBlocks = 32;  // C <= 2048
+
+// Completion tickets of the fused level-1 + finalize kernel: one counter per channel
+// block, reset to zero by the block that finalizes, so a set is reusable as soon as its
+// launch retired; launches rotate over kTicketSlots sets.
+__device__ uint32_t g_bn_tickets[kTicketSlots * kMaxChBlocks];
+
+// finalize operands (forward or backward)
+struct FinArgs {
+  const float* gamma;
+  const float* beta;
+  float eps, momentum;
+  float* rmean;
+  float* rvar;
+  float* save_mean;
+  float* save_rstd;
+  const float* mean;
+  const float* rstd;
+  float* dgamma;
+  float* dbeta;
+  float* coef;
+};
+
 template <typename T, bool CHAN>
-__global__ __launch_bounds__(64 * kTileLanes) void bn_tiles_reduce_kernel(const float* __restrict__ part, int nt,
-                                                                          int C, int64_t M, const T* __restrict__ x,
-                                                                          int rows_per_group,
-                                                                          float* __restrict__ out) {
+__global__ __launch_bounds__(64 * kTileLanes) void bn_tiles_finalize_kernel(const float* __restrict__ part, int nt,
+                                                                            int C, int64_t M, const T* __restrict__ x,
+                                                                            int rows_per_group, float* lvl,
+                                                                            uint32_t* tickets, FinArgs fa) {
   __shared__ double sa[kTileLanes][64], sb[kTileLanes][64];
+  __shared__ uint32_t prev;
   const int cl = threadIdx.x % 64, kl = threadIdx.x / 64;
   const int c = blockIdx.x * 64 + cl, grp = blockIdx.y;
   double a = 0, b = 0;
@@ -222,32 +270,86 @@ __global__ __launch_bounds__(64 * kTileLanes) void bn_tiles_reduce_kernel(const 
   sa[kl][cl] = a;
   sb[kl][cl] = b;
   __syncthreads();
+  if (kl == 0 && c < C) {
+#pragma unroll
+    for (int k = 1; k < kTileLanes; ++k) {
+      a += sa[k][cl];
+      b += sb[k][cl];
+    }
+    // write-through (sc1) stores: visible to a reader on any XCD without an L2 write-back
+    __hip_atomic_store(&lvl[(size_t(grp) * 2 + 0) * C + c], float(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&lvl[(size_t(grp) * 2 + 1) * C + c], float(b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // Hand-off (MI355X_MICROARCH.md, cross-workgroup table row 1): every storing wave waits
+  // for its stores, a barrier, one agent-scope add per workgroup; the workgroup whose add
+  // came last reads all groups with sc1 loads (L1 bypass) in group order — no fences.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) prev = atomicAdd(&tickets[blockIdx.x], 1u);
+  __syncthreads();
+  if (prev != gridDim.y - 1) return;
+  // consumer: one agent acquire (invalidates this CU's L1), its wait, a barrier, then
+  // plain loads the compiler can batch
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  a = b = 0;
+  if (c < C) {
+#pragma unroll 4
+    for (int g = kl; g < int(gridDim.y); g += kTileLanes) {
+      a += double(lvl[(size_t(g) * 2 + 0) * C + c]);
+      b += double(lvl[(size_t(g) * 2 + 1) * C + c]);
+    }
+  }
+  __syncthreads();
+  sa[kl][cl] = a;
+  sb[kl][cl] = b;
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(&tickets[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (kl != 0 || c >= C) return;
 #pragma unroll
   for (int k = 1; k < kTileLanes; ++k) {
     a += sa[k][cl];
     b += sb[k][cl];
   }
-  out[(size_t(grp) * 2 + 0) * C + c] = float(a);
-  out[(size_t(grp) * 2 + 1) * C + c] = float(b);
+  if constexpr (CHAN)
+    fin_fwd_channel(c, a, b, C, M, x, fa.gamma, fa.beta, fa.eps, fa.momentum, fa.rmean, fa.rvar, fa.save_mean,
+                    fa.save_rstd, fa.coef);
+  else
+    fin_bwd_channel(c, a, b, C, M, fa.gamma, fa.mean, fa.rstd, fa.dgamma, fa.dbeta, fa.coef);
 }
 
-// groups for level 1: >= 16 tile rows each, at most kMaxStatBlocks (the finalize input)
+// groups for level 1: >= 16 tile rows each, at most 64 (the last group combines them all)
 int tile_groups(int64_t nt, int* rows_per_group) {
-  int g = int(std::min<int64_t>(256, std::max<int64_t>(1, (nt + 15) / 16)));
+  int g = int(std::min<int64_t>(64, std::max<int64_t>(1, (nt + 15) / 16)));
   *rows_per_group = int((nt + g - 1) / g);
   g = int((nt + *rows_per_group - 1) / *rows_per_group);
   return g;
 }
 
+// Partials emitted by a GEMM epilogue (gemm.hip), one row pair per 128-row tile — up to
+// thousands of rows, too many for one finalize block per 64 channels. One launch: groups
+// of tile rows are folded in parallel (grid: channel blocks x groups) into lvl[groups][2][C],
+// and the last group to finish for a channel block (ticket) combines the groups and writes
+// the BN coefficients (deterministic: fixed group order, fp64):
+//   CHAN (forward statistics): tile k holds (mean_k, M2_k) of n_k = min(128, M - 128k)
+//        rows; level 1 = sum n_k d_k, sum M2_k + n_k d_k^2 with d_k = mean_k - x[0][c], the
+//        shifted sums of the stand-alone statistics pass;
+//   plain (backward reductions): tile sums are added.
 template <typename T, bool CHAN>
-int launch_tiles_reduce(hipStream_t s, const float* part, int64_t nt, int C, int64_t M, const T* x, float* out) {
+void launch_tiles_finalize(hipStream_t s, const float* part, int64_t nt, int C, int64_t M, const T* x, float* lvl,
+                           const FinArgs& fa) {
   if (nt <= 0 || nt > INT32_MAX) throw std::invalid_argument("bn_act: bad partial count");
+  const int nchb = (C + 63) / 64;
+  if (nchb > kMaxChBlocks) throw std::invalid_argument("bn_act: too many channels for the tile reduction");
+  static std::atomic<uint32_t> launches{0};
+  uint32_t* base = nullptr;
+  hip_check(hipGetSymbolAddress(reinterpret_cast<void**>(&base), HIP_SYMBOL(g_bn_tickets)), "ticket symbol");
+  uint32_t* tick = base + size_t(launches.fetch_add(1) % kTicketSlots) * kMaxChBlocks;
   int rpg;
   const int g = tile_groups(nt, &rpg);
-  hipLaunchKernelGGL((bn_tiles_reduce_kernel<T, CHAN>), dim3((C + 63) / 64, g), dim3(64 * kTileLanes), 0, s, part,
-                     int(nt), C, M, x, rpg, out);
-  return g;
+  hipLaunchKernelGGL((bn_tiles_finalize_kernel<T, CHAN>), dim3(nchb, g), dim3(64 * kTileLanes), 0, s, part, int(nt),
+                     C, M, x, rpg, lvl, tick, fa);
 }
 
 // ---------------------------------------------------------------- forward: apply
@@ -367,7 +469,14 @@ __global__ __launch_bounds__(kFinCh * kFinK) void bn_finalize_bwd_kernel(
     float* __restrict__ coef /*[3][C] a c b*/) {
   double a, b;
   if (!fin_combine(part, nb, C, a, b)) return;
-  const int c = blockIdx.x * kFinCh + int(threadIdx.x % kFinCh);
+  fin_bwd_channel(blockIdx.x * kFinCh + int(threadIdx.x % kFinCh), a, b, C, M, gamma, mean, rstd, dgamma, dbeta, coef);
+}
+
+// channel c of the backward finalize from the sums a = sum dz, b = sum dz (x - mean)
+__device__ __forceinline__ void fin_bwd_channel(int c, double a, double b, int C, int64_t M,
+                                                const float* __restrict__ gamma, const float* __restrict__ mean,
+                                                const float* __restrict__ rstd, float* __restrict__ dgamma,
+                                                float* __restrict__ dbeta, float* __restrict__ coef) {
   const float rs = rstd[c];
   if (dgamma) dgamma[c] = float(b) * rs;
   if (dbeta) dbeta[c] = float(a);
@@ -466,10 +575,17 @@ void fwd_impl(int dev, hipStream_t s, const T* x, const T* res, T* y, int64_t M,
   float* coef = ws;  // [2][C]
   if (tstats) {  // statistics from the producing GEMM's epilogue: no pass over x
     if (nstat != (M + kTileRows - 1) / kTileRows) throw std::invalid_argument("bn_act: stats tiles do not match M");
-    float* part = ws + 2 * C;
-    const int nb = launch_tiles_reduce<T, true>(s, tstats, nstat, C, M, x, part);
-    hipLaunchKernelGGL(bn_finalize_fwd_kernel<T>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinK), 0, s, part,
-                       nb, C, M, x, gamma, beta, eps, momentum, rmean, rvar, save_mean, save_rstd, coef);
+    FinArgs fa{};
+    fa.gamma = gamma;
+    fa.beta = beta;
+    fa.eps = eps;
+    fa.momentum = momentum;
+    fa.rmean = rmean;
+    fa.rvar = rvar;
+    fa.save_mean = save_mean;
+    fa.save_rstd = save_rstd;
+    fa.coef = coef;
+    launch_tiles_finalize<T, true>(s, tstats, nstat, C, M, x, ws + 2 * C, fa);
     launch_apply<T>(s, x, res, y, M, C, coef, relu, mask);
     hip_check(hipGetLastError(), "bn_act forward launch");
     return;
@@ -502,9 +618,14 @@ void bwd_impl(hipStream_t s, const T* dy, const uint8_t* mask, const T* x, T* dx
   float* part = ws + 3 * C;
   const size_t shm = size_t(R) * 2 * C * sizeof(float);
   if (gpart) {  // reductions already produced by the GEMM that wrote dy (gemm.hip EPI_BNRED)
-    const int ng = launch_tiles_reduce<T, false>(s, gpart, npart, C, M, x, part);
-    hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinK), 0, s, part, ng,
-                       C, M, gamma, mean, rstd, dgamma, dbeta, coef);
+    FinArgs fa{};
+    fa.gamma = gamma;
+    fa.mean = mean;
+    fa.rstd = rstd;
+    fa.dgamma = dgamma;
+    fa.dbeta = dbeta;
+    fa.coef = coef;
+    launch_tiles_finalize<T, false>(s, gpart, npart, C, M, x, part, fa);
   } else {
     if (relu)
       hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true>), dim3(nb), dim3(blk), shm, s, dy, mask, x, mean, M, C, rpb,

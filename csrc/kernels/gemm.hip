@@ -133,8 +133,13 @@ __device__ __forceinline__ int xcd_tile(int bid, int nb) {
 //              produces (a convolution's backward-data): dz = round(C) * relu_mask,
 //              (sum dz, sum dz*(x - mean)) per column with x the BN's input — the separate
 //              reduction pass over (dz, x) of the BN backward disappears.
-// Per element the reductions cost 3-5 VALU ops on values already in registers; the
-// per-column sums over the 32 rows a wave holds use one transposing butterfly.
+// The epilogue stages the bf16 tile in LDS and runs row-major (see phase B), so every
+// global access of a wave covers whole row segments; the column partials of the rows a
+// thread walks are combined through LDS.
+//
+// Waves: BM/64 x 2, each owning a 64 x BN/2 sub-tile (BM = 128: 4 waves). BM = 256 (8 waves,
+// 25 % fewer L2->LDS bytes per FLOP) compiles and passes the tests but measured no faster on
+// the ResNet-50 shapes (profiles/gemm_tile_ab_r01.jsonl), so it is not launched.
 //
 // Staging: global_load_lds (16-B LDS DMA, no VGPRs) into a ring of STAGES buffers with
 // STAGES-1 k-tiles in flight; a counted s_waitcnt vmcnt + raw s_barrier retires exactly
@@ -142,15 +147,16 @@ __device__ __forceinline__ int xcd_tile(int bid, int nb) {
 // is lane-linear per wave instruction (16 rows x 64 B); the swizzle is applied on the
 // global source address.
 template <int BM, int BN, int STAGES, int EPI, bool CONV>
-__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda,
+__global__ __launch_bounds__(BM / 64 * 128, BM == 256 ? 1 : 2) void gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda,
                                                          const uint16_t* __restrict__ B, int64_t ldb,
                                                          uint16_t* C, int64_t ldc, int64_t M, int N, int K,
                                                          int ntn, EpiArgs ep, const uint16_t* Cin,
                                                          const uint8_t* __restrict__ Cmask,
                                                          const float* __restrict__ bias, int relu, ConvGeo geo) {
-  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int NW = BM / 64 * 2, NT = NW * 64;  // waves, threads
+  constexpr int WM = 64, WN = BN / 2;
   constexpr int TM = WM / 32, TN = WN / 32;
-  constexpr int IA = BM / 16 / 4, IB = BN / 16 / 4;  // glds instructions per wave per tile
+  constexpr int IA = BM / 16 / NW, IB = BN / 16 / NW;  // glds instructions per wave per tile
   constexpr int NI = IA + IB;
   constexpr int TILE = (BM + BN) * kBK;  // elements per stage
   static_assert(IA >= 1 && IB >= 1, "tile too small");
@@ -296,8 +302,12 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const uint16_t* __restr
   // ---- phase B: row-major. A thread owns one 16-B chunk (8 channels) of a row and walks
   // the rows RPP apart, so every global access of a wave covers whole 256-B (BN = 128) row
   // segments: the C store, the Cin / Cmask / BN x / BN mask loads.
-  constexpr int CPR = BN / 8, RPP = 256 / CPR, NP = BM / RPP;
-  const int ch = t % CPR, rr = t / CPR;
+  // Partials are per 128-row tile whatever BM is: with BM = 256 the row-threads split into
+  // two halves of 128 rows (HALVES = BM / 128), each thread staying in one.
+  constexpr int CPR = BN / 8, RPP = NT / CPR, NP = BM / RPP;
+  constexpr int HALVES = BM / 128, RPH = RPP / HALVES;  // row-threads per 128-row half
+  const int ch = t % CPR, rg = t / CPR;
+  const int rr = (rg / RPH) * 128 + rg % RPH;  // first row of this thread; rows rr + p*RPH
   const int nc = n0 + ch * 8;  // first global column of this thread
   float s1[8], s2[8], sf[8], mu[8];
   int nv = 0;
@@ -316,7 +326,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const uint16_t* __restr
   uint32_t cmb[NP], xmb[NP];
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
-    const int64_t m = m0 + rr + p * RPP;
+    const int64_t m = m0 + rr + p * RPH;
     orow[p] = m;  // output row (pixel) of GEMM row m
     if constexpr (CONV) {
       if (geo.ostr > 1) {
@@ -339,7 +349,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const uint16_t* __restr
   }
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
-    const int rl = rr + p * RPP;
+    const int rl = rr + p * RPH;
     if (m0 + rl >= M) continue;
     const int64_t o = orow[p] * ldc + nc;
     const uint4 hv = *reinterpret_cast<const uint4*>(tl + rl * LDT + ch * 8);
@@ -401,23 +411,26 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const uint16_t* __restr
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float d = nv ? s1[e] / n : 0.f;
-        red[(rr * 3 + 0) * BN + ch * 8 + e] = n;
-        red[(rr * 3 + 1) * BN + ch * 8 + e] = nv ? sf[e] + d : 0.f;
-        red[(rr * 3 + 2) * BN + ch * 8 + e] = nv ? fmaxf(s2[e] - s1[e] * d, 0.f) : 0.f;
+        red[(rg * 3 + 0) * BN + ch * 8 + e] = n;
+        red[(rg * 3 + 1) * BN + ch * 8 + e] = nv ? sf[e] + d : 0.f;
+        red[(rg * 3 + 2) * BN + ch * 8 + e] = nv ? fmaxf(s2[e] - s1[e] * d, 0.f) : 0.f;
       }
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        red[(rr * 3 + 0) * BN + ch * 8 + e] = s1[e];
-        red[(rr * 3 + 1) * BN + ch * 8 + e] = s2[e];
+        red[(rg * 3 + 0) * BN + ch * 8 + e] = s1[e];
+        red[(rg * 3 + 1) * BN + ch * 8 + e] = s2[e];
       }
     }
     __syncthreads();
-    float* prow = ep.part + (ep.row0 + mt) * 2 * int64_t(N) + n0;
-    for (int n = t; n < BN; n += 256) {
-      if constexpr (EPI == EPI_STATS) {  // merge the RPP (n, mean, M2) triples (Chan et al.)
+    for (int q = t; q < BN * HALVES; q += NT) {
+      const int hf = q / BN, n = q % BN;
+      const int64_t tile = int64_t(mt) * HALVES + hf;  // 128-row partial row
+      if (tile * 128 >= M) continue;
+      float* prow = ep.part + (ep.row0 + tile) * 2 * int64_t(N) + n0;
+      if constexpr (EPI == EPI_STATS) {  // merge the half's (n, mean, M2) triples (Chan et al.)
         float na = 0.f, mean = 0.f, m2 = 0.f;
-        for (int k = 0; k < RPP; ++k) {
+        for (int k = hf * RPH; k < (hf + 1) * RPH; ++k) {
           const float nb = red[(k * 3 + 0) * BN + n];
           if (nb == 0.f) continue;
           const float mb = red[(k * 3 + 1) * BN + n], tot = na + nb, d = mb - mean;
@@ -429,7 +442,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const uint16_t* __restr
         prow[N + n] = m2;
       } else {
         float a = 0.f, b = 0.f;
-        for (int k = 0; k < RPP; ++k) {
+        for (int k = hf * RPH; k < (hf + 1) * RPH; ++k) {
           a += red[(k * 3 + 0) * BN + n];
           b += red[(k * 3 + 1) * BN + n];
         }
@@ -752,39 +765,38 @@ static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t
   const auto* bs = reinterpret_cast<const float*>(bias);
   const int rl = relu ? 1 : 0;
   const ConvGeo g = geo ? *geo : ConvGeo{};
-  constexpr int BM = 128;
-  const int64_t mtn = (M + BM - 1) / BM;
   const int nk = K / kBK;
   const int stages = nk >= 4 ? 4 : (nk == 3 ? 3 : 2);
   // (kernel templates are named at a non-template call site so their host stubs are emitted)
-#define MPIT_NT_LAUNCH1(BN, ST, EPI, CONV)                                                                   \
-  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, ST, EPI, CONV>), dim3(unsigned(nb)), dim3(256), shm, s, a, lda, b, \
-                     ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g)
-#define MPIT_NT_LAUNCH2(BN, ST, CONV)                                   \
-  do {                                                                  \
-    if (epi == EPI_STATS) MPIT_NT_LAUNCH1(BN, ST, EPI_STATS, CONV);     \
-    else if (epi == EPI_BNRED) MPIT_NT_LAUNCH1(BN, ST, EPI_BNRED, CONV); \
-    else MPIT_NT_LAUNCH1(BN, ST, EPI_NONE, CONV);                       \
+#define MPIT_NT_LAUNCH1(BM, BN, ST, EPI, CONV)                                                                    \
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, ST, EPI, CONV>), dim3(unsigned(nb)), dim3(BM / 64 * 128), shm, s, a, \
+                     lda, b, ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g)
+#define MPIT_NT_LAUNCH2(BM, BN, ST, CONV)                                   \
+  do {                                                                      \
+    if (epi == EPI_STATS) MPIT_NT_LAUNCH1(BM, BN, ST, EPI_STATS, CONV);     \
+    else if (epi == EPI_BNRED) MPIT_NT_LAUNCH1(BM, BN, ST, EPI_BNRED, CONV); \
+    else MPIT_NT_LAUNCH1(BM, BN, ST, EPI_NONE, CONV);                       \
   } while (0)
-#define MPIT_NT_LAUNCH(BN, ST)                                                   \
-  do {                                                                           \
-    const int ntn = N / BN;                                                      \
-    const int64_t nb = mtn * ntn;                                                \
-    if (nb > INT32_MAX) throw std::invalid_argument("gemm_nt: too many tiles");  \
-    /* LDS: the k-tile ring, reused by the epilogue's bf16 tile and reduction table */      \
-    const size_t shm = std::max({size_t(ST) * (BM + BN) * kBK * 2, size_t(BM) * (BN + 8) * 2,     \
-                                 size_t(256) * 8 * 3 * sizeof(float)});                          \
-    if (geo) MPIT_NT_LAUNCH2(BN, ST, true);                                      \
-    else MPIT_NT_LAUNCH2(BN, ST, false);                                         \
+#define MPIT_NT_LAUNCH(BM, BN, ST)                                                                             \
+  do {                                                                                                         \
+    const int64_t mtn = (M + BM - 1) / BM;                                                                     \
+    const int ntn = N / BN;                                                                                    \
+    const int64_t nb = mtn * ntn;                                                                              \
+    if (nb > INT32_MAX) throw std::invalid_argument("gemm_nt: too many tiles");                               \
+    /* LDS: the k-tile ring, reused by the epilogue's bf16 tile and reduction table */                        \
+    const size_t shm = std::max({size_t(ST) * (BM + BN) * kBK * 2, size_t(BM) * (BN + 8) * 2,                  \
+                                 size_t(BM / 64 * 128) * 8 * 3 * sizeof(float)});                             \
+    if (geo) MPIT_NT_LAUNCH2(BM, BN, ST, true);                                                                \
+    else MPIT_NT_LAUNCH2(BM, BN, ST, false);                                                                   \
   } while (0)
   if (N % 128 == 0) {
-    if (stages == 4) MPIT_NT_LAUNCH(128, 4);
-    else if (stages == 3) MPIT_NT_LAUNCH(128, 3);
-    else MPIT_NT_LAUNCH(128, 2);
+    if (stages == 4) MPIT_NT_LAUNCH(128, 128, 4);
+    else if (stages == 3) MPIT_NT_LAUNCH(128, 128, 3);
+    else MPIT_NT_LAUNCH(128, 128, 2);
   } else {
-    if (stages == 4) MPIT_NT_LAUNCH(64, 4);
-    else if (stages == 3) MPIT_NT_LAUNCH(64, 3);
-    else MPIT_NT_LAUNCH(64, 2);
+    if (stages == 4) MPIT_NT_LAUNCH(128, 64, 4);
+    else if (stages == 3) MPIT_NT_LAUNCH(128, 64, 3);
+    else MPIT_NT_LAUNCH(128, 64, 2);
   }
 #undef MPIT_NT_LAUNCH
 #undef MPIT_NT_LAUNCH2

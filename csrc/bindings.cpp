@@ -119,6 +119,13 @@ PYBIND11_MODULE(_mpit, m) {
       },
       py::arg("dev"), py::arg("stream"), py::arg("w"), py::arg("R"), py::arg("Cc"), py::arg("wb"), py::arg("wt"),
       py::arg("taps") = 1);
+  m.def("cast_job_bytes", &cast_job_bytes);
+  m.def("cast_jobs_build", [](uintptr_t table, std::vector<std::array<int64_t, 10>> specs) {
+    return cast_jobs_build(table, specs);
+  });
+  m.def("cast_jobs_run", [](int dev, uintptr_t s, uintptr_t table, int njobs, int64_t nblocks) {
+    cast_jobs_run(dev, S(s), table, njobs, nblocks);
+  });
   m.def("maxpool_fwd", [](int dev, uintptr_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t x,
                           uintptr_t y, uintptr_t idx) { maxpool_fwd(dev, S(s), N, H, W, C, K, stride, pad, x, y, idx); });
   m.def("maxpool_bwd", [](int dev, uintptr_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t dy,

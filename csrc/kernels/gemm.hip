@@ -39,6 +39,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
+#include <vector>
 #include <stdexcept>
 #include <string>
 
@@ -686,11 +688,11 @@ struct TapMap {
   int16_t tc[kMaxTaps], dt[kMaxTaps];
 };
 
-__global__ __launch_bounds__(256) void cast_transpose_kernel(const float* __restrict__ w, int R, int Cc, int T,
-                                                             uint16_t* __restrict__ wb, uint16_t* __restrict__ wt,
-                                                             TapMap map) {
+// one 32 x 32 (channel x row) tile of tap `tap`, 256 threads
+__device__ __forceinline__ void cast_tile(const float* __restrict__ w, int R, int Cc, int T, uint16_t* __restrict__ wb,
+                                          uint16_t* __restrict__ wt, const TapMap& map, int cx, int ry, int tap) {
   __shared__ uint16_t tile[32][33];
-  const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32, tap = blockIdx.z;
+  const int c0 = cx * 32, r0 = ry * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 8 rows per pass
   for (int y = ty; y < 32; y += 8) {
     const int r = r0 + y, c = c0 + tx;
@@ -709,6 +711,42 @@ __global__ __launch_bounds__(256) void cast_transpose_kernel(const float* __rest
     const int c = c0 + y, r = r0 + tx;
     if (r < R && c < Cc) wt[base + (int64_t(c) * tc + dt) * R + r] = tile[tx][y];
   }
+}
+
+__global__ __launch_bounds__(256) void cast_transpose_kernel(const float* __restrict__ w, int R, int Cc, int T,
+                                                             uint16_t* __restrict__ wb, uint16_t* __restrict__ wt,
+                                                             TapMap map) {
+  cast_tile(w, R, Cc, T, wb, wt, map, blockIdx.x, blockIdx.y, blockIdx.z);
+}
+
+// Every convolution weight of a model in one launch (the per-step bf16 casts of the fp32
+// master weights): block b belongs to the job whose block0 is the largest <= b.
+struct CastJob {
+  const float* w;
+  uint16_t* wb;
+  uint16_t* wt;
+  int R, Cc, T, tcx, tcy;  // tiles along Cc and R
+  int64_t block0;
+  TapMap map;
+};
+
+__global__ __launch_bounds__(256) void cast_batch_kernel(const CastJob* __restrict__ jobs, int njobs) {
+  __shared__ int jsel;
+  if (threadIdx.x == 0) {
+    int lo = 0, hi = njobs - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (jobs[mid].block0 <= int64_t(blockIdx.x)) lo = mid;
+      else hi = mid - 1;
+    }
+    jsel = lo;
+  }
+  __syncthreads();
+  const CastJob& J = jobs[jsel];
+  const int64_t local = int64_t(blockIdx.x) - J.block0;
+  const int per_tap = J.tcx * J.tcy;
+  const int tap = int(local / per_tap), rem = int(local % per_tap);
+  cast_tile(J.w, J.R, J.Cc, J.T, J.wb, J.wt, J.map, rem % J.tcx, rem / J.tcx, tap);
 }
 
 void check_ptr(uintptr_t p, const char* what) {
@@ -1054,6 +1092,51 @@ int64_t conv_dgrad_strided_tiles(int Nb, int H, int W, int C, int Co, int R, int
   for (int k = 0; k < P.ncls; ++k)
     if (P.cls[k].Hc > 0 && P.cls[k].Wc > 0) t += gemm_nt_tiles(int64_t(Nb) * P.cls[k].Hc * P.cls[k].Wc);
   return t;
+}
+
+int64_t cast_job_bytes() { return int64_t(sizeof(CastJob)); }
+
+int64_t cast_jobs_build(uintptr_t host_table, const std::vector<std::array<int64_t, 10>>& specs) {
+  auto* jobs = reinterpret_cast<CastJob*>(host_table);
+  int64_t blocks = 0;
+  for (size_t k = 0; k < specs.size(); ++k) {
+    const auto& q = specs[k];
+    const int kind = int(q[0]), Co = int(q[4]), C = int(q[5]), R = int(q[6]), S = int(q[7]);
+    const int stride = int(q[8]), pad = int(q[9]);
+    CastJob J{};
+    J.w = reinterpret_cast<const float*>(q[1]);
+    J.wb = reinterpret_cast<uint16_t*>(q[2]);
+    J.wt = reinterpret_cast<uint16_t*>(q[3]);
+    J.R = Co;
+    J.Cc = C;
+    J.T = R * S;
+    if (J.T < 1 || J.T > kMaxTaps) throw std::invalid_argument("cast_jobs_build: 1 <= taps <= 49");
+    if (kind == 1) {  // strided backward-data: parity-class packed weights
+      J.map = strided_plan(2 * stride, 2 * stride, C, Co, R, S, stride, pad).map;
+    } else {  // tap-flipped transpose (a plain transpose for 1x1), or no transpose (kind 2)
+      for (int t = 0; t < J.T; ++t) {
+        J.map.base[t] = 0;
+        J.map.tc[t] = int16_t(J.T);
+        J.map.dt[t] = int16_t(J.T - 1 - t);
+      }
+      if (kind == 2) J.wt = nullptr;
+    }
+    J.tcx = (C + 31) / 32;
+    J.tcy = (Co + 31) / 32;
+    J.block0 = blocks;
+    blocks += int64_t(J.tcx) * J.tcy * J.T;
+    jobs[k] = J;
+  }
+  if (blocks > INT32_MAX) throw std::invalid_argument("cast_jobs_build: too many blocks");
+  return blocks;
+}
+
+void cast_jobs_run(int dev, hipStream_t s, uintptr_t dev_table, int njobs, int64_t nblocks) {
+  if (njobs <= 0 || nblocks <= 0) return;
+  hip_check(hipSetDevice(dev), "hipSetDevice");
+  hipLaunchKernelGGL(cast_batch_kernel, dim3(unsigned(nblocks)), dim3(256), 0, s,
+                     reinterpret_cast<const CastJob*>(dev_table), njobs);
+  hip_check(hipGetLastError(), "cast_batch launch");
 }
 
 void conv_dgrad_strided(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad,

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <array>
 #include <vector>
 
 namespace mpit {
@@ -111,6 +112,13 @@ void gemm_tn(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t Y, int64
 // fp32 w[R][T][Cc] -> bf16 wb[R][T][Cc] (optional) and bf16 tap-flipped transpose
 // wt[Cc][T-1-t][R] (optional); T = 1 is the plain transpose
 void cast_transpose(int dev, hipStream_t s, uintptr_t w, int R, int Cc, uintptr_t wb, uintptr_t wt, int taps = 1);
+// Many casts in one launch. Job spec: {kind, w, wb, wt, Co, C, R, S, stride, pad}, kind 0 =
+// cast + tap-flipped transpose (conv_weights / cast_transpose), 1 = cast + strided
+// parity-class weights (conv_dgrad_strided_weights), 2 = cast only. The table is built on the
+// host (cast_job_bytes() per job) and uploaded once; cast_jobs_run launches it.
+int64_t cast_job_bytes();
+int64_t cast_jobs_build(uintptr_t host_table, const std::vector<std::array<int64_t, 10>>& specs);
+void cast_jobs_run(int dev, hipStream_t s, uintptr_t dev_table, int njobs, int64_t nblocks);
 
 // ---- NHWC RxS convolutions as implicit GEMMs on the same MFMA kernels ----------------
 // x [Nb,H,W,C], w [Co,R,S,C] (bf16), y [Nb,Ho,Wo,Co] (bf16); stats / cin as gemm_nt.

@@ -185,14 +185,14 @@ def park_grad(x: torch.Tensor, slot: GradSlot) -> torch.Tensor:
 
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, slot=None, hold=None, link=None):
+    def forward(ctx, x, weight, slot=None, hold=None, link=None, wcast=None):
         x = _cl(x)
         if x.dtype != torch.bfloat16:
             x = x.to(torch.bfloat16)
         n, ci, h, w = x.shape
         co = weight.shape[0]
         M = n * h * w
-        wb, wt = cast_transpose(weight)
+        wb, wt = wcast if wcast is not None else cast_transpose(weight)
         y = torch.empty((n, co, h, w), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
         m = native()
         st = None
@@ -244,7 +244,7 @@ class _Conv1x1Fn(torch.autograd.Function):
             ws = torch.empty(nws, dtype=torch.float32, device=x.device) if nws else None
             m.gemm_tn(dev, s, M, co, ci, dy.data_ptr(), co, x.data_ptr(), ci, dw.data_ptr(),
                       ws.data_ptr() if ws is not None else 0, 0.0)
-        return dx, dw, None, None, None
+        return dx, dw, None, None, None, None
 
 
 def conv1x1_supported(x: torch.Tensor, weight: torch.Tensor) -> bool:
@@ -261,7 +261,7 @@ def conv1x1_supported(x: torch.Tensor, weight: torch.Tensor) -> bool:
 def conv1x1(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     """Stride-1, unpadded, bias-free 1x1 convolution (MFMA GEMM path when supported)."""
     if conv1x1_supported(x, weight):
-        return _Conv1x1Fn.apply(x, weight, None, None, None)
+        return _Conv1x1Fn.apply(x, weight, None, None, None, None)
     return F.conv2d(x, weight)
 
 
@@ -280,7 +280,8 @@ class Conv1x1(nn.Conv2d):
     def forward(self, x: torch.Tensor, slot: "GradSlot" = None) -> torch.Tensor:
         if self.fused(x):
             hold = [] if (self.emit_stats and self.training) else None
-            y = _Conv1x1Fn.apply(x, self.weight, slot, hold, _link_of(x) if torch.is_grad_enabled() else None)
+            y = _Conv1x1Fn.apply(x, self.weight, slot, hold, _link_of(x) if torch.is_grad_enabled() else None,
+                                 WeightCastPlan.cached(self))
             return _attach_stats(y, hold)
         if slot is not None:
             raise RuntimeError("GradSlot needs the MFMA path (see Conv1x1.fused)")
@@ -378,13 +379,16 @@ class _ConvFn(torch.autograd.Function):
     of the ReLU / bias is one pass over (dy, y) (csrc/kernels/act.hip)."""
 
     @staticmethod
-    def forward(ctx, x, weight, stride: int, pad: int, bias=None, relu: bool = False, hold=None, link=None):
+    def forward(ctx, x, weight, stride: int, pad: int, bias=None, relu: bool = False, hold=None, link=None,
+                wcast=None):
         x = _bf16_cl(x)
         nb, c, h, w = x.shape
         co, _, r, s = weight.shape
         ho, wo = (h + 2 * pad - r) // stride + 1, (w + 2 * pad - s) // stride + 1
         need_dx = ctx.needs_input_grad[0]
-        if need_dx and stride > 1 and strided_dgrad_supported(c, co, stride):
+        if wcast is not None:  # cast for this step by the model's WeightCastPlan
+            wb, wt = wcast
+        elif need_dx and stride > 1 and strided_dgrad_supported(c, co, stride):
             wb, wt = strided_dgrad_weights(weight, stride, pad)
         else:
             wb, wt = conv_weights(weight, dgrad=need_dx and stride == 1)
@@ -425,7 +429,7 @@ class _ConvFn(torch.autograd.Function):
             if has_bias and ctx.needs_input_grad[4]:
                 db = dy.float().sum(dim=(0, 2, 3))
         dx, dw = _conv_backward(ctx, x, wb, wt, dz, stride, pad, ctx.link)
-        return dx, dw, None, None, db, None, None, None
+        return dx, dw, None, None, db, None, None, None, None
 
 
 def conv_supported(x: torch.Tensor, weight: torch.Tensor) -> bool:
@@ -454,7 +458,8 @@ class ConvAct2d(nn.Conv2d):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.fused(x):
-            return _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0], self.bias, self.act, None, None)
+            return _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0], self.bias, self.act, None, None,
+                                 None)
         y = super().forward(x)
         return F.relu(y) if self.act else y
 
@@ -475,6 +480,82 @@ class ConvNHWC(nn.Conv2d):
         if self.fused(x):
             hold = [] if (self.emit_stats and self.training) else None
             y = _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0], None, False, hold,
-                              _link_of(x) if torch.is_grad_enabled() else None)
+                              _link_of(x) if torch.is_grad_enabled() else None, WeightCastPlan.cached(self))
             return _attach_stats(y, hold)
         return super().forward(x)
+
+
+class WeightCastPlan:
+    """bf16 copies of every MFMA convolution weight of a model, made in ONE launch per step
+    (csrc/kernels/gemm.hip ``cast_batch_kernel``) instead of one cast kernel per conv.
+
+    ``run()`` casts the current fp32 master weights into persistent bf16 buffers (plain +
+    tap-flipped transposes, or the strided parity-class weights), exactly what each
+    convolution's forward would otherwise make; until ``invalidate()`` the convolutions
+    use them. The trainer brackets its forward/backward with the two calls, so a weight
+    update in between (PS pull, optimizer) is never missed; forwards outside that window
+    cast per call as before."""
+
+    def __init__(self, model: nn.Module):
+        self.model = model
+        self.valid = False
+        self._build()
+
+    def _build(self):
+        specs, self.mods = [], []
+        m = native()
+        for mod in self.model.modules():
+            kind = None
+            if isinstance(mod, Conv1x1) and mod.stride == (1, 1):
+                kind = 0
+            elif isinstance(mod, ConvNHWC):
+                st = mod.stride[0]
+                co, c = mod.weight.shape[0], mod.weight.shape[1]
+                kind = 0 if st == 1 else (1 if strided_dgrad_supported(c, co, st) else 2)
+            if kind is None:
+                continue
+            w = mod.weight
+            if not w.is_cuda or w.dtype != torch.float32 or not w.is_contiguous(memory_format=torch.channels_last):
+                continue
+            co, c, r, sw = w.shape
+            wb = torch.empty((co, r, sw, c), dtype=torch.bfloat16, device=w.device)
+            if kind == 0:
+                wt = torch.empty((c, r, sw, co), dtype=torch.bfloat16, device=w.device)
+            elif kind == 1:
+                wt = torch.empty(m.conv_dgrad_strided_wfloats(c, co, r, sw, mod.stride[0], mod.padding[0]),
+                                 dtype=torch.bfloat16, device=w.device)
+            else:
+                wt = None
+            if isinstance(mod, Conv1x1):  # the 1x1 path takes 2-D [co, ci] / [ci, co] views
+                wb, wt = wb.view(co, c), wt.view(c, co)
+            specs.append([kind, w.data_ptr(), wb.data_ptr(), wt.data_ptr() if wt is not None else 0, co, c, r, sw,
+                          mod.stride[0], mod.padding[0]])
+            self.mods.append((mod, w.data_ptr(), (wb, wt)))
+        self.njobs = len(specs)
+        self.table = None
+        if specs:
+            host = torch.empty(self.njobs * m.cast_job_bytes(), dtype=torch.uint8)
+            self.nblocks = m.cast_jobs_build(host.data_ptr(), specs)
+            self.table = host.to(self.mods[0][0].weight.device)
+
+    def run(self):
+        if any(mod.weight.data_ptr() != ptr for mod, ptr, _ in self.mods):
+            self._build()  # parameters moved (FlatParams.rebind)
+        if self.table is not None:
+            dev = self.table.device
+            native().cast_jobs_run(dev.index, torch.cuda.current_stream(dev).cuda_stream, self.table.data_ptr(),
+                                   self.njobs, self.nblocks)
+        for mod, _, pair in self.mods:
+            mod._mpit_wcast = (self, pair)
+        self.valid = True
+
+    def invalidate(self):
+        self.valid = False
+
+    @staticmethod
+    def cached(mod):
+        """The (wb, wt) cast for ``mod`` by a valid plan, else None."""
+        c = getattr(mod, "_mpit_wcast", None)
+        if c is None or not c[0].valid:
+            return None
+        return c[1]

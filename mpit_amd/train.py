@@ -92,6 +92,13 @@ class Trainer:
                       and cfg.extra.get("steal_grads", True))
         if self.steal:
             self.flat.steal_grads()
+        # bf16 casts of every MFMA conv weight in one launch per step (ops/conv.py)
+        self.wcast = None
+        if self.on_gpu and cfg.extra.get("batched_weight_casts", True):
+            from .ops.conv import WeightCastPlan
+
+            plan = WeightCastPlan(self.model)
+            self.wcast = plan if plan.njobs else None
         self.steps = 0
 
     # ------------------------------------------------------------------ setup
@@ -152,14 +159,20 @@ class Trainer:
     def _feval(self, w):
         if not getattr(self, "steal", False):
             self.flat.zero_grad()
-        if self.on_gpu and self.cfg.amp:
-            with torch.autocast("cuda", dtype=torch.bfloat16):
+        if self.wcast is not None:  # the weights as they are now, for this forward/backward only
+            self.wcast.run()
+        try:
+            if self.on_gpu and self.cfg.amp:
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    out = self.model(self.x)
+                loss = F.cross_entropy(out.float(), self.y)
+            else:
                 out = self.model(self.x)
-            loss = F.cross_entropy(out.float(), self.y)
-        else:
-            out = self.model(self.x)
-            loss = F.nll_loss(out, self.y) if self.cfg.model in ("cnn7", "lenet") else F.cross_entropy(out, self.y)
-        loss.backward()
+                loss = F.nll_loss(out, self.y) if self.cfg.model in ("cnn7", "lenet") else F.cross_entropy(out, self.y)
+            loss.backward()
+        finally:
+            if self.wcast is not None:
+                self.wcast.invalidate()
         if getattr(self, "steal", False):
             return loss.detach(), self.flat.stolen()
         return loss.detach(), self.flat.grad

@@ -135,3 +135,39 @@ def test_chained_blocks_fold_bn_passes(stride):
     print(errs)
     for k, (fused, lib) in errs.items():
         assert fused < 1.5 * lib + 1e-2, (k, fused, lib)
+
+
+@pytest.mark.gpu
+def test_weight_cast_plan_matches_per_call_casts():
+    """One batched launch produces exactly the bf16 weights (plain, tap-flipped transposes,
+    strided parity classes) the convolutions would cast per call."""
+    from mpit_amd.ops import conv as C
+
+    torch.manual_seed(3)
+    down = torch.nn.Sequential(conv1x1(256, 512, 2), BatchNormAct2d(512, act=False))
+    net = torch.nn.Sequential(Bottleneck(256, 128, 2, down), Bottleneck(512, 128)).cuda().to(
+        memory_format=torch.channels_last)
+    plan = C.WeightCastPlan(net)
+    assert plan.njobs == 7
+    plan.run()
+    for mod, _, (wb, wt) in plan.mods:
+        w = mod.weight
+        if isinstance(mod, C.Conv1x1):
+            rb, rt = C.cast_transpose(w)
+        elif mod.stride[0] > 1 and C.strided_dgrad_supported(w.shape[1], w.shape[0], mod.stride[0]):
+            rb, rt = C.strided_dgrad_weights(w, mod.stride[0], mod.padding[0])
+        elif mod.stride[0] > 1:
+            rb, rt = C.conv_weights(w, dgrad=False)
+        else:
+            rb, rt = C.conv_weights(w, dgrad=True)
+        assert torch.equal(wb.view(-1), rb.reshape(-1))
+        assert (wt is None) == (rt is None)
+        if wt is not None:
+            assert torch.equal(wt.view(-1), rt.reshape(-1))
+    # a forward inside the plan's window uses the cast weights and gives the same output
+    x = torch.randn(2, 256, 14, 14, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y1 = net(x)
+        plan.invalidate()
+        y2 = net(x)
+    assert torch.equal(y1, y2)

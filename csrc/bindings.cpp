@@ -305,6 +305,7 @@ PYBIND11_MODULE(_mpit, m) {
       .def(py::init<Engine&, int, std::vector<int>, std::vector<int64_t>, std::vector<int64_t>>(), py::keep_alive<1, 2>())
       .def("start", &PSClient::start)
       .def("send_grad", [](PSClient& c, uintptr_t s, bool pull) { c.send_grad(S(s), pull); })
+      .def("send_grad_to", [](PSClient& c, uintptr_t s, int k, bool pull) { c.send_grad_to(S(s), k, pull); })
       .def("recv_param", [](PSClient& c, uintptr_t s) { c.recv_param(S(s)); })
       .def("send_param", [](PSClient& c, uintptr_t s) { c.send_param(S(s)); })
       .def("stop", &PSClient::stop, py::call_guard<py::gil_scoped_release>())

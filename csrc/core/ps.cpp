@@ -471,6 +471,15 @@ void PSClient::send_grad(hipStream_t s, bool with_pull) {
   });
 }
 
+void PSClient::send_grad_to(hipStream_t s, int k, bool with_pull) {
+  if (k < 0 || k >= int(servers_.size())) throw std::out_of_range("PSClient::send_grad_to: bad shard");
+  pending_.fetch_add(with_pull ? 2 : 1);
+  const int srv = servers_[k];
+  gate(s, [this, srv, with_pull] {
+    eng_.send_am(srv, ps_am_id(ps_id_, kTagGrad), nullptr, 0, with_pull ? kPsWithPull : 0);
+  });
+}
+
 void PSClient::recv_param(hipStream_t s) {
   pending_.fetch_add(int64_t(servers_.size()));
   // ordered behind any gated push of this client

@@ -143,6 +143,9 @@ class PSClient {
   ~PSClient();
   void start();            // register reply handlers, send shard info (tag 1)
   void send_grad(hipStream_t s, bool with_pull);  // gated on the work queued on s
+  // the same for ONE shard (server index k): pushes overlapped with the backward as soon
+  // as a shard's gradients are complete
+  void send_grad_to(hipStream_t s, int k, bool with_pull);
   void recv_param(hipStream_t s);  // tag 5 header -> tag 3 once the shard landed in rx;
                                    // gated on s when rx is still being read there
   void send_param(hipStream_t s);

@@ -66,6 +66,20 @@ def downpour(opfunc, w, config, state=None):
     state.setdefault("dusync", 0.0)
     if lrd != 0:
         lr = lr / (1 + pv * lrd)
+    pusher = config.get("pusher")
+    if pusher is not None and pc is not None and su == 1:
+        # shards pushed (with their pulls) from inside the backward as they complete
+        # (parallel/overlap.py); what is left here is the last shards' round trip
+        pusher.arm(-lr * gscale, w if l2wd else None, -lr * l2wd)
+        try:
+            fx, _ = opfunc(w)
+        finally:
+            pusher.finish()
+        t0 = time.perf_counter()
+        pc.wait()
+        state["dusync"] += time.perf_counter() - t0
+        state["pversion"] = pv + 1
+        return w, [fx]
     fx, dfdx = opfunc(w)
     from ..utils.flat import StolenGrads
 

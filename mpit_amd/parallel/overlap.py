@@ -1,0 +1,99 @@
+"""Downpour pushes overlapped with the backward pass, shard by shard.
+
+The reference pushes the whole gradient after the backward and waits for the pulls
+(asyncsgd/optim-downpour.lua:48-53). Here the flat parameter vector is split into the
+servers' contiguous shards (asyncsgd/pclient.lua:116-128) and the backward produces
+gradients last layer first, so the shards holding the last layers are complete long
+before the backward ends. :class:`ShardPusher` watches the parameters with
+post-accumulate-grad hooks; when every parameter overlapping shard k has its gradient it
+gathers them into the push window with the Downpour scale (K12+K9, one launch) and sends
+that shard with a fused pull, gated on an event of the compute stream. The servers apply
+the update and write the refreshed shard back while the backward of the earlier layers
+is still running, so only the last shard's round trip is left to wait for.
+
+Safe because a shard is pushed only after every kernel that reads its parameters in
+this step has been queued ahead of the gate: the convolutions and the classifier run on
+bf16 copies made in the forward, and a BN layer reads its fp32 gamma before it emits its
+gradient.
+"""
+from __future__ import annotations
+
+from typing import List
+
+import torch
+
+from ..ops.fused import gather_scale_
+
+
+class ShardPusher:
+    def __init__(self, flat, pclient):
+        self.flat, self.pc = flat, pclient
+        ranges = [pclient.sinfo[s] for s in pclient.sranks]  # (offset, length) per shard
+        self.nshards = len(ranges)
+        self.params = list(flat.params)
+        self.spans = []  # shards each parameter overlaps
+        self.members: List[List[int]] = [[] for _ in ranges]
+        for i, (p, off) in enumerate(zip(self.params, flat.offsets)):
+            lo, hi = off, off + p.numel()
+            ks = [k for k, (so, sl) in enumerate(ranges) if lo < so + sl and so < hi]
+            self.spans.append(ks)
+            for k in ks:
+                self.members[k].append(i)
+        self.index = {id(p): i for i, p in enumerate(self.params)}
+        self.armed = False
+        self.handles = [p.register_post_accumulate_grad_hook(self._hook) for p in self.params]
+
+    def close(self):
+        for h in self.handles:
+            h.remove()
+        self.handles = []
+
+    def arm(self, a: float, aux=None, b: float = 0.0):
+        """Before the backward: gradients will be pushed as ``a*g + b*aux``."""
+        self.a, self.aux, self.b = a, aux, b
+        self.left = [len(m) for m in self.members]
+        self.gathered = [False] * len(self.params)
+        self.fired = [False] * self.nshards
+        self.armed = True
+
+    def _hook(self, p):
+        if not self.armed:
+            return
+        i = self.index[id(p)]
+        for k in self.spans[i]:
+            self.left[k] -= 1
+            if self.left[k] == 0:
+                self._fire(k)
+
+    def _fire(self, k: int):
+        srcs, offs, ns = [], [], []
+        for i in self.members[k]:
+            if self.gathered[i]:
+                continue
+            p = self.params[i]
+            g = p.grad
+            if g is None:  # unused this step: its slice of the push window is zero
+                self.pc.tx[self.flat.offsets[i]: self.flat.offsets[i] + p.numel()].zero_()
+            else:
+                if g.dim() == 4 and self.flat.channels_last:
+                    g = g.contiguous(memory_format=torch.channels_last)
+                else:
+                    g = g.contiguous()
+                srcs.append(g.data_ptr())
+                offs.append(self.flat.offsets[i])
+                ns.append(g.numel())
+                p.grad = g  # keeps the source alive until the gather is queued
+            self.gathered[i] = True
+        if srcs:
+            gather_scale_(self.pc.tx, srcs, offs, ns, self.a, self.aux, self.b)
+        for i in self.members[k]:
+            self.params[i].grad = None  # the caching allocator orders reuse on the stream
+        self.pc.async_send_grad_shard(k, pull=True)
+        self.fired[k] = True
+
+    def finish(self):
+        """After the backward: push the shards whose parameters never all got a gradient."""
+        for k in range(self.nshards):
+            if not self.fired[k]:
+                self._fire(k)
+        self.armed = False

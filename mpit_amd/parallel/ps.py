@@ -334,6 +334,13 @@ class PClient:
         if pull:
             self._pull_pending = True
 
+    def async_send_grad_shard(self, k: int, pull: bool = False):
+        """Push shard ``k`` (index into ``sranks``) of the gradient buffer only, gated on
+        the work queued so far on the current stream (see parallel/overlap.py)."""
+        self.native.send_grad_to(self._stream(), int(k), bool(pull))
+        if pull:
+            self._pull_pending = True
+
     def async_recv_param(self):
         self.native.recv_param(self._stream())
         self._pull_pending = True

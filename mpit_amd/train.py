@@ -92,6 +92,11 @@ class Trainer:
                       and cfg.extra.get("steal_grads", True))
         if self.steal:
             self.flat.steal_grads()
+            # push each shard during the backward as soon as its gradients are complete
+            if cfg.extra.get("overlap_push", True):
+                from .parallel.overlap import ShardPusher
+
+                self.opt_config["pusher"] = ShardPusher(self.flat, self.pc)
         # bf16 casts of every MFMA conv weight in one launch per step (ops/conv.py)
         self.wcast = None
         if self.on_gpu and cfg.extra.get("batched_weight_casts", True):

@@ -39,6 +39,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <array>
 #include <vector>
 #include <stdexcept>
@@ -804,7 +805,12 @@ static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t
   const int rl = relu ? 1 : 0;
   const ConvGeo g = geo ? *geo : ConvGeo{};
   const int nk = K / kBK;
-  const int stages = nk >= 4 ? 4 : (nk == 3 ? 3 : 2);
+  // MPIT_GEMM_STAGES caps the ring depth (A/B measurements)
+  static const int max_stages = [] {
+    const char* e = std::getenv("MPIT_GEMM_STAGES");
+    return e ? std::max(2, std::min(4, std::atoi(e))) : 2;
+  }();
+  const int stages = std::min(max_stages, nk >= 4 ? 4 : (nk == 3 ? 3 : 2));
   // (kernel templates are named at a non-template call site so their host stubs are emitted)
 #define MPIT_NT_LAUNCH1(BM, BN, ST, EPI, CONV)                                                                    \
   hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, ST, EPI, CONV>), dim3(unsigned(nb)), dim3(BM / 64 * 128), shm, s, a, \
@@ -921,10 +927,14 @@ static void launch_tn(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t
   const auto* x = reinterpret_cast<const uint16_t*>(X);
   const ConvGeo g = geo ? *geo : ConvGeo{};
   const dim3 grid(unsigned(int64_t(ntiles) * ns));
-  constexpr int ST = 4;
-  const size_t shm = size_t(ST) * kRows * (tbn + tbk) * sizeof(uint16_t);
-#define MPIT_TN_LAUNCH(A, B)                                                                                       \
+  // MPIT_GEMM_TN_STAGES: ring depth (A/B measurements; 4 by default)
+  static const int tn_stages = [] {
+    const char* e = std::getenv("MPIT_GEMM_TN_STAGES");
+    return e && std::atoi(e) <= 2 ? 2 : 4;
+  }();
+#define MPIT_TN_LAUNCH1(A, B, ST)                                                                                  \
   do {                                                                                                             \
+    const size_t shm = size_t(ST) * kRows * (tbn + tbk) * sizeof(uint16_t);                                      \
     if (geo)                                                                                                       \
       hipLaunchKernelGGL((gemm_tn_kernel<A, B, ST, true>), grid, dim3(256), shm, s, y, ldy, x, ldx, part, M, N, K, \
                          rps, ntk, ntiles, g);                                                                     \
@@ -932,11 +942,17 @@ static void launch_tn(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t
       hipLaunchKernelGGL((gemm_tn_kernel<A, B, ST, false>), grid, dim3(256), shm, s, y, ldy, x, ldx, part, M, N,  \
                          K, rps, ntk, ntiles, g);                                                                  \
   } while (0)
+#define MPIT_TN_LAUNCH(A, B)               \
+  do {                                     \
+    if (tn_stages == 2) MPIT_TN_LAUNCH1(A, B, 2); \
+    else MPIT_TN_LAUNCH1(A, B, 4);         \
+  } while (0)
   if (tbn == 128 && tbk == 128) MPIT_TN_LAUNCH(128, 128);
   else if (tbn == 128) MPIT_TN_LAUNCH(128, 64);
   else if (tbk == 128) MPIT_TN_LAUNCH(64, 128);
   else MPIT_TN_LAUNCH(64, 64);
 #undef MPIT_TN_LAUNCH
+#undef MPIT_TN_LAUNCH1
   hip_check(hipGetLastError(), "gemm_tn launch");
   if (!direct) {
     const int64_t n4 = int64_t(N) * K / 4;

@@ -150,7 +150,7 @@ __device__ __forceinline__ int xcd_tile(int bid, int nb) {
 // is lane-linear per wave instruction (16 rows x 64 B); the swizzle is applied on the
 // global source address.
 template <int BM, int BN, int STAGES, int EPI, bool CONV>
-__global__ __launch_bounds__(BM / 64 * 128, BM == 256 ? 1 : 2) void gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda,
+__global__ __launch_bounds__(BM / 64 * 128, BM == 256 ? 1 : (STAGES == 2 ? (CONV ? 4 : 5) : 2)) void gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda,
                                                          const uint16_t* __restrict__ B, int64_t ldb,
                                                          uint16_t* C, int64_t ldc, int64_t M, int N, int K,
                                                          int ntn, EpiArgs ep, const uint16_t* Cin,
@@ -275,7 +275,10 @@ __global__ __launch_bounds__(BM / 64 * 128, BM == 256 ? 1 : 2) void gemm_nt_kern
   // ---- epilogue, phase A: accumulators (+ bias, ReLU) -> bf16 tile in LDS. Lane holds
   // D[n][m] with m = lane&31, n = (v&3) + 8*(v>>2) + 4*(lane>>5): 4 consecutive columns of
   // one row, one 8-B LDS store each.
-  constexpr int LDT = BN + 8;  // LDS row stride (elements): 16-B aligned rows
+  // Unpadded rows (the tile fits in the 2-slot ring, keeping 5 blocks/CU possible); the
+  // 16-B chunk index is XOR-swizzled by the row so phase A's column writes spread over banks
+  constexpr int LDT = BN, CPRS = BN / 8;
+  auto tsw = [](int row, int n) { return row * LDT + (((n >> 3) ^ (row % CPRS)) << 3) + (n & 7); };
   uint16_t* tl = smem;         // reuses the ring
   __syncthreads();             // every wave is done reading the ring
 #pragma unroll
@@ -298,7 +301,7 @@ __global__ __launch_bounds__(BM / 64 * 128, BM == 256 ? 1 : 2) void gemm_nt_kern
         }
         const uint32_t lo = uint32_t(f2bf(acc[i][j][4 * g])) | (uint32_t(f2bf(acc[i][j][4 * g + 1])) << 16);
         const uint32_t hi = uint32_t(f2bf(acc[i][j][4 * g + 2])) | (uint32_t(f2bf(acc[i][j][4 * g + 3])) << 16);
-        *reinterpret_cast<uint2*>(tl + (wm * WM + i * 32 + fr) * LDT + nl) = make_uint2(lo, hi);
+        *reinterpret_cast<uint2*>(tl + tsw(wm * WM + i * 32 + fr, nl)) = make_uint2(lo, hi);
       }
   __syncthreads();
 
@@ -322,46 +325,51 @@ __global__ __launch_bounds__(BM / 64 * 128, BM == 256 ? 1 : 2) void gemm_nt_kern
     mu[0] = a0.x; mu[1] = a0.y; mu[2] = a0.z; mu[3] = a0.w;
     mu[4] = a1.x; mu[5] = a1.y; mu[6] = a1.z; mu[7] = a1.w;
   }
-  // all loads of the thread's NP rows are issued before its first store (C may alias
-  // Cin, so the compiler would otherwise serialise load -> store per row)
-  int64_t orow[NP];
-  uint4 cv[NP], xq[NP];
-  uint32_t cmb[NP], xmb[NP];
+  // Rows go in batches of PB: all loads of a batch are issued before its first store (C
+  // may alias Cin, so the compiler would otherwise serialise load -> store per row), and
+  // batches keep the live registers low enough for 5 resident blocks per CU.
+  constexpr int PB = NP < 4 ? NP : 4;
 #pragma unroll
-  for (int p = 0; p < NP; ++p) {
+  for (int pb = 0; pb < NP; pb += PB) {
+  int64_t orow[PB];
+  uint4 cv[PB], xq[PB];
+  uint32_t cmb[PB], xmb[PB];
+#pragma unroll
+  for (int q = 0; q < PB; ++q) {
+    const int p = pb + q;
     const int64_t m = m0 + rr + p * RPH;
-    orow[p] = m;  // output row (pixel) of GEMM row m
+    orow[q] = m;  // output row (pixel) of GEMM row m
     if constexpr (CONV) {
       if (geo.ostr > 1) {
         const int hw = geo.Ho * geo.Wo;
         const int64_t nimg = m / hw;
         const int rem = int(m - nimg * hw), gi = rem / geo.Wo, gj = rem - gi * geo.Wo;
-        orow[p] = (nimg * geo.OH + gi * geo.ostr + geo.oph) * geo.OW + gj * geo.ostr + geo.opw;
+        orow[q] = (nimg * geo.OH + gi * geo.ostr + geo.oph) * geo.OW + gj * geo.ostr + geo.opw;
       }
     }
     const bool ok = m < M;
-    const int64_t o = orow[p] * ldc + nc;
+    const int64_t o = orow[q] * ldc + nc;
     if (Cin != nullptr) {
-      cv[p] = ok ? *reinterpret_cast<const uint4*>(Cin + o) : make_uint4(0, 0, 0, 0);
-      cmb[p] = Cmask ? (ok ? uint32_t(Cmask[o >> 3]) : 0u) : 0xffu;
+      cv[q] = ok ? *reinterpret_cast<const uint4*>(Cin + o) : make_uint4(0, 0, 0, 0);
+      cmb[q] = Cmask ? (ok ? uint32_t(Cmask[o >> 3]) : 0u) : 0xffu;
     }
     if constexpr (EPI == EPI_BNRED) {
-      xq[p] = ok ? *reinterpret_cast<const uint4*>(ep.x + o) : make_uint4(0, 0, 0, 0);
-      xmb[p] = ok ? (ep.mask ? uint32_t(ep.mask[o >> 3]) : 0xffu) : 0u;
+      xq[q] = ok ? *reinterpret_cast<const uint4*>(ep.x + o) : make_uint4(0, 0, 0, 0);
+      xmb[q] = ok ? (ep.mask ? uint32_t(ep.mask[o >> 3]) : 0xffu) : 0u;
     }
   }
 #pragma unroll
-  for (int p = 0; p < NP; ++p) {
-    const int rl = rr + p * RPH;
+  for (int q = 0; q < PB; ++q) {
+    const int rl = rr + (pb + q) * RPH;
     if (m0 + rl >= M) continue;
-    const int64_t o = orow[p] * ldc + nc;
-    const uint4 hv = *reinterpret_cast<const uint4*>(tl + rl * LDT + ch * 8);
+    const int64_t o = orow[q] * ldc + nc;
+    const uint4 hv = *reinterpret_cast<const uint4*>(tl + tsw(rl, ch * 8));
     uint32_t hw4[4] = {hv.x, hv.y, hv.z, hv.w};
     if (Cin != nullptr) {  // C = A.B^T + Cin
       // Cmask: Cin is a ReLU'd gradient given as (dy, forward bit mask: one byte per 8
       // channels, bit e = channel 8k+e positive) — dy*mask is never materialised
-      const uint32_t mb = cmb[p];
-      const uint32_t cw[4] = {cv[p].x, cv[p].y, cv[p].z, cv[p].w};
+      const uint32_t mb = cmb[q];
+      const uint32_t cw[4] = {cv[q].x, cv[q].y, cv[q].z, cv[q].w};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const float v0 = bf2f(uint16_t(hw4[q] & 0xffff)) + ((mb >> (2 * q)) & 1u ? bf2f(uint16_t(cw[q] & 0xffff)) : 0.f);
@@ -372,7 +380,7 @@ __global__ __launch_bounds__(BM / 64 * 128, BM == 256 ? 1 : 2) void gemm_nt_kern
     *reinterpret_cast<uint4*>(C + o) = make_uint4(hw4[0], hw4[1], hw4[2], hw4[3]);
     if constexpr (CONV) {
       if (geo.ozero) {  // class (0,0) of a stride-2 conv whose other parities have no taps
-        const int64_t pix = orow[p] % (int64_t(geo.OH) * geo.OW);
+        const int64_t pix = orow[q] % (int64_t(geo.OH) * geo.OW);
         const int oh = int(pix / geo.OW), ow = int(pix % geo.OW);
         const uint4 z = make_uint4(0, 0, 0, 0);
         if (ow + 1 < geo.OW) *reinterpret_cast<uint4*>(C + o + ldc) = z;
@@ -393,8 +401,8 @@ __global__ __launch_bounds__(BM / 64 * 128, BM == 256 ? 1 : 2) void gemm_nt_kern
       }
       ++nv;
     } else if constexpr (EPI == EPI_BNRED) {  // dz = C * mask; (sum dz, sum dz (x - mean))
-      const uint32_t xb = xmb[p];
-      const uint32_t xw[4] = {xq[p].x, xq[p].y, xq[p].z, xq[p].w};
+      const uint32_t xb = xmb[q];
+      const uint32_t xw[4] = {xq[q].x, xq[q].y, xq[q].z, xq[q].w};
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const uint32_t hwd = hw4[e >> 1], xwd = xw[e >> 1];
@@ -404,6 +412,7 @@ __global__ __launch_bounds__(BM / 64 * 128, BM == 256 ? 1 : 2) void gemm_nt_kern
         s2[e] = fmaf(dz, xe - mu[e], s2[e]);
       }
     }
+  }
   }
   if constexpr (EPI != EPI_NONE) {
     // combine the RPP threads of each chunk through LDS: [RPP][3][BN] floats
@@ -828,7 +837,7 @@ static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t
     const int64_t nb = mtn * ntn;                                                                              \
     if (nb > INT32_MAX) throw std::invalid_argument("gemm_nt: too many tiles");                               \
     /* LDS: the k-tile ring, reused by the epilogue's bf16 tile and reduction table */                        \
-    const size_t shm = std::max({size_t(ST) * (BM + BN) * kBK * 2, size_t(BM) * (BN + 8) * 2,                  \
+    const size_t shm = std::max({size_t(ST) * (BM + BN) * kBK * 2, size_t(BM) * BN * 2,                        \
                                  size_t(BM / 64 * 128) * 8 * 3 * sizeof(float)});                             \
     if (geo) MPIT_NT_LAUNCH2(BM, BN, ST, true);                                                                \
     else MPIT_NT_LAUNCH2(BM, BN, ST, false);                                                                   \

@@ -211,7 +211,7 @@ __device__ __forceinline__ void fin_fwd_channel(int c, double a, double b, int C
 //        shifted sums bn_finalize_fwd_kernel expects (shift = row 0 of x), fp64 inside;
 //   plain (backward reductions): tile sums are added.
 constexpr int kTileRows = 128;
-constexpr int kTileLanes = 4;     // row lanes per channel (64 channels x 4 = 256 threads)
+constexpr int kTileLanes = 16;    // row lanes per channel (64 channels x 16 = 1024 threads)
 constexpr int kTicketSlots = 64;  // rotating ticket sets (one per launch in flight)
 constexpr int kMaxChBlocks = 32;  // C <= 2048
 
@@ -319,9 +319,10 @@ __global__ __launch_bounds__(64 * kTileLanes) void bn_tiles_finalize_kernel(cons
     fin_bwd_channel(c, a, b, C, M, fa.gamma, fa.mean, fa.rstd, fa.dgamma, fa.dbeta, fa.coef);
 }
 
-// groups for level 1: >= 16 tile rows each, at most 64 (the last group combines them all)
+// groups for level 1: >= 32 tile rows each (2 per lane), at most 128 (the last group
+// combines them all, 8 per lane)
 int tile_groups(int64_t nt, int* rows_per_group) {
-  int g = int(std::min<int64_t>(64, std::max<int64_t>(1, (nt + 15) / 16)));
+  int g = int(std::min<int64_t>(128, std::max<int64_t>(1, (nt + 31) / 32)));
   *rows_per_group = int((nt + g - 1) / g);
   g = int((nt + *rows_per_group - 1) / *rows_per_group);
   return g;

@@ -62,12 +62,24 @@ __global__ __launch_bounds__(1024) void relu_bias_bwd_kernel(const uint16_t* __r
   }
 }
 
-__global__ __launch_bounds__(256) void sum_parts_kernel(const float* __restrict__ part, int nb, int C,
-                                                        float* __restrict__ out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// Combine the per-block partials: a block owns 64 channels, 16 lanes per channel stride
+// over the partial rows (coalesced 256-B rows, many loads in flight), then fixed-order
+// combine in LDS (deterministic).
+constexpr int kSumCh = 64, kSumLanes = 16;
+__global__ __launch_bounds__(kSumCh * kSumLanes) void sum_parts_kernel(const float* __restrict__ part, int nb, int C,
+                                                                       float* __restrict__ out) {
+  __shared__ float sm[kSumLanes][kSumCh];
+  const int cl = threadIdx.x % kSumCh, kl = threadIdx.x / kSumCh;
+  const int c = blockIdx.x * kSumCh + cl;
   float s = 0.f;
-  for (int k = 0; k < nb; ++k) s += part[int64_t(k) * C + c];
+  if (c < C) {
+#pragma unroll 8
+    for (int k = kl; k < nb; k += kSumLanes) s += part[int64_t(k) * C + c];
+  }
+  sm[kl][cl] = s;
+  __syncthreads();
+  if (kl != 0 || c >= C) return;
+  for (int k = 1; k < kSumLanes; ++k) s += sm[k][cl];
   out[c] = s;
 }
 
@@ -93,8 +105,8 @@ void relu_bias_bwd(int dev, hipStream_t s, int64_t M, int C, uintptr_t dy, uintp
                      reinterpret_cast<const uint16_t*>(y), reinterpret_cast<uint16_t*>(dz), M, C, rpb, part);
   hip_check(hipGetLastError(), "relu_bias_bwd launch");
   if (db) {
-    hipLaunchKernelGGL(sum_parts_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, int(nb), C,
-                       reinterpret_cast<float*>(db));
+    hipLaunchKernelGGL(sum_parts_kernel, dim3((C + kSumCh - 1) / kSumCh), dim3(kSumCh * kSumLanes), 0, s, part,
+                       int(nb), C, reinterpret_cast<float*>(db));
     hip_check(hipGetLastError(), "relu_bias_bwd sum launch");
   }
 }

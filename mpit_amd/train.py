@@ -88,10 +88,15 @@ class Trainer:
             self._start_ps()
         # Downpour su=1 on the GPU: let autograd hand over its gradient tensors and gather
         # them into the push window in one fused kernel (utils/flat.py StolenGrads)
-        self.steal = (self.on_gpu and cfg.optimizer == "downpour" and cfg.su <= 1 and self.pc is not None
-                      and cfg.extra.get("steal_grads", True))
+        # The other GPU optimizers (EASGD / MSGD / Downpour su > 1) steal too: one gather into
+        # the flat gradient replaces its memset plus one "grad += new" kernel per parameter.
+        self.push_steal = (self.on_gpu and cfg.optimizer == "downpour" and cfg.su <= 1 and self.pc is not None
+                           and cfg.extra.get("steal_grads", True))
+        self.steal = self.push_steal or (self.on_gpu and cfg.optimizer != "allreduce"
+                                         and cfg.extra.get("steal_grads", True))
         if self.steal:
             self.flat.steal_grads()
+        if self.push_steal:
             # push each shard during the backward as soon as its gradients are complete
             if cfg.extra.get("overlap_push", True):
                 from .parallel.overlap import ShardPusher
@@ -178,8 +183,10 @@ class Trainer:
         finally:
             if self.wcast is not None:
                 self.wcast.invalidate()
+        if getattr(self, "push_steal", False):
+            return loss.detach(), self.flat.stolen()  # gathered straight into the push window
         if getattr(self, "steal", False):
-            return loss.detach(), self.flat.stolen()
+            return loss.detach(), self.flat.stolen().materialize()
         return loss.detach(), self.flat.grad
 
     def step(self):

@@ -93,6 +93,13 @@ PYBIND11_MODULE(_mpit, m) {
       py::arg("dev"), py::arg("stream"), py::arg("bf16"), py::arg("dy"), py::arg("mask"), py::arg("x"), py::arg("dx"),
       py::arg("dres"), py::arg("M"), py::arg("C"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
       py::arg("dgamma"), py::arg("dbeta"), py::arg("ws"), py::arg("relu"), py::arg("part") = 0, py::arg("npart") = 0);
+  m.def("bn_pair_apply", [](int dev, uintptr_t s, uintptr_t x1, uintptr_t coef1, uintptr_t x2, uintptr_t coef2,
+                            uintptr_t y, int64_t M, int C,
+                            uintptr_t mask) { bn_pair_apply(dev, S(s), x1, coef1, x2, coef2, y, M, C, mask); });
+  m.def("bn_pair_bwd_apply", [](int dev, uintptr_t s, uintptr_t dy, uintptr_t mask, uintptr_t x1, uintptr_t coef1,
+                                uintptr_t dx1, uintptr_t x2, uintptr_t coef2, uintptr_t dx2, int64_t M, int C) {
+    bn_pair_bwd_apply(dev, S(s), dy, mask, x1, coef1, dx1, x2, coef2, dx2, M, C);
+  });
   m.def("gemm_nt_supported", &gemm_nt_supported);
   m.def("gemm_nt_stats_floats", &gemm_nt_stats_floats);
   m.def("gemm_nt_tiles", &gemm_nt_tiles);
@@ -100,14 +107,16 @@ PYBIND11_MODULE(_mpit, m) {
       "gemm_nt",
       [](int dev, uintptr_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B, int64_t ldb, uintptr_t C,
          int64_t ldc, uintptr_t stats, uintptr_t cin, uintptr_t cmask, uintptr_t red_part, uintptr_t red_x,
-         uintptr_t red_mask, uintptr_t red_mean, int64_t red_row0) {
-        const BnRed r{red_part, red_x, red_mask, red_mean, red_row0};
+         uintptr_t red_mask, uintptr_t red_mean, int64_t red_row0, uintptr_t red_part2, uintptr_t red_x2,
+         uintptr_t red_mean2) {
+        const BnRed r{red_part, red_x, red_mask, red_mean, red_row0, red_part2, red_x2, red_mean2};
         gemm_nt(dev, S(s), M, N, K, A, lda, B, ldb, C, ldc, stats, cin, cmask, &r);
       },
       py::arg("dev"), py::arg("stream"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("A"), py::arg("lda"),
       py::arg("B"), py::arg("ldb"), py::arg("C"), py::arg("ldc"), py::arg("stats") = 0, py::arg("cin") = 0,
       py::arg("cmask") = 0, py::arg("red_part") = 0, py::arg("red_x") = 0, py::arg("red_mask") = 0,
-      py::arg("red_mean") = 0, py::arg("red_row0") = 0);
+      py::arg("red_mean") = 0, py::arg("red_row0") = 0, py::arg("red_part2") = 0, py::arg("red_x2") = 0,
+      py::arg("red_mean2") = 0);
   m.def("gemm_tn_supported", &gemm_tn_supported);
   m.def("gemm_tn_ws_floats", &gemm_tn_ws_floats);
   m.def("gemm_tn", [](int dev, uintptr_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X, int64_t ldx,
@@ -135,14 +144,16 @@ PYBIND11_MODULE(_mpit, m) {
       "conv_fwd",
       [](int dev, uintptr_t s, int Nb, int H, int W, int C, int Co, int R, int S_, int stride, int pad, uintptr_t x,
          uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t cin, uintptr_t bias, bool relu, uintptr_t red_part,
-         uintptr_t red_x, uintptr_t red_mask, uintptr_t red_mean, int64_t red_row0) {
-        const BnRed r{red_part, red_x, red_mask, red_mean, red_row0};
+         uintptr_t red_x, uintptr_t red_mask, uintptr_t red_mean, int64_t red_row0, uintptr_t red_part2,
+         uintptr_t red_x2, uintptr_t red_mean2) {
+        const BnRed r{red_part, red_x, red_mask, red_mean, red_row0, red_part2, red_x2, red_mean2};
         conv_fwd(dev, S(s), Nb, H, W, C, Co, R, S_, stride, pad, x, w, y, stats, cin, bias, relu, &r);
       },
       py::arg("dev"), py::arg("stream"), py::arg("Nb"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("Co"),
       py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("x"), py::arg("w"), py::arg("y"),
       py::arg("stats") = 0, py::arg("cin") = 0, py::arg("bias") = 0, py::arg("relu") = false, py::arg("red_part") = 0,
-      py::arg("red_x") = 0, py::arg("red_mask") = 0, py::arg("red_mean") = 0, py::arg("red_row0") = 0);
+      py::arg("red_x") = 0, py::arg("red_mask") = 0, py::arg("red_mean") = 0, py::arg("red_row0") = 0,
+      py::arg("red_part2") = 0, py::arg("red_x2") = 0, py::arg("red_mean2") = 0);
   m.def("conv_dgrad_strided_wfloats", &conv_dgrad_strided_wfloats);
   m.def("conv_dgrad_strided_weights", [](int dev, uintptr_t s, uintptr_t w, int Co, int C, int R, int S_, int stride,
                                          int pad, uintptr_t wb, uintptr_t wcls) {
@@ -152,13 +163,15 @@ PYBIND11_MODULE(_mpit, m) {
   m.def(
       "conv_dgrad_strided",
       [](int dev, uintptr_t s, int Nb, int H, int W, int C, int Co, int R, int S_, int stride, int pad, uintptr_t dy,
-         uintptr_t wcls, uintptr_t dx, uintptr_t red_part, uintptr_t red_x, uintptr_t red_mask, uintptr_t red_mean) {
-        const BnRed r{red_part, red_x, red_mask, red_mean, 0};
+         uintptr_t wcls, uintptr_t dx, uintptr_t red_part, uintptr_t red_x, uintptr_t red_mask, uintptr_t red_mean,
+         uintptr_t red_part2, uintptr_t red_x2, uintptr_t red_mean2) {
+        const BnRed r{red_part, red_x, red_mask, red_mean, 0, red_part2, red_x2, red_mean2};
         conv_dgrad_strided(dev, S(s), Nb, H, W, C, Co, R, S_, stride, pad, dy, wcls, dx, &r);
       },
       py::arg("dev"), py::arg("stream"), py::arg("Nb"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("Co"),
       py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("dy"), py::arg("wcls"), py::arg("dx"),
-      py::arg("red_part") = 0, py::arg("red_x") = 0, py::arg("red_mask") = 0, py::arg("red_mean") = 0);
+      py::arg("red_part") = 0, py::arg("red_x") = 0, py::arg("red_mask") = 0, py::arg("red_mean") = 0,
+      py::arg("red_part2") = 0, py::arg("red_x2") = 0, py::arg("red_mean2") = 0);
   m.def("relu_bias_bwd_ws_floats", &relu_bias_bwd_ws_floats);
   m.def("relu_bias_bwd", [](int dev, uintptr_t s, int64_t M, int C, uintptr_t dy, uintptr_t y, uintptr_t dz, uintptr_t db,
                             uintptr_t ws) { relu_bias_bwd(dev, S(s), M, C, dy, y, dz, db, ws); });

@@ -65,27 +65,30 @@ __global__ __launch_bounds__(1024) void relu_bias_bwd_kernel(const uint16_t* __r
 // Combine the per-block partials: a block owns 64 channels, 16 lanes per channel stride
 // over the partial rows (coalesced 256-B rows, many loads in flight), then fixed-order
 // combine in LDS (deterministic).
-constexpr int kSumCh = 64, kSumLanes = 16;
+// Two launches for many partial rows: blockIdx.y splits the rows into gridDim.y groups
+// (level 1 writes [groups][C]), the second launch combines the groups.
+constexpr int kSumCh = 64, kSumLanes = 16, kSumGroups = 16;
 __global__ __launch_bounds__(kSumCh * kSumLanes) void sum_parts_kernel(const float* __restrict__ part, int nb, int C,
                                                                        float* __restrict__ out) {
   __shared__ float sm[kSumLanes][kSumCh];
   const int cl = threadIdx.x % kSumCh, kl = threadIdx.x / kSumCh;
   const int c = blockIdx.x * kSumCh + cl;
+  const int per = (nb + gridDim.y - 1) / gridDim.y, r0 = blockIdx.y * per, r1 = min(nb, r0 + per);
   float s = 0.f;
   if (c < C) {
 #pragma unroll 8
-    for (int k = kl; k < nb; k += kSumLanes) s += part[int64_t(k) * C + c];
+    for (int k = r0 + kl; k < r1; k += kSumLanes) s += part[int64_t(k) * C + c];
   }
   sm[kl][cl] = s;
   __syncthreads();
   if (kl != 0 || c >= C) return;
   for (int k = 1; k < kSumLanes; ++k) s += sm[k][cl];
-  out[c] = s;
+  out[int64_t(blockIdx.y) * C + c] = s;
 }
 
 }  // namespace
 
-int64_t relu_bias_bwd_ws_floats(int C) { return int64_t(kMaxBlocks) * C; }
+int64_t relu_bias_bwd_ws_floats(int C) { return int64_t(kMaxBlocks + kSumGroups) * C; }
 
 void relu_bias_bwd(int dev, hipStream_t s, int64_t M, int C, uintptr_t dy, uintptr_t y, uintptr_t dz, uintptr_t db,
                    uintptr_t ws) {
@@ -105,8 +108,17 @@ void relu_bias_bwd(int dev, hipStream_t s, int64_t M, int C, uintptr_t dy, uintp
                      reinterpret_cast<const uint16_t*>(y), reinterpret_cast<uint16_t*>(dz), M, C, rpb, part);
   hip_check(hipGetLastError(), "relu_bias_bwd launch");
   if (db) {
-    hipLaunchKernelGGL(sum_parts_kernel, dim3((C + kSumCh - 1) / kSumCh), dim3(kSumCh * kSumLanes), 0, s, part,
-                       int(nb), C, reinterpret_cast<float*>(db));
+    const dim3 cb((C + kSumCh - 1) / kSumCh);
+    if (nb > 4 * kSumLanes) {  // level 1 into the workspace tail, then the group combine
+      float* mid = part + int64_t(kMaxBlocks) * C;
+      hipLaunchKernelGGL(sum_parts_kernel, dim3(cb.x, kSumGroups), dim3(kSumCh * kSumLanes), 0, s, part, int(nb), C,
+                         mid);
+      hipLaunchKernelGGL(sum_parts_kernel, cb, dim3(kSumCh * kSumLanes), 0, s, mid, kSumGroups, C,
+                         reinterpret_cast<float*>(db));
+    } else {
+      hipLaunchKernelGGL(sum_parts_kernel, cb, dim3(kSumCh * kSumLanes), 0, s, part, int(nb), C,
+                         reinterpret_cast<float*>(db));
+    }
     hip_check(hipGetLastError(), "relu_bias_bwd sum launch");
   }
 }

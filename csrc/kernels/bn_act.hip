@@ -524,6 +524,80 @@ __global__ __launch_bounds__(1024) void bn_bwd_apply_kernel(const T* __restrict_
   }
 }
 
+// ---------------------------------------------------------------- BN pair (ResNet downsample)
+// y = relu(x1*sc1 + sh1 + x2*sc2 + sh2): a block's last BN plus its downsample shortcut's BN
+// (no ReLU on the shortcut), one pass over (x1, x2) instead of materialising bn2(x2).
+__global__ __launch_bounds__(1024) void bn_pair_apply_kernel(const uint16_t* __restrict__ x1,
+                                                             const uint16_t* __restrict__ x2,
+                                                             uint16_t* __restrict__ y, const float* __restrict__ coef1,
+                                                             const float* __restrict__ coef2, int64_t nvec, int C,
+                                                             uint8_t* __restrict__ mask) {
+  constexpr int V = 8;
+  const int G = C / V;
+  int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;  // multiple of G
+  const int g = int(i % G);
+  float a1[V], b1[V], a2[V], b2[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    a1[v] = coef1[g * V + v];
+    b1[v] = coef1[C + g * V + v];
+    a2[v] = coef2[g * V + v];
+    b2[v] = coef2[C + g * V + v];
+  }
+  for (; i < nvec; i += stride) {
+    float p[V], q[V];
+    Vec<uint16_t>::load(x1 + i * V, p);
+    Vec<uint16_t>::load(x2 + i * V, q);
+    uint32_t bits = 0;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const float t = fmaxf(fmaf(p[v], a1[v], b1[v]) + fmaf(q[v], a2[v], b2[v]), 0.f);
+      p[v] = t;
+      bits |= uint32_t(t > 0.f) << v;
+    }
+    Vec<uint16_t>::store(y + i * V, p);
+    mask[i] = uint8_t(bits);
+  }
+}
+
+// dz = dy * mask; dx1 = A1 dz + C1 x1 + B1, dx2 = A2 dz + C2 x2 + B2 (coef [3][C] each)
+__global__ __launch_bounds__(1024) void bn_pair_bwd_apply_kernel(
+    const uint16_t* __restrict__ dy, const uint8_t* __restrict__ mask, const uint16_t* __restrict__ x1,
+    const float* __restrict__ coef1, uint16_t* __restrict__ dx1, const uint16_t* __restrict__ x2,
+    const float* __restrict__ coef2, uint16_t* __restrict__ dx2, int64_t nvec, int C) {
+  constexpr int V = 8;
+  const int G = C / V;
+  int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  const int g = int(i % G);
+  float A1[V], C1[V], B1[V], A2[V], C2[V], B2[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    A1[v] = coef1[g * V + v];
+    C1[v] = coef1[C + g * V + v];
+    B1[v] = coef1[2 * C + g * V + v];
+    A2[v] = coef2[g * V + v];
+    C2[v] = coef2[C + g * V + v];
+    B2[v] = coef2[2 * C + g * V + v];
+  }
+  for (; i < nvec; i += stride) {
+    float d[V], p[V], q[V];
+    Vec<uint16_t>::load(dy + i * V, d);
+    Vec<uint16_t>::load(x1 + i * V, p);
+    Vec<uint16_t>::load(x2 + i * V, q);
+    const uint32_t mb = mask[i];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      const float dz = (mb >> v) & 1u ? d[v] : 0.f;
+      p[v] = fmaf(A1[v], dz, fmaf(C1[v], p[v], B1[v]));
+      q[v] = fmaf(A2[v], dz, fmaf(C2[v], q[v], B2[v]));
+    }
+    Vec<uint16_t>::store(dx1 + i * V, p);
+    Vec<uint16_t>::store(dx2 + i * V, q);
+  }
+}
+
 void check_shape(int64_t M, int C, int V, uintptr_t ptr) {
   if (M <= 0 || C <= 0) throw std::invalid_argument("bn_act: empty tensor");
   if (C % V) throw std::invalid_argument("bn_act: channels must be a multiple of " + std::to_string(V));
@@ -587,7 +661,7 @@ void fwd_impl(int dev, hipStream_t s, const T* x, const T* res, T* y, int64_t M,
     fa.save_rstd = save_rstd;
     fa.coef = coef;
     launch_tiles_finalize<T, true>(s, tstats, nstat, C, M, x, ws + 2 * C, fa);
-    launch_apply<T>(s, x, res, y, M, C, coef, relu, mask);
+    if (y) launch_apply<T>(s, x, res, y, M, C, coef, relu, mask);
     hip_check(hipGetLastError(), "bn_act forward launch");
     return;
   }
@@ -599,7 +673,7 @@ void fwd_impl(int dev, hipStream_t s, const T* x, const T* res, T* y, int64_t M,
   hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(nb), dim3(blk), shm, s, x, M, C, rpb, part);
   hipLaunchKernelGGL(bn_finalize_fwd_kernel<T>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinK), 0, s, part, nb,
                      C, M, x, gamma, beta, eps, momentum, rmean, rvar, save_mean, save_rstd, coef);
-  launch_apply<T>(s, x, res, y, M, C, coef, relu, mask);
+  if (y) launch_apply<T>(s, x, res, y, M, C, coef, relu, mask);  // y == nullptr: coefficients only
   hip_check(hipGetLastError(), "bn_act forward launch");
 }
 
@@ -639,6 +713,10 @@ void bwd_impl(hipStream_t s, const T* dy, const uint8_t* mask, const T* x, T* dx
   }
   const int64_t nvec = M * G;
   const dim3 g(apply_grid(nvec, blk)), b(blk);
+  if (!dx) {  // coefficients only (ws[0, 3C)), dgamma / dbeta
+    hip_check(hipGetLastError(), "bn_act backward launch");
+    return;
+  }
   if (relu) {
     if (dres) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, true>), g, b, 0, s, dy, mask, x, coef, dx, dres, nvec, C);
     else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, false>), g, b, 0, s, dy, mask, x, coef, dx, dres, nvec, C);
@@ -701,6 +779,36 @@ void bn_act_bwd(int dev, hipStream_t s, bool bf16, uintptr_t dy, uintptr_t mask,
     bwd_impl<float>(s, reinterpret_cast<const float*>(dy), mk, reinterpret_cast<const float*>(x),
                     reinterpret_cast<float*>(dx), reinterpret_cast<float*>(dres), M, C, F(gamma), F(mean), F(rstd),
                     F(dgamma), F(dbeta), F(ws), relu, F(part), npart);
+}
+
+void bn_pair_apply(int dev, hipStream_t s, uintptr_t x1, uintptr_t coef1, uintptr_t x2, uintptr_t coef2, uintptr_t y,
+                   int64_t M, int C, uintptr_t mask) {
+  hip_check(hipSetDevice(dev), "hipSetDevice");
+  check_shape(M, C, 8, x1);
+  check_shape(M, C, 8, x2);
+  if (!mask) throw std::invalid_argument("bn_pair_apply: needs the ReLU mask buffer");
+  const int G = C / 8, blk = block_for(G);
+  const int64_t nvec = M * G;
+  hipLaunchKernelGGL(bn_pair_apply_kernel, dim3(apply_grid(nvec, blk)), dim3(blk), 0, s,
+                     reinterpret_cast<const uint16_t*>(x1), reinterpret_cast<const uint16_t*>(x2),
+                     reinterpret_cast<uint16_t*>(y), reinterpret_cast<const float*>(coef1),
+                     reinterpret_cast<const float*>(coef2), nvec, C, reinterpret_cast<uint8_t*>(mask));
+  hip_check(hipGetLastError(), "bn_pair_apply launch");
+}
+
+void bn_pair_bwd_apply(int dev, hipStream_t s, uintptr_t dy, uintptr_t mask, uintptr_t x1, uintptr_t coef1,
+                       uintptr_t dx1, uintptr_t x2, uintptr_t coef2, uintptr_t dx2, int64_t M, int C) {
+  hip_check(hipSetDevice(dev), "hipSetDevice");
+  check_shape(M, C, 8, x1);
+  check_shape(M, C, 8, x2);
+  const int G = C / 8, blk = block_for(G);
+  const int64_t nvec = M * G;
+  hipLaunchKernelGGL(bn_pair_bwd_apply_kernel, dim3(apply_grid(nvec, blk)), dim3(blk), 0, s,
+                     reinterpret_cast<const uint16_t*>(dy), reinterpret_cast<const uint8_t*>(mask),
+                     reinterpret_cast<const uint16_t*>(x1), reinterpret_cast<const float*>(coef1),
+                     reinterpret_cast<uint16_t*>(dx1), reinterpret_cast<const uint16_t*>(x2),
+                     reinterpret_cast<const float*>(coef2), reinterpret_cast<uint16_t*>(dx2), nvec, C);
+  hip_check(hipGetLastError(), "bn_pair_bwd_apply launch");
 }
 
 }  // namespace mpit

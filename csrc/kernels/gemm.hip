@@ -70,7 +70,7 @@ struct ConvGeo {
   int ostr, oph, opw, OH, OW, ozero;
 };
 
-enum { EPI_NONE = 0, EPI_STATS = 1, EPI_BNRED = 2 };
+enum { EPI_NONE = 0, EPI_STATS = 1, EPI_BNRED = 2, EPI_BNRED2 = 3 };
 
 // column-reduction epilogue operands (see gemm_nt_kernel)
 struct EpiArgs {
@@ -79,6 +79,9 @@ struct EpiArgs {
   const uint8_t* mask;         // EPI_BNRED: the BN's ReLU bit mask (1 byte / 8 channels) or null
   const float* mean;           // EPI_BNRED: the BN's batch mean [N]
   int64_t row0;                // first partial row of this launch
+  float* part2;                // EPI_BNRED2: the second BN of a bn_pair (same gradient and mask)
+  const uint16_t* x2;
+  const float* mean2;
 };
 
 // source line for padding taps: LDS DMA of zeros
@@ -150,7 +153,7 @@ __device__ __forceinline__ int xcd_tile(int bid, int nb) {
 // is lane-linear per wave instruction (16 rows x 64 B); the swizzle is applied on the
 // global source address.
 template <int BM, int BN, int STAGES, int EPI, bool CONV>
-__global__ __launch_bounds__(BM / 64 * 128, BM == 256 ? 1 : (STAGES == 2 ? (CONV ? 4 : 5) : 2)) void gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda,
+__global__ __launch_bounds__(BM / 64 * 128, BM == 256 ? 1 : (STAGES == 2 ? (CONV || EPI == 3 ? 4 : 5) : 2)) void gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda,
                                                          const uint16_t* __restrict__ B, int64_t ldb,
                                                          uint16_t* C, int64_t ldc, int64_t M, int N, int K,
                                                          int ntn, EpiArgs ep, const uint16_t* Cin,
@@ -319,11 +322,21 @@ __global__ __launch_bounds__(BM / 64 * 128, BM == 256 ? 1 : (STAGES == 2 ? (CONV
   int nv = 0;
 #pragma unroll
   for (int e = 0; e < 8; ++e) s1[e] = s2[e] = sf[e] = mu[e] = 0.f;
-  if constexpr (EPI == EPI_BNRED) {
+  constexpr bool BNRED = EPI == EPI_BNRED || EPI == EPI_BNRED2, DUAL = EPI == EPI_BNRED2;
+  float s3[8], mu2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s3[e] = mu2[e] = 0.f;
+  if constexpr (BNRED) {
     const float4 a0 = *reinterpret_cast<const float4*>(ep.mean + nc);
     const float4 a1 = *reinterpret_cast<const float4*>(ep.mean + nc + 4);
     mu[0] = a0.x; mu[1] = a0.y; mu[2] = a0.z; mu[3] = a0.w;
     mu[4] = a1.x; mu[5] = a1.y; mu[6] = a1.z; mu[7] = a1.w;
+  }
+  if constexpr (DUAL) {
+    const float4 a0 = *reinterpret_cast<const float4*>(ep.mean2 + nc);
+    const float4 a1 = *reinterpret_cast<const float4*>(ep.mean2 + nc + 4);
+    mu2[0] = a0.x; mu2[1] = a0.y; mu2[2] = a0.z; mu2[3] = a0.w;
+    mu2[4] = a1.x; mu2[5] = a1.y; mu2[6] = a1.z; mu2[7] = a1.w;
   }
   // Rows go in batches of PB: all loads of a batch are issued before its first store (C
   // may alias Cin, so the compiler would otherwise serialise load -> store per row), and
@@ -332,7 +345,7 @@ __global__ __launch_bounds__(BM / 64 * 128, BM == 256 ? 1 : (STAGES == 2 ? (CONV
 #pragma unroll
   for (int pb = 0; pb < NP; pb += PB) {
   int64_t orow[PB];
-  uint4 cv[PB], xq[PB];
+  uint4 cv[PB], xq[PB], xq2[PB];
   uint32_t cmb[PB], xmb[PB];
 #pragma unroll
   for (int q = 0; q < PB; ++q) {
@@ -353,10 +366,11 @@ __global__ __launch_bounds__(BM / 64 * 128, BM == 256 ? 1 : (STAGES == 2 ? (CONV
       cv[q] = ok ? *reinterpret_cast<const uint4*>(Cin + o) : make_uint4(0, 0, 0, 0);
       cmb[q] = Cmask ? (ok ? uint32_t(Cmask[o >> 3]) : 0u) : 0xffu;
     }
-    if constexpr (EPI == EPI_BNRED) {
+    if constexpr (BNRED) {
       xq[q] = ok ? *reinterpret_cast<const uint4*>(ep.x + o) : make_uint4(0, 0, 0, 0);
       xmb[q] = ok ? (ep.mask ? uint32_t(ep.mask[o >> 3]) : 0xffu) : 0u;
     }
+    if constexpr (DUAL) xq2[q] = ok ? *reinterpret_cast<const uint4*>(ep.x2 + o) : make_uint4(0, 0, 0, 0);
   }
 #pragma unroll
   for (int q = 0; q < PB; ++q) {
@@ -400,9 +414,10 @@ __global__ __launch_bounds__(BM / 64 * 128, BM == 256 ? 1 : (STAGES == 2 ? (CONV
         s2[e] = fmaf(d, d, s2[e]);
       }
       ++nv;
-    } else if constexpr (EPI == EPI_BNRED) {  // dz = C * mask; (sum dz, sum dz (x - mean))
+    } else if constexpr (BNRED) {  // dz = C * mask; (sum dz, sum dz (x - mean) [, sum dz (x2 - mean2)])
       const uint32_t xb = xmb[q];
       const uint32_t xw[4] = {xq[q].x, xq[q].y, xq[q].z, xq[q].w};
+      const uint32_t xw2[4] = {xq2[q].x, xq2[q].y, xq2[q].z, xq2[q].w};
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const uint32_t hwd = hw4[e >> 1], xwd = xw[e >> 1];
@@ -410,6 +425,10 @@ __global__ __launch_bounds__(BM / 64 * 128, BM == 256 ? 1 : (STAGES == 2 ? (CONV
         const float xe = bf2f(uint16_t((e & 1) ? (xwd >> 16) : (xwd & 0xffff)));
         s1[e] += dz;
         s2[e] = fmaf(dz, xe - mu[e], s2[e]);
+        if constexpr (DUAL) {
+          const uint32_t xwd2 = xw2[e >> 1];
+          s3[e] = fmaf(dz, bf2f(uint16_t((e & 1) ? (xwd2 >> 16) : (xwd2 & 0xffff))) - mu2[e], s3[e]);
+        }
       }
     }
   }
@@ -432,6 +451,7 @@ __global__ __launch_bounds__(BM / 64 * 128, BM == 256 ? 1 : (STAGES == 2 ? (CONV
       for (int e = 0; e < 8; ++e) {
         red[(rg * 3 + 0) * BN + ch * 8 + e] = s1[e];
         red[(rg * 3 + 1) * BN + ch * 8 + e] = s2[e];
+        if constexpr (DUAL) red[(rg * 3 + 2) * BN + ch * 8 + e] = s3[e];
       }
     }
     __syncthreads();
@@ -453,13 +473,19 @@ __global__ __launch_bounds__(BM / 64 * 128, BM == 256 ? 1 : (STAGES == 2 ? (CONV
         prow[n] = mean;
         prow[N + n] = m2;
       } else {
-        float a = 0.f, b = 0.f;
+        float a = 0.f, b = 0.f, c3 = 0.f;
         for (int k = hf * RPH; k < (hf + 1) * RPH; ++k) {
           a += red[(k * 3 + 0) * BN + n];
           b += red[(k * 3 + 1) * BN + n];
+          if constexpr (DUAL) c3 += red[(k * 3 + 2) * BN + n];
         }
         prow[n] = a;
         prow[N + n] = b;
+        if constexpr (DUAL) {
+          float* prow2 = ep.part2 + (ep.row0 + tile) * 2 * int64_t(N) + n0;
+          prow2[n] = a;
+          prow2[N + n] = c3;
+        }
       }
     }
   }
@@ -795,7 +821,8 @@ static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t
     throw std::invalid_argument("gemm_nt: bad leading dimensions");
   if (epi != EPI_NONE) {
     if (!ep.part) throw std::invalid_argument("gemm_nt: reduction epilogue needs a partials buffer");
-    if (epi == EPI_BNRED) {
+    if (epi == EPI_BNRED2 && geo) throw std::invalid_argument("gemm_nt: paired BN reduction is for 1x1 GEMMs");
+    if (epi == EPI_BNRED || epi == EPI_BNRED2) {
       if (!ep.x || !ep.mean || ldc != N) throw std::invalid_argument("gemm_nt: BN reduction needs x, mean, ldc == N");
       check_ptr(reinterpret_cast<uintptr_t>(ep.x), "BN x");
       check_ptr(reinterpret_cast<uintptr_t>(ep.mean), "BN mean");
@@ -828,6 +855,7 @@ static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t
   do {                                                                      \
     if (epi == EPI_STATS) MPIT_NT_LAUNCH1(BM, BN, ST, EPI_STATS, CONV);     \
     else if (epi == EPI_BNRED) MPIT_NT_LAUNCH1(BM, BN, ST, EPI_BNRED, CONV); \
+    else if (epi == EPI_BNRED2 && !CONV) MPIT_NT_LAUNCH1(BM, BN, ST, EPI_BNRED2, false); \
     else MPIT_NT_LAUNCH1(BM, BN, ST, EPI_NONE, CONV);                       \
   } while (0)
 #define MPIT_NT_LAUNCH(BM, BN, ST)                                                                             \
@@ -872,6 +900,13 @@ static EpiArgs epi_args(uintptr_t stats, const BnRed* r, int* mode) {
     ep.mean = reinterpret_cast<const float*>(r->mean);
     ep.row0 = r->row0;
     *mode = EPI_BNRED;
+    if (r->part2) {
+      if (!r->x2 || !r->mean2) throw std::invalid_argument("gemm_nt: second BN reduction needs x2 and mean2");
+      ep.part2 = reinterpret_cast<float*>(r->part2);
+      ep.x2 = reinterpret_cast<const uint16_t*>(r->x2);
+      ep.mean2 = reinterpret_cast<const float*>(r->mean2);
+      *mode = EPI_BNRED2;
+    }
   }
   return ep;
 }

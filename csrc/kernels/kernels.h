@@ -85,6 +85,16 @@ void bn_act_bwd(int dev, hipStream_t s, bool bf16, uintptr_t dy, uintptr_t mask,
                 uintptr_t dres, int64_t M, int C, uintptr_t gamma, uintptr_t mean, uintptr_t rstd, uintptr_t dgamma,
                 uintptr_t dbeta, uintptr_t ws, bool relu, uintptr_t part = 0, int64_t npart = 0);
 
+// bn_act_fwd with y == 0 / bn_act_bwd with dx == 0 only compute the coefficients into
+// ws[0, 2C) (scale, shift) / ws[0, 3C) (A, C, B) and the running stats / dgamma, dbeta.
+// A block's last BN and its downsample shortcut's BN as one op (bf16, ReLU):
+// y = relu(bn1(x1) + bn2(x2)) from the two forward coefficient sets, and the backward
+// dx1 / dx2 from the two backward sets, one pass each.
+void bn_pair_apply(int dev, hipStream_t s, uintptr_t x1, uintptr_t coef1, uintptr_t x2, uintptr_t coef2, uintptr_t y,
+                   int64_t M, int C, uintptr_t mask);
+void bn_pair_bwd_apply(int dev, hipStream_t s, uintptr_t dy, uintptr_t mask, uintptr_t x1, uintptr_t coef1,
+                       uintptr_t dx1, uintptr_t x2, uintptr_t coef2, uintptr_t dx2, int64_t M, int C);
+
 // ---- MFMA GEMMs for NHWC 1x1 convolutions (gemm.hip), bf16 operands, fp32 accumulate --
 // C[M,N] (bf16) = A[M,K] . B[N,K]^T; optional per-column (mean, M2) partials of C per
 // 128-row tile into stats[ceil(M/128)][2][N] (gemm_nt_stats_floats); optional bf16 cin
@@ -94,9 +104,12 @@ void bn_act_bwd(int dev, hipStream_t s, bool bf16, uintptr_t dy, uintptr_t mask,
 // input / ReLU mask / batch mean, [.., N] like C): the GEMM also writes that layer's
 // backward reduction partials (sum dz, sum dz*(x-mean)), dz = C*mask, one row pair per
 // 128-row tile at part[row0 + tile][2][N] — bn_act_bwd(part, npart) then skips its pass.
+// x2 / mean2 / part2 (optional): a second BN fed by the same gradient (the downsample
+// shortcut's BN of a bn_pair): its (sum dz, sum dz*(x2-mean2)) go to part2.
 struct BnRed {
   uintptr_t part = 0, x = 0, mask = 0, mean = 0;
   int64_t row0 = 0;
+  uintptr_t part2 = 0, x2 = 0, mean2 = 0;
 };
 bool gemm_nt_supported(int64_t M, int N, int K);
 int64_t gemm_nt_tiles(int64_t M);

@@ -17,7 +17,7 @@ import os
 import torch
 import torch.nn as nn
 
-from ..ops.bn import BatchNormAct2d
+from ..ops.bn import BatchNormAct2d, bn_pair
 from ..ops.conv import Conv1x1, ConvNHWC, GradSlot, park_grad
 from ..ops.pool import MaxPool2dNHWC
 
@@ -118,6 +118,11 @@ class Bottleneck(nn.Module):
                 out = self.bn1(self.conv1(x, slot))
                 out = self.bn2(self.conv2(out))
                 out = self.conv3(out)
+                conv_ds, bn_ds = self.downsample[0], self.downsample[1]
+                if isinstance(bn_ds, BatchNormAct2d) and len(self.downsample) == 2:
+                    # relu(bn3(out) + bn_ds(conv_ds(x))) as one op: no shortcut tensor, one
+                    # pass each way for both BNs (ops/bn.py bn_pair)
+                    return bn_pair(self.bn3, out, bn_ds, conv_ds(park_grad(x, slot)))
                 idt = self.downsample(park_grad(x, slot))
                 return self.bn3(out, idt)
             idt = x if self.downsample is None else self.downsample(x)

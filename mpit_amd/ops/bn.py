@@ -51,10 +51,11 @@ class BNLink:
     if it receives exactly that tensor, unmodified — when autograd summed gradients from
     several consumers it falls back to its own reduction pass."""
 
-    __slots__ = ("x", "mask", "mean", "part", "npart", "dy_ptr", "dy_ver")
+    __slots__ = ("x", "mask", "mean", "part", "npart", "dy_ptr", "dy_ver", "x2", "mean2", "part2")
 
     def __init__(self):
         self.x = self.mask = self.mean = self.part = None
+        self.x2 = self.mean2 = self.part2 = None  # the shortcut BN of a bn_pair
         self.npart = 0
         self.dy_ptr = self.dy_ver = None
 
@@ -63,14 +64,17 @@ class BNLink:
         return (self.x is not None and self.mean is not None and x.dtype == torch.bfloat16
                 and self.x.shape == x.shape)
 
-    def publish(self, part: torch.Tensor, npart: int, dy: torch.Tensor):
-        self.part, self.npart = part, int(npart)
+    def publish(self, part: torch.Tensor, npart: int, dy: torch.Tensor, part2: torch.Tensor = None):
+        self.part, self.npart, self.part2 = part, int(npart), part2
         self.dy_ptr, self.dy_ver = dy.data_ptr(), dy._version
 
-    def take(self, dy: torch.Tensor):
-        part, npart = self.part, self.npart
+    def take(self, dy: torch.Tensor, pair: bool = False):
+        part, npart, part2 = self.part, self.npart, self.part2
         ok = part is not None and dy.data_ptr() == self.dy_ptr and dy._version == self.dy_ver
-        self.part, self.x, self.mask, self.mean = None, None, None, None
+        ok = ok and (part2 is not None or not pair)
+        self.part = self.x = self.mask = self.mean = self.x2 = self.mean2 = self.part2 = None
+        if pair:
+            return (part, npart, part2) if ok else (None, 0, None)
         return (part, npart) if ok else (None, 0)
 
 
@@ -205,6 +209,20 @@ class BatchNormAct2d(nn.BatchNorm2d):
         self.sync_num_batches_tracked()
         super()._save_to_state_dict(destination, prefix, keep_vars)
 
+    def _train_args(self):
+        """(momentum, running_mean, running_var) of one training-mode forward (counts it)."""
+        momentum = self.momentum
+        if self.training and self.track_running_stats:
+            if momentum is None:
+                self.sync_num_batches_tracked()
+                self.num_batches_tracked.add_(1)
+                momentum = 1.0 / float(self.num_batches_tracked)
+            else:
+                self._nbt_pending += 1
+        rm = self.running_mean if (self.training and self.track_running_stats) else None
+        rv = self.running_var if (self.training and self.track_running_stats) else None
+        return momentum or 0.0, rm, rv
+
     def fused(self, x: torch.Tensor) -> bool:
         """True when a training forward of ``x`` runs the fused kernels (honours res_slot)."""
         return _supported(x) and (self.training or not self.track_running_stats)
@@ -220,20 +238,103 @@ class BatchNormAct2d(nn.BatchNorm2d):
                 y = y + residual
             return F.relu(y) if self.act else y
         if self.training or not self.track_running_stats:
-            momentum = self.momentum
-            if self.training and self.track_running_stats:
-                if momentum is None:
-                    self.sync_num_batches_tracked()
-                    self.num_batches_tracked.add_(1)
-                    momentum = 1.0 / float(self.num_batches_tracked)
-                else:
-                    self._nbt_pending += 1
-            rm = self.running_mean if (self.training and self.track_running_stats) else None
-            rv = self.running_var if (self.training and self.track_running_stats) else None
+            momentum, rm, rv = self._train_args()
             link = BNLink() if (torch.is_grad_enabled() and x.dtype == torch.bfloat16) else None
-            y = _BNActFn.apply(x, self.weight, self.bias, rm, rv, residual, momentum or 0.0, self.eps, self.act,
+            y = _BNActFn.apply(x, self.weight, self.bias, rm, rv, residual, momentum, self.eps, self.act,
                                res_slot, tile_stats_of(x), link)
             if link is not None:
                 y._mpit_bnlink = link
             return y
         return bn_act_eval(x, self.weight, self.bias, self.running_mean, self.running_var, self.eps, residual, self.act)
+
+
+class _BNPairFn(torch.autograd.Function):
+    """relu(bn1(x1) + bn2(x2)) for a ResNet block's last BN (bn1) and its downsample
+    shortcut's BN (bn2): forward = the two coefficient sets (from the producing convs'
+    tile statistics) and ONE pass writing y and the ReLU mask; backward = the two
+    coefficient sets (from the consumer conv's paired epilogue reduction, BNLink.x2) and
+    ONE pass writing dx1 and dx2. Replaces bn2's apply pass, its reduction pass and the
+    residual-gradient tensor of the unpaired form."""
+
+    @staticmethod
+    def forward(ctx, x1, w1, b1, rm1, rv1, x2, w2, b2, rm2, rv2, mom1, eps1, mom2, eps2, ts1, ts2, link):
+        x1, x2 = _cl(x1), _cl(x2).to(x1.dtype)
+        M, C = _rows(x1)
+        m = native()
+        dev, stream = x1.device.index, torch.cuda.current_stream(x1.device).cuda_stream
+        f32 = dict(dtype=torch.float32, device=x1.device)
+        outs = []
+        for x, w, b, rm, rv, mom, eps, ts in ((x1, w1, b1, rm1, rv1, mom1, eps1, ts1),
+                                             (x2, w2, b2, rm2, rv2, mom2, eps2, ts2)):
+            mean, rstd = torch.empty(C, **f32), torch.empty(C, **f32)
+            ws = torch.empty(m.bn_workspace_floats(C), **f32)
+            wf = w.float().contiguous() if w is not None else None
+            bf = b.float().contiguous() if b is not None else None
+            ts = ts if (ts is not None and ts[1] == m.gemm_nt_tiles(M)) else None
+            if ts is not None:
+                COUNTERS["fwd_tile_stats"] += 1
+            m.bn_act_fwd(dev, stream, True, x.data_ptr(), 0, 0, M, C, wf.data_ptr() if wf is not None else 0,
+                         bf.data_ptr() if bf is not None else 0, rm.data_ptr() if rm is not None else 0,
+                         rv.data_ptr() if rv is not None else 0, mean.data_ptr(), rstd.data_ptr(), ws.data_ptr(),
+                         float(mom), float(eps), False, 0, stats=ts[0].data_ptr() if ts is not None else 0,
+                         nstat=ts[1] if ts is not None else 0)
+            outs.append((wf, mean, rstd, ws))
+        y = torch.empty_like(x1, memory_format=torch.channels_last)
+        mask = torch.empty(m.bn_mask_bytes(True, M, C), dtype=torch.uint8, device=x1.device)
+        m.bn_pair_apply(dev, stream, x1.data_ptr(), outs[0][3].data_ptr(), x2.data_ptr(), outs[1][3].data_ptr(),
+                        y.data_ptr(), M, C, mask.data_ptr())
+        (wf1, mean1, rstd1, _), (wf2, mean2, rstd2, _) = outs
+        ctx.save_for_backward(x1, x2, mask, wf1, mean1, rstd1, wf2, mean2, rstd2)
+        ctx.has = (w1 is not None, b1 is not None, w2 is not None, b2 is not None)
+        ctx.link = link
+        if link is not None:
+            link.x, link.mask, link.mean, link.x2, link.mean2 = x1, mask, mean1, x2, mean2
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x1, x2, mask, wf1, mean1, rstd1, wf2, mean2, rstd2 = ctx.saved_tensors
+        dy = _cl(dy).to(x1.dtype)
+        M, C = _rows(x1)
+        m = native()
+        dev, stream = x1.device.index, torch.cuda.current_stream(x1.device).cuda_stream
+        part, npart, part2 = ctx.link.take(dy, pair=True) if ctx.link is not None else (None, 0, None)
+        if part is not None:
+            COUNTERS["bwd_linked"] += 2
+        f32 = dict(dtype=torch.float32, device=x1.device)
+        grads, wss = [], []
+        for x, wf, mean, rstd, p, hw, hb in ((x1, wf1, mean1, rstd1, part, ctx.has[0], ctx.has[1]),
+                                            (x2, wf2, mean2, rstd2, part2, ctx.has[2], ctx.has[3])):
+            dg = torch.empty(C, **f32) if hw else None
+            db = torch.empty(C, **f32) if hb else None
+            ws = torch.empty(m.bn_workspace_floats(C), **f32)
+            m.bn_act_bwd(dev, stream, True, dy.data_ptr(), mask.data_ptr(), x.data_ptr(), 0, 0, M, C,
+                         wf.data_ptr() if wf is not None else 0, mean.data_ptr(), rstd.data_ptr(),
+                         dg.data_ptr() if dg is not None else 0, db.data_ptr() if db is not None else 0, ws.data_ptr(),
+                         True, part=p.data_ptr() if p is not None else 0, npart=npart if p is not None else 0)
+            grads.append((dg, db))
+            wss.append(ws)
+        dx1 = torch.empty_like(x1, memory_format=torch.channels_last)
+        dx2 = torch.empty_like(x2, memory_format=torch.channels_last)
+        m.bn_pair_bwd_apply(dev, stream, dy.data_ptr(), mask.data_ptr(), x1.data_ptr(), wss[0].data_ptr(),
+                            dx1.data_ptr(), x2.data_ptr(), wss[1].data_ptr(), dx2.data_ptr(), M, C)
+        (dg1, db1), (dg2, db2) = grads
+        return (dx1, dg1, db1, None, None, dx2, dg2, db2, None, None, None, None, None, None, None, None, None)
+
+
+def bn_pair(bn1: "BatchNormAct2d", x1: torch.Tensor, bn2: "BatchNormAct2d", x2: torch.Tensor) -> torch.Tensor:
+    """``relu(bn1(x1) + bn2(x2))`` (bn1 with ReLU, bn2 without): one fused op on the GPU
+    training path (:class:`_BNPairFn`), the two modules otherwise."""
+    ok = (bn1.act and not bn2.act and bn1.training and bn2.training and bn1.track_running_stats
+          and bn2.track_running_stats and _supported(x1) and x1.dtype == torch.bfloat16 and x2.shape == x1.shape
+          and x2.is_cuda and x2.dtype in (torch.bfloat16, torch.float32))
+    if not ok:
+        return bn1(x1, bn2(x2))
+    mom1, rm1, rv1 = bn1._train_args()
+    mom2, rm2, rv2 = bn2._train_args()
+    link = BNLink() if torch.is_grad_enabled() else None
+    y = _BNPairFn.apply(x1, bn1.weight, bn1.bias, rm1, rv1, x2, bn2.weight, bn2.bias, rm2, rv2, mom1, bn1.eps, mom2,
+                        bn2.eps, tile_stats_of(x1), tile_stats_of(x2), link)
+    if link is not None:
+        y._mpit_bnlink = link
+    return y

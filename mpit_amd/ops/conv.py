@@ -102,17 +102,26 @@ def cast_transpose(w: torch.Tensor):
 
 
 def _red_args(link, c: int, ntiles: int, device):
-    """(kernel keyword arguments, partials tensor) of a BN backward reduction folded into a
-    backward-data GEMM (see ops/bn.py BNLink)."""
+    """(kernel keyword arguments, partials, second partials or None) of a BN backward
+    reduction folded into a backward-data GEMM (see ops/bn.py BNLink; a bn_pair link also
+    reduces for its shortcut BN)."""
     part = torch.empty(ntiles * 2 * c, dtype=torch.float32, device=device)
-    return dict(red_part=part.data_ptr(), red_x=link.x.data_ptr(),
-                red_mask=link.mask.data_ptr() if link.mask is not None else 0,
-                red_mean=link.mean.data_ptr()), part
+    kw = dict(red_part=part.data_ptr(), red_x=link.x.data_ptr(),
+              red_mask=link.mask.data_ptr() if link.mask is not None else 0, red_mean=link.mean.data_ptr())
+    part2 = None
+    if link.x2 is not None:
+        part2 = torch.empty(ntiles * 2 * c, dtype=torch.float32, device=device)
+        kw.update(red_part2=part2.data_ptr(), red_x2=link.x2.data_ptr(), red_mean2=link.mean2.data_ptr())
+    return kw, part, part2
 
 
-def _link_of(x: torch.Tensor):
+def _link_of(x: torch.Tensor, pair_ok: bool = True):
+    """The BNLink of the BN layer that produced ``x``; a bn_pair link only for consumers
+    whose backward-data GEMM can run the paired reduction (``pair_ok``: the 1x1 GEMMs)."""
     link = getattr(x, "_mpit_bnlink", None)
-    return link if (link is not None and link.ready(x)) else None
+    if link is None or not link.ready(x) or (link.x2 is not None and not pair_ok):
+        return None
+    return link
 
 
 def _tile_stats(co: int, M: int, device):
@@ -222,10 +231,10 @@ class _Conv1x1Fn(torch.autograd.Function):
         extra, emask = ctx.slot.take() if ctx.slot is not None else (None, None)
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x, memory_format=torch.channels_last)
-            kw, part = {}, None
+            kw, part, part2 = {}, None, None
             if ctx.link is not None:  # the producing BN's backward reduction, in the epilogue
                 nt = m.gemm_nt_tiles(M)
-                kw, part = _red_args(ctx.link, ci, nt, x.device)
+                kw, part, part2 = _red_args(ctx.link, ci, nt, x.device)
             if extra is not None:  # gradient parked by the block (GradSlot): added in the epilogue
                 extra = _cl(extra)
                 if extra.dtype != torch.bfloat16:
@@ -237,7 +246,7 @@ class _Conv1x1Fn(torch.autograd.Function):
             else:
                 m.gemm_nt(dev, s, M, ci, co, dy.data_ptr(), co, wt.data_ptr(), co, dx.data_ptr(), ci, 0, **kw)
             if part is not None:
-                ctx.link.publish(part, nt, dx)
+                ctx.link.publish(part, nt, dx, part2)
         if ctx.needs_input_grad[1]:
             dw = torch.empty(ctx.wshape, dtype=torch.float32, device=x.device)
             nws = m.gemm_tn_ws_floats(dev, M, co, ci)
@@ -323,7 +332,7 @@ def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None):
             kw, part, nt = {}, None, 0
             if link is not None:
                 nt = m.gemm_nt_tiles(nb * h * w)
-                kw, part = _red_args(link, c, nt, x.device)
+                kw, part, _ = _red_args(link, c, nt, x.device)
             m.conv_fwd(dev, st, nb, ho, wo, co, c, r, s, 1, r - 1 - pad, dz.data_ptr(), wt.data_ptr(), dx.data_ptr(),
                        **kw)
             if part is not None:
@@ -335,7 +344,7 @@ def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None):
             kw, part, nt = {}, None, 0
             if link is not None:
                 nt = m.conv_dgrad_strided_tiles(nb, h, w, c, co, r, s, stride, pad)
-                kw, part = _red_args(link, c, nt, x.device)
+                kw, part, _ = _red_args(link, c, nt, x.device)
             m.conv_dgrad_strided(dev, st, nb, h, w, c, co, r, s, stride, pad, dz.data_ptr(), wt.data_ptr(),
                                  dx.data_ptr(), **kw)
             if part is not None:
@@ -480,7 +489,8 @@ class ConvNHWC(nn.Conv2d):
         if self.fused(x):
             hold = [] if (self.emit_stats and self.training) else None
             y = _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0], None, False, hold,
-                              _link_of(x) if torch.is_grad_enabled() else None, WeightCastPlan.cached(self))
+                              _link_of(x, pair_ok=False) if torch.is_grad_enabled() else None,
+                              WeightCastPlan.cached(self))
             return _attach_stats(y, hold)
         return super().forward(x)
 

@@ -160,6 +160,7 @@ def test_park_grad_slot_protocol():
 
 @gpu
 @pytest.mark.parametrize("n,ci,co,hw,k,relu", [(2, 64, 192, 13, 5, True), (3, 192, 384, 13, 3, True),
+                                               (16, 64, 64, 56, 3, True),
                                                (2, 128, 64, 9, 3, False)])
 def test_conv_act_bias_relu(n, ci, co, hw, k, relu):
     """conv + bias + ReLU with the bias / ReLU in the GEMM epilogue and the one-pass

@@ -112,8 +112,9 @@ def test_chained_blocks_fold_bn_passes(stride):
     fired = {k: bnmod.COUNTERS[k] - c0[k] for k in c0}
     nbn = sum(isinstance(m, BatchNormAct2d) for m in net.modules())
     assert fired["fwd_tile_stats"] == nbn, fired
-    # bn1, bn2 of both blocks + bn3 of block 1 (block 2's bn3 output is the loss input)
-    assert fired["bwd_linked"] == 5, fired
+    # bn1, bn2 of both blocks + bn3 of block 1 (block 2's bn3 output is the loss input); with
+    # a downsample shortcut block 1's bn3 and shortcut BN are one pair, both linked
+    assert fired["bwd_linked"] == (6 if down is not None else 5), fired
     grads1 = {n: p.grad.detach().clone() for n, p in net.named_parameters()}
     net.zero_grad(set_to_none=True)
 

@@ -1,0 +1,42 @@
+"""Bandwidth of the fused update kernels (csrc/kernels/ew.h engine) on PS-sized shards.
+
+    python benchmarks/ew_probe.py [n_millions ...]
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+from mpit_amd import ops
+
+
+def timeit(fn, it=30):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(it):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / it
+
+
+for nm in [float(a) for a in sys.argv[1:]] or [25.6, 3.2]:
+    n = int(nm * 1e6) // 64 * 64
+    p, g, w = (torch.randn(n, device="cuda") for _ in range(3))
+    m, v = torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda")
+    cases = {
+        "apply(p+=a*g, w=p) 16B/elem": (lambda: ops.apply_(p, g, 0.5, out=w), 16),
+        "apply(p+=a*g) 12B/elem": (lambda: ops.apply_(p, g, 0.5), 12),
+        "adam 28B/elem": (lambda: ops.adam_(p, g, m, v, 0.9, 0.999, 1e-8, 1e-3), 28),
+        "copy 8B/elem": (lambda: ops.copy_(w, p), 8),
+        "torch add_ 12B/elem": (lambda: p.add_(g, alpha=0.5), 12),
+    }
+    for name, (fn, bpe) in cases.items():
+        ms = timeit(fn)
+        print(json.dumps({"n": n, "op": name, "us": round(ms * 1e3, 1), "tb_s": round(n * bpe / ms / 1e9, 2)}),
+              flush=True)

@@ -73,8 +73,10 @@ def downpour(opfunc, w, config, state=None):
         pusher.arm(-lr * gscale, w if l2wd else None, -lr * l2wd)
         try:
             fx, _ = opfunc(w)
-        finally:
-            pusher.finish()
+        except BaseException:
+            pusher.abort()  # no pushes of half-computed shards
+            raise
+        pusher.finish()
         t0 = time.perf_counter()
         pc.wait()
         state["dusync"] += time.perf_counter() - t0

@@ -91,6 +91,10 @@ class ShardPusher:
         self.pc.async_send_grad_shard(k, pull=True)
         self.fired[k] = True
 
+    def abort(self):
+        """The backward failed: push nothing more (shards already pushed were complete)."""
+        self.armed = False
+
     def finish(self):
         """After the backward: push the shards whose parameters never all got a gradient."""
         for k in range(self.nshards):

@@ -454,7 +454,9 @@ void PSClient::start() {
 
 void PSClient::gate(hipStream_t s, std::function<void()> send) {
   GateQueue::Gate g{nullptr, std::move(send)};
-  if (eng_.device() >= 0 && s) {
+  // s == 0 is the null stream (PyTorch's default stream on ROCm), not "no stream": a device
+  // client always gates its AM on the work queued so far on s
+  if (eng_.device() >= 0) {
     hipp(hipSetDevice(eng_.device()), "hipSetDevice");
     hipp(hipEventCreateWithFlags(&g.ev, hipEventDisableTiming), "hipEventCreate");
     hipp(hipEventRecord(g.ev, s), "hipEventRecord");

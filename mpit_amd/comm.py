@@ -473,6 +473,8 @@ class Comm:
             buf = datatype.pack(buf, count)
             count = None
         t = _flat(buf, count)
+        if t.is_cuda:  # the receiver pulls the bytes: what the stream is still producing must land first
+            torch.cuda.current_stream(t.device).synchronize()
         rid = _rt.engine().isend(t.data_ptr(), _nbytes(t), t.is_cuda, self._to_world(dest), int(tag), ctx, sync)
         return Request(self, rid, keep=(t,), itemsize=t.element_size())
 

@@ -90,6 +90,17 @@ __device__ __attribute__((aligned(256))) uint16_t g_zero_line[128] = {};
 // 16-B chunk swizzle of a 64-B LDS row: any 16 consecutive rows read at one logical chunk
 // hit 16 distinct (row%4, chunk) bank groups = all 64 banks.
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }
+// the same for 128-B rows (BK = 64, 8 chunks): 16 rows at one logical chunk hit 16 distinct
+// (row%2, chunk) bank groups
+template <int BK>
+__device__ __forceinline__ int swzk(int row, int chunk) {
+  if constexpr (BK == 32) return swz(row, chunk);
+  else return chunk ^ ((row >> 1) & 7);
+}
+
+// k-depth of one staged tile of gemm_nt: the 256x256 tile (1 block/CU) stages 64-deep tiles
+// (16 MFMAs per wave between fragment refills, half the barriers per FLOP of BK = 32)
+__host__ __device__ constexpr int nt_bk(int BM, int BN) { return BM == 256 && BN == 256 ? 64 : kBK; }
 
 typedef __attribute__((address_space(3))) void lds_void;
 
@@ -143,28 +154,31 @@ __device__ __forceinline__ int xcd_tile(int bid, int nb) {
 // global access of a wave covers whole row segments; the column partials of the rows a
 // thread walks are combined through LDS.
 //
-// Waves: BM/64 x 2, each owning a 64 x BN/2 sub-tile (BM = 128: 4 waves). BM = 256 (8 waves,
-// 25 % fewer L2->LDS bytes per FLOP) compiles and passes the tests but measured no faster on
-// the ResNet-50 shapes (profiles/gemm_tile_ab_r01.jsonl), so it is not launched.
+// Waves: 2 x 2, each owning a BM/2 x BN/2 sub-tile. 128x128 (64x64 per wave, 4 MFMAs per
+// k16 step, up to 5 resident blocks per CU) for the memory-bound short-K GEMMs; 256x128 and
+// 256x256 (128x64 / 128x128 per wave: 8 / 16 MFMAs per k16 between barriers, half the LDS
+// fragment reads per MFMA, 2 / 1 blocks per CU) for the compute-bound deep-K ones — the
+// shape of tile the library GEMMs run at ~1 PFLOP/s on these problems (see launch_nt).
 //
 // Staging: global_load_lds (16-B LDS DMA, no VGPRs) into a ring of STAGES buffers with
 // STAGES-1 k-tiles in flight; a counted s_waitcnt vmcnt + raw s_barrier retires exactly
 // the tile about to be used (a __syncthreads() would drain the whole ring). The LDS image
 // is lane-linear per wave instruction (16 rows x 64 B); the swizzle is applied on the
 // global source address.
-template <int BM, int BN, int STAGES, int EPI, bool CONV>
-__global__ __launch_bounds__(BM / 64 * 128, BM == 256 ? 1 : (STAGES == 2 ? (CONV || EPI == 3 ? 4 : 5) : 2)) void gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda,
+template <int BM, int BN, int STAGES, int EPI, bool CONV, int BKX = 0>
+__global__ __launch_bounds__(256, BM == 256 ? (BN == 256 ? 1 : 2) : (STAGES == 2 ? (CONV || EPI == 3 ? 4 : 5) : 2)) void gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda,
                                                          const uint16_t* __restrict__ B, int64_t ldb,
                                                          uint16_t* C, int64_t ldc, int64_t M, int N, int K,
                                                          int ntn, EpiArgs ep, const uint16_t* Cin,
                                                          const uint8_t* __restrict__ Cmask,
                                                          const float* __restrict__ bias, int relu, ConvGeo geo) {
-  constexpr int NW = BM / 64 * 2, NT = NW * 64;  // waves, threads
-  constexpr int WM = 64, WN = BN / 2;
+  constexpr int NW = 4, NT = NW * 64;  // waves, threads
+  constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 32, TN = WN / 32;
-  constexpr int IA = BM / 16 / NW, IB = BN / 16 / NW;  // glds instructions per wave per tile
+  constexpr int BK = BKX ? BKX : nt_bk(BM, BN), CPK = BK / 8, RPI = 64 / CPK;  // 16-B chunks per row, rows per glds
+  constexpr int IA = BM / RPI / NW, IB = BN / RPI / NW;  // glds instructions per wave per tile
   constexpr int NI = IA + IB;
-  constexpr int TILE = (BM + BN) * kBK;  // elements per stage
+  constexpr int TILE = (BM + BN) * BK;  // elements per stage
   static_assert(IA >= 1 && IB >= 1, "tile too small");
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
 
@@ -181,7 +195,7 @@ __global__ __launch_bounds__(BM / 64 * 128, BM == 256 ? 1 : (STAGES == 2 ? (CONV
   int hi0[IA], wi0[IA], ca[IA], img[IA];
 #pragma unroll
   for (int i = 0; i < IA; ++i) {
-    const int row = (w * IA + i) * 16 + (lane >> 2), c = swz(row, lane & 3);
+    const int row = (w * IA + i) * RPI + lane / CPK, c = swzk<BK>(row, lane % CPK);
     const int64_t gm = min(m0 + row, M - 1);  // clamp: tail rows compute garbage, never stored
     if constexpr (CONV) {
       const int hw = geo.Ho * geo.Wo;
@@ -198,28 +212,28 @@ __global__ __launch_bounds__(BM / 64 * 128, BM == 256 ? 1 : (STAGES == 2 ? (CONV
   int kc = 0, kr = 0, ks = 0;  // CONV: channel offset and tap of the next tile issued
 #pragma unroll
   for (int i = 0; i < IB; ++i) {
-    const int row = (w * IB + i) * 16 + (lane >> 2), c = swz(row, lane & 3);
+    const int row = (w * IB + i) * RPI + lane / CPK, c = swzk<BK>(row, lane % CPK);
     pb[i] = B + int64_t(n0 + row) * ldb + c * 8;
   }
   auto issue = [&](int kt, int buf) {
     uint16_t* As = smem + buf * TILE;
-    uint16_t* Bs = As + BM * kBK;
+    uint16_t* Bs = As + BM * BK;
 #pragma unroll
     for (int i = 0; i < IA; ++i) {
       if constexpr (CONV) {
         const int hi = hi0[i] + kr, wi = wi0[i] + ks;
         const bool ok = unsigned(hi) < unsigned(geo.H) && unsigned(wi) < unsigned(geo.W);
         const uint16_t* src = ok ? A + (((img[i] + hi) * geo.W + wi) * geo.C + kc + ca[i]) : g_zero_line + ca[i];
-        glds16(src, As + (w * IA + i) * 16 * kBK);
+        glds16(src, As + (w * IA + i) * RPI * BK);
       } else {
-        glds16(pa[i] + kt * kBK, As + (w * IA + i) * 16 * kBK);
+        glds16(pa[i] + kt * BK, As + (w * IA + i) * RPI * BK);
       }
     }
 #pragma unroll
     for (int i = 0; i < IB; ++i)
-      glds16(pb[i] + kt * kBK, Bs + (w * IB + i) * 16 * kBK);
+      glds16(pb[i] + kt * BK, Bs + (w * IB + i) * RPI * BK);
     if constexpr (CONV) {  // tiles are issued in k order: step to the next (tap, channel) slab
-      kc += kBK;
+      kc += BK;
       if (kc == geo.C) {
         kc = 0;
         if (++ks == geo.S) {
@@ -239,7 +253,7 @@ __global__ __launch_bounds__(BM / 64 * 128, BM == 256 ? 1 : (STAGES == 2 ? (CONV
       for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
 
   const int fr = lane & 31, fh = lane >> 5;
-  const int nk = K / kBK;
+  const int nk = K / BK;
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
     if (s < nk) issue(s, s);
@@ -253,20 +267,56 @@ __global__ __launch_bounds__(BM / 64 * 128, BM == 256 ? 1 : (STAGES == 2 ? (CONV
     asm volatile("" ::: "memory");
     if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
     const uint16_t* As = smem + (kt % STAGES) * TILE;
-    const uint16_t* Bs = As + BM * kBK;
+    const uint16_t* Bs = As + BM * BK;
+    if constexpr (TM * TN >= 8) {
+      // big wave tiles run one or two waves per SIMD, so nothing else hides a fragment read:
+      // the fragments of k16 step kk+1 are read while step kk's MFMAs run (two register
+      // sets), pinned so the scheduler does not re-serialise read -> wait -> MFMAs
+      constexpr int KK = BK / 16;
+      bf16x8 af[2][TM], bfg[2][TN];
+      auto frag = [&](int kk, int slot) {
+        const int c = 2 * kk + fh;
 #pragma unroll
-    for (int kk = 0; kk < kBK / 16; ++kk) {
+        for (int i = 0; i < TM; ++i) {
+          const int r = wm * WM + i * 32 + fr;
+          af[slot][i] = *reinterpret_cast<const bf16x8*>(As + r * BK + swzk<BK>(r, c) * 8);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int r = wn * WN + j * 32 + fr;
+          bfg[slot][j] = *reinterpret_cast<const bf16x8*>(Bs + r * BK + swzk<BK>(r, c) * 8);
+        }
+      };
+      frag(0, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, TM + TN, 0);
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        if (kk + 1 < KK) {
+          frag(kk + 1, (kk + 1) & 1);
+          __builtin_amdgcn_sched_group_barrier(0x100, TM + TN, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfg[kk & 1][j], af[kk & 1][i], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, TM * TN, 0);
+      }
+      continue;
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK / 16; ++kk) {
       bf16x8 af[TM], bfg[TN];
       const int c = 2 * kk + fh;
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int r = wm * WM + i * 32 + fr;
-        af[i] = *reinterpret_cast<const bf16x8*>(As + r * kBK + swz(r, c) * 8);
+        af[i] = *reinterpret_cast<const bf16x8*>(As + r * BK + swzk<BK>(r, c) * 8);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int r = wn * WN + j * 32 + fr;
-        bfg[j] = *reinterpret_cast<const bf16x8*>(Bs + r * kBK + swz(r, c) * 8);
+        bfg[j] = *reinterpret_cast<const bf16x8*>(Bs + r * BK + swzk<BK>(r, c) * 8);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -808,6 +858,26 @@ int64_t gemm_nt_stats_floats(int64_t M, int N) { return gemm_nt_tiles(M) * 2 * i
 
 int64_t gemm_nt_tiles(int64_t M) { return (M + 127) / 128; }
 
+// Block tile of gemm_nt: 0 = 128 x (128 | 64), 1 = 256 x 128, 2 = 256 x 256;
+// MPIT_GEMM_TILE=128|256x128|256 selects one (A/B runs, large plain GEMMs).
+static int nt_tile_config(int N, int K, bool conv, int cin_conv) {
+  static const int forced = [] {
+    const char* e = std::getenv("MPIT_GEMM_TILE");
+    if (!e) return -1;
+    const std::string v(e);
+    return v == "256" ? 2 : v == "256x128" ? 1 : v == "128" ? 0 : -1;
+  }();
+  int cfg = forced >= 0 ? forced : 0;
+  // Measured (profiles/gemm_big_tile_ab_r01.jsonl, gemm_bk64_128tile_ab_r01.jsonl): 256x256
+  // (BK 64) beats 128x128 on large square GEMMs (8192^3: 944 vs 611 TFLOP/s) and 256x128 on
+  // 50176x256x2304 (+18 %), yet inside the models both lose end to end (ResNet-50 -1.6 %,
+  // VGG-16 -2.7 %, AlexNet -2.7 %: one or two blocks per CU leave the epilogue and the
+  // other streams nothing to overlap with), so the automatic choice stays 128x128.
+  if (cfg == 2 && (N % 256 || K % 64 || (conv && cin_conv % 64))) cfg = N % 128 ? 0 : 1;
+  if (cfg == 1 && N % 128) cfg = 0;
+  return cfg;
+}
+
 static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B,
                       int64_t ldb, uintptr_t C, int64_t ldc, uintptr_t cin, uintptr_t cmask, const ConvGeo* geo,
                       const EpiArgs& ep, int epi, uintptr_t bias = 0, bool relu = false) {
@@ -848,29 +918,43 @@ static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t
   }();
   const int stages = std::min(max_stages, nk >= 4 ? 4 : (nk == 3 ? 3 : 2));
   // (kernel templates are named at a non-template call site so their host stubs are emitted)
-#define MPIT_NT_LAUNCH1(BM, BN, ST, EPI, CONV)                                                                    \
-  hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, ST, EPI, CONV>), dim3(unsigned(nb)), dim3(BM / 64 * 128), shm, s, a, \
-                     lda, b, ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g)
-#define MPIT_NT_LAUNCH2(BM, BN, ST, CONV)                                   \
-  do {                                                                      \
-    if (epi == EPI_STATS) MPIT_NT_LAUNCH1(BM, BN, ST, EPI_STATS, CONV);     \
-    else if (epi == EPI_BNRED) MPIT_NT_LAUNCH1(BM, BN, ST, EPI_BNRED, CONV); \
-    else if (epi == EPI_BNRED2 && !CONV) MPIT_NT_LAUNCH1(BM, BN, ST, EPI_BNRED2, false); \
-    else MPIT_NT_LAUNCH1(BM, BN, ST, EPI_NONE, CONV);                       \
+#define MPIT_NT_LAUNCH1(BM, BN, ST, EPI, CONV, BKX)                                                                  \
+  do {                                                                                                             \
+    if (shm > 65536) { /* beyond the default dynamic-LDS cap: opt in once per instantiation */                    \
+      static const bool opted = (hip_check(hipFuncSetAttribute(                                                      \
+                                               reinterpret_cast<const void*>(&gemm_nt_kernel<BM, BN, ST, EPI, CONV, BKX>), \
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, int(shm)),                \
+                                           "hipFuncSetAttribute"),                                                   \
+                                 true);                                                                              \
+      (void)opted;                                                                                                   \
+    }                                                                                                                \
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, ST, EPI, CONV, BKX>), dim3(unsigned(nb)), dim3(256), shm, s, a,          \
+                       lda, b, ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g);                             \
   } while (0)
-#define MPIT_NT_LAUNCH(BM, BN, ST)                                                                             \
+#define MPIT_NT_LAUNCH2(BM, BN, ST, CONV, BKX)                                                    \
+  do {                                                                                              \
+    if (epi == EPI_STATS) MPIT_NT_LAUNCH1(BM, BN, ST, EPI_STATS, CONV, BKX);                        \
+    else if (epi == EPI_BNRED) MPIT_NT_LAUNCH1(BM, BN, ST, EPI_BNRED, CONV, BKX);                   \
+    else if (epi == EPI_BNRED2 && !CONV) MPIT_NT_LAUNCH1(BM, BN, ST, EPI_BNRED2, false, BKX);       \
+    else MPIT_NT_LAUNCH1(BM, BN, ST, EPI_NONE, CONV, BKX);                                          \
+  } while (0)
+#define MPIT_NT_LAUNCHB(BM, BN, ST, BKX)                                                                       \
   do {                                                                                                         \
     const int64_t mtn = (M + BM - 1) / BM;                                                                     \
     const int ntn = N / BN;                                                                                    \
     const int64_t nb = mtn * ntn;                                                                              \
     if (nb > INT32_MAX) throw std::invalid_argument("gemm_nt: too many tiles");                               \
     /* LDS: the k-tile ring, reused by the epilogue's bf16 tile and reduction table */                        \
-    const size_t shm = std::max({size_t(ST) * (BM + BN) * kBK * 2, size_t(BM) * BN * 2,                        \
-                                 size_t(BM / 64 * 128) * 8 * 3 * sizeof(float)});                             \
-    if (geo) MPIT_NT_LAUNCH2(BM, BN, ST, true);                                                                \
-    else MPIT_NT_LAUNCH2(BM, BN, ST, false);                                                                   \
+    const size_t shm = std::max({size_t(ST) * (BM + BN) * size_t(BKX ? BKX : nt_bk(BM, BN)) * 2,               \
+                                 size_t(BM) * BN * 2, size_t(256) * 8 * 3 * sizeof(float)});                  \
+    if (geo) MPIT_NT_LAUNCH2(BM, BN, ST, true, BKX);                                                           \
+    else MPIT_NT_LAUNCH2(BM, BN, ST, false, BKX);                                                              \
   } while (0)
-  if (N % 128 == 0) {
+#define MPIT_NT_LAUNCH(BM, BN, ST) MPIT_NT_LAUNCHB(BM, BN, ST, 0)
+  const int tcfg = nt_tile_config(N, K, geo != nullptr, geo ? geo->C : 0);
+  if (tcfg == 2) MPIT_NT_LAUNCH(256, 256, 2);  // 2 x 64-deep stages = the 128 KB epilogue tile
+  else if (tcfg == 1) MPIT_NT_LAUNCH(256, 128, 3);
+  else if (N % 128 == 0) {
     if (stages == 4) MPIT_NT_LAUNCH(128, 128, 4);
     else if (stages == 3) MPIT_NT_LAUNCH(128, 128, 3);
     else MPIT_NT_LAUNCH(128, 128, 2);
@@ -879,6 +963,7 @@ static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t
     else if (stages == 3) MPIT_NT_LAUNCH(128, 64, 3);
     else MPIT_NT_LAUNCH(128, 64, 2);
   }
+#undef MPIT_NT_LAUNCHB
 #undef MPIT_NT_LAUNCH
 #undef MPIT_NT_LAUNCH2
 #undef MPIT_NT_LAUNCH1

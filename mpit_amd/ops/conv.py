@@ -25,6 +25,8 @@ stays on MIOpen.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -34,6 +36,50 @@ from .._ext import native
 
 def _stream(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
+
+
+class WgradStream:
+    """Weight-gradient GEMMs on a second HIP stream.
+
+    In a convolution's backward the input gradient is on the critical path (the next
+    layer's BN backward needs it) while the weight gradient is only read by the optimizer
+    step, so the backward-weight GEMM (compute-bound, ~18 % of a ResNet-50 step) is queued
+    on a side stream and overlaps the memory-bound BN / ReLU kernels of the layers below.
+    Both wait on the gradient of the convolution's output; the side stream joins back into
+    the compute stream at :meth:`join`, which every consumer of the weight gradients calls
+    first (the trainer after ``backward()``, the shard pusher before a gather). Only
+    enabled by a trainer whose gradients are stolen (no autograd kernel reads them before
+    that join); tensors the side stream touches are ``record_stream``-ed so the caching
+    allocator does not recycle them early. MPIT_WGRAD_STREAM=0 disables it.
+    """
+
+    enabled = False
+    _side = {}
+    _pending = set()
+
+    @classmethod
+    def enable(cls, on: bool = True):
+        cls.enabled = bool(on) and os.environ.get("MPIT_WGRAD_STREAM", "1") != "0"
+
+    @classmethod
+    def begin(cls, dev: torch.device):
+        """The side stream, ordered after everything queued so far on the current stream
+        (issue before the input-gradient kernel so the side stream does not wait for it)."""
+        if not cls.enabled:
+            return None
+        st = cls._side.get(dev.index)
+        if st is None:
+            st = cls._side[dev.index] = torch.cuda.Stream(dev)
+        st.wait_stream(torch.cuda.current_stream(dev))
+        cls._pending.add(dev.index)
+        return st
+
+    @classmethod
+    def join(cls):
+        """Order the current stream after every weight gradient issued so far."""
+        for idx in list(cls._pending):
+            torch.cuda.current_stream(idx).wait_stream(cls._side[idx])
+        cls._pending.clear()
 
 
 def _cl(x: torch.Tensor) -> torch.Tensor:
@@ -228,6 +274,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         m = native()
         dev, s = x.device.index, _stream(x)
         dx = dw = None
+        side = WgradStream.begin(x.device) if ctx.needs_input_grad[1] else None
         extra, emask = ctx.slot.take() if ctx.slot is not None else (None, None)
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x, memory_format=torch.channels_last)
@@ -251,8 +298,9 @@ class _Conv1x1Fn(torch.autograd.Function):
             dw = torch.empty(ctx.wshape, dtype=torch.float32, device=x.device)
             nws = m.gemm_tn_ws_floats(dev, M, co, ci)
             ws = torch.empty(nws, dtype=torch.float32, device=x.device) if nws else None
-            m.gemm_tn(dev, s, M, co, ci, dy.data_ptr(), co, x.data_ptr(), ci, dw.data_ptr(),
-                      ws.data_ptr() if ws is not None else 0, 0.0)
+            m.gemm_tn(dev, side.cuda_stream if side is not None else s, M, co, ci, dy.data_ptr(), co, x.data_ptr(),
+                      ci, dw.data_ptr(), ws.data_ptr() if ws is not None else 0, 0.0)
+            _used_on(side, dy, x, dw, ws)
         return dx, dw, None, None, None, None
 
 
@@ -316,6 +364,13 @@ def conv_weights(weight: torch.Tensor, dgrad: bool):
     return wb, wt
 
 
+def _used_on(side, *ts):
+    if side is not None:
+        for t in ts:
+            if t is not None:
+                t.record_stream(side)
+
+
 def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None):
     """(dx, dw) of an NHWC implicit-GEMM conv from the gradient ``dz`` of its output; with a
     BNLink the backward-data GEMM also produces the producing BN's backward reduction."""
@@ -325,6 +380,7 @@ def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None):
     m = native()
     dev, st = x.device.index, _stream(x)
     dx = dw = None
+    side = WgradStream.begin(x.device) if ctx.needs_input_grad[1] else None
     if ctx.needs_input_grad[0]:
         if stride == 1 and wt is not None:
             # backward-data = forward conv of dz with the flipped, transposed weight
@@ -357,8 +413,9 @@ def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None):
         dw = torch.empty((co, c, r, s), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
         nws = m.conv_wgrad_ws_floats(dev, nb, h, w, c, co, r, s, stride, pad)
         ws = torch.empty(nws, dtype=torch.float32, device=x.device) if nws else None
-        m.conv_wgrad(dev, st, nb, h, w, c, co, r, s, stride, pad, dz.data_ptr(), x.data_ptr(), dw.data_ptr(),
-                     ws.data_ptr() if ws is not None else 0, 0.0)
+        m.conv_wgrad(dev, side.cuda_stream if side is not None else st, nb, h, w, c, co, r, s, stride, pad,
+                     dz.data_ptr(), x.data_ptr(), dw.data_ptr(), ws.data_ptr() if ws is not None else 0, 0.0)
+        _used_on(side, dz, x, dw, ws)
     return dx, dw
 
 

@@ -22,6 +22,7 @@ from typing import List
 
 import torch
 
+from ..ops.conv import WgradStream
 from ..ops.fused import gather_scale_
 
 
@@ -66,6 +67,7 @@ class ShardPusher:
                 self._fire(k)
 
     def _fire(self, k: int):
+        WgradStream.join()  # weight gradients may still be in flight on the side stream
         srcs, offs, ns = [], [], []
         for i in self.members[k]:
             if self.gathered[i]:

@@ -22,17 +22,20 @@ struct PoolGeo {
   int N, H, W, C, Ho, Wo, K, stride, pad;
 };
 
+// I: index type of the pixel decomposition — uint32_t whenever the tensor allows (64-bit
+// divisions are emulated and made these kernels 2.5x slower than their bytes)
+template <typename I>
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
                                                           uint8_t* __restrict__ idx, PoolGeo g) {
-  const int cv = g.C / 8;
-  const int64_t total = int64_t(g.N) * g.Ho * g.Wo * cv;
-  for (int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; t < total; t += int64_t(gridDim.x) * blockDim.x) {
+  const I cv = I(g.C / 8);
+  const I total = I(g.N) * I(g.Ho) * I(g.Wo) * cv;
+  for (I t = I(blockIdx.x) * blockDim.x + threadIdx.x; t < total; t += I(gridDim.x) * blockDim.x) {
     const int c8 = int(t % cv);
-    const int64_t pix = t / cv;
-    const int wo = int(pix % g.Wo);
-    const int64_t r = pix / g.Wo;
-    const int ho = int(r % g.Ho);
-    const int64_t n = r / g.Ho;
+    const I pix = t / cv;
+    const int wo = int(pix % I(g.Wo));
+    const I r = pix / I(g.Wo);
+    const int ho = int(r % I(g.Ho));
+    const int64_t n = int64_t(r / I(g.Ho));
     float best[8];
     uint8_t arg[8];
 #pragma unroll
@@ -64,26 +67,27 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint16_t* __rest
     uint32_t* op = &o.x;
 #pragma unroll
     for (int e = 0; e < 4; ++e) op[e] = uint32_t(f2bf(best[2 * e])) | (uint32_t(f2bf(best[2 * e + 1])) << 16);
-    *reinterpret_cast<uint4*>(y + pix * g.C + c8 * 8) = o;
+    *reinterpret_cast<uint4*>(y + int64_t(pix) * g.C + c8 * 8) = o;
     uint2 a;
     a.x = uint32_t(arg[0]) | (uint32_t(arg[1]) << 8) | (uint32_t(arg[2]) << 16) | (uint32_t(arg[3]) << 24);
     a.y = uint32_t(arg[4]) | (uint32_t(arg[5]) << 8) | (uint32_t(arg[6]) << 16) | (uint32_t(arg[7]) << 24);
-    *reinterpret_cast<uint2*>(idx + pix * g.C + c8 * 8) = a;
+    *reinterpret_cast<uint2*>(idx + int64_t(pix) * g.C + c8 * 8) = a;
   }
 }
 
+template <typename I>
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const uint16_t* __restrict__ dy,
                                                           const uint8_t* __restrict__ idx, uint16_t* __restrict__ dx,
                                                           PoolGeo g) {
-  const int cv = g.C / 8;
-  const int64_t total = int64_t(g.N) * g.H * g.W * cv;
-  for (int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; t < total; t += int64_t(gridDim.x) * blockDim.x) {
+  const I cv = I(g.C / 8);
+  const I total = I(g.N) * I(g.H) * I(g.W) * cv;
+  for (I t = I(blockIdx.x) * blockDim.x + threadIdx.x; t < total; t += I(gridDim.x) * blockDim.x) {
     const int c8 = int(t % cv);
-    const int64_t pix = t / cv;
-    const int w = int(pix % g.W);
-    const int64_t r = pix / g.W;
-    const int h = int(r % g.H);
-    const int64_t n = r / g.H;
+    const I pix = t / cv;
+    const int w = int(pix % I(g.W));
+    const I r = pix / I(g.W);
+    const int h = int(r % I(g.H));
+    const int64_t n = int64_t(r / I(g.H));
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     // output windows containing h: ho*stride - pad <= h <= ho*stride - pad + K - 1
     const int hlo = max(0, (h + g.pad - g.K + g.stride) / g.stride), hhi = min(g.Ho - 1, (h + g.pad) / g.stride);
@@ -110,7 +114,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const uint16_t* __rest
     uint32_t* op = &o.x;
 #pragma unroll
     for (int e = 0; e < 4; ++e) op[e] = uint32_t(f2bf(acc[2 * e])) | (uint32_t(f2bf(acc[2 * e + 1])) << 16);
-    *reinterpret_cast<uint4*>(dx + pix * g.C + c8 * 8) = o;
+    *reinterpret_cast<uint4*>(dx + int64_t(pix) * g.C + c8 * 8) = o;
   }
 }
 
@@ -122,7 +126,7 @@ PoolGeo pool_geo(int N, int H, int W, int C, int K, int stride, int pad) {
   return g;
 }
 
-unsigned grid_for(int64_t work) { return unsigned(std::min<int64_t>((work + 255) / 256, 8192)); }
+unsigned grid_for(int64_t work) { return unsigned(std::min<int64_t>((work + 255) / 256, 65536)); }
 
 }  // namespace
 
@@ -131,9 +135,12 @@ void maxpool_fwd(int dev, hipStream_t s, int N, int H, int W, int C, int K, int 
   const PoolGeo g = pool_geo(N, H, W, C, K, stride, pad);
   if ((x | y) % 16 || idx % 8) throw std::invalid_argument("maxpool_fwd: misaligned buffers");
   hip_check(hipSetDevice(dev), "hipSetDevice");
-  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(int64_t(N) * g.Ho * g.Wo * (C / 8))), dim3(256), 0, s,
-                     reinterpret_cast<const uint16_t*>(x), reinterpret_cast<uint16_t*>(y),
-                     reinterpret_cast<uint8_t*>(idx), g);
+  const int64_t work = int64_t(N) * g.Ho * g.Wo * (C / 8);
+  // 32-bit indexing while the grid-stride index cannot wrap (work + one grid < 2^32)
+  const bool narrow = work + int64_t(grid_for(work)) * 256 < (int64_t(1) << 32);
+  auto* k = narrow ? maxpool_fwd_kernel<uint32_t> : maxpool_fwd_kernel<int64_t>;
+  hipLaunchKernelGGL(k, dim3(grid_for(work)), dim3(256), 0, s, reinterpret_cast<const uint16_t*>(x),
+                     reinterpret_cast<uint16_t*>(y), reinterpret_cast<uint8_t*>(idx), g);
   hip_check(hipGetLastError(), "maxpool_fwd launch");
 }
 
@@ -142,9 +149,11 @@ void maxpool_bwd(int dev, hipStream_t s, int N, int H, int W, int C, int K, int 
   const PoolGeo g = pool_geo(N, H, W, C, K, stride, pad);
   if ((dy | dx) % 16 || idx % 8) throw std::invalid_argument("maxpool_bwd: misaligned buffers");
   hip_check(hipSetDevice(dev), "hipSetDevice");
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(int64_t(N) * H * W * (C / 8))), dim3(256), 0, s,
-                     reinterpret_cast<const uint16_t*>(dy), reinterpret_cast<const uint8_t*>(idx),
-                     reinterpret_cast<uint16_t*>(dx), g);
+  const int64_t work = int64_t(N) * H * W * (C / 8);
+  const bool narrow = work + int64_t(grid_for(work)) * 256 < (int64_t(1) << 32);
+  auto* k = narrow ? maxpool_bwd_kernel<uint32_t> : maxpool_bwd_kernel<int64_t>;
+  hipLaunchKernelGGL(k, dim3(grid_for(work)), dim3(256), 0, s, reinterpret_cast<const uint16_t*>(dy),
+                     reinterpret_cast<const uint8_t*>(idx), reinterpret_cast<uint16_t*>(dx), g);
   hip_check(hipGetLastError(), "maxpool_bwd launch");
 }
 

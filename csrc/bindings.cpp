@@ -175,6 +175,15 @@ PYBIND11_MODULE(_mpit, m) {
   m.def("relu_bias_bwd_ws_floats", &relu_bias_bwd_ws_floats);
   m.def("relu_bias_bwd", [](int dev, uintptr_t s, int64_t M, int C, uintptr_t dy, uintptr_t y, uintptr_t dz, uintptr_t db,
                             uintptr_t ws) { relu_bias_bwd(dev, S(s), M, C, dy, y, dz, db, ws); });
+  m.def("conv_stem_fwd", [](int dev, uintptr_t s, int Nb, int Hp, int Wp, int Co, int Ho, int Wo, int stride,
+                            uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats) {
+    conv_stem_fwd(dev, S(s), Nb, Hp, Wp, Co, Ho, Wo, stride, x, w, y, stats);
+  });
+  m.def("conv_stem_wgrad_ws_floats", &conv_stem_wgrad_ws_floats);
+  m.def("conv_stem_wgrad", [](int dev, uintptr_t s, int Nb, int Hp, int Wp, int Co, int Ho, int Wo, int stride,
+                              uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws) {
+    conv_stem_wgrad(dev, S(s), Nb, Hp, Wp, Co, Ho, Wo, stride, dy, x, dw, ws);
+  });
   m.def("conv_wgrad_ws_floats", &conv_wgrad_ws_floats);
   m.def("conv_wgrad", [](int dev, uintptr_t s, int Nb, int H, int W, int C, int Co, int R, int S_, int stride, int pad,
                          uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, float beta) {

@@ -57,6 +57,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 constexpr int kBK = 32;  // k-depth of one staged tile (gemm_nt): 64-B LDS rows
+constexpr int kStemTap = 32, kStemK = 8 * kStemTap;  // row-tap stem: 8 pixels x 4 channels per row
 
 // NHWC convolution geometry for the implicit-GEMM (CONV) kernel variants
 struct ConvGeo {
@@ -68,6 +69,10 @@ struct ConvGeo {
   // (i*ostr + oph, j*ostr + opw) of an OH x OW image (one parity class of a strided conv's
   // backward-data); ozero also writes zeros to the other three parities (stride 2 only)
   int ostr, oph, opw, OH, OW, ozero;
+  // elements per input pixel when a tap is not one pixel's channels (0: C). The "row tap"
+  // stem conv (conv_stem_*) reads C = 32 contiguous elements = 8 pixels of 4 channels per
+  // kernel row: a 7x7 / 3-channel stem as an 8-row implicit GEMM over a padded NHWC4 image
+  int pitch;
 };
 
 enum { EPI_NONE = 0, EPI_STATS = 1, EPI_BNRED = 2, EPI_BNRED2 = 3 };
@@ -210,6 +215,7 @@ __global__ __launch_bounds__(256, BM == 256 ? (BN == 256 ? 1 : 2) : (STAGES == 2
     }
   }
   int kc = 0, kr = 0, ks = 0;  // CONV: channel offset and tap of the next tile issued
+  const int pitch = geo.pitch ? geo.pitch : geo.C;
 #pragma unroll
   for (int i = 0; i < IB; ++i) {
     const int row = (w * IB + i) * RPI + lane / CPK, c = swzk<BK>(row, lane % CPK);
@@ -223,7 +229,7 @@ __global__ __launch_bounds__(256, BM == 256 ? (BN == 256 ? 1 : 2) : (STAGES == 2
       if constexpr (CONV) {
         const int hi = hi0[i] + kr, wi = wi0[i] + ks;
         const bool ok = unsigned(hi) < unsigned(geo.H) && unsigned(wi) < unsigned(geo.W);
-        const uint16_t* src = ok ? A + (((img[i] + hi) * geo.W + wi) * geo.C + kc + ca[i]) : g_zero_line + ca[i];
+        const uint16_t* src = ok ? A + (((img[i] + hi) * geo.W + wi) * pitch + kc + ca[i]) : g_zero_line + ca[i];
         glds16(src, As + (w * IA + i) * RPI * BK);
       } else {
         glds16(pa[i] + kt * BK, As + (w * IA + i) * RPI * BK);
@@ -609,13 +615,19 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const uint16_t* __restr
     }
   }
   const int64_t ystep = int64_t(kRows) * ldy, xstep = int64_t(kRows) * ldx;
-  int xr = 0, xs = 0, xc = 0, dn = 0, dh = 0, dw = 0;
-  int pn[IX], pho[IX], pwo[IX];
+  int dn = 0, dh = 0, dw = 0;
+  // CONV: tap (xr, xs) and element offset xc inside the tap of each lane's 8-column chunk
+  // (per lane: a column tile may span taps when a tap is narrower than the tile, stem)
+  int pn[IX], pho[IX], pwo[IX], xr[IX], xs[IX], xc[IX];
+  const int pitch = geo.pitch ? geo.pitch : geo.C;
   if constexpr (CONV) {
-    const int tap = k0 / geo.C;
-    xc = k0 - tap * geo.C;
-    xr = tap / geo.S;
-    xs = tap - xr * geo.S;
+#pragma unroll
+    for (int i = 0; i < IX; ++i) {
+      const int kcol = k0 + ox[i], tap = kcol / geo.C;
+      xc[i] = kcol - tap * geo.C;
+      xr[i] = tap / geo.S;
+      xs[i] = tap - xr[i] * geo.S;
+    }
     const int hw = geo.Ho * geo.Wo;
     dn = kRows / hw;
     dh = (kRows - dn * hw) / geo.Wo;
@@ -642,9 +654,9 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const uint16_t* __restr
 #pragma unroll
     for (int i = 0; i < IX; ++i) {
       if constexpr (CONV) {
-        const int hi = pho[i] * geo.stride - geo.pad + xr, wi = pwo[i] * geo.stride - geo.padw + xs;
+        const int hi = pho[i] * geo.stride - geo.pad + xr[i], wi = pwo[i] * geo.stride - geo.padw + xs[i];
         const bool ok = rs + rx[i] < nrows && unsigned(hi) < unsigned(geo.H) && unsigned(wi) < unsigned(geo.W);
-        const int off = ((pn[i] * geo.H + hi) * geo.W + wi) * geo.C + xc + ox[i];  // < 2^31 (host-checked)
+        const int off = ((pn[i] * geo.H + hi) * geo.W + wi) * pitch + xc[i];  // < 2^31 (host-checked)
         glds16_asm(ok ? X + off : g_zero_line + (ox[i] & 63), Xs + (w * IX + i) * RX * TBK);
         pwo[i] += dw;  // next step's rows (issued strictly in order)
         const int cw = pwo[i] >= geo.Wo;
@@ -1151,6 +1163,39 @@ void conv_wgrad(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int
   const ConvGeo g = conv_geo(H, W, C, R, S, stride, pad, &Ho, &Wo);
   const int64_t M = int64_t(Nb) * Ho * Wo;
   launch_tn(dev, s, M, Co, R * S * C, dy, Co, x, C, dw, ws, beta, &g);
+}
+
+// Row-tap stem convolution: x is a zero-padded NHWC4 image [Nb][Hp][Wp][4] (bf16), the
+// kernel has 8 rows of 8 pixels x 4 channels (K = 256; a 7x7x3 kernel zero-extended), output
+// pixel (ho, wo) reads rows ho*stride + r, pixels wo*stride .. +7 of each.
+static ConvGeo stem_geo(int Nb, int Hp, int Wp, int Ho, int Wo, int stride) {
+  if (Nb <= 0 || Ho <= 0 || Wo <= 0 || stride <= 0 || Hp < (Ho - 1) * stride + 8 || Wp < (Wo - 1) * stride + 8)
+    throw std::invalid_argument("conv_stem: padded image too small for the output");
+  if (int64_t(Nb) * Hp * Wp * 4 >= (int64_t(1) << 31)) throw std::invalid_argument("conv_stem: input too large");
+  return ConvGeo{Hp, Wp, kStemTap, Ho, Wo, 1, stride, 0, 0, 1, 0, 0, Ho, Wo, 0, 4};
+}
+
+void conv_stem_fwd(int dev, hipStream_t s, int Nb, int Hp, int Wp, int Co, int Ho, int Wo, int stride, uintptr_t x,
+                   uintptr_t w, uintptr_t y, uintptr_t stats) {
+  if (Co % 64) throw std::invalid_argument("conv_stem_fwd: need Co % 64 == 0");
+  const ConvGeo g = stem_geo(Nb, Hp, Wp, Ho, Wo, stride);
+  int mode;
+  const EpiArgs ep = epi_args(stats, nullptr, &mode);
+  launch_nt(dev, s, int64_t(Nb) * Ho * Wo, Co, kStemK, x, kStemTap, w, kStemK, y, Co, 0, 0, &g, ep, mode);
+}
+
+int64_t conv_stem_wgrad_ws_floats(int dev, int Nb, int Ho, int Wo, int Co) {
+  int64_t rps;
+  int tbn, tbk;
+  const int ns = tn_plan(dev, int64_t(Nb) * Ho * Wo, Co, kStemK, &rps, &tbn, &tbk, kStemTap);
+  return ns > 1 ? (int64_t(ns) + tn_groups(ns)) * Co * kStemK : 0;
+}
+
+void conv_stem_wgrad(int dev, hipStream_t s, int Nb, int Hp, int Wp, int Co, int Ho, int Wo, int stride, uintptr_t dy,
+                     uintptr_t x, uintptr_t dw, uintptr_t ws) {
+  if (Co % 64) throw std::invalid_argument("conv_stem_wgrad: need Co % 64 == 0");
+  const ConvGeo g = stem_geo(Nb, Hp, Wp, Ho, Wo, stride);
+  launch_tn(dev, s, int64_t(Nb) * Ho * Wo, Co, kStemK, dy, Co, x, kStemTap, dw, ws, 0.f, &g);
 }
 
 static void launch_cast(int dev, hipStream_t s, uintptr_t w, int R, int Cc, uintptr_t wb, uintptr_t wt, int taps,

@@ -162,6 +162,15 @@ int64_t conv_wgrad_ws_floats(int dev, int Nb, int H, int W, int C, int Co, int R
 void conv_wgrad(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad,
                 uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, float beta);
 
+// Row-tap stem conv (7x7 / stride-2 / 3-channel ResNet stem on MFMA): x = zero-padded NHWC4
+// image [Nb][Hp][Wp][4], w = [Co][8][8][4] (bf16, zero-extended kernel), y = [Nb][Ho][Wo][Co];
+// dw = [Co][8][8][4] fp32; stats: BN statistics of y as conv_fwd
+void conv_stem_fwd(int dev, hipStream_t s, int Nb, int Hp, int Wp, int Co, int Ho, int Wo, int stride, uintptr_t x,
+                   uintptr_t w, uintptr_t y, uintptr_t stats);
+int64_t conv_stem_wgrad_ws_floats(int dev, int Nb, int Ho, int Wo, int Co);
+void conv_stem_wgrad(int dev, hipStream_t s, int Nb, int Hp, int Wp, int Co, int Ho, int Wo, int stride, uintptr_t dy,
+                     uintptr_t x, uintptr_t dw, uintptr_t ws);
+
 // ---- NHWC bf16 max pooling with a uint8 argmax per output element (pool.hip) ---------
 // x [N,H,W,C] -> y, idx [N,Ho,Wo,C]; dx [N,H,W,C] gathered from dy + idx (no atomics).
 void maxpool_fwd(int dev, hipStream_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t x,

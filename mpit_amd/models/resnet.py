@@ -4,9 +4,10 @@ workload "ResNet-50 synthetic ImageNet". Written from the architecture definitio
 ResNet-50 / 1000 classes, the standard figure.
 
 Runs channels_last + bf16 autocast on MI355X: stride-1 1x1 convolutions on the
-hand-written MFMA GEMMs and the 3x3s on MFMA implicit GEMMs (mpit_amd/ops/conv.py), the
-7x7 stem, the strided 1x1 shortcuts and the strided 3x3 backward-data on MIOpen's NHWC
-kernels, and every BatchNorm(+add)(+ReLU) on the fused HIP kernels (ops/bn.py).
+hand-written MFMA GEMMs, the 3x3s and strided 1x1 shortcuts on MFMA implicit GEMMs (strided
+backward-data as parity classes), the 7x7 stem on the row-tap implicit GEMM
+(mpit_amd/ops/conv.py), and every BatchNorm(+add)(+ReLU) on the fused HIP kernels
+(ops/bn.py), whose statistics and backward reductions come from the GEMM epilogues.
 """
 from __future__ import annotations
 
@@ -18,7 +19,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.bn import BatchNormAct2d, bn_pair
-from ..ops.conv import Conv1x1, ConvNHWC, GradSlot, park_grad
+from ..ops.conv import Conv1x1, ConvNHWC, GradSlot, StemConv, park_grad
 from ..ops.pool import MaxPool2dNHWC
 
 # Fused BN(+add)(+ReLU) HIP kernels on MI355X (mpit_amd/ops/bn.py); same parameters and
@@ -141,8 +142,10 @@ class ResNet(nn.Module):
                  zero_init_residual: bool = False):
         super().__init__()
         self.inplanes = 64
-        self.conv1 = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
+        # 7x7 stem on the MFMA row-tap kernels (ops/conv.py StemConv), emitting bn1's statistics
+        self.conv1 = StemConv(3, 64, 7, 2, 3) if MFMA_CONV else nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
         self.bn1 = _bn(64, True)
+        _feeds_bn(self.conv1)
         self.relu = nn.ReLU(inplace=True)
         self.maxpool = MaxPool2dNHWC(3, stride=2, padding=1) if MFMA_CONV else nn.MaxPool2d(3, stride=2, padding=1)
         self.layer1 = self._make(block, 64, layers[0])

@@ -626,3 +626,91 @@ class WeightCastPlan:
         if c is None or not c[0].valid:
             return None
         return c[1]
+
+
+# ------------------------------------------------------------------ the 7x7 stem
+
+def _stem_pack_input(x: torch.Tensor, pad: int, hp: int, wp: int) -> torch.Tensor:
+    """[N, 3, H, W] -> zero-padded NHWC4 bf16 [N, hp, wp, 4] (one pad kernel)."""
+    v = _bf16_cl(x).permute(0, 2, 3, 1)  # NHWC view of the channels_last tensor
+    n, h, w, c = v.shape
+    return F.pad(v, (0, 4 - c, pad, wp - w - pad, pad, hp - h - pad))
+
+
+def _stem_pack_weight(weight: torch.Tensor) -> torch.Tensor:
+    """[Co, C<=4, R<=8, S<=8] -> bf16 [Co, 8, 8, 4], zero-extended."""
+    co, c, r, s = weight.shape
+    wp = torch.zeros((co, 8, 8, 4), dtype=torch.bfloat16, device=weight.device)
+    wp[:, :r, :s, :c] = weight.permute(0, 2, 3, 1)
+    return wp
+
+
+class _StemConvFn(torch.autograd.Function):
+    """7x7 (<= 8x8), <= 4-channel strided stem convolution as an 8-row implicit GEMM on the
+    MFMA kernels (csrc/kernels/gemm.hip ``conv_stem_*``): each kernel row is one 32-element
+    tap = 8 pixels x 4 channels of a zero-padded NHWC4 copy of the image, so the 3-channel
+    input needs no im2col and no per-channel gather. Forward also emits the BN statistics
+    of its output; backward computes the weight gradient only (the image needs none)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride: int, pad: int, hold=None):
+        nb, _, h, w = x.shape
+        co, _, r, s = weight.shape
+        ho, wo = (h + 2 * pad - r) // stride + 1, (w + 2 * pad - s) // stride + 1
+        hp, wp = max(h + 2 * pad, (ho - 1) * stride + 8), max(w + 2 * pad, (wo - 1) * stride + 8)
+        xp = _stem_pack_input(x, pad, hp, wp)
+        wb = _stem_pack_weight(weight)
+        y = torch.empty((nb, co, ho, wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+        st = None
+        if hold is not None:
+            st, nt = _tile_stats(co, nb * ho * wo, x.device)
+            hold.append((st, nt))
+        native().conv_stem_fwd(x.device.index, _stream(x), nb, hp, wp, co, ho, wo, stride, xp.data_ptr(),
+                               wb.data_ptr(), y.data_ptr(), st.data_ptr() if st is not None else 0)
+        ctx.save_for_backward(xp)
+        ctx.geo = (nb, hp, wp, co, ho, wo, stride, tuple(weight.shape))
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (xp,) = ctx.saved_tensors
+        nb, hp, wp, co, ho, wo, stride, wshape = ctx.geo
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dy = _bf16_cl(dy)
+            m = native()
+            dev = xp.device.index
+            dwp = torch.empty((co, 8, 8, 4), dtype=torch.float32, device=xp.device)
+            nws = m.conv_stem_wgrad_ws_floats(dev, nb, ho, wo, co)
+            ws = torch.empty(nws, dtype=torch.float32, device=xp.device) if nws else None
+            m.conv_stem_wgrad(dev, _stream(xp), nb, hp, wp, co, ho, wo, stride, dy.data_ptr(), xp.data_ptr(),
+                              dwp.data_ptr(), ws.data_ptr() if ws is not None else 0)
+            _, c, r, s = wshape
+            dw = dwp[:, :r, :s, :c].permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
+        return None, dw, None, None, None
+
+
+class StemConv(nn.Conv2d):
+    """``nn.Conv2d(c <= 4, co, k <= 8, stride, pad, bias=False)`` — the ResNet stem — on the
+    MFMA row-tap kernels on MI355X when the input needs no gradient (see _StemConvFn);
+    nn.Conv2d (MIOpen / CPU) otherwise. ``emit_stats`` as Conv1x1."""
+
+    def __init__(self, in_channels: int, out_channels: int, kernel_size: int, stride: int, padding: int):
+        super().__init__(in_channels, out_channels, kernel_size, stride=stride, padding=padding, bias=False)
+        self.emit_stats = False
+
+    def fused(self, x: torch.Tensor) -> bool:
+        co, c, r, s = self.weight.shape
+        bf16 = x.dtype == torch.bfloat16 or (torch.is_autocast_enabled("cuda")
+                                             and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+        return (x.is_cuda and bf16 and x.dim() == 4 and not x.requires_grad and c <= 4 and r <= 8 and s <= 8
+                and co % 64 == 0 and self.dilation == (1, 1) and self.groups == 1
+                and self.stride[0] == self.stride[1] and self.padding[0] == self.padding[1]
+                and os.environ.get("MPIT_MFMA_STEM", "1") != "0")
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.fused(x):
+            hold = [] if (self.emit_stats and self.training) else None
+            y = _StemConvFn.apply(x, self.weight, self.stride[0], self.padding[0], hold)
+            return _attach_stats(y, hold)
+        return super().forward(x)

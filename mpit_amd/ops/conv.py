@@ -61,17 +61,30 @@ class WgradStream:
     def enable(cls, on: bool = True):
         cls.enabled = bool(on) and os.environ.get("MPIT_WGRAD_STREAM", "1") != "0"
 
+    @staticmethod
+    def forced() -> bool:
+        """MPIT_WGRAD_STREAM=force: enable even where ranks share a GPU (correctness runs)."""
+        return os.environ.get("MPIT_WGRAD_STREAM", "1") == "force"
+
     @classmethod
     def begin(cls, dev: torch.device):
         """The side stream, ordered after everything queued so far on the current stream
         (issue before the input-gradient kernel so the side stream does not wait for it)."""
         if not cls.enabled:
             return None
+        st = cls.side(dev)
+        st.wait_stream(torch.cuda.current_stream(dev))
+        cls._pending.add(dev.index)
+        return st
+
+    @classmethod
+    def side(cls, dev: torch.device):
+        """The side stream of ``dev`` when enabled (created on first use), else None."""
+        if not cls.enabled:
+            return None
         st = cls._side.get(dev.index)
         if st is None:
             st = cls._side[dev.index] = torch.cuda.Stream(dev)
-        st.wait_stream(torch.cuda.current_stream(dev))
-        cls._pending.add(dev.index)
         return st
 
     @classmethod

@@ -18,12 +18,18 @@ gradient.
 """
 from __future__ import annotations
 
+import os
 from typing import List
 
 import torch
 
 from ..ops.conv import WgradStream
 from ..ops.fused import gather_scale_
+
+
+# MPIT_PUSH_ON_SIDE=1: gather + push gate on the side stream instead of joining it. Measured
+# at N=1 (one shard, fired at the end of the backward): 11.1k vs 11.65k img/s, so off.
+_PUSH_ON_SIDE = os.environ.get("MPIT_PUSH_ON_SIDE", "0") == "1"
 
 
 class ShardPusher:
@@ -67,7 +73,20 @@ class ShardPusher:
                 self._fire(k)
 
     def _fire(self, k: int):
-        WgradStream.join()  # weight gradients may still be in flight on the side stream
+        # With backward-weight GEMMs on the side stream (ops/conv.py WgradStream) either the
+        # compute stream joins it before the gather (default) or, MPIT_PUSH_ON_SIDE=1, the
+        # gather and the push gate go on the side stream behind the compute stream's work so
+        # far (the BN gradients), so the compute stream never waits for a shard
+        side = WgradStream.side(self.pc.tx.device) if (self.pc.tx.is_cuda and _PUSH_ON_SIDE) else None
+        if side is None:
+            WgradStream.join()  # weight gradients may still be in flight on the side stream
+            self._fire_on(k, None)
+            return
+        side.wait_stream(torch.cuda.current_stream(self.pc.tx.device))
+        with torch.cuda.stream(side):
+            self._fire_on(k, side)
+
+    def _fire_on(self, k: int, side):
         srcs, offs, ns = [], [], []
         for i in self.members[k]:
             if self.gathered[i]:
@@ -85,6 +104,8 @@ class ShardPusher:
                 offs.append(self.flat.offsets[i])
                 ns.append(g.numel())
                 p.grad = g  # keeps the source alive until the gather is queued
+                if side is not None:  # produced on the compute stream, read on the side one
+                    g.record_stream(side)
             self.gathered[i] = True
         if srcs:
             gather_scale_(self.pc.tx, srcs, offs, ns, self.a, self.aux, self.b)

@@ -101,7 +101,8 @@ class Trainer:
 
             # not when several ranks share one GPU (1-GPU rehearsals): their extra queues
             # time-slice the card (4 ranks: 8136 -> 1809 img/s)
-            WgradStream.enable(self.on_gpu and not st.shared_devices and cfg.extra.get("wgrad_stream", True))
+            WgradStream.enable(self.on_gpu and (not st.shared_devices or WgradStream.forced())
+                               and cfg.extra.get("wgrad_stream", True))
         if self.push_steal:
             # push each shard during the backward as soon as its gradients are complete
             if cfg.extra.get("overlap_push", True):

@@ -170,7 +170,7 @@ __device__ __forceinline__ int xcd_tile(int bid, int nb) {
 // the tile about to be used (a __syncthreads() would drain the whole ring). The LDS image
 // is lane-linear per wave instruction (16 rows x 64 B); the swizzle is applied on the
 // global source address.
-template <int BM, int BN, int STAGES, int EPI, bool CONV, int BKX = 0>
+template <int BM, int BN, int STAGES, int EPI, bool CONV>
 __global__ __launch_bounds__(256, BM == 256 ? (BN == 256 ? 1 : 2) : (STAGES == 2 ? (CONV || EPI == 3 ? 4 : 5) : 2)) void gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda,
                                                          const uint16_t* __restrict__ B, int64_t ldb,
                                                          uint16_t* C, int64_t ldc, int64_t M, int N, int K,
@@ -180,7 +180,7 @@ __global__ __launch_bounds__(256, BM == 256 ? (BN == 256 ? 1 : 2) : (STAGES == 2
   constexpr int NW = 4, NT = NW * 64;  // waves, threads
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 32, TN = WN / 32;
-  constexpr int BK = BKX ? BKX : nt_bk(BM, BN), CPK = BK / 8, RPI = 64 / CPK;  // 16-B chunks per row, rows per glds
+  constexpr int BK = nt_bk(BM, BN), CPK = BK / 8, RPI = 64 / CPK;  // 16-B chunks per row, rows per glds
   constexpr int IA = BM / RPI / NW, IB = BN / RPI / NW;  // glds instructions per wave per tile
   constexpr int NI = IA + IB;
   constexpr int TILE = (BM + BN) * BK;  // elements per stage
@@ -930,39 +930,38 @@ static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t
   }();
   const int stages = std::min(max_stages, nk >= 4 ? 4 : (nk == 3 ? 3 : 2));
   // (kernel templates are named at a non-template call site so their host stubs are emitted)
-#define MPIT_NT_LAUNCH1(BM, BN, ST, EPI, CONV, BKX)                                                                  \
+#define MPIT_NT_LAUNCH1(BM, BN, ST, EPI, CONV)                                                                       \
   do {                                                                                                             \
     if (shm > 65536) { /* beyond the default dynamic-LDS cap: opt in once per instantiation */                    \
       static const bool opted = (hip_check(hipFuncSetAttribute(                                                      \
-                                               reinterpret_cast<const void*>(&gemm_nt_kernel<BM, BN, ST, EPI, CONV, BKX>), \
+                                               reinterpret_cast<const void*>(&gemm_nt_kernel<BM, BN, ST, EPI, CONV>), \
                                                hipFuncAttributeMaxDynamicSharedMemorySize, int(shm)),                \
                                            "hipFuncSetAttribute"),                                                   \
                                  true);                                                                              \
       (void)opted;                                                                                                   \
     }                                                                                                                \
-    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, ST, EPI, CONV, BKX>), dim3(unsigned(nb)), dim3(256), shm, s, a,          \
+    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, ST, EPI, CONV>), dim3(unsigned(nb)), dim3(256), shm, s, a,          \
                        lda, b, ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g);                             \
   } while (0)
-#define MPIT_NT_LAUNCH2(BM, BN, ST, CONV, BKX)                                                    \
+#define MPIT_NT_LAUNCH2(BM, BN, ST, CONV)                                                         \
   do {                                                                                              \
-    if (epi == EPI_STATS) MPIT_NT_LAUNCH1(BM, BN, ST, EPI_STATS, CONV, BKX);                        \
-    else if (epi == EPI_BNRED) MPIT_NT_LAUNCH1(BM, BN, ST, EPI_BNRED, CONV, BKX);                   \
-    else if (epi == EPI_BNRED2 && !CONV) MPIT_NT_LAUNCH1(BM, BN, ST, EPI_BNRED2, false, BKX);       \
-    else MPIT_NT_LAUNCH1(BM, BN, ST, EPI_NONE, CONV, BKX);                                          \
+    if (epi == EPI_STATS) MPIT_NT_LAUNCH1(BM, BN, ST, EPI_STATS, CONV);                        \
+    else if (epi == EPI_BNRED) MPIT_NT_LAUNCH1(BM, BN, ST, EPI_BNRED, CONV);                   \
+    else if (epi == EPI_BNRED2 && !CONV) MPIT_NT_LAUNCH1(BM, BN, ST, EPI_BNRED2, false);       \
+    else MPIT_NT_LAUNCH1(BM, BN, ST, EPI_NONE, CONV);                                          \
   } while (0)
-#define MPIT_NT_LAUNCHB(BM, BN, ST, BKX)                                                                       \
+#define MPIT_NT_LAUNCH(BM, BN, ST)                                                                             \
   do {                                                                                                         \
     const int64_t mtn = (M + BM - 1) / BM;                                                                     \
     const int ntn = N / BN;                                                                                    \
     const int64_t nb = mtn * ntn;                                                                              \
     if (nb > INT32_MAX) throw std::invalid_argument("gemm_nt: too many tiles");                               \
     /* LDS: the k-tile ring, reused by the epilogue's bf16 tile and reduction table */                        \
-    const size_t shm = std::max({size_t(ST) * (BM + BN) * size_t(BKX ? BKX : nt_bk(BM, BN)) * 2,               \
+    const size_t shm = std::max({size_t(ST) * (BM + BN) * size_t(nt_bk(BM, BN)) * 2,               \
                                  size_t(BM) * BN * 2, size_t(256) * 8 * 3 * sizeof(float)});                  \
-    if (geo) MPIT_NT_LAUNCH2(BM, BN, ST, true, BKX);                                                           \
-    else MPIT_NT_LAUNCH2(BM, BN, ST, false, BKX);                                                              \
+    if (geo) MPIT_NT_LAUNCH2(BM, BN, ST, true);                                                           \
+    else MPIT_NT_LAUNCH2(BM, BN, ST, false);                                                              \
   } while (0)
-#define MPIT_NT_LAUNCH(BM, BN, ST) MPIT_NT_LAUNCHB(BM, BN, ST, 0)
   const int tcfg = nt_tile_config(N, K, geo != nullptr, geo ? geo->C : 0);
   if (tcfg == 2) MPIT_NT_LAUNCH(256, 256, 2);  // 2 x 64-deep stages = the 128 KB epilogue tile
   else if (tcfg == 1) MPIT_NT_LAUNCH(256, 128, 3);
@@ -975,7 +974,6 @@ static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t
     else if (stages == 3) MPIT_NT_LAUNCH(128, 64, 3);
     else MPIT_NT_LAUNCH(128, 64, 2);
   }
-#undef MPIT_NT_LAUNCHB
 #undef MPIT_NT_LAUNCH
 #undef MPIT_NT_LAUNCH2
 #undef MPIT_NT_LAUNCH1

@@ -93,14 +93,21 @@ PYBIND11_MODULE(_mpit, m) {
       py::arg("dev"), py::arg("stream"), py::arg("bf16"), py::arg("dy"), py::arg("mask"), py::arg("x"), py::arg("dx"),
       py::arg("dres"), py::arg("M"), py::arg("C"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
       py::arg("dgamma"), py::arg("dbeta"), py::arg("ws"), py::arg("relu"), py::arg("part") = 0, py::arg("npart") = 0);
-  m.def("bn_pair_apply", [](int dev, uintptr_t s, uintptr_t x1, uintptr_t coef1, uintptr_t x2, uintptr_t coef2,
-                            uintptr_t y, int64_t M, int C,
-                            uintptr_t mask) { bn_pair_apply(dev, S(s), x1, coef1, x2, coef2, y, M, C, mask); });
-  m.def("bn_pair_bwd_apply", [](int dev, uintptr_t s, uintptr_t dy, uintptr_t mask, uintptr_t x1, uintptr_t coef1,
-                                uintptr_t dx1, uintptr_t x2, uintptr_t coef2, uintptr_t dx2, int64_t M, int C) {
-    bn_pair_bwd_apply(dev, S(s), dy, mask, x1, coef1, dx1, x2, coef2, dx2, M, C);
-  });
-  m.def("gemm_nt_supported", &gemm_nt_supported);
+  m.def(
+      "bn_pair_apply",
+      [](int dev, uintptr_t s, uintptr_t x1, uintptr_t coef1, uintptr_t x2, uintptr_t coef2, uintptr_t y, int64_t M,
+         int C, uintptr_t mask, bool f32) { bn_pair_apply(dev, S(s), x1, coef1, x2, coef2, y, M, C, mask, f32); },
+      py::arg("dev"), py::arg("stream"), py::arg("x1"), py::arg("coef1"), py::arg("x2"), py::arg("coef2"), py::arg("y"),
+      py::arg("M"), py::arg("C"), py::arg("mask"), py::arg("f32") = false);
+  m.def(
+      "bn_pair_bwd_apply",
+      [](int dev, uintptr_t s, uintptr_t dy, uintptr_t mask, uintptr_t x1, uintptr_t coef1, uintptr_t dx1, uintptr_t x2,
+         uintptr_t coef2, uintptr_t dx2, int64_t M, int C,
+         bool f32) { bn_pair_bwd_apply(dev, S(s), dy, mask, x1, coef1, dx1, x2, coef2, dx2, M, C, f32); },
+      py::arg("dev"), py::arg("stream"), py::arg("dy"), py::arg("mask"), py::arg("x1"), py::arg("coef1"),
+      py::arg("dx1"), py::arg("x2"), py::arg("coef2"), py::arg("dx2"), py::arg("M"), py::arg("C"),
+      py::arg("f32") = false);
+  m.def("gemm_nt_supported", &gemm_nt_supported, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("f32") = false);
   m.def("gemm_nt_stats_floats", &gemm_nt_stats_floats);
   m.def("gemm_nt_tiles", &gemm_nt_tiles);
   m.def(
@@ -108,26 +115,30 @@ PYBIND11_MODULE(_mpit, m) {
       [](int dev, uintptr_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B, int64_t ldb, uintptr_t C,
          int64_t ldc, uintptr_t stats, uintptr_t cin, uintptr_t cmask, uintptr_t red_part, uintptr_t red_x,
          uintptr_t red_mask, uintptr_t red_mean, int64_t red_row0, uintptr_t red_part2, uintptr_t red_x2,
-         uintptr_t red_mean2) {
+         uintptr_t red_mean2, bool f32) {
         const BnRed r{red_part, red_x, red_mask, red_mean, red_row0, red_part2, red_x2, red_mean2};
-        gemm_nt(dev, S(s), M, N, K, A, lda, B, ldb, C, ldc, stats, cin, cmask, &r);
+        gemm_nt(dev, S(s), M, N, K, A, lda, B, ldb, C, ldc, stats, cin, cmask, &r, f32);
       },
       py::arg("dev"), py::arg("stream"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("A"), py::arg("lda"),
       py::arg("B"), py::arg("ldb"), py::arg("C"), py::arg("ldc"), py::arg("stats") = 0, py::arg("cin") = 0,
       py::arg("cmask") = 0, py::arg("red_part") = 0, py::arg("red_x") = 0, py::arg("red_mask") = 0,
       py::arg("red_mean") = 0, py::arg("red_row0") = 0, py::arg("red_part2") = 0, py::arg("red_x2") = 0,
-      py::arg("red_mean2") = 0);
+      py::arg("red_mean2") = 0, py::arg("f32") = false);
   m.def("gemm_tn_supported", &gemm_tn_supported);
   m.def("gemm_tn_ws_floats", &gemm_tn_ws_floats);
-  m.def("gemm_tn", [](int dev, uintptr_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X, int64_t ldx,
-                      uintptr_t out, uintptr_t ws, float beta) { gemm_tn(dev, S(s), M, N, K, Y, ldy, X, ldx, out, ws, beta); });
+  m.def(
+      "gemm_tn",
+      [](int dev, uintptr_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X, int64_t ldx,
+         uintptr_t out, uintptr_t ws, float beta, bool f32) { gemm_tn(dev, S(s), M, N, K, Y, ldy, X, ldx, out, ws, beta, f32); },
+      py::arg("dev"), py::arg("stream"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("Y"), py::arg("ldy"),
+      py::arg("X"), py::arg("ldx"), py::arg("out"), py::arg("ws"), py::arg("beta"), py::arg("f32") = false);
   m.def(
       "cast_transpose",
-      [](int dev, uintptr_t s, uintptr_t w, int R, int Cc, uintptr_t wb, uintptr_t wt, int taps) {
-        cast_transpose(dev, S(s), w, R, Cc, wb, wt, taps);
+      [](int dev, uintptr_t s, uintptr_t w, int R, int Cc, uintptr_t wb, uintptr_t wt, int taps, bool f32) {
+        cast_transpose(dev, S(s), w, R, Cc, wb, wt, taps, f32);
       },
       py::arg("dev"), py::arg("stream"), py::arg("w"), py::arg("R"), py::arg("Cc"), py::arg("wb"), py::arg("wt"),
-      py::arg("taps") = 1);
+      py::arg("taps") = 1, py::arg("f32") = false);
   m.def("cast_job_bytes", &cast_job_bytes);
   m.def("cast_jobs_build", [](uintptr_t table, std::vector<std::array<int64_t, 10>> specs) {
     return cast_jobs_build(table, specs);
@@ -135,60 +146,85 @@ PYBIND11_MODULE(_mpit, m) {
   m.def("cast_jobs_run", [](int dev, uintptr_t s, uintptr_t table, int njobs, int64_t nblocks) {
     cast_jobs_run(dev, S(s), table, njobs, nblocks);
   });
-  m.def("maxpool_fwd", [](int dev, uintptr_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t x,
-                          uintptr_t y, uintptr_t idx) { maxpool_fwd(dev, S(s), N, H, W, C, K, stride, pad, x, y, idx); });
-  m.def("maxpool_bwd", [](int dev, uintptr_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t dy,
-                          uintptr_t idx, uintptr_t dx) { maxpool_bwd(dev, S(s), N, H, W, C, K, stride, pad, dy, idx, dx); });
+  m.def(
+      "maxpool_fwd",
+      [](int dev, uintptr_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t x, uintptr_t y,
+         uintptr_t idx, bool f32) { maxpool_fwd(dev, S(s), N, H, W, C, K, stride, pad, x, y, idx, f32); },
+      py::arg("dev"), py::arg("stream"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("K"),
+      py::arg("stride"), py::arg("pad"), py::arg("x"), py::arg("y"), py::arg("idx"), py::arg("f32") = false);
+  m.def(
+      "maxpool_bwd",
+      [](int dev, uintptr_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t dy, uintptr_t idx,
+         uintptr_t dx, bool f32) { maxpool_bwd(dev, S(s), N, H, W, C, K, stride, pad, dy, idx, dx, f32); },
+      py::arg("dev"), py::arg("stream"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("K"),
+      py::arg("stride"), py::arg("pad"), py::arg("dy"), py::arg("idx"), py::arg("dx"), py::arg("f32") = false);
   m.def("conv_supported", &conv_supported);
   m.def(
       "conv_fwd",
       [](int dev, uintptr_t s, int Nb, int H, int W, int C, int Co, int R, int S_, int stride, int pad, uintptr_t x,
          uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t cin, uintptr_t bias, bool relu, uintptr_t red_part,
          uintptr_t red_x, uintptr_t red_mask, uintptr_t red_mean, int64_t red_row0, uintptr_t red_part2,
-         uintptr_t red_x2, uintptr_t red_mean2) {
+         uintptr_t red_x2, uintptr_t red_mean2, bool f32) {
         const BnRed r{red_part, red_x, red_mask, red_mean, red_row0, red_part2, red_x2, red_mean2};
-        conv_fwd(dev, S(s), Nb, H, W, C, Co, R, S_, stride, pad, x, w, y, stats, cin, bias, relu, &r);
+        conv_fwd(dev, S(s), Nb, H, W, C, Co, R, S_, stride, pad, x, w, y, stats, cin, bias, relu, &r, f32);
       },
       py::arg("dev"), py::arg("stream"), py::arg("Nb"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("Co"),
       py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("x"), py::arg("w"), py::arg("y"),
       py::arg("stats") = 0, py::arg("cin") = 0, py::arg("bias") = 0, py::arg("relu") = false, py::arg("red_part") = 0,
       py::arg("red_x") = 0, py::arg("red_mask") = 0, py::arg("red_mean") = 0, py::arg("red_row0") = 0,
-      py::arg("red_part2") = 0, py::arg("red_x2") = 0, py::arg("red_mean2") = 0);
+      py::arg("red_part2") = 0, py::arg("red_x2") = 0, py::arg("red_mean2") = 0, py::arg("f32") = false);
   m.def("conv_dgrad_strided_wfloats", &conv_dgrad_strided_wfloats);
-  m.def("conv_dgrad_strided_weights", [](int dev, uintptr_t s, uintptr_t w, int Co, int C, int R, int S_, int stride,
-                                         int pad, uintptr_t wb, uintptr_t wcls) {
-    conv_dgrad_strided_weights(dev, S(s), w, Co, C, R, S_, stride, pad, wb, wcls);
-  });
+  m.def(
+      "conv_dgrad_strided_weights",
+      [](int dev, uintptr_t s, uintptr_t w, int Co, int C, int R, int S_, int stride, int pad, uintptr_t wb,
+         uintptr_t wcls, bool f32) { conv_dgrad_strided_weights(dev, S(s), w, Co, C, R, S_, stride, pad, wb, wcls, f32); },
+      py::arg("dev"), py::arg("stream"), py::arg("w"), py::arg("Co"), py::arg("C"), py::arg("R"), py::arg("S"),
+      py::arg("stride"), py::arg("pad"), py::arg("wb"), py::arg("wcls"), py::arg("f32") = false);
   m.def("conv_dgrad_strided_tiles", &conv_dgrad_strided_tiles);
   m.def(
       "conv_dgrad_strided",
       [](int dev, uintptr_t s, int Nb, int H, int W, int C, int Co, int R, int S_, int stride, int pad, uintptr_t dy,
          uintptr_t wcls, uintptr_t dx, uintptr_t red_part, uintptr_t red_x, uintptr_t red_mask, uintptr_t red_mean,
-         uintptr_t red_part2, uintptr_t red_x2, uintptr_t red_mean2) {
+         uintptr_t red_part2, uintptr_t red_x2, uintptr_t red_mean2, bool f32) {
         const BnRed r{red_part, red_x, red_mask, red_mean, 0, red_part2, red_x2, red_mean2};
-        conv_dgrad_strided(dev, S(s), Nb, H, W, C, Co, R, S_, stride, pad, dy, wcls, dx, &r);
+        conv_dgrad_strided(dev, S(s), Nb, H, W, C, Co, R, S_, stride, pad, dy, wcls, dx, &r, f32);
       },
       py::arg("dev"), py::arg("stream"), py::arg("Nb"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("Co"),
       py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("dy"), py::arg("wcls"), py::arg("dx"),
       py::arg("red_part") = 0, py::arg("red_x") = 0, py::arg("red_mask") = 0, py::arg("red_mean") = 0,
-      py::arg("red_part2") = 0, py::arg("red_x2") = 0, py::arg("red_mean2") = 0);
+      py::arg("red_part2") = 0, py::arg("red_x2") = 0, py::arg("red_mean2") = 0, py::arg("f32") = false);
   m.def("relu_bias_bwd_ws_floats", &relu_bias_bwd_ws_floats);
-  m.def("relu_bias_bwd", [](int dev, uintptr_t s, int64_t M, int C, uintptr_t dy, uintptr_t y, uintptr_t dz, uintptr_t db,
-                            uintptr_t ws) { relu_bias_bwd(dev, S(s), M, C, dy, y, dz, db, ws); });
-  m.def("conv_stem_fwd", [](int dev, uintptr_t s, int Nb, int Hp, int Wp, int Co, int Ho, int Wo, int stride,
-                            uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats) {
-    conv_stem_fwd(dev, S(s), Nb, Hp, Wp, Co, Ho, Wo, stride, x, w, y, stats);
-  });
+  m.def(
+      "relu_bias_bwd",
+      [](int dev, uintptr_t s, int64_t M, int C, uintptr_t dy, uintptr_t y, uintptr_t dz, uintptr_t db, uintptr_t ws,
+         bool f32) { relu_bias_bwd(dev, S(s), M, C, dy, y, dz, db, ws, f32); },
+      py::arg("dev"), py::arg("stream"), py::arg("M"), py::arg("C"), py::arg("dy"), py::arg("y"), py::arg("dz"),
+      py::arg("db"), py::arg("ws"), py::arg("f32") = false);
+  m.def(
+      "conv_stem_fwd",
+      [](int dev, uintptr_t s, int Nb, int Hp, int Wp, int Co, int Ho, int Wo, int stride, uintptr_t x, uintptr_t w,
+         uintptr_t y, uintptr_t stats, bool f32) { conv_stem_fwd(dev, S(s), Nb, Hp, Wp, Co, Ho, Wo, stride, x, w, y, stats, f32); },
+      py::arg("dev"), py::arg("stream"), py::arg("Nb"), py::arg("Hp"), py::arg("Wp"), py::arg("Co"), py::arg("Ho"),
+      py::arg("Wo"), py::arg("stride"), py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stats"),
+      py::arg("f32") = false);
   m.def("conv_stem_wgrad_ws_floats", &conv_stem_wgrad_ws_floats);
-  m.def("conv_stem_wgrad", [](int dev, uintptr_t s, int Nb, int Hp, int Wp, int Co, int Ho, int Wo, int stride,
-                              uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws) {
-    conv_stem_wgrad(dev, S(s), Nb, Hp, Wp, Co, Ho, Wo, stride, dy, x, dw, ws);
-  });
+  m.def(
+      "conv_stem_wgrad",
+      [](int dev, uintptr_t s, int Nb, int Hp, int Wp, int Co, int Ho, int Wo, int stride, uintptr_t dy, uintptr_t x,
+         uintptr_t dw, uintptr_t ws, bool f32) { conv_stem_wgrad(dev, S(s), Nb, Hp, Wp, Co, Ho, Wo, stride, dy, x, dw, ws, f32); },
+      py::arg("dev"), py::arg("stream"), py::arg("Nb"), py::arg("Hp"), py::arg("Wp"), py::arg("Co"), py::arg("Ho"),
+      py::arg("Wo"), py::arg("stride"), py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("ws"),
+      py::arg("f32") = false);
   m.def("conv_wgrad_ws_floats", &conv_wgrad_ws_floats);
-  m.def("conv_wgrad", [](int dev, uintptr_t s, int Nb, int H, int W, int C, int Co, int R, int S_, int stride, int pad,
-                         uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, float beta) {
-    conv_wgrad(dev, S(s), Nb, H, W, C, Co, R, S_, stride, pad, dy, x, dw, ws, beta);
-  });
+  m.def(
+      "conv_wgrad",
+      [](int dev, uintptr_t s, int Nb, int H, int W, int C, int Co, int R, int S_, int stride, int pad, uintptr_t dy,
+         uintptr_t x, uintptr_t dw, uintptr_t ws, float beta, bool f32) {
+        conv_wgrad(dev, S(s), Nb, H, W, C, Co, R, S_, stride, pad, dy, x, dw, ws, beta, f32);
+      },
+      py::arg("dev"), py::arg("stream"), py::arg("Nb"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("Co"),
+      py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("dy"), py::arg("x"), py::arg("dw"),
+      py::arg("ws"), py::arg("beta"), py::arg("f32") = false);
 
   py::class_<Engine>(m, "Engine")
       .def(py::init<const std::string&, int, int, bool, int, int64_t>(), py::arg("name"), py::arg("world"),

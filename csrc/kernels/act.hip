@@ -1,6 +1,6 @@
 // ReLU + bias backward for the conv(+bias)(+ReLU) layers whose forward runs the bias and
 // the ReLU in the GEMM epilogue (VGG / AlexNet on the MFMA implicit-GEMM path):
-//   dz = dy * (y > 0)            (bf16 [M, C], y = the layer's saved output)
+//   dz = dy * (y > 0)            (bf16 or fp32 [M, C], y = the layer's saved output)
 //   db[c] = sum over rows of dz  (fp32, optional)
 // One pass over dy and y (the masked gradient is what the dgrad / wgrad GEMMs consume, so
 // it has to be written once anyway); the bias gradient rides along as a per-thread
@@ -19,9 +19,10 @@ namespace {
 
 constexpr int kMaxBlocks = 1024;
 
-__global__ __launch_bounds__(1024) void relu_bias_bwd_kernel(const uint16_t* __restrict__ dy,
-                                                             const uint16_t* __restrict__ y,
-                                                             uint16_t* __restrict__ dz, int64_t M, int C,
+template <typename T>
+__global__ __launch_bounds__(1024) void relu_bias_bwd_kernel(const T* __restrict__ dy,
+                                                             const T* __restrict__ y,
+                                                             T* __restrict__ dz, int64_t M, int C,
                                                              int64_t rows_per_block, float* __restrict__ part) {
   extern __shared__ float lds[];  // [R][C]
   const int G = C / 8;
@@ -31,6 +32,26 @@ __global__ __launch_bounds__(1024) void relu_bias_bwd_kernel(const uint16_t* __r
   const int64_t r1 = min(M, r0 + rows_per_block);
   for (int64_t r = r0 + rs; r < r1; r += R) {
     const int64_t o = r * C + g * 8;
+    if constexpr (sizeof(T) == 4) {
+      float4 a[2], b[2];
+      a[0] = reinterpret_cast<const float4*>(dy + o)[0];
+      a[1] = reinterpret_cast<const float4*>(dy + o)[1];
+      b[0] = reinterpret_cast<const float4*>(y + o)[0];
+      b[1] = reinterpret_cast<const float4*>(y + o)[1];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        a[k].x = b[k].x > 0.f ? a[k].x : 0.f;
+        a[k].y = b[k].y > 0.f ? a[k].y : 0.f;
+        a[k].z = b[k].z > 0.f ? a[k].z : 0.f;
+        a[k].w = b[k].w > 0.f ? a[k].w : 0.f;
+        acc[4 * k] += a[k].x;
+        acc[4 * k + 1] += a[k].y;
+        acc[4 * k + 2] += a[k].z;
+        acc[4 * k + 3] += a[k].w;
+        reinterpret_cast<float4*>(dz + o)[k] = a[k];
+      }
+      continue;
+    } else {
     const uint4 a = *reinterpret_cast<const uint4*>(dy + o);
     const uint4 b = *reinterpret_cast<const uint4*>(y + o);
     const uint32_t av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
@@ -50,6 +71,7 @@ __global__ __launch_bounds__(1024) void relu_bias_bwd_kernel(const uint16_t* __r
       ov[k] = w;
     }
     *reinterpret_cast<uint4*>(dz + o) = make_uint4(ov[0], ov[1], ov[2], ov[3]);
+    }
   }
   if (!part) return;
 #pragma unroll
@@ -91,7 +113,7 @@ __global__ __launch_bounds__(kSumCh * kSumLanes) void sum_parts_kernel(const flo
 int64_t relu_bias_bwd_ws_floats(int C) { return int64_t(kMaxBlocks + kSumGroups) * C; }
 
 void relu_bias_bwd(int dev, hipStream_t s, int64_t M, int C, uintptr_t dy, uintptr_t y, uintptr_t dz, uintptr_t db,
-                   uintptr_t ws) {
+                   uintptr_t ws, bool f32) {
   if (M <= 0 || C <= 0 || C % 8 || C / 8 > 1024) throw std::invalid_argument("relu_bias_bwd: need C % 8 == 0, C <= 8192");
   if ((dy | y | dz) % 16) throw std::invalid_argument("relu_bias_bwd: buffers must be 16-byte aligned");
   if (db && !ws) throw std::invalid_argument("relu_bias_bwd: bias gradient needs the workspace");
@@ -104,8 +126,14 @@ void relu_bias_bwd(int dev, hipStream_t s, int64_t M, int C, uintptr_t dy, uintp
   nb = (M + rpb - 1) / rpb;
   float* part = db ? reinterpret_cast<float*>(ws) : nullptr;
   const size_t shm = db ? size_t(R) * C * sizeof(float) : 0;
-  hipLaunchKernelGGL(relu_bias_bwd_kernel, dim3(unsigned(nb)), dim3(blk), shm, s, reinterpret_cast<const uint16_t*>(dy),
-                     reinterpret_cast<const uint16_t*>(y), reinterpret_cast<uint16_t*>(dz), M, C, rpb, part);
+  if (f32)
+    hipLaunchKernelGGL(relu_bias_bwd_kernel<float>, dim3(unsigned(nb)), dim3(blk), shm, s,
+                       reinterpret_cast<const float*>(dy), reinterpret_cast<const float*>(y),
+                       reinterpret_cast<float*>(dz), M, C, rpb, part);
+  else
+    hipLaunchKernelGGL(relu_bias_bwd_kernel<uint16_t>, dim3(unsigned(nb)), dim3(blk), shm, s,
+                       reinterpret_cast<const uint16_t*>(dy), reinterpret_cast<const uint16_t*>(y),
+                       reinterpret_cast<uint16_t*>(dz), M, C, rpb, part);
   hip_check(hipGetLastError(), "relu_bias_bwd launch");
   if (db) {
     const dim3 cb((C + kSumCh - 1) / kSumCh);

@@ -9,8 +9,9 @@
 //   backward: reduce pass (read dy, mask, x) + apply pass (read dy, mask, x, write dx [, dres])
 // The ReLU mask is one bit per element (1/16 of a bf16 tensor), so the backward never
 // re-reads the forward output y.
-// Layout: the activation is a row-major [M = N*H*W, C] matrix. A thread owns VEC
-// consecutive channels (16 B: 8 bf16 or 4 fp32) and walks rows; since every block size
+// Layout: the activation is a row-major [M = N*H*W, C] matrix. A thread owns VEC = 8
+// consecutive channels (16 B bf16, 32 B fp32; the ReLU mask is one byte per 8 channels in
+// both, the layout the GEMM epilogues read) and walks rows; since every block size
 // and grid stride is a multiple of G = C/VEC, a thread keeps the same channel group for
 // its whole life, so per-channel coefficients stay in registers.
 // Statistics use shifted sums (shift = row 0 of each channel) accumulated in fp32 per
@@ -59,13 +60,15 @@ struct Vec<uint16_t> {  // bf16
 };
 template <>
 struct Vec<float> {
-  static constexpr int N = 4;
-  static __device__ __forceinline__ void load(const float* p, float (&v)[4]) {
-    const float4 r = *reinterpret_cast<const float4*>(p);
+  static constexpr int N = 8;
+  static __device__ __forceinline__ void load(const float* p, float (&v)[8]) {
+    const float4 r = reinterpret_cast<const float4*>(p)[0], q = reinterpret_cast<const float4*>(p)[1];
     v[0] = r.x; v[1] = r.y; v[2] = r.z; v[3] = r.w;
+    v[4] = q.x; v[5] = q.y; v[6] = q.z; v[7] = q.w;
   }
-  static __device__ __forceinline__ void store(float* p, const float (&v)[4]) {
-    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  static __device__ __forceinline__ void store(float* p, const float (&v)[8]) {
+    reinterpret_cast<float4*>(p)[0] = make_float4(v[0], v[1], v[2], v[3]);
+    reinterpret_cast<float4*>(p)[1] = make_float4(v[4], v[5], v[6], v[7]);
   }
 };
 
@@ -355,7 +358,7 @@ void launch_tiles_finalize(hipStream_t s, const float* part, int64_t nt, int C, 
 
 // ---------------------------------------------------------------- forward: apply
 // MASK: also store the ReLU mask, one byte per vector (bit v = element v of the vector is
-// positive), so the backward never re-reads y (1/16 of its bytes for bf16).
+// positive), so the backward never re-reads y (1/16 of its bytes for bf16, 1/32 for fp32).
 template <typename T, bool RES, bool RELU, bool MASK>
 __global__ __launch_bounds__(1024) void bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res,
                                                         T* __restrict__ y, const float* __restrict__ coef, int64_t nvec,
@@ -527,9 +530,10 @@ __global__ __launch_bounds__(1024) void bn_bwd_apply_kernel(const T* __restrict_
 // ---------------------------------------------------------------- BN pair (ResNet downsample)
 // y = relu(x1*sc1 + sh1 + x2*sc2 + sh2): a block's last BN plus its downsample shortcut's BN
 // (no ReLU on the shortcut), one pass over (x1, x2) instead of materialising bn2(x2).
-__global__ __launch_bounds__(1024) void bn_pair_apply_kernel(const uint16_t* __restrict__ x1,
-                                                             const uint16_t* __restrict__ x2,
-                                                             uint16_t* __restrict__ y, const float* __restrict__ coef1,
+template <typename T>
+__global__ __launch_bounds__(1024) void bn_pair_apply_kernel(const T* __restrict__ x1,
+                                                             const T* __restrict__ x2,
+                                                             T* __restrict__ y, const float* __restrict__ coef1,
                                                              const float* __restrict__ coef2, int64_t nvec, int C,
                                                              uint8_t* __restrict__ mask) {
   constexpr int V = 8;
@@ -547,8 +551,8 @@ __global__ __launch_bounds__(1024) void bn_pair_apply_kernel(const uint16_t* __r
   }
   for (; i < nvec; i += stride) {
     float p[V], q[V];
-    Vec<uint16_t>::load(x1 + i * V, p);
-    Vec<uint16_t>::load(x2 + i * V, q);
+    Vec<T>::load(x1 + i * V, p);
+    Vec<T>::load(x2 + i * V, q);
     uint32_t bits = 0;
 #pragma unroll
     for (int v = 0; v < V; ++v) {
@@ -556,16 +560,17 @@ __global__ __launch_bounds__(1024) void bn_pair_apply_kernel(const uint16_t* __r
       p[v] = t;
       bits |= uint32_t(t > 0.f) << v;
     }
-    Vec<uint16_t>::store(y + i * V, p);
+    Vec<T>::store(y + i * V, p);
     mask[i] = uint8_t(bits);
   }
 }
 
 // dz = dy * mask; dx1 = A1 dz + C1 x1 + B1, dx2 = A2 dz + C2 x2 + B2 (coef [3][C] each)
+template <typename T>
 __global__ __launch_bounds__(1024) void bn_pair_bwd_apply_kernel(
-    const uint16_t* __restrict__ dy, const uint8_t* __restrict__ mask, const uint16_t* __restrict__ x1,
-    const float* __restrict__ coef1, uint16_t* __restrict__ dx1, const uint16_t* __restrict__ x2,
-    const float* __restrict__ coef2, uint16_t* __restrict__ dx2, int64_t nvec, int C) {
+    const T* __restrict__ dy, const uint8_t* __restrict__ mask, const T* __restrict__ x1,
+    const float* __restrict__ coef1, T* __restrict__ dx1, const T* __restrict__ x2,
+    const float* __restrict__ coef2, T* __restrict__ dx2, int64_t nvec, int C) {
   constexpr int V = 8;
   const int G = C / V;
   int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -583,9 +588,9 @@ __global__ __launch_bounds__(1024) void bn_pair_bwd_apply_kernel(
   }
   for (; i < nvec; i += stride) {
     float d[V], p[V], q[V];
-    Vec<uint16_t>::load(dy + i * V, d);
-    Vec<uint16_t>::load(x1 + i * V, p);
-    Vec<uint16_t>::load(x2 + i * V, q);
+    Vec<T>::load(dy + i * V, d);
+    Vec<T>::load(x1 + i * V, p);
+    Vec<T>::load(x2 + i * V, q);
     const uint32_t mb = mask[i];
 #pragma unroll
     for (int v = 0; v < V; ++v) {
@@ -593,8 +598,8 @@ __global__ __launch_bounds__(1024) void bn_pair_bwd_apply_kernel(
       p[v] = fmaf(A1[v], dz, fmaf(C1[v], p[v], B1[v]));
       q[v] = fmaf(A2[v], dz, fmaf(C2[v], q[v], B2[v]));
     }
-    Vec<uint16_t>::store(dx1 + i * V, p);
-    Vec<uint16_t>::store(dx2 + i * V, q);
+    Vec<T>::store(dx1 + i * V, p);
+    Vec<T>::store(dx2 + i * V, q);
   }
 }
 
@@ -731,7 +736,7 @@ void bwd_impl(hipStream_t s, const T* dy, const uint8_t* mask, const T* x, T* dx
 
 int64_t bn_workspace_floats(int C) { return int64_t(3) * C + int64_t(2) * kMaxStatBlocks * C; }
 
-int64_t bn_mask_bytes(bool bf16, int64_t M, int C) { return M * (C / (bf16 ? 8 : 4)); }
+int64_t bn_mask_bytes(bool bf16, int64_t M, int C) { (void)bf16; return M * (C / 8); }
 
 void bn_act_fwd(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C,
                 uintptr_t gamma, uintptr_t beta, uintptr_t rmean, uintptr_t rvar, uintptr_t save_mean,
@@ -758,7 +763,7 @@ void bn_act_apply(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res,
     launch_apply<uint16_t>(s, reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(res),
                            reinterpret_cast<uint16_t*>(y), M, C, reinterpret_cast<const float*>(coef), relu, nullptr);
   } else {
-    check_shape(M, C, 4, x);
+    check_shape(M, C, 8, x);
     launch_apply<float>(s, reinterpret_cast<const float*>(x), reinterpret_cast<const float*>(res),
                         reinterpret_cast<float*>(y), M, C, reinterpret_cast<const float*>(coef), relu, nullptr);
   }
@@ -781,33 +786,47 @@ void bn_act_bwd(int dev, hipStream_t s, bool bf16, uintptr_t dy, uintptr_t mask,
                     F(dgamma), F(dbeta), F(ws), relu, F(part), npart);
 }
 
+template <typename T>
+static void pair_apply_t(hipStream_t s, uintptr_t x1, uintptr_t coef1, uintptr_t x2, uintptr_t coef2, uintptr_t y,
+                         int64_t M, int C, uintptr_t mask) {
+  const int G = C / 8, blk = block_for(G);
+  const int64_t nvec = M * G;
+  hipLaunchKernelGGL(bn_pair_apply_kernel<T>, dim3(apply_grid(nvec, blk)), dim3(blk), 0, s,
+                     reinterpret_cast<const T*>(x1), reinterpret_cast<const T*>(x2), reinterpret_cast<T*>(y),
+                     reinterpret_cast<const float*>(coef1), reinterpret_cast<const float*>(coef2), nvec, C,
+                     reinterpret_cast<uint8_t*>(mask));
+}
+
+template <typename T>
+static void pair_bwd_t(hipStream_t s, uintptr_t dy, uintptr_t mask, uintptr_t x1, uintptr_t coef1, uintptr_t dx1,
+                       uintptr_t x2, uintptr_t coef2, uintptr_t dx2, int64_t M, int C) {
+  const int G = C / 8, blk = block_for(G);
+  const int64_t nvec = M * G;
+  hipLaunchKernelGGL(bn_pair_bwd_apply_kernel<T>, dim3(apply_grid(nvec, blk)), dim3(blk), 0, s,
+                     reinterpret_cast<const T*>(dy), reinterpret_cast<const uint8_t*>(mask),
+                     reinterpret_cast<const T*>(x1), reinterpret_cast<const float*>(coef1), reinterpret_cast<T*>(dx1),
+                     reinterpret_cast<const T*>(x2), reinterpret_cast<const float*>(coef2), reinterpret_cast<T*>(dx2),
+                     nvec, C);
+}
+
 void bn_pair_apply(int dev, hipStream_t s, uintptr_t x1, uintptr_t coef1, uintptr_t x2, uintptr_t coef2, uintptr_t y,
-                   int64_t M, int C, uintptr_t mask) {
+                   int64_t M, int C, uintptr_t mask, bool f32) {
   hip_check(hipSetDevice(dev), "hipSetDevice");
   check_shape(M, C, 8, x1);
   check_shape(M, C, 8, x2);
   if (!mask) throw std::invalid_argument("bn_pair_apply: needs the ReLU mask buffer");
-  const int G = C / 8, blk = block_for(G);
-  const int64_t nvec = M * G;
-  hipLaunchKernelGGL(bn_pair_apply_kernel, dim3(apply_grid(nvec, blk)), dim3(blk), 0, s,
-                     reinterpret_cast<const uint16_t*>(x1), reinterpret_cast<const uint16_t*>(x2),
-                     reinterpret_cast<uint16_t*>(y), reinterpret_cast<const float*>(coef1),
-                     reinterpret_cast<const float*>(coef2), nvec, C, reinterpret_cast<uint8_t*>(mask));
+  if (f32) pair_apply_t<float>(s, x1, coef1, x2, coef2, y, M, C, mask);
+  else pair_apply_t<uint16_t>(s, x1, coef1, x2, coef2, y, M, C, mask);
   hip_check(hipGetLastError(), "bn_pair_apply launch");
 }
 
 void bn_pair_bwd_apply(int dev, hipStream_t s, uintptr_t dy, uintptr_t mask, uintptr_t x1, uintptr_t coef1,
-                       uintptr_t dx1, uintptr_t x2, uintptr_t coef2, uintptr_t dx2, int64_t M, int C) {
+                       uintptr_t dx1, uintptr_t x2, uintptr_t coef2, uintptr_t dx2, int64_t M, int C, bool f32) {
   hip_check(hipSetDevice(dev), "hipSetDevice");
   check_shape(M, C, 8, x1);
   check_shape(M, C, 8, x2);
-  const int G = C / 8, blk = block_for(G);
-  const int64_t nvec = M * G;
-  hipLaunchKernelGGL(bn_pair_bwd_apply_kernel, dim3(apply_grid(nvec, blk)), dim3(blk), 0, s,
-                     reinterpret_cast<const uint16_t*>(dy), reinterpret_cast<const uint8_t*>(mask),
-                     reinterpret_cast<const uint16_t*>(x1), reinterpret_cast<const float*>(coef1),
-                     reinterpret_cast<uint16_t*>(dx1), reinterpret_cast<const uint16_t*>(x2),
-                     reinterpret_cast<const float*>(coef2), reinterpret_cast<uint16_t*>(dx2), nvec, C);
+  if (f32) pair_bwd_t<float>(s, dy, mask, x1, coef1, dx1, x2, coef2, dx2, M, C);
+  else pair_bwd_t<uint16_t>(s, dy, mask, x1, coef1, dx1, x2, coef2, dx2, M, C);
   hip_check(hipGetLastError(), "bn_pair_bwd_apply launch");
 }
 

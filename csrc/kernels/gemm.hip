@@ -56,8 +56,63 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
-constexpr int kBK = 32;  // k-depth of one staged tile (gemm_nt): 64-B LDS rows
+constexpr int kBK = 32;  // k-depth of one staged bf16 tile (gemm_nt): 64-B LDS rows
 constexpr int kStemTap = 32, kStemK = 8 * kStemTap;  // row-tap stem: 8 pixels x 4 channels per row
+
+// Element types: uint16_t = bf16 operands on v_mfma_f32_32x32x16_bf16; float = fp32
+// operands on v_mfma_f32_32x32x2_f32 (exact fp32 products, fp32 accumulate: the
+// reference's fp32 training precision). Staging, LDS images and the epilogue are written
+// in bytes / 16-byte chunks, so both share them: a chunk is 8 bf16 or 4 fp32.
+template <typename T>
+__host__ __device__ constexpr int epc() { return 16 / int(sizeof(T)); }  // elements per 16-B chunk
+template <typename T>
+__host__ __device__ constexpr int nt_bk_of() { return 64 / int(sizeof(T)); }  // k of one 64-B LDS row
+
+// 8 consecutive elements of T held raw in registers (loads issued ahead of their use)
+template <typename T>
+struct V8;
+template <>
+struct V8<uint16_t> {
+  uint4 r;
+  __device__ __forceinline__ void load(const uint16_t* p) { r = *reinterpret_cast<const uint4*>(p); }
+  __device__ __forceinline__ void zero() { r = make_uint4(0, 0, 0, 0); }
+  __device__ __forceinline__ float get(int e) const {
+    const uint32_t w = e < 2 ? r.x : e < 4 ? r.y : e < 6 ? r.z : r.w;
+    return bf2f(uint16_t((e & 1) ? (w >> 16) : (w & 0xffff)));
+  }
+};
+template <>
+struct V8<float> {
+  float4 a, b;
+  __device__ __forceinline__ void load(const float* p) {
+    a = reinterpret_cast<const float4*>(p)[0];
+    b = reinterpret_cast<const float4*>(p)[1];
+  }
+  __device__ __forceinline__ void zero() { a = b = make_float4(0.f, 0.f, 0.f, 0.f); }
+  __device__ __forceinline__ float get(int e) const {
+    const float4& q = e < 4 ? a : b;
+    const int k = e & 3;
+    return k == 0 ? q.x : k == 1 ? q.y : k == 2 ? q.z : q.w;
+  }
+};
+__device__ __forceinline__ void store8(uint16_t* p, const float (&v)[8]) {
+  uint4 r;
+  r.x = uint32_t(f2bf(v[0])) | (uint32_t(f2bf(v[1])) << 16);
+  r.y = uint32_t(f2bf(v[2])) | (uint32_t(f2bf(v[3])) << 16);
+  r.z = uint32_t(f2bf(v[4])) | (uint32_t(f2bf(v[5])) << 16);
+  r.w = uint32_t(f2bf(v[6])) | (uint32_t(f2bf(v[7])) << 16);
+  *reinterpret_cast<uint4*>(p) = r;
+}
+__device__ __forceinline__ void store8(float* p, const float (&v)[8]) {
+  reinterpret_cast<float4*>(p)[0] = make_float4(v[0], v[1], v[2], v[3]);
+  reinterpret_cast<float4*>(p)[1] = make_float4(v[4], v[5], v[6], v[7]);
+}
+// value as stored in T (the epilogue's statistics see exactly what is written)
+template <typename T>
+__device__ __forceinline__ float rnd(float v) {
+  if constexpr (sizeof(T) == 2) return bf2f(f2bf(v));
+  else return v;
+}
 
 // NHWC convolution geometry for the implicit-GEMM (CONV) kernel variants
 struct ConvGeo {
@@ -80,32 +135,32 @@ enum { EPI_NONE = 0, EPI_STATS = 1, EPI_BNRED = 2, EPI_BNRED2 = 3 };
 // column-reduction epilogue operands (see gemm_nt_kernel)
 struct EpiArgs {
   float* part;                 // [row0 + tiles][2][N] fp32 partials
-  const uint16_t* x;           // EPI_BNRED: the BN's input, laid out like C (ldc == N)
+  const void* x;               // EPI_BNRED: the BN's input (element type of C), laid out like C (ldc == N)
   const uint8_t* mask;         // EPI_BNRED: the BN's ReLU bit mask (1 byte / 8 channels) or null
   const float* mean;           // EPI_BNRED: the BN's batch mean [N]
   int64_t row0;                // first partial row of this launch
   float* part2;                // EPI_BNRED2: the second BN of a bn_pair (same gradient and mask)
-  const uint16_t* x2;
+  const void* x2;
   const float* mean2;
 };
 
-// source line for padding taps: LDS DMA of zeros
-__device__ __attribute__((aligned(256))) uint16_t g_zero_line[128] = {};
+// source line for padding taps: LDS DMA of zeros (any chunk of a 256-B row, either type)
+__device__ __attribute__((aligned(256))) uint16_t g_zero_line[256] = {};
 
 // 16-B chunk swizzle of a 64-B LDS row: any 16 consecutive rows read at one logical chunk
 // hit 16 distinct (row%4, chunk) bank groups = all 64 banks.
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }
-// the same for 128-B rows (BK = 64, 8 chunks): 16 rows at one logical chunk hit 16 distinct
-// (row%2, chunk) bank groups
-template <int BK>
+// the same for 128-B rows (8 chunks): 16 rows at one logical chunk hit 16 distinct
+// (row%2, chunk) bank groups. BKB = bytes per LDS row.
+template <int BKB>
 __device__ __forceinline__ int swzk(int row, int chunk) {
-  if constexpr (BK == 32) return swz(row, chunk);
+  if constexpr (BKB == 64) return swz(row, chunk);
   else return chunk ^ ((row >> 1) & 7);
 }
 
-// k-depth of one staged tile of gemm_nt: the 256x256 tile (1 block/CU) stages 64-deep tiles
-// (16 MFMAs per wave between fragment refills, half the barriers per FLOP of BK = 32)
-__host__ __device__ constexpr int nt_bk(int BM, int BN) { return BM == 256 && BN == 256 ? 64 : kBK; }
+// bytes of one staged row of gemm_nt: the 256x256 tile (1 block/CU) stages 128-B rows
+// (64 bf16: 16 MFMAs per wave between fragment refills, half the barriers per FLOP)
+__host__ __device__ constexpr int nt_bkb(int BM, int BN) { return BM == 256 && BN == 256 ? 128 : 64; }
 
 typedef __attribute__((address_space(3))) void lds_void;
 
@@ -170,22 +225,28 @@ __device__ __forceinline__ int xcd_tile(int bid, int nb) {
 // the tile about to be used (a __syncthreads() would drain the whole ring). The LDS image
 // is lane-linear per wave instruction (16 rows x 64 B); the swizzle is applied on the
 // global source address.
-template <int BM, int BN, int STAGES, int EPI, bool CONV>
-__global__ __launch_bounds__(256, BM == 256 ? (BN == 256 ? 1 : 2) : (STAGES == 2 ? (CONV || EPI == 3 ? 4 : 5) : 2)) void gemm_nt_kernel(const uint16_t* __restrict__ A, int64_t lda,
-                                                         const uint16_t* __restrict__ B, int64_t ldb,
-                                                         uint16_t* C, int64_t ldc, int64_t M, int N, int K,
-                                                         int ntn, EpiArgs ep, const uint16_t* Cin,
+template <typename T, int BM, int BN, int STAGES, int EPI, bool CONV>
+__global__ __launch_bounds__(256, sizeof(T) == 4 ? 2 : (BM == 256 ? (BN == 256 ? 1 : 2) : (STAGES == 2 ? (CONV || EPI == 3 ? 4 : 5) : 2))) void gemm_nt_kernel(const T* __restrict__ A, int64_t lda,
+                                                         const T* __restrict__ B, int64_t ldb,
+                                                         T* C, int64_t ldc, int64_t M, int N, int K,
+                                                         int ntn, EpiArgs ep, const T* Cin,
                                                          const uint8_t* __restrict__ Cmask,
                                                          const float* __restrict__ bias, int relu, ConvGeo geo) {
   constexpr int NW = 4, NT = NW * 64;  // waves, threads
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 32, TN = WN / 32;
-  constexpr int BK = nt_bk(BM, BN), CPK = BK / 8, RPI = 64 / CPK;  // 16-B chunks per row, rows per glds
+  constexpr int EPC = epc<T>();                          // elements per 16-B chunk
+  constexpr int BKB = nt_bkb(BM, BN), BK = BKB / int(sizeof(T));
+  constexpr int CPK = BKB / 16, RPI = 64 / CPK;          // 16-B chunks per row, rows per glds
   constexpr int IA = BM / RPI / NW, IB = BN / RPI / NW;  // glds instructions per wave per tile
   constexpr int NI = IA + IB;
   constexpr int TILE = (BM + BN) * BK;  // elements per stage
+  constexpr bool F32 = sizeof(T) == 4;
   static_assert(IA >= 1 && IB >= 1, "tile too small");
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  static_assert(!F32 || BKB == 64, "fp32 tiles stage 64-B rows");
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem_raw[];
+  T* smem = reinterpret_cast<T*>(smem_raw);
+  const T* zline = reinterpret_cast<const T*>(g_zero_line);
 
   const int tile = xcd_tile(blockIdx.x, gridDim.x);
   const int mt = tile / ntn, nt = tile % ntn;
@@ -195,12 +256,12 @@ __global__ __launch_bounds__(256, BM == 256 ? (BN == 256 ? 1 : 2) : (STAGES == 2
 
   // source of this lane for each of the wave's glds instructions (k offset added per tile);
   // CONV: the output pixel of the row (first input pixel of its window) instead
-  const uint16_t* pa[IA];
-  const uint16_t* pb[IB];
+  const T* pa[IA];
+  const T* pb[IB];
   int hi0[IA], wi0[IA], ca[IA], img[IA];
 #pragma unroll
   for (int i = 0; i < IA; ++i) {
-    const int row = (w * IA + i) * RPI + lane / CPK, c = swzk<BK>(row, lane % CPK);
+    const int row = (w * IA + i) * RPI + lane / CPK, c = swzk<BKB>(row, lane % CPK);
     const int64_t gm = min(m0 + row, M - 1);  // clamp: tail rows compute garbage, never stored
     if constexpr (CONV) {
       const int hw = geo.Ho * geo.Wo;
@@ -209,27 +270,27 @@ __global__ __launch_bounds__(256, BM == 256 ? (BN == 256 ? 1 : 2) : (STAGES == 2
       hi0[i] = ho * geo.stride - geo.pad;
       wi0[i] = wo * geo.stride - geo.padw;
       img[i] = int(n) * geo.H;
-      ca[i] = c * 8;
+      ca[i] = c * EPC;
     } else {
-      pa[i] = A + gm * lda + c * 8;
+      pa[i] = A + gm * lda + c * EPC;
     }
   }
   int kc = 0, kr = 0, ks = 0;  // CONV: channel offset and tap of the next tile issued
   const int pitch = geo.pitch ? geo.pitch : geo.C;
 #pragma unroll
   for (int i = 0; i < IB; ++i) {
-    const int row = (w * IB + i) * RPI + lane / CPK, c = swzk<BK>(row, lane % CPK);
-    pb[i] = B + int64_t(n0 + row) * ldb + c * 8;
+    const int row = (w * IB + i) * RPI + lane / CPK, c = swzk<BKB>(row, lane % CPK);
+    pb[i] = B + int64_t(n0 + row) * ldb + c * EPC;
   }
   auto issue = [&](int kt, int buf) {
-    uint16_t* As = smem + buf * TILE;
-    uint16_t* Bs = As + BM * BK;
+    T* As = smem + buf * TILE;
+    T* Bs = As + BM * BK;
 #pragma unroll
     for (int i = 0; i < IA; ++i) {
       if constexpr (CONV) {
         const int hi = hi0[i] + kr, wi = wi0[i] + ks;
         const bool ok = unsigned(hi) < unsigned(geo.H) && unsigned(wi) < unsigned(geo.W);
-        const uint16_t* src = ok ? A + (((img[i] + hi) * geo.W + wi) * pitch + kc + ca[i]) : g_zero_line + ca[i];
+        const T* src = ok ? A + (((img[i] + hi) * geo.W + wi) * pitch + kc + ca[i]) : zline + ca[i];
         glds16(src, As + (w * IA + i) * RPI * BK);
       } else {
         glds16(pa[i] + kt * BK, As + (w * IA + i) * RPI * BK);
@@ -258,6 +319,15 @@ __global__ __launch_bounds__(256, BM == 256 ? (BN == 256 ? 1 : 2) : (STAGES == 2
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
 
+  // fp32: the running chain of the current block of tiles (see the MFMA loop)
+  f32x16 tacc[F32 ? TM : 1][F32 ? TN : 1];
+#pragma unroll
+  for (int i = 0; i < (F32 ? TM : 1); ++i)
+#pragma unroll
+    for (int j = 0; j < (F32 ? TN : 1); ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) tacc[i][j][v] = 0.f;
+
   const int fr = lane & 31, fh = lane >> 5;
   const int nk = K / BK;
 #pragma unroll
@@ -272,8 +342,53 @@ __global__ __launch_bounds__(256, BM == 256 ? (BN == 256 ? 1 : 2) : (STAGES == 2
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
-    const uint16_t* As = smem + (kt % STAGES) * TILE;
-    const uint16_t* Bs = As + BM * BK;
+    const T* As = smem + (kt % STAGES) * TILE;
+    const T* Bs = As + BM * BK;
+    if constexpr (F32) {
+      // v_mfma_f32_32x32x2_f32: lane (fr, fh) supplies A[row fr][k] and B[col fr][k] of one
+      // k per instruction. The 16-deep tile is split by lane half: half fh runs k = 8fh + s
+      // in step s (any bijection onto the tile's k works when A and B use the same one), so
+      // a lane's 8 values of a row are two contiguous chunks: 2 ds_read_b128 per fragment.
+      float4 af[TM][2], bfg[TN][2];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int r = wm * WM + i * 32 + fr;
+        af[i][0] = *reinterpret_cast<const float4*>(As + r * BK + swzk<BKB>(r, 2 * fh) * 4);
+        af[i][1] = *reinterpret_cast<const float4*>(As + r * BK + swzk<BKB>(r, 2 * fh + 1) * 4);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int r = wn * WN + j * 32 + fr;
+        bfg[j][0] = *reinterpret_cast<const float4*>(Bs + r * BK + swzk<BKB>(r, 2 * fh) * 4);
+        bfg[j][1] = *reinterpret_cast<const float4*>(Bs + r * BK + swzk<BKB>(r, 2 * fh + 1) * 4);
+      }
+      auto el = [](const float4 (&q)[2], int s) -> float {
+        const float4& h = q[s >> 2];
+        const int k = s & 3;
+        return k == 0 ? h.x : k == 1 ? h.y : k == 2 ? h.z : h.w;
+      };
+      // Blocked accumulation: the MFMA is a k-ordered fmaf chain, so a 4608-deep K summed
+      // in one chain loses ~sqrt(K) ulps; chains of 32 (two tiles) into tacc, folded into
+      // acc once per block, keep the error at the level of a blocked fp32 library GEMM.
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            tacc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(el(bfg[j], s), el(af[i], s), tacc[i][j], 0, 0, 0);
+      if ((kt & 1) || kt == nk - 1) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            acc[i][j] += tacc[i][j];
+#pragma unroll
+            for (int v = 0; v < 16; ++v) tacc[i][j][v] = 0.f;
+          }
+      }
+      continue;
+    } else {
     if constexpr (TM * TN >= 8) {
       // big wave tiles run one or two waves per SIMD, so nothing else hides a fragment read:
       // the fragments of k16 step kk+1 are read while step kk's MFMAs run (two register
@@ -285,12 +400,12 @@ __global__ __launch_bounds__(256, BM == 256 ? (BN == 256 ? 1 : 2) : (STAGES == 2
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           const int r = wm * WM + i * 32 + fr;
-          af[slot][i] = *reinterpret_cast<const bf16x8*>(As + r * BK + swzk<BK>(r, c) * 8);
+          af[slot][i] = *reinterpret_cast<const bf16x8*>(As + r * BK + swzk<BKB>(r, c) * 8);
         }
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int r = wn * WN + j * 32 + fr;
-          bfg[slot][j] = *reinterpret_cast<const bf16x8*>(Bs + r * BK + swzk<BK>(r, c) * 8);
+          bfg[slot][j] = *reinterpret_cast<const bf16x8*>(Bs + r * BK + swzk<BKB>(r, c) * 8);
         }
       };
       frag(0, 0);
@@ -317,28 +432,29 @@ __global__ __launch_bounds__(256, BM == 256 ? (BN == 256 ? 1 : 2) : (STAGES == 2
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int r = wm * WM + i * 32 + fr;
-        af[i] = *reinterpret_cast<const bf16x8*>(As + r * BK + swzk<BK>(r, c) * 8);
+        af[i] = *reinterpret_cast<const bf16x8*>(As + r * BK + swzk<BKB>(r, c) * 8);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int r = wn * WN + j * 32 + fr;
-        bfg[j] = *reinterpret_cast<const bf16x8*>(Bs + r * BK + swzk<BK>(r, c) * 8);
+        bfg[j] = *reinterpret_cast<const bf16x8*>(Bs + r * BK + swzk<BKB>(r, c) * 8);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfg[j], af[i], acc[i][j], 0, 0, 0);
     }
+    }
   }
 
-  // ---- epilogue, phase A: accumulators (+ bias, ReLU) -> bf16 tile in LDS. Lane holds
+  // ---- epilogue, phase A: accumulators (+ bias, ReLU) -> T tile in LDS. Lane holds
   // D[n][m] with m = lane&31, n = (v&3) + 8*(v>>2) + 4*(lane>>5): 4 consecutive columns of
-  // one row, one 8-B LDS store each.
-  // Unpadded rows (the tile fits in the 2-slot ring, keeping 5 blocks/CU possible); the
+  // one row, one 8-B (bf16) / 16-B (fp32) LDS store each (the C/D layout of both MFMAs).
+  // Unpadded rows (the bf16 tile fits in the 2-slot ring, keeping 5 blocks/CU possible); the
   // 16-B chunk index is XOR-swizzled by the row so phase A's column writes spread over banks
-  constexpr int LDT = BN, CPRS = BN / 8;
-  auto tsw = [](int row, int n) { return row * LDT + (((n >> 3) ^ (row % CPRS)) << 3) + (n & 7); };
-  uint16_t* tl = smem;         // reuses the ring
+  constexpr int LDT = BN, CPRS = BN / EPC;
+  auto tsw = [](int row, int n) { return row * LDT + (((n / EPC) ^ (row % CPRS)) * EPC) + (n % EPC); };
+  T* tl = smem;                // reuses the ring
   __syncthreads();             // every wave is done reading the ring
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -358,14 +474,19 @@ __global__ __launch_bounds__(256, BM == 256 ? (BN == 256 ? 1 : 2) : (STAGES == 2
 #pragma unroll
           for (int e = 0; e < 4; ++e) acc[i][j][4 * g + e] = fmaxf(acc[i][j][4 * g + e], 0.f);
         }
-        const uint32_t lo = uint32_t(f2bf(acc[i][j][4 * g])) | (uint32_t(f2bf(acc[i][j][4 * g + 1])) << 16);
-        const uint32_t hi = uint32_t(f2bf(acc[i][j][4 * g + 2])) | (uint32_t(f2bf(acc[i][j][4 * g + 3])) << 16);
-        *reinterpret_cast<uint2*>(tl + tsw(wm * WM + i * 32 + fr, nl)) = make_uint2(lo, hi);
+        if constexpr (F32) {
+          *reinterpret_cast<float4*>(tl + tsw(wm * WM + i * 32 + fr, nl)) =
+              make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]);
+        } else {
+          const uint32_t lo = uint32_t(f2bf(acc[i][j][4 * g])) | (uint32_t(f2bf(acc[i][j][4 * g + 1])) << 16);
+          const uint32_t hi = uint32_t(f2bf(acc[i][j][4 * g + 2])) | (uint32_t(f2bf(acc[i][j][4 * g + 3])) << 16);
+          *reinterpret_cast<uint2*>(tl + tsw(wm * WM + i * 32 + fr, nl)) = make_uint2(lo, hi);
+        }
       }
   __syncthreads();
 
-  // ---- phase B: row-major. A thread owns one 16-B chunk (8 channels) of a row and walks
-  // the rows RPP apart, so every global access of a wave covers whole 256-B (BN = 128) row
+  // ---- phase B: row-major. A thread owns 8 channels (one bf16 / two fp32 16-B chunks) of a
+  // row and walks the rows RPP apart, so every global access of a wave covers whole row
   // segments: the C store, the Cin / Cmask / BN x / BN mask loads.
   // Partials are per 128-row tile whatever BM is: with BM = 256 the row-threads split into
   // two halves of 128 rows (HALVES = BM / 128), each thread staying in one.
@@ -394,6 +515,8 @@ __global__ __launch_bounds__(256, BM == 256 ? (BN == 256 ? 1 : 2) : (STAGES == 2
     mu2[0] = a0.x; mu2[1] = a0.y; mu2[2] = a0.z; mu2[3] = a0.w;
     mu2[4] = a1.x; mu2[5] = a1.y; mu2[6] = a1.z; mu2[7] = a1.w;
   }
+  const T* epx = reinterpret_cast<const T*>(ep.x);
+  const T* epx2 = reinterpret_cast<const T*>(ep.x2);
   // Rows go in batches of PB: all loads of a batch are issued before its first store (C
   // may alias Cin, so the compiler would otherwise serialise load -> store per row), and
   // batches keep the live registers low enough for 5 resident blocks per CU.
@@ -401,7 +524,7 @@ __global__ __launch_bounds__(256, BM == 256 ? (BN == 256 ? 1 : 2) : (STAGES == 2
 #pragma unroll
   for (int pb = 0; pb < NP; pb += PB) {
   int64_t orow[PB];
-  uint4 cv[PB], xq[PB], xq2[PB];
+  V8<T> cv[PB], xq[PB], xq2[PB];
   uint32_t cmb[PB], xmb[PB];
 #pragma unroll
   for (int q = 0; q < PB; ++q) {
@@ -419,51 +542,61 @@ __global__ __launch_bounds__(256, BM == 256 ? (BN == 256 ? 1 : 2) : (STAGES == 2
     const bool ok = m < M;
     const int64_t o = orow[q] * ldc + nc;
     if (Cin != nullptr) {
-      cv[q] = ok ? *reinterpret_cast<const uint4*>(Cin + o) : make_uint4(0, 0, 0, 0);
+      if (ok) cv[q].load(Cin + o);
+      else cv[q].zero();
       cmb[q] = Cmask ? (ok ? uint32_t(Cmask[o >> 3]) : 0u) : 0xffu;
     }
     if constexpr (BNRED) {
-      xq[q] = ok ? *reinterpret_cast<const uint4*>(ep.x + o) : make_uint4(0, 0, 0, 0);
+      if (ok) xq[q].load(epx + o);
+      else xq[q].zero();
       xmb[q] = ok ? (ep.mask ? uint32_t(ep.mask[o >> 3]) : 0xffu) : 0u;
     }
-    if constexpr (DUAL) xq2[q] = ok ? *reinterpret_cast<const uint4*>(ep.x2 + o) : make_uint4(0, 0, 0, 0);
+    if constexpr (DUAL) {
+      if (ok) xq2[q].load(epx2 + o);
+      else xq2[q].zero();
+    }
   }
 #pragma unroll
   for (int q = 0; q < PB; ++q) {
     const int rl = rr + (pb + q) * RPH;
     if (m0 + rl >= M) continue;
     const int64_t o = orow[q] * ldc + nc;
-    const uint4 hv = *reinterpret_cast<const uint4*>(tl + tsw(rl, ch * 8));
-    uint32_t hw4[4] = {hv.x, hv.y, hv.z, hv.w};
+    float v[8];
+    if constexpr (F32) {
+      const float4 h0 = *reinterpret_cast<const float4*>(tl + tsw(rl, ch * 8));
+      const float4 h1 = *reinterpret_cast<const float4*>(tl + tsw(rl, ch * 8 + 4));
+      v[0] = h0.x; v[1] = h0.y; v[2] = h0.z; v[3] = h0.w;
+      v[4] = h1.x; v[5] = h1.y; v[6] = h1.z; v[7] = h1.w;
+    } else {
+      V8<uint16_t> hv;
+      hv.load(tl + tsw(rl, ch * 8));
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = hv.get(e);
+    }
     if (Cin != nullptr) {  // C = A.B^T + Cin
       // Cmask: Cin is a ReLU'd gradient given as (dy, forward bit mask: one byte per 8
       // channels, bit e = channel 8k+e positive) — dy*mask is never materialised
       const uint32_t mb = cmb[q];
-      const uint32_t cw[4] = {cv[q].x, cv[q].y, cv[q].z, cv[q].w};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float v0 = bf2f(uint16_t(hw4[q] & 0xffff)) + ((mb >> (2 * q)) & 1u ? bf2f(uint16_t(cw[q] & 0xffff)) : 0.f);
-        const float v1 = bf2f(uint16_t(hw4[q] >> 16)) + ((mb >> (2 * q + 1)) & 1u ? bf2f(uint16_t(cw[q] >> 16)) : 0.f);
-        hw4[q] = uint32_t(f2bf(v0)) | (uint32_t(f2bf(v1)) << 16);
-      }
+      for (int e = 0; e < 8; ++e) v[e] = rnd<T>(v[e] + ((mb >> e) & 1u ? cv[q].get(e) : 0.f));
     }
-    *reinterpret_cast<uint4*>(C + o) = make_uint4(hw4[0], hw4[1], hw4[2], hw4[3]);
+    store8(C + o, v);
     if constexpr (CONV) {
       if (geo.ozero) {  // class (0,0) of a stride-2 conv whose other parities have no taps
         const int64_t pix = orow[q] % (int64_t(geo.OH) * geo.OW);
         const int oh = int(pix / geo.OW), ow = int(pix % geo.OW);
-        const uint4 z = make_uint4(0, 0, 0, 0);
-        if (ow + 1 < geo.OW) *reinterpret_cast<uint4*>(C + o + ldc) = z;
+        const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (ow + 1 < geo.OW) store8(C + o + ldc, z);
         if (oh + 1 < geo.OH) {
-          *reinterpret_cast<uint4*>(C + o + int64_t(geo.OW) * ldc) = z;
-          if (ow + 1 < geo.OW) *reinterpret_cast<uint4*>(C + o + int64_t(geo.OW + 1) * ldc) = z;
+          store8(C + o + int64_t(geo.OW) * ldc, z);
+          if (ow + 1 < geo.OW) store8(C + o + int64_t(geo.OW + 1) * ldc, z);
         }
       }
     }
     if constexpr (EPI == EPI_STATS) {  // shifted by this thread's first row
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float y = bf2f(uint16_t((e & 1) ? (hw4[e >> 1] >> 16) : (hw4[e >> 1] & 0xffff)));
+        const float y = v[e];
         if (nv == 0) sf[e] = y;
         const float d = y - sf[e];
         s1[e] += d;
@@ -472,19 +605,12 @@ __global__ __launch_bounds__(256, BM == 256 ? (BN == 256 ? 1 : 2) : (STAGES == 2
       ++nv;
     } else if constexpr (BNRED) {  // dz = C * mask; (sum dz, sum dz (x - mean) [, sum dz (x2 - mean2)])
       const uint32_t xb = xmb[q];
-      const uint32_t xw[4] = {xq[q].x, xq[q].y, xq[q].z, xq[q].w};
-      const uint32_t xw2[4] = {xq2[q].x, xq2[q].y, xq2[q].z, xq2[q].w};
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const uint32_t hwd = hw4[e >> 1], xwd = xw[e >> 1];
-        const float dz = (xb >> e) & 1u ? bf2f(uint16_t((e & 1) ? (hwd >> 16) : (hwd & 0xffff))) : 0.f;
-        const float xe = bf2f(uint16_t((e & 1) ? (xwd >> 16) : (xwd & 0xffff)));
+        const float dz = (xb >> e) & 1u ? v[e] : 0.f;
         s1[e] += dz;
-        s2[e] = fmaf(dz, xe - mu[e], s2[e]);
-        if constexpr (DUAL) {
-          const uint32_t xwd2 = xw2[e >> 1];
-          s3[e] = fmaf(dz, bf2f(uint16_t((e & 1) ? (xwd2 >> 16) : (xwd2 & 0xffff))) - mu2[e], s3[e]);
-        }
+        s2[e] = fmaf(dz, xq[q].get(e) - mu[e], s2[e]);
+        if constexpr (DUAL) s3[e] = fmaf(dz, xq2[q].get(e) - mu2[e], s3[e]);
       }
     }
   }
@@ -557,27 +683,34 @@ __global__ __launch_bounds__(256, BM == 256 ? (BN == 256 ? 1 : 2) : (STAGES == 2
 // global source address. A partial last step (M % kRows) is zero-filled in LDS.
 constexpr int kRows = 32;  // rows (reduction) per staged step
 
-// 16-B chunk swizzle of a row of CPR chunks (CPR = 16: 256-B rows, 8: 128-B rows)
-template <int CPR>
+// 16-B chunk swizzle of a row of CPR chunks (bf16: CPR = 16: 256-B rows, 8: 128-B rows).
+// fp32 fragments are read one element per lane (ds_read_b32, 32 consecutive columns per
+// half-wave): conflict-free on the plain row-major image, no swizzle.
+template <typename T, int CPR>
 __device__ __forceinline__ int tswz(int row, int ch) {
-  if constexpr (CPR == 16) return ch ^ (((row & 3) << 2) | ((row >> 2) & 3));
+  if constexpr (sizeof(T) == 4) return ch;
+  else if constexpr (CPR == 16) return ch ^ (((row & 3) << 2) | ((row >> 2) & 3));
   else return ch ^ (((row >> 1) & 1) << 2);
 }
 
-template <int TBN, int TBK, int STAGES, bool CONV>
-__global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const uint16_t* __restrict__ Y, int64_t ldy,
-                                                         const uint16_t* __restrict__ X, int64_t ldx,
+template <typename T, int TBN, int TBK, int STAGES, bool CONV>
+__global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y, int64_t ldy,
+                                                         const T* __restrict__ X, int64_t ldx,
                                                          float* __restrict__ part, int64_t M, int N, int K,
                                                          int64_t rows_per_split, int ntk, int ntiles, ConvGeo geo) {
   constexpr int WN = TBN / 2, WK = TBK / 2;
   constexpr int TM = WN / 32, TN = WK / 32;
-  constexpr int CY = TBN / 8, CX = TBK / 8;           // 16-B chunks per row
+  constexpr int EPC = epc<T>();
+  constexpr int CY = TBN / EPC, CX = TBK / EPC;        // 16-B chunks per row
   constexpr int RY = 64 / CY, RX = 64 / CX;           // rows per glds wave-instruction
   constexpr int IY = kRows / RY / 4, IX = kRows / RX / 4;  // glds per wave per tile
   constexpr int NI = IY + IX;
   constexpr int TILE = kRows * (TBN + TBK);
+  constexpr bool F32 = sizeof(T) == 4;
   static_assert(IY >= 1 && IX >= 1, "tile too small");
-  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem_raw[];
+  T* smem = reinterpret_cast<T*>(smem_raw);
+  const T* zline = reinterpret_cast<const T*>(g_zero_line);
 
   const int id = xcd_tile(blockIdx.x, gridDim.x);
   const int tile = id % ntiles, split = id / ntiles;
@@ -594,21 +727,21 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const uint16_t* __restr
   // by the step's (dn, dh, dw) decomposition of kRows with at most one carry per digit.
   const int nrows = int(r1 - r0);
   int ry[IY], rx[IX], ox[IX];
-  const uint16_t* py[IY];
-  const uint16_t* pyl[IY];
-  const uint16_t* px[IX];
-  const uint16_t* pxl[IX];
+  const T* py[IY];
+  const T* pyl[IY];
+  const T* px[IX];
+  const T* pxl[IX];
 #pragma unroll
   for (int i = 0; i < IY; ++i) {
     ry[i] = (w * IY + i) * RY + lane / CY;
-    const int oy = n0 + tswz<CY>(ry[i], lane % CY) * 8;
+    const int oy = n0 + tswz<T, CY>(ry[i], lane % CY) * EPC;
     py[i] = Y + (r0 + ry[i]) * ldy + oy;
     pyl[i] = Y + (r1 - 1) * ldy + oy;
   }
 #pragma unroll
   for (int i = 0; i < IX; ++i) {
     rx[i] = (w * IX + i) * RX + lane / CX;
-    ox[i] = tswz<CX>(rx[i], lane % CX) * 8;  // channel offset inside the tile
+    ox[i] = tswz<T, CX>(rx[i], lane % CX) * EPC;  // channel offset inside the tile
     if constexpr (!CONV) {
       px[i] = X + (r0 + rx[i]) * ldx + k0 + ox[i];
       pxl[i] = X + (r1 - 1) * ldx + k0 + ox[i];
@@ -616,7 +749,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const uint16_t* __restr
   }
   const int64_t ystep = int64_t(kRows) * ldy, xstep = int64_t(kRows) * ldx;
   int dn = 0, dh = 0, dw = 0;
-  // CONV: tap (xr, xs) and element offset xc inside the tap of each lane's 8-column chunk
+  // CONV: tap (xr, xs) and element offset xc inside the tap of each lane's chunk
   // (per lane: a column tile may span taps when a tap is narrower than the tile, stem)
   int pn[IX], pho[IX], pwo[IX], xr[IX], xs[IX], xc[IX];
   const int pitch = geo.pitch ? geo.pitch : geo.C;
@@ -643,8 +776,8 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const uint16_t* __restr
   }
   const int64_t nsteps = r1 > r0 ? (r1 - r0 + kRows - 1) / kRows : 0;
   auto issue = [&](int64_t st, int buf) {
-    uint16_t* Ys = smem + buf * TILE;
-    uint16_t* Xs = Ys + kRows * TBN;
+    T* Ys = smem + buf * TILE;
+    T* Xs = Ys + kRows * TBN;
     const int rs = int(st) * kRows;  // first row of the step, relative to r0
 #pragma unroll
     for (int i = 0; i < IY; ++i) {
@@ -657,7 +790,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const uint16_t* __restr
         const int hi = pho[i] * geo.stride - geo.pad + xr[i], wi = pwo[i] * geo.stride - geo.padw + xs[i];
         const bool ok = rs + rx[i] < nrows && unsigned(hi) < unsigned(geo.H) && unsigned(wi) < unsigned(geo.W);
         const int off = ((pn[i] * geo.H + hi) * geo.W + wi) * pitch + xc[i];  // < 2^31 (host-checked)
-        glds16_asm(ok ? X + off : g_zero_line + (ox[i] & 63), Xs + (w * IX + i) * RX * TBK);
+        glds16_asm(ok ? X + off : zline + (ox[i] & (128 / int(sizeof(T)) - 1)), Xs + (w * IX + i) * RX * TBK);
         pwo[i] += dw;  // next step's rows (issued strictly in order)
         const int cw = pwo[i] >= geo.Wo;
         pwo[i] -= cw ? geo.Wo : 0;
@@ -684,6 +817,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const uint16_t* __restr
   const int g = lane >> 4, gi = lane & 15, q = gi >> 2, p = gi & 3;
   const int h = g >> 1;
   const int cbase = 2 * (g & 1) + (p >> 1), cbyte = 4 * (p & 1);  // chunk / element offset in it
+  const int fr = lane & 31, fh = lane >> 5;
 
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
@@ -696,21 +830,48 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const uint16_t* __restr
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     const int buf = int(st % STAGES);
-    uint16_t* Ys = smem + buf * TILE;
-    uint16_t* Xs = Ys + kRows * TBN;
+    T* Ys = smem + buf * TILE;
+    T* Xs = Ys + kRows * TBN;
     const int64_t valid = r1 - (r0 + st * kRows);
     if (valid < kRows) {  // last, partial step of this split (nothing else in flight)
-      for (int e = t; e < kRows * (TBN + TBK) / 8; e += 256) {
+      for (int e = t; e < kRows * (CY + CX); e += 256) {
         const int ey = e < kRows * CY;
         const int row = ey ? e / CY : (e - kRows * CY) / CX;
-        if (row >= valid) {
-          uint4* dst = ey ? reinterpret_cast<uint4*>(Ys) + e : reinterpret_cast<uint4*>(Xs) + (e - kRows * CY);
-          *dst = make_uint4(0, 0, 0, 0);
-        }
+        if (row >= valid) reinterpret_cast<uint4*>(Ys)[e] = make_uint4(0, 0, 0, 0);  // Xs follows Ys
       }
       __syncthreads();
     }
     if (st + STAGES - 1 < nsteps) issue(st + STAGES - 1, int((st + STAGES - 1) % STAGES));
+    if constexpr (F32) {
+      // v_mfma_f32_32x32x2_f32: lane (fr, fh) supplies Y[row][n0' + fr] and X[row][k0' + fr]
+      // of row 2s + fh in step s (32 consecutive floats per half-wave: ds_read_b32, no
+      // conflicts). Each staged step is one fresh 32-long fmaf chain folded into acc (blocked
+      // accumulation, as gemm_nt's fp32 loop).
+      f32x16 tacc[TM][TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int v = 0; v < 16; ++v) tacc[i][j][v] = 0.f;
+#pragma unroll
+      for (int s = 0; s < kRows / 2; ++s) {
+        const int rrow = 2 * s + fh;
+        float af[TM], bfg[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[i] = Ys[rrow * TBN + wn * WN + i * 32 + fr];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bfg[j] = Xs[rrow * TBK + wk * WK + j * 32 + fr];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) tacc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bfg[j], tacc[i][j], 0, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] += tacc[i][j];
+    } else {
 #pragma unroll
     for (int kk = 0; kk < kRows / 16; ++kk) {
       const int rr = 16 * kk + 8 * h + q;  // row of this lane in the first 4-row block
@@ -718,15 +879,15 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const uint16_t* __restr
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int ch = (wn * WN + i * 32) / 8 + cbase;
-        const s16x4 lo = ds_tr16(Ys + rr * TBN + tswz<CY>(rr, ch) * 8 + cbyte);
-        const s16x4 hi = ds_tr16(Ys + (rr + 4) * TBN + tswz<CY>(rr + 4, ch) * 8 + cbyte);
+        const s16x4 lo = ds_tr16(Ys + rr * TBN + tswz<T, CY>(rr, ch) * 8 + cbyte);
+        const s16x4 hi = ds_tr16(Ys + (rr + 4) * TBN + tswz<T, CY>(rr + 4, ch) * 8 + cbyte);
         af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int ch = (wk * WK + j * 32) / 8 + cbase;
-        const s16x4 lo = ds_tr16(Xs + rr * TBK + tswz<CX>(rr, ch) * 8 + cbyte);
-        const s16x4 hi = ds_tr16(Xs + (rr + 4) * TBK + tswz<CX>(rr + 4, ch) * 8 + cbyte);
+        const s16x4 lo = ds_tr16(Xs + rr * TBK + tswz<T, CX>(rr, ch) * 8 + cbyte);
+        const s16x4 hi = ds_tr16(Xs + (rr + 4) * TBK + tswz<T, CX>(rr + 4, ch) * 8 + cbyte);
         bfg[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
       }
 #pragma unroll
@@ -734,10 +895,10 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const uint16_t* __restr
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
     }
+    }
   }
   // D[n][k]: column k = lane&31, row n = (v&3) + 8*(v>>2) + 4*(lane>>5)
   float* out = part + int64_t(split) * N * K;
-  const int fr = lane & 31, fh = lane >> 5;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -786,17 +947,25 @@ struct TapMap {
   int16_t tc[kMaxTaps], dt[kMaxTaps];
 };
 
-// one 32 x 32 (channel x row) tile of tap `tap`, 256 threads
-__device__ __forceinline__ void cast_tile(const float* __restrict__ w, int R, int Cc, int T, uint16_t* __restrict__ wb,
-                                          uint16_t* __restrict__ wt, const TapMap& map, int cx, int ry, int tap) {
-  __shared__ uint16_t tile[32][33];
+// one 32 x 32 (channel x row) tile of tap `tap`, 256 threads. O = output element type:
+// uint16_t (bf16 cast + transpose) or float (fp32 transpose; the plain copy is the master
+// weight itself, so wb is null).
+template <typename O>
+__device__ __forceinline__ O cvt_out(float v) {
+  if constexpr (sizeof(O) == 2) return f2bf(v);
+  else return v;
+}
+template <typename O>
+__device__ __forceinline__ void cast_tile(const float* __restrict__ w, int R, int Cc, int T, O* __restrict__ wb,
+                                          O* __restrict__ wt, const TapMap& map, int cx, int ry, int tap) {
+  __shared__ O tile[32][33];
   const int c0 = cx * 32, r0 = ry * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 8 rows per pass
   for (int y = ty; y < 32; y += 8) {
     const int r = r0 + y, c = c0 + tx;
     if (r < R && c < Cc) {
       const int64_t i = (int64_t(r) * T + tap) * Cc + c;
-      const uint16_t b = f2bf(w[i]);
+      const O b = cvt_out<O>(w[i]);
       if (wb) wb[i] = b;
       tile[y][tx] = b;
     }
@@ -811,19 +980,21 @@ __device__ __forceinline__ void cast_tile(const float* __restrict__ w, int R, in
   }
 }
 
+template <typename O>
 __global__ __launch_bounds__(256) void cast_transpose_kernel(const float* __restrict__ w, int R, int Cc, int T,
-                                                             uint16_t* __restrict__ wb, uint16_t* __restrict__ wt,
-                                                             TapMap map) {
-  cast_tile(w, R, Cc, T, wb, wt, map, blockIdx.x, blockIdx.y, blockIdx.z);
+                                                             O* __restrict__ wb, O* __restrict__ wt, TapMap map) {
+  cast_tile<O>(w, R, Cc, T, wb, wt, map, blockIdx.x, blockIdx.y, blockIdx.z);
 }
 
 // Every convolution weight of a model in one launch (the per-step bf16 casts of the fp32
-// master weights): block b belongs to the job whose block0 is the largest <= b.
+// master weights, or the fp32 transposes of an fp32 step): block b belongs to the job whose
+// block0 is the largest <= b.
 struct CastJob {
   const float* w;
-  uint16_t* wb;
-  uint16_t* wt;
+  void* wb;
+  void* wt;
   int R, Cc, T, tcx, tcy;  // tiles along Cc and R
+  int f32;                 // outputs are fp32 (no plain copy)
   int64_t block0;
   TapMap map;
 };
@@ -844,7 +1015,12 @@ __global__ __launch_bounds__(256) void cast_batch_kernel(const CastJob* __restri
   const int64_t local = int64_t(blockIdx.x) - J.block0;
   const int per_tap = J.tcx * J.tcy;
   const int tap = int(local / per_tap), rem = int(local % per_tap);
-  cast_tile(J.w, J.R, J.Cc, J.T, J.wb, J.wt, J.map, rem % J.tcx, rem / J.tcx, tap);
+  if (J.f32)
+    cast_tile<float>(J.w, J.R, J.Cc, J.T, static_cast<float*>(J.wb), static_cast<float*>(J.wt), J.map, rem % J.tcx,
+                     rem / J.tcx, tap);
+  else
+    cast_tile<uint16_t>(J.w, J.R, J.Cc, J.T, static_cast<uint16_t*>(J.wb), static_cast<uint16_t*>(J.wt), J.map,
+                        rem % J.tcx, rem / J.tcx, tap);
 }
 
 void check_ptr(uintptr_t p, const char* what) {
@@ -864,21 +1040,25 @@ int cu_count(int dev) {
 
 }  // namespace
 
-bool gemm_nt_supported(int64_t M, int N, int K) { return M > 0 && N > 0 && K > 0 && N % 64 == 0 && K % kBK == 0; }
+bool gemm_nt_supported(int64_t M, int N, int K, bool f32) {
+  return M > 0 && N > 0 && K > 0 && N % 64 == 0 && K % (f32 ? 16 : kBK) == 0;
+}
 
 int64_t gemm_nt_stats_floats(int64_t M, int N) { return gemm_nt_tiles(M) * 2 * int64_t(N); }
 
 int64_t gemm_nt_tiles(int64_t M) { return (M + 127) / 128; }
 
 // Block tile of gemm_nt: 0 = 128 x (128 | 64), 1 = 256 x 128, 2 = 256 x 256;
-// MPIT_GEMM_TILE=128|256x128|256 selects one (A/B runs, large plain GEMMs).
-static int nt_tile_config(int N, int K, bool conv, int cin_conv) {
+// MPIT_GEMM_TILE=128|256x128|256 selects one (A/B runs, large plain GEMMs). fp32 runs the
+// 128-row tiles only (its MFMA is 16x slower per FLOP: LDS-bound tile shapes do not matter).
+static int nt_tile_config(int N, int K, bool conv, int cin_conv, bool f32) {
   static const int forced = [] {
     const char* e = std::getenv("MPIT_GEMM_TILE");
     if (!e) return -1;
     const std::string v(e);
     return v == "256" ? 2 : v == "256x128" ? 1 : v == "128" ? 0 : -1;
   }();
+  if (f32) return 0;
   int cfg = forced >= 0 ? forced : 0;
   // Measured (profiles/gemm_big_tile_ab_r01.jsonl, gemm_bk64_128tile_ab_r01.jsonl): 256x256
   // (BK 64) beats 128x128 on large square GEMMs (8192^3: 944 vs 611 TFLOP/s) and 256x128 on
@@ -890,16 +1070,20 @@ static int nt_tile_config(int N, int K, bool conv, int cin_conv) {
   return cfg;
 }
 
-static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B,
-                      int64_t ldb, uintptr_t C, int64_t ldc, uintptr_t cin, uintptr_t cmask, const ConvGeo* geo,
-                      const EpiArgs& ep, int epi, uintptr_t bias = 0, bool relu = false) {
-  if (!gemm_nt_supported(M, N, K))
-    throw std::invalid_argument("gemm_nt: need N % 64 == 0 and K % 32 == 0 (M=" + std::to_string(M) +
-                                " N=" + std::to_string(N) + " K=" + std::to_string(K) + ")");
+template <typename T>
+static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B,
+                        int64_t ldb, uintptr_t C, int64_t ldc, uintptr_t cin, uintptr_t cmask, const ConvGeo* geo,
+                        const EpiArgs& ep, int epi, uintptr_t bias, bool relu) {
+  constexpr bool F32 = sizeof(T) == 4;
+  constexpr int EPC = epc<T>();
+  if (!gemm_nt_supported(M, N, K, F32))
+    throw std::invalid_argument(std::string("gemm_nt: need N % 64 == 0 and K % ") + (F32 ? "16" : "32") +
+                                " == 0 (M=" + std::to_string(M) + " N=" + std::to_string(N) + " K=" + std::to_string(K) +
+                                ")");
   check_ptr(A, "A");
   check_ptr(B, "B");
   check_ptr(C, "C");
-  if (lda % 8 || ldb % 8 || ldc % 8 || (!geo && lda < K) || ldb < K || ldc < N)
+  if (lda % EPC || ldb % EPC || ldc % 8 || (!geo && lda < K) || ldb < K || ldc < N)
     throw std::invalid_argument("gemm_nt: bad leading dimensions");
   if (epi != EPI_NONE) {
     if (!ep.part) throw std::invalid_argument("gemm_nt: reduction epilogue needs a partials buffer");
@@ -911,10 +1095,10 @@ static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t
     }
   }
   hip_check(hipSetDevice(dev), "hipSetDevice");
-  const auto* a = reinterpret_cast<const uint16_t*>(A);
-  const auto* b = reinterpret_cast<const uint16_t*>(B);
-  auto* c = reinterpret_cast<uint16_t*>(C);
-  const auto* ci = reinterpret_cast<const uint16_t*>(cin);
+  const auto* a = reinterpret_cast<const T*>(A);
+  const auto* b = reinterpret_cast<const T*>(B);
+  auto* c = reinterpret_cast<T*>(C);
+  const auto* ci = reinterpret_cast<const T*>(cin);
   if (cin) check_ptr(cin, "Cin");
   if (cmask && (!cin || ldc != N)) throw std::invalid_argument("gemm_nt: cmask needs cin with ldc == N");
   const auto* cm = reinterpret_cast<const uint8_t*>(cmask);
@@ -922,25 +1106,27 @@ static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t
   const auto* bs = reinterpret_cast<const float*>(bias);
   const int rl = relu ? 1 : 0;
   const ConvGeo g = geo ? *geo : ConvGeo{};
-  const int nk = K / kBK;
-  // MPIT_GEMM_STAGES caps the ring depth (A/B measurements)
+  const int nk = K / nt_bk_of<T>();
+  // MPIT_GEMM_STAGES caps the ring depth (A/B measurements). fp32: the 64 KB epilogue tile
+  // of a 128x128 block holds a 4-deep ring for free.
   static const int max_stages = [] {
     const char* e = std::getenv("MPIT_GEMM_STAGES");
     return e ? std::max(2, std::min(4, std::atoi(e))) : 2;
   }();
-  const int stages = std::min(max_stages, nk >= 4 ? 4 : (nk == 3 ? 3 : 2));
+  const int cap = F32 && N % 128 == 0 ? 4 : max_stages;
+  const int stages = std::min(cap, nk >= 4 ? 4 : (nk == 3 ? 3 : 2));
   // (kernel templates are named at a non-template call site so their host stubs are emitted)
 #define MPIT_NT_LAUNCH1(BM, BN, ST, EPI, CONV)                                                                       \
   do {                                                                                                             \
     if (shm > 65536) { /* beyond the default dynamic-LDS cap: opt in once per instantiation */                    \
       static const bool opted = (hip_check(hipFuncSetAttribute(                                                      \
-                                               reinterpret_cast<const void*>(&gemm_nt_kernel<BM, BN, ST, EPI, CONV>), \
+                                               reinterpret_cast<const void*>(&gemm_nt_kernel<T, BM, BN, ST, EPI, CONV>), \
                                                hipFuncAttributeMaxDynamicSharedMemorySize, int(shm)),                \
                                            "hipFuncSetAttribute"),                                                   \
                                  true);                                                                              \
       (void)opted;                                                                                                   \
     }                                                                                                                \
-    hipLaunchKernelGGL((gemm_nt_kernel<BM, BN, ST, EPI, CONV>), dim3(unsigned(nb)), dim3(256), shm, s, a,          \
+    hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, ST, EPI, CONV>), dim3(unsigned(nb)), dim3(256), shm, s, a,       \
                        lda, b, ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g);                             \
   } while (0)
 #define MPIT_NT_LAUNCH2(BM, BN, ST, CONV)                                                         \
@@ -956,16 +1142,26 @@ static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t
     const int ntn = N / BN;                                                                                    \
     const int64_t nb = mtn * ntn;                                                                              \
     if (nb > INT32_MAX) throw std::invalid_argument("gemm_nt: too many tiles");                               \
-    /* LDS: the k-tile ring, reused by the epilogue's bf16 tile and reduction table */                        \
-    const size_t shm = std::max({size_t(ST) * (BM + BN) * size_t(nt_bk(BM, BN)) * 2,               \
-                                 size_t(BM) * BN * 2, size_t(256) * 8 * 3 * sizeof(float)});                  \
+    /* LDS: the k-tile ring, reused by the epilogue's output tile and reduction table */                      \
+    const size_t shm = std::max({size_t(ST) * (BM + BN) * size_t(nt_bkb(BM, BN)),                              \
+                                 size_t(BM) * BN * sizeof(T), size_t(256) * 8 * 3 * sizeof(float)});          \
     if (geo) MPIT_NT_LAUNCH2(BM, BN, ST, true);                                                           \
     else MPIT_NT_LAUNCH2(BM, BN, ST, false);                                                              \
   } while (0)
-  const int tcfg = nt_tile_config(N, K, geo != nullptr, geo ? geo->C : 0);
-  if (tcfg == 2) MPIT_NT_LAUNCH(256, 256, 2);  // 2 x 64-deep stages = the 128 KB epilogue tile
-  else if (tcfg == 1) MPIT_NT_LAUNCH(256, 128, 3);
-  else if (N % 128 == 0) {
+  const int tcfg = nt_tile_config(N, K, geo != nullptr, geo ? geo->C : 0, F32);
+  if constexpr (!F32) {
+    if (tcfg == 2) {
+      MPIT_NT_LAUNCH(256, 256, 2);  // 2 x 64-deep stages = the 128 KB epilogue tile
+      hip_check(hipGetLastError(), "gemm_nt launch");
+      return;
+    }
+    if (tcfg == 1) {
+      MPIT_NT_LAUNCH(256, 128, 3);
+      hip_check(hipGetLastError(), "gemm_nt launch");
+      return;
+    }
+  }
+  if (N % 128 == 0) {
     if (stages == 4) MPIT_NT_LAUNCH(128, 128, 4);
     else if (stages == 3) MPIT_NT_LAUNCH(128, 128, 3);
     else MPIT_NT_LAUNCH(128, 128, 2);
@@ -980,6 +1176,13 @@ static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t
   hip_check(hipGetLastError(), "gemm_nt launch");
 }
 
+static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B,
+                      int64_t ldb, uintptr_t C, int64_t ldc, uintptr_t cin, uintptr_t cmask, const ConvGeo* geo,
+                      const EpiArgs& ep, int epi, bool f32, uintptr_t bias = 0, bool relu = false) {
+  if (f32) launch_nt_t<float>(dev, s, M, N, K, A, lda, B, ldb, C, ldc, cin, cmask, geo, ep, epi, bias, relu);
+  else launch_nt_t<uint16_t>(dev, s, M, N, K, A, lda, B, ldb, C, ldc, cin, cmask, geo, ep, epi, bias, relu);
+}
+
 // the reduction epilogue selected by the (stats, BN reduction) operands
 static EpiArgs epi_args(uintptr_t stats, const BnRed* r, int* mode) {
   EpiArgs ep{};
@@ -990,7 +1193,7 @@ static EpiArgs epi_args(uintptr_t stats, const BnRed* r, int* mode) {
     *mode = EPI_STATS;
   } else if (r && r->part) {
     ep.part = reinterpret_cast<float*>(r->part);
-    ep.x = reinterpret_cast<const uint16_t*>(r->x);
+    ep.x = reinterpret_cast<const void*>(r->x);
     ep.mask = reinterpret_cast<const uint8_t*>(r->mask);
     ep.mean = reinterpret_cast<const float*>(r->mean);
     ep.row0 = r->row0;
@@ -998,7 +1201,7 @@ static EpiArgs epi_args(uintptr_t stats, const BnRed* r, int* mode) {
     if (r->part2) {
       if (!r->x2 || !r->mean2) throw std::invalid_argument("gemm_nt: second BN reduction needs x2 and mean2");
       ep.part2 = reinterpret_cast<float*>(r->part2);
-      ep.x2 = reinterpret_cast<const uint16_t*>(r->x2);
+      ep.x2 = reinterpret_cast<const void*>(r->x2);
       ep.mean2 = reinterpret_cast<const float*>(r->mean2);
       *mode = EPI_BNRED2;
     }
@@ -1007,16 +1210,17 @@ static EpiArgs epi_args(uintptr_t stats, const BnRed* r, int* mode) {
 }
 
 void gemm_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B, int64_t ldb,
-             uintptr_t C, int64_t ldc, uintptr_t stats, uintptr_t cin, uintptr_t cmask, const BnRed* red) {
+             uintptr_t C, int64_t ldc, uintptr_t stats, uintptr_t cin, uintptr_t cmask, const BnRed* red, bool f32) {
   int mode;
   const EpiArgs ep = epi_args(stats, red, &mode);
-  launch_nt(dev, s, M, N, K, A, lda, B, ldb, C, ldc, cin, cmask, nullptr, ep, mode);
+  launch_nt(dev, s, M, N, K, A, lda, B, ldb, C, ldc, cin, cmask, nullptr, ep, mode, f32);
 }
 
 bool gemm_tn_supported(int64_t M, int N, int K) { return M > 0 && N % 64 == 0 && K % 64 == 0 && N > 0 && K > 0; }
 
 // split-K plan: number of splits over M and rows per split, sized so the grid holds
-// about as many blocks as can be resident (4-stage ring: 64 KiB of LDS per 128x128 tile)
+// about as many blocks as can be resident (bf16 4-stage / fp32 2-stage ring: 64 KiB of
+// LDS per 128x128 tile)
 static int tn_plan(int dev, int64_t M, int N, int K, int64_t* rows_per_split, int* tbn, int* tbk, int cin = 0) {
   *tbn = N % 128 == 0 ? 128 : 64;
   *tbk = (cin ? cin : K) % 128 == 0 ? 128 : 64;  // conv: a column tile never straddles two taps
@@ -1044,14 +1248,18 @@ int64_t gemm_tn_ws_floats(int dev, int64_t M, int N, int K) {
   return ns > 1 ? (int64_t(ns) + tn_groups(ns)) * N * K : 0;
 }
 
-static void launch_tn(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X,
-                      int64_t ldx, uintptr_t out, uintptr_t ws, float beta, const ConvGeo* geo) {
+template <typename T>
+static void launch_tn_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X,
+                        int64_t ldx, uintptr_t out, uintptr_t ws, float beta, const ConvGeo* geo) {
+  constexpr bool F32 = sizeof(T) == 4;
+  constexpr int EPC = epc<T>();
   if (!gemm_tn_supported(M, N, K))
     throw std::invalid_argument("gemm_tn: need N % 64 == 0 and K % 64 == 0");
   check_ptr(Y, "Y");
   check_ptr(X, "X");
   check_ptr(out, "out");
-  if (ldy % 8 || ldx % 8 || ldy < N || (!geo && ldx < K)) throw std::invalid_argument("gemm_tn: bad leading dimensions");
+  if (ldy % EPC || ldx % EPC || ldy < N || (!geo && ldx < K))
+    throw std::invalid_argument("gemm_tn: bad leading dimensions");
   hip_check(hipSetDevice(dev), "hipSetDevice");
   int64_t rps;
   int tbn, tbk;
@@ -1062,28 +1270,30 @@ static void launch_tn(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t
   if (!direct && ws == 0) throw std::invalid_argument("gemm_tn: workspace required");
   if (!direct) check_ptr(ws, "ws");
   float* part = reinterpret_cast<float*>(direct ? out : ws);
-  const auto* y = reinterpret_cast<const uint16_t*>(Y);
-  const auto* x = reinterpret_cast<const uint16_t*>(X);
+  const auto* y = reinterpret_cast<const T*>(Y);
+  const auto* x = reinterpret_cast<const T*>(X);
   const ConvGeo g = geo ? *geo : ConvGeo{};
   const dim3 grid(unsigned(int64_t(ntiles) * ns));
-  // MPIT_GEMM_TN_STAGES: ring depth (A/B measurements; 4 by default)
+  // MPIT_GEMM_TN_STAGES: ring depth (A/B measurements; bf16 4 by default). fp32 stages
+  // twice the bytes per row and computes 16x longer per staged step: 2 stages.
   static const int tn_stages = [] {
     const char* e = std::getenv("MPIT_GEMM_TN_STAGES");
     return e && std::atoi(e) <= 2 ? 2 : 4;
   }();
+  const int stages = F32 ? 2 : tn_stages;
 #define MPIT_TN_LAUNCH1(A, B, ST)                                                                                  \
   do {                                                                                                             \
-    const size_t shm = size_t(ST) * kRows * (tbn + tbk) * sizeof(uint16_t);                                      \
+    const size_t shm = size_t(ST) * kRows * (tbn + tbk) * sizeof(T);                                             \
     if (geo)                                                                                                       \
-      hipLaunchKernelGGL((gemm_tn_kernel<A, B, ST, true>), grid, dim3(256), shm, s, y, ldy, x, ldx, part, M, N, K, \
-                         rps, ntk, ntiles, g);                                                                     \
-    else                                                                                                           \
-      hipLaunchKernelGGL((gemm_tn_kernel<A, B, ST, false>), grid, dim3(256), shm, s, y, ldy, x, ldx, part, M, N,  \
+      hipLaunchKernelGGL((gemm_tn_kernel<T, A, B, ST, true>), grid, dim3(256), shm, s, y, ldy, x, ldx, part, M, N, \
                          K, rps, ntk, ntiles, g);                                                                  \
+    else                                                                                                           \
+      hipLaunchKernelGGL((gemm_tn_kernel<T, A, B, ST, false>), grid, dim3(256), shm, s, y, ldy, x, ldx, part, M,   \
+                         N, K, rps, ntk, ntiles, g);                                                               \
   } while (0)
 #define MPIT_TN_LAUNCH(A, B)               \
   do {                                     \
-    if (tn_stages == 2) MPIT_TN_LAUNCH1(A, B, 2); \
+    if (stages == 2) MPIT_TN_LAUNCH1(A, B, 2); \
     else MPIT_TN_LAUNCH1(A, B, 4);         \
   } while (0)
   if (tbn == 128 && tbk == 128) MPIT_TN_LAUNCH(128, 128);
@@ -1112,9 +1322,15 @@ static void launch_tn(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t
   }
 }
 
+static void launch_tn(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X,
+                      int64_t ldx, uintptr_t out, uintptr_t ws, float beta, const ConvGeo* geo, bool f32) {
+  if (f32) launch_tn_t<float>(dev, s, M, N, K, Y, ldy, X, ldx, out, ws, beta, geo);
+  else launch_tn_t<uint16_t>(dev, s, M, N, K, Y, ldy, X, ldx, out, ws, beta, geo);
+}
+
 void gemm_tn(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X, int64_t ldx,
-             uintptr_t out, uintptr_t ws, float beta) {
-  launch_tn(dev, s, M, N, K, Y, ldy, X, ldx, out, ws, beta, nullptr);
+             uintptr_t out, uintptr_t ws, float beta, bool f32) {
+  launch_tn(dev, s, M, N, K, Y, ldy, X, ldx, out, ws, beta, nullptr, f32);
 }
 
 // ------------------------------------------------------------------ convolutions
@@ -1131,7 +1347,7 @@ bool conv_supported(int C, int Co) { return C % 32 == 0 && Co % 64 == 0; }
 
 void conv_fwd(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad,
               uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t cin, uintptr_t bias, bool relu,
-              const BnRed* red) {
+              const BnRed* red, bool f32) {
   if (!conv_supported(C, Co)) throw std::invalid_argument("conv_fwd: need C % 32 == 0 and Co % 64 == 0");
   if (int64_t(Nb) * H * W * C >= (int64_t(1) << 31)) throw std::invalid_argument("conv_fwd: input too large");
   int Ho, Wo;
@@ -1139,7 +1355,7 @@ void conv_fwd(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R
   const int64_t M = int64_t(Nb) * Ho * Wo;
   int mode;
   const EpiArgs ep = epi_args(stats, red, &mode);
-  launch_nt(dev, s, M, Co, R * S * C, x, C, w, int64_t(R) * S * C, y, Co, cin, 0, &g, ep, mode, bias, relu);
+  launch_nt(dev, s, M, Co, R * S * C, x, C, w, int64_t(R) * S * C, y, Co, cin, 0, &g, ep, mode, f32, bias, relu);
 }
 
 int64_t conv_wgrad_ws_floats(int dev, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad) {
@@ -1154,16 +1370,16 @@ int64_t conv_wgrad_ws_floats(int dev, int Nb, int H, int W, int C, int Co, int R
 }
 
 void conv_wgrad(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad,
-                uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, float beta) {
+                uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, float beta, bool f32) {
   if (C % 64 || Co % 64) throw std::invalid_argument("conv_wgrad: need C % 64 == 0 and Co % 64 == 0");
   if (int64_t(Nb) * H * W * C >= (int64_t(1) << 31)) throw std::invalid_argument("conv_wgrad: input too large");
   int Ho, Wo;
   const ConvGeo g = conv_geo(H, W, C, R, S, stride, pad, &Ho, &Wo);
   const int64_t M = int64_t(Nb) * Ho * Wo;
-  launch_tn(dev, s, M, Co, R * S * C, dy, Co, x, C, dw, ws, beta, &g);
+  launch_tn(dev, s, M, Co, R * S * C, dy, Co, x, C, dw, ws, beta, &g, f32);
 }
 
-// Row-tap stem convolution: x is a zero-padded NHWC4 image [Nb][Hp][Wp][4] (bf16), the
+// Row-tap stem convolution: x is a zero-padded NHWC4 image [Nb][Hp][Wp][4] (bf16 / fp32), the
 // kernel has 8 rows of 8 pixels x 4 channels (K = 256; a 7x7x3 kernel zero-extended), output
 // pixel (ho, wo) reads rows ho*stride + r, pixels wo*stride .. +7 of each.
 static ConvGeo stem_geo(int Nb, int Hp, int Wp, int Ho, int Wo, int stride) {
@@ -1174,12 +1390,12 @@ static ConvGeo stem_geo(int Nb, int Hp, int Wp, int Ho, int Wo, int stride) {
 }
 
 void conv_stem_fwd(int dev, hipStream_t s, int Nb, int Hp, int Wp, int Co, int Ho, int Wo, int stride, uintptr_t x,
-                   uintptr_t w, uintptr_t y, uintptr_t stats) {
+                   uintptr_t w, uintptr_t y, uintptr_t stats, bool f32) {
   if (Co % 64) throw std::invalid_argument("conv_stem_fwd: need Co % 64 == 0");
   const ConvGeo g = stem_geo(Nb, Hp, Wp, Ho, Wo, stride);
   int mode;
   const EpiArgs ep = epi_args(stats, nullptr, &mode);
-  launch_nt(dev, s, int64_t(Nb) * Ho * Wo, Co, kStemK, x, kStemTap, w, kStemK, y, Co, 0, 0, &g, ep, mode);
+  launch_nt(dev, s, int64_t(Nb) * Ho * Wo, Co, kStemK, x, kStemTap, w, kStemK, y, Co, 0, 0, &g, ep, mode, f32);
 }
 
 int64_t conv_stem_wgrad_ws_floats(int dev, int Nb, int Ho, int Wo, int Co) {
@@ -1190,30 +1406,34 @@ int64_t conv_stem_wgrad_ws_floats(int dev, int Nb, int Ho, int Wo, int Co) {
 }
 
 void conv_stem_wgrad(int dev, hipStream_t s, int Nb, int Hp, int Wp, int Co, int Ho, int Wo, int stride, uintptr_t dy,
-                     uintptr_t x, uintptr_t dw, uintptr_t ws) {
+                     uintptr_t x, uintptr_t dw, uintptr_t ws, bool f32) {
   if (Co % 64) throw std::invalid_argument("conv_stem_wgrad: need Co % 64 == 0");
   const ConvGeo g = stem_geo(Nb, Hp, Wp, Ho, Wo, stride);
-  launch_tn(dev, s, int64_t(Nb) * Ho * Wo, Co, kStemK, dy, Co, x, kStemTap, dw, ws, 0.f, &g);
+  launch_tn(dev, s, int64_t(Nb) * Ho * Wo, Co, kStemK, dy, Co, x, kStemTap, dw, ws, 0.f, &g, f32);
 }
 
 static void launch_cast(int dev, hipStream_t s, uintptr_t w, int R, int Cc, uintptr_t wb, uintptr_t wt, int taps,
-                        const TapMap& map) {
+                        const TapMap& map, bool f32) {
   if (taps < 1 || taps > kMaxTaps) throw std::invalid_argument("cast_transpose: 1 <= taps <= 49");
   hip_check(hipSetDevice(dev), "hipSetDevice");
   const dim3 grid((Cc + 31) / 32, (R + 31) / 32, taps);
-  hipLaunchKernelGGL(cast_transpose_kernel, grid, dim3(256), 0, s, reinterpret_cast<const float*>(w), R, Cc, taps,
-                     reinterpret_cast<uint16_t*>(wb), reinterpret_cast<uint16_t*>(wt), map);
+  if (f32)
+    hipLaunchKernelGGL(cast_transpose_kernel<float>, grid, dim3(256), 0, s, reinterpret_cast<const float*>(w), R, Cc,
+                       taps, reinterpret_cast<float*>(wb), reinterpret_cast<float*>(wt), map);
+  else
+    hipLaunchKernelGGL(cast_transpose_kernel<uint16_t>, grid, dim3(256), 0, s, reinterpret_cast<const float*>(w), R,
+                       Cc, taps, reinterpret_cast<uint16_t*>(wb), reinterpret_cast<uint16_t*>(wt), map);
   hip_check(hipGetLastError(), "cast_transpose launch");
 }
 
-void cast_transpose(int dev, hipStream_t s, uintptr_t w, int R, int Cc, uintptr_t wb, uintptr_t wt, int taps) {
+void cast_transpose(int dev, hipStream_t s, uintptr_t w, int R, int Cc, uintptr_t wb, uintptr_t wt, int taps, bool f32) {
   TapMap map{};
   for (int t = 0; t < taps && t < kMaxTaps; ++t) {
     map.base[t] = 0;
     map.tc[t] = int16_t(taps);
     map.dt[t] = int16_t(taps - 1 - t);
   }
-  launch_cast(dev, s, w, R, Cc, wb, wt, taps, map);
+  launch_cast(dev, s, w, R, Cc, wb, wt, taps, map, f32);
 }
 
 // ---- backward-data of a strided conv as stride^2 parity classes ----------------------
@@ -1269,9 +1489,9 @@ int64_t conv_dgrad_strided_wfloats(int C, int Co, int R, int S, int stride, int 
 }
 
 void conv_dgrad_strided_weights(int dev, hipStream_t s, uintptr_t w, int Co, int C, int R, int S, int stride, int pad,
-                                uintptr_t wb, uintptr_t wcls) {
+                                uintptr_t wb, uintptr_t wcls, bool f32) {
   const StridedPlan P = strided_plan(2 * stride, 2 * stride, C, Co, R, S, stride, pad);
-  launch_cast(dev, s, w, Co, C, wb, wcls, R * S, P.map);
+  launch_cast(dev, s, w, Co, C, wb, wcls, R * S, P.map, f32);
 }
 
 int64_t conv_dgrad_strided_tiles(int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad) {
@@ -1289,12 +1509,14 @@ int64_t cast_jobs_build(uintptr_t host_table, const std::vector<std::array<int64
   int64_t blocks = 0;
   for (size_t k = 0; k < specs.size(); ++k) {
     const auto& q = specs[k];
-    const int kind = int(q[0]), Co = int(q[4]), C = int(q[5]), R = int(q[6]), S = int(q[7]);
+    // q[0] = kind | f32 << 8 (fp32 outputs: transposes only, the plain copy is the master weight)
+    const int kind = int(q[0] & 0xff), Co = int(q[4]), C = int(q[5]), R = int(q[6]), S = int(q[7]);
     const int stride = int(q[8]), pad = int(q[9]);
     CastJob J{};
     J.w = reinterpret_cast<const float*>(q[1]);
-    J.wb = reinterpret_cast<uint16_t*>(q[2]);
-    J.wt = reinterpret_cast<uint16_t*>(q[3]);
+    J.f32 = int((q[0] >> 8) & 1);
+    J.wb = J.f32 ? nullptr : reinterpret_cast<void*>(q[2]);
+    J.wt = reinterpret_cast<void*>(q[3]);
     J.R = Co;
     J.Cc = C;
     J.T = R * S;
@@ -1328,7 +1550,7 @@ void cast_jobs_run(int dev, hipStream_t s, uintptr_t dev_table, int njobs, int64
 }
 
 void conv_dgrad_strided(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad,
-                        uintptr_t dy, uintptr_t wcls, uintptr_t dx, const BnRed* red) {
+                        uintptr_t dy, uintptr_t wcls, uintptr_t dx, const BnRed* red, bool f32) {
   if (C % 64 || Co % 32) throw std::invalid_argument("conv_dgrad_strided: need C % 64 == 0 and Co % 32 == 0");
   int Ho, Wo;
   conv_geo(H, W, C, R, S, stride, pad, &Ho, &Wo);
@@ -1338,7 +1560,7 @@ void conv_dgrad_strided(int dev, hipStream_t s, int Nb, int H, int W, int C, int
   const bool ozero = P.any_empty && stride == 2 && P.ncls == 1 && P.cls[0].ph == 0 && P.cls[0].pw == 0;
   if (P.any_empty && !ozero) {
     hip_check(hipSetDevice(dev), "hipSetDevice");
-    hip_check(hipMemsetAsync(reinterpret_cast<void*>(dx), 0, size_t(Nb) * H * W * C * 2, s), "dgrad zero fill");
+    hip_check(hipMemsetAsync(reinterpret_cast<void*>(dx), 0, size_t(Nb) * H * W * C * (f32 ? 4 : 2), s), "dgrad zero fill");
   }
   int64_t row0 = 0;
   for (int k = 0; k < P.ncls; ++k) {
@@ -1353,7 +1575,7 @@ void conv_dgrad_strided(int dev, hipStream_t s, int Nb, int H, int W, int C, int
     EpiArgs ep = epi_args(0, red, &mode);
     ep.row0 += row0;
     row0 += gemm_nt_tiles(M);
-    launch_nt(dev, s, M, C, K, dy, Co, wcls + uintptr_t(c.base) * 2, K, dx, C, 0, 0, &g, ep, mode);
+    launch_nt(dev, s, M, C, K, dy, Co, wcls + uintptr_t(c.base) * (f32 ? 4 : 2), K, dx, C, 0, 0, &g, ep, mode, f32);
   }
 }
 

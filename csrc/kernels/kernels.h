@@ -66,7 +66,8 @@ void gather_scale(int dev, hipStream_t s, const std::vector<uintptr_t>& srcs, co
 
 // ---- fused BatchNorm (+residual) (+ReLU), NHWC, training (bn_act.hip) -------------
 // x / res / y / dy / dx / dres: [M, C] row-major (channels_last), bf16 or fp32.
-// mask: ReLU bit mask written by the forward (bn_mask_bytes) and read by the backward.
+// mask: ReLU bit mask written by the forward (bn_mask_bytes: one byte per 8 channels, either
+// dtype) and read by the backward. C % 8 == 0.
 int64_t bn_workspace_floats(int C);
 int64_t bn_mask_bytes(bool bf16, int64_t M, int C);
 // stats / nstat (optional): the statistics of x as per-128-row-tile (mean, M2) partials
@@ -87,15 +88,18 @@ void bn_act_bwd(int dev, hipStream_t s, bool bf16, uintptr_t dy, uintptr_t mask,
 
 // bn_act_fwd with y == 0 / bn_act_bwd with dx == 0 only compute the coefficients into
 // ws[0, 2C) (scale, shift) / ws[0, 3C) (A, C, B) and the running stats / dgamma, dbeta.
-// A block's last BN and its downsample shortcut's BN as one op (bf16, ReLU):
+// A block's last BN and its downsample shortcut's BN as one op (bf16 or fp32, ReLU):
 // y = relu(bn1(x1) + bn2(x2)) from the two forward coefficient sets, and the backward
 // dx1 / dx2 from the two backward sets, one pass each.
 void bn_pair_apply(int dev, hipStream_t s, uintptr_t x1, uintptr_t coef1, uintptr_t x2, uintptr_t coef2, uintptr_t y,
-                   int64_t M, int C, uintptr_t mask);
+                   int64_t M, int C, uintptr_t mask, bool f32 = false);
 void bn_pair_bwd_apply(int dev, hipStream_t s, uintptr_t dy, uintptr_t mask, uintptr_t x1, uintptr_t coef1,
-                       uintptr_t dx1, uintptr_t x2, uintptr_t coef2, uintptr_t dx2, int64_t M, int C);
+                       uintptr_t dx1, uintptr_t x2, uintptr_t coef2, uintptr_t dx2, int64_t M, int C, bool f32 = false);
 
-// ---- MFMA GEMMs for NHWC 1x1 convolutions (gemm.hip), bf16 operands, fp32 accumulate --
+// ---- MFMA GEMMs for NHWC 1x1 convolutions (gemm.hip), fp32 accumulate -------------------
+// Operands and outputs are bf16 (v_mfma_f32_32x32x16_bf16) or, with f32 = true, fp32
+// (v_mfma_f32_32x32x2_f32: exact fp32 products). Everything said below of bf16 tensors holds
+// for fp32 ones in an f32 call; ReLU bit masks are one byte per 8 channels either way.
 // C[M,N] (bf16) = A[M,K] . B[N,K]^T; optional per-column (mean, M2) partials of C per
 // 128-row tile into stats[ceil(M/128)][2][N] (gemm_nt_stats_floats); optional bf16 cin
 // [M, ldc] added to the product before rounding (may alias C); optional cmask (with cin,
@@ -111,20 +115,21 @@ struct BnRed {
   int64_t row0 = 0;
   uintptr_t part2 = 0, x2 = 0, mean2 = 0;
 };
-bool gemm_nt_supported(int64_t M, int N, int K);
+bool gemm_nt_supported(int64_t M, int N, int K, bool f32 = false);
 int64_t gemm_nt_tiles(int64_t M);
 int64_t gemm_nt_stats_floats(int64_t M, int N);
 void gemm_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B, int64_t ldb,
              uintptr_t C, int64_t ldc, uintptr_t stats, uintptr_t cin, uintptr_t cmask = 0,
-             const BnRed* red = nullptr);
+             const BnRed* red = nullptr, bool f32 = false);
 // out[N,K] (fp32) = beta*out + Y[M,N]^T . X[M,K]  (split over M; ws: gemm_tn_ws_floats)
 bool gemm_tn_supported(int64_t M, int N, int K);
 int64_t gemm_tn_ws_floats(int dev, int64_t M, int N, int K);
 void gemm_tn(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X, int64_t ldx,
-             uintptr_t out, uintptr_t ws, float beta);
+             uintptr_t out, uintptr_t ws, float beta, bool f32 = false);
 // fp32 w[R][T][Cc] -> bf16 wb[R][T][Cc] (optional) and bf16 tap-flipped transpose
 // wt[Cc][T-1-t][R] (optional); T = 1 is the plain transpose
-void cast_transpose(int dev, hipStream_t s, uintptr_t w, int R, int Cc, uintptr_t wb, uintptr_t wt, int taps = 1);
+void cast_transpose(int dev, hipStream_t s, uintptr_t w, int R, int Cc, uintptr_t wb, uintptr_t wt, int taps = 1,
+                    bool f32 = false);
 // Many casts in one launch. Job spec: {kind, w, wb, wt, Co, C, R, S, stride, pad}, kind 0 =
 // cast + tap-flipped transpose (conv_weights / cast_transpose), 1 = cast + strided
 // parity-class weights (conv_dgrad_strided_weights), 2 = cast only. The table is built on the
@@ -141,7 +146,7 @@ bool conv_supported(int C, int Co);
 // bias (fp32 [Co], optional) and ReLU are applied in the epilogue.
 void conv_fwd(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad,
               uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t cin, uintptr_t bias = 0,
-              bool relu = false, const BnRed* red = nullptr);
+              bool relu = false, const BnRed* red = nullptr, bool f32 = false);
 // ReLU + bias backward: dz = dy * (y > 0) (bf16 [M, C]), db[c] = sum_m dz (fp32, optional,
 // deterministic); ws: relu_bias_bwd_ws_floats(C)
 // Backward-data of a strided conv (stride 2..4) as stride^2 parity-class implicit GEMMs
@@ -149,33 +154,33 @@ void conv_fwd(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R
 // conv_dgrad_strided_weights from the fp32 master (also writes wb like cast_transpose).
 int64_t conv_dgrad_strided_wfloats(int C, int Co, int R, int S, int stride, int pad);
 void conv_dgrad_strided_weights(int dev, hipStream_t s, uintptr_t w, int Co, int C, int R, int S, int stride, int pad,
-                                uintptr_t wb, uintptr_t wcls);
+                                uintptr_t wb, uintptr_t wcls, bool f32 = false);
 // partial rows a BN reduction over the strided backward-data writes (all classes)
 int64_t conv_dgrad_strided_tiles(int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad);
 void conv_dgrad_strided(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad,
-                        uintptr_t dy, uintptr_t wcls, uintptr_t dx, const BnRed* red = nullptr);
+                        uintptr_t dy, uintptr_t wcls, uintptr_t dx, const BnRed* red = nullptr, bool f32 = false);
 int64_t relu_bias_bwd_ws_floats(int C);
 void relu_bias_bwd(int dev, hipStream_t s, int64_t M, int C, uintptr_t dy, uintptr_t y, uintptr_t dz, uintptr_t db,
-                   uintptr_t ws);
+                   uintptr_t ws, bool f32 = false);
 // dw [Co,R,S,C] (fp32) = beta*dw + dY^T . im2col(x)   (C % 64 == 0, Co % 64 == 0)
 int64_t conv_wgrad_ws_floats(int dev, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad);
 void conv_wgrad(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad,
-                uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, float beta);
+                uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, float beta, bool f32 = false);
 
 // Row-tap stem conv (7x7 / stride-2 / 3-channel ResNet stem on MFMA): x = zero-padded NHWC4
 // image [Nb][Hp][Wp][4], w = [Co][8][8][4] (bf16, zero-extended kernel), y = [Nb][Ho][Wo][Co];
 // dw = [Co][8][8][4] fp32; stats: BN statistics of y as conv_fwd
 void conv_stem_fwd(int dev, hipStream_t s, int Nb, int Hp, int Wp, int Co, int Ho, int Wo, int stride, uintptr_t x,
-                   uintptr_t w, uintptr_t y, uintptr_t stats);
+                   uintptr_t w, uintptr_t y, uintptr_t stats, bool f32 = false);
 int64_t conv_stem_wgrad_ws_floats(int dev, int Nb, int Ho, int Wo, int Co);
 void conv_stem_wgrad(int dev, hipStream_t s, int Nb, int Hp, int Wp, int Co, int Ho, int Wo, int stride, uintptr_t dy,
-                     uintptr_t x, uintptr_t dw, uintptr_t ws);
+                     uintptr_t x, uintptr_t dw, uintptr_t ws, bool f32 = false);
 
-// ---- NHWC bf16 max pooling with a uint8 argmax per output element (pool.hip) ---------
+// ---- NHWC bf16 / fp32 max pooling with a uint8 argmax per output element (pool.hip) ---
 // x [N,H,W,C] -> y, idx [N,Ho,Wo,C]; dx [N,H,W,C] gathered from dy + idx (no atomics).
 void maxpool_fwd(int dev, hipStream_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t x,
-                 uintptr_t y, uintptr_t idx);
+                 uintptr_t y, uintptr_t idx, bool f32 = false);
 void maxpool_bwd(int dev, hipStream_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t dy,
-                 uintptr_t idx, uintptr_t dx);
+                 uintptr_t idx, uintptr_t dx, bool f32 = false);
 
 }  // namespace mpit

@@ -1,6 +1,6 @@
-// NHWC bf16 max pooling (ResNet stem: 3x3, stride 2, pad 1) with a one-byte argmax.
+// NHWC bf16 / fp32 max pooling (ResNet stem: 3x3, stride 2, pad 1) with a one-byte argmax.
 //
-// Forward: one thread owns 8 channels (16 B) of one output pixel, reads its KxK window
+// Forward: one thread owns 8 channels (16 B bf16 / 32 B fp32) of one output pixel, reads its KxK window
 // (16-B loads, channels contiguous), writes the max and the window index of the max
 // (uint8, first maximum in scan order like PyTorch; a NaN wins and propagates).
 // Backward: one thread owns 8 channels of one INPUT pixel and gathers the gradients of
@@ -22,10 +22,34 @@ struct PoolGeo {
   int N, H, W, C, Ho, Wo, K, stride, pad;
 };
 
+// 8 channels of T as floats
+__device__ __forceinline__ void ld8(const uint16_t* p, float (&f)[8]) {
+  const uint4 v = *reinterpret_cast<const uint4*>(p);
+  const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int e = 0; e < 8; ++e) f[e] = bf2f(uint16_t((u[e >> 1] >> (16 * (e & 1))) & 0xffff));
+}
+__device__ __forceinline__ void ld8(const float* p, float (&f)[8]) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
+  f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+__device__ __forceinline__ void st8(uint16_t* p, const float (&f)[8]) {
+  uint4 o;
+  uint32_t* op = &o.x;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) op[e] = uint32_t(f2bf(f[2 * e])) | (uint32_t(f2bf(f[2 * e + 1])) << 16);
+  *reinterpret_cast<uint4*>(p) = o;
+}
+__device__ __forceinline__ void st8(float* p, const float (&f)[8]) {
+  reinterpret_cast<float4*>(p)[0] = make_float4(f[0], f[1], f[2], f[3]);
+  reinterpret_cast<float4*>(p)[1] = make_float4(f[4], f[5], f[6], f[7]);
+}
+
 // I: index type of the pixel decomposition — uint32_t whenever the tensor allows (64-bit
 // divisions are emulated and made these kernels 2.5x slower than their bytes)
-template <typename I>
-__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+template <typename T, typename I>
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                           uint8_t* __restrict__ idx, PoolGeo g) {
   const I cv = I(g.C / 8);
   const I total = I(g.N) * I(g.Ho) * I(g.Wo) * cv;
@@ -50,12 +74,12 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint16_t* __rest
       for (int j = 0; j < g.K; ++j) {
         const int w = w0 + j;
         if (unsigned(w) >= unsigned(g.W)) continue;
-        const uint4 v = *reinterpret_cast<const uint4*>(x + ((n * g.H + h) * g.W + w) * g.C + c8 * 8);
-        const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+        float fv[8];
+        ld8(x + ((n * g.H + h) * g.W + w) * g.C + c8 * 8, fv);
         const uint8_t k = uint8_t(i * g.K + j);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const float f = bf2f(uint16_t((u[e >> 1] >> (16 * (e & 1))) & 0xffff));
+          const float f = fv[e];
           if (f > best[e] || (f != f && best[e] == best[e])) {
             best[e] = f;
             arg[e] = k;
@@ -63,11 +87,7 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint16_t* __rest
         }
       }
     }
-    uint4 o;
-    uint32_t* op = &o.x;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) op[e] = uint32_t(f2bf(best[2 * e])) | (uint32_t(f2bf(best[2 * e + 1])) << 16);
-    *reinterpret_cast<uint4*>(y + int64_t(pix) * g.C + c8 * 8) = o;
+    st8(y + int64_t(pix) * g.C + c8 * 8, best);
     uint2 a;
     a.x = uint32_t(arg[0]) | (uint32_t(arg[1]) << 8) | (uint32_t(arg[2]) << 16) | (uint32_t(arg[3]) << 24);
     a.y = uint32_t(arg[4]) | (uint32_t(arg[5]) << 8) | (uint32_t(arg[6]) << 16) | (uint32_t(arg[7]) << 24);
@@ -75,9 +95,9 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const uint16_t* __rest
   }
 }
 
-template <typename I>
-__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const uint16_t* __restrict__ dy,
-                                                          const uint8_t* __restrict__ idx, uint16_t* __restrict__ dx,
+template <typename T, typename I>
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ dy,
+                                                          const uint8_t* __restrict__ idx, T* __restrict__ dx,
                                                           PoolGeo g) {
   const I cv = I(g.C / 8);
   const I total = I(g.N) * I(g.H) * I(g.W) * cv;
@@ -100,21 +120,17 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const uint16_t* __rest
         if (j < 0 || j >= g.K) continue;
         const int64_t o = ((n * g.Ho + ho) * g.Wo + wo) * g.C + c8 * 8;
         const uint2 a = *reinterpret_cast<const uint2*>(idx + o);
-        const uint4 v = *reinterpret_cast<const uint4*>(dy + o);
-        const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+        float gv[8];
+        ld8(dy + o, gv);
         const uint8_t k = uint8_t(i * g.K + j);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const uint8_t ae = uint8_t(((e < 4 ? a.x : a.y) >> (8 * (e & 3))) & 0xff);
-          if (ae == k) acc[e] += bf2f(uint16_t((u[e >> 1] >> (16 * (e & 1))) & 0xffff));
+          if (ae == k) acc[e] += gv[e];
         }
       }
     }
-    uint4 o;
-    uint32_t* op = &o.x;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) op[e] = uint32_t(f2bf(acc[2 * e])) | (uint32_t(f2bf(acc[2 * e + 1])) << 16);
-    *reinterpret_cast<uint4*>(dx + int64_t(pix) * g.C + c8 * 8) = o;
+    st8(dx + int64_t(pix) * g.C + c8 * 8, acc);
   }
 }
 
@@ -130,31 +146,45 @@ unsigned grid_for(int64_t work) { return unsigned(std::min<int64_t>((work + 255)
 
 }  // namespace
 
-void maxpool_fwd(int dev, hipStream_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t x,
-                 uintptr_t y, uintptr_t idx) {
+template <typename T>
+void maxpool_fwd_t(int dev, hipStream_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t x,
+                   uintptr_t y, uintptr_t idx) {
   const PoolGeo g = pool_geo(N, H, W, C, K, stride, pad);
   if ((x | y) % 16 || idx % 8) throw std::invalid_argument("maxpool_fwd: misaligned buffers");
   hip_check(hipSetDevice(dev), "hipSetDevice");
   const int64_t work = int64_t(N) * g.Ho * g.Wo * (C / 8);
   // 32-bit indexing while the grid-stride index cannot wrap (work + one grid < 2^32)
   const bool narrow = work + int64_t(grid_for(work)) * 256 < (int64_t(1) << 32);
-  auto* k = narrow ? maxpool_fwd_kernel<uint32_t> : maxpool_fwd_kernel<int64_t>;
-  hipLaunchKernelGGL(k, dim3(grid_for(work)), dim3(256), 0, s, reinterpret_cast<const uint16_t*>(x),
-                     reinterpret_cast<uint16_t*>(y), reinterpret_cast<uint8_t*>(idx), g);
+  auto* k = narrow ? maxpool_fwd_kernel<T, uint32_t> : maxpool_fwd_kernel<T, int64_t>;
+  hipLaunchKernelGGL(k, dim3(grid_for(work)), dim3(256), 0, s, reinterpret_cast<const T*>(x),
+                     reinterpret_cast<T*>(y), reinterpret_cast<uint8_t*>(idx), g);
   hip_check(hipGetLastError(), "maxpool_fwd launch");
 }
 
-void maxpool_bwd(int dev, hipStream_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t dy,
-                 uintptr_t idx, uintptr_t dx) {
+template <typename T>
+void maxpool_bwd_t(int dev, hipStream_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t dy,
+                   uintptr_t idx, uintptr_t dx) {
   const PoolGeo g = pool_geo(N, H, W, C, K, stride, pad);
   if ((dy | dx) % 16 || idx % 8) throw std::invalid_argument("maxpool_bwd: misaligned buffers");
   hip_check(hipSetDevice(dev), "hipSetDevice");
   const int64_t work = int64_t(N) * H * W * (C / 8);
   const bool narrow = work + int64_t(grid_for(work)) * 256 < (int64_t(1) << 32);
-  auto* k = narrow ? maxpool_bwd_kernel<uint32_t> : maxpool_bwd_kernel<int64_t>;
-  hipLaunchKernelGGL(k, dim3(grid_for(work)), dim3(256), 0, s, reinterpret_cast<const uint16_t*>(dy),
-                     reinterpret_cast<const uint8_t*>(idx), reinterpret_cast<uint16_t*>(dx), g);
+  auto* k = narrow ? maxpool_bwd_kernel<T, uint32_t> : maxpool_bwd_kernel<T, int64_t>;
+  hipLaunchKernelGGL(k, dim3(grid_for(work)), dim3(256), 0, s, reinterpret_cast<const T*>(dy),
+                     reinterpret_cast<const uint8_t*>(idx), reinterpret_cast<T*>(dx), g);
   hip_check(hipGetLastError(), "maxpool_bwd launch");
+}
+
+void maxpool_fwd(int dev, hipStream_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t x,
+                 uintptr_t y, uintptr_t idx, bool f32) {
+  if (f32) maxpool_fwd_t<float>(dev, s, N, H, W, C, K, stride, pad, x, y, idx);
+  else maxpool_fwd_t<uint16_t>(dev, s, N, H, W, C, K, stride, pad, x, y, idx);
+}
+
+void maxpool_bwd(int dev, hipStream_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t dy,
+                 uintptr_t idx, uintptr_t dx, bool f32) {
+  if (f32) maxpool_bwd_t<float>(dev, s, N, H, W, C, K, stride, pad, dy, idx, dx);
+  else maxpool_bwd_t<uint16_t>(dev, s, N, H, W, C, K, stride, pad, dy, idx, dx);
 }
 
 }  // namespace mpit

@@ -60,8 +60,9 @@ class BNLink:
         self.dy_ptr = self.dy_ver = None
 
     def ready(self, x: torch.Tensor) -> bool:
-        """True when ``x`` (a consumer's input) is this layer's output shape, bf16."""
-        return (self.x is not None and self.mean is not None and x.dtype == torch.bfloat16
+        """True when ``x`` (a consumer's input) is this layer's output: same shape and dtype
+        (bf16 or fp32 — the consumer's epilogue reads the BN input in its own dtype)."""
+        return (self.x is not None and self.mean is not None and x.dtype == self.x.dtype
                 and self.x.shape == x.shape)
 
     def publish(self, part: torch.Tensor, npart: int, dy: torch.Tensor, part2: torch.Tensor = None):
@@ -106,7 +107,7 @@ class _BNActFn(torch.autograd.Function):
         bf16 = x.dtype == torch.bfloat16
         # ReLU: one mask bit per element replaces keeping / re-reading y in the backward
         mask = torch.empty(m.bn_mask_bytes(bf16, M, C), dtype=torch.uint8, device=x.device) if relu else None
-        ts = tstats if (tstats is not None and bf16 and tstats[1] == m.gemm_nt_tiles(M)) else None
+        ts = tstats if (tstats is not None and tstats[1] == m.gemm_nt_tiles(M)) else None
         if ts is not None:
             COUNTERS["fwd_tile_stats"] += 1
         m.bn_act_fwd(dev, stream, bf16, x.data_ptr(),
@@ -119,7 +120,7 @@ class _BNActFn(torch.autograd.Function):
                      stats=ts[0].data_ptr() if ts is not None else 0, nstat=ts[1] if ts is not None else 0)
         ctx.save_for_backward(x, mask, w, mean, rstd)
         ctx.link = link
-        if link is not None and bf16:
+        if link is not None:
             link.x, link.mask, link.mean = x, mask, mean
         ctx.relu = relu
         ctx.has_res = residual is not None
@@ -139,7 +140,7 @@ class _BNActFn(torch.autograd.Function):
         dx = torch.empty_like(x, memory_format=torch.channels_last)
         # residual gradient of act(bn(x) + res) = dy*mask: with a GradSlot consumer it is
         # handed over as (dy, mask) and never written
-        park = ctx.has_res and ctx.res_slot is not None and ctx.relu and mask is not None and dy.dtype == torch.bfloat16
+        park = ctx.has_res and ctx.res_slot is not None and ctx.relu and mask is not None
         dres = torch.empty_like(x, memory_format=torch.channels_last) if (ctx.has_res and not park) else None
         dgamma = torch.empty(C, dtype=torch.float32, device=x.device) if ctx.has_w else None
         dbeta = torch.empty(C, dtype=torch.float32, device=x.device) if ctx.has_b else None
@@ -184,8 +185,7 @@ def bn_act_eval(x, weight, bias, running_mean, running_var, eps, residual=None, 
 def _supported(x: torch.Tensor) -> bool:
     if not x.is_cuda or x.dim() != 4 or x.dtype not in (torch.bfloat16, torch.float32):
         return False
-    v = 8 if x.dtype == torch.bfloat16 else 4
-    return x.shape[1] % v == 0
+    return x.shape[1] % 8 == 0  # 8 channels per thread and per ReLU-mask byte, either dtype
 
 
 class BatchNormAct2d(nn.BatchNorm2d):
@@ -239,7 +239,7 @@ class BatchNormAct2d(nn.BatchNorm2d):
             return F.relu(y) if self.act else y
         if self.training or not self.track_running_stats:
             momentum, rm, rv = self._train_args()
-            link = BNLink() if (torch.is_grad_enabled() and x.dtype == torch.bfloat16) else None
+            link = BNLink() if torch.is_grad_enabled() else None
             y = _BNActFn.apply(x, self.weight, self.bias, rm, rv, residual, momentum, self.eps, self.act,
                                res_slot, tile_stats_of(x), link)
             if link is not None:
@@ -262,6 +262,7 @@ class _BNPairFn(torch.autograd.Function):
         M, C = _rows(x1)
         m = native()
         dev, stream = x1.device.index, torch.cuda.current_stream(x1.device).cuda_stream
+        bf16 = x1.dtype == torch.bfloat16
         f32 = dict(dtype=torch.float32, device=x1.device)
         outs = []
         for x, w, b, rm, rv, mom, eps, ts in ((x1, w1, b1, rm1, rv1, mom1, eps1, ts1),
@@ -273,16 +274,16 @@ class _BNPairFn(torch.autograd.Function):
             ts = ts if (ts is not None and ts[1] == m.gemm_nt_tiles(M)) else None
             if ts is not None:
                 COUNTERS["fwd_tile_stats"] += 1
-            m.bn_act_fwd(dev, stream, True, x.data_ptr(), 0, 0, M, C, wf.data_ptr() if wf is not None else 0,
+            m.bn_act_fwd(dev, stream, bf16, x.data_ptr(), 0, 0, M, C, wf.data_ptr() if wf is not None else 0,
                          bf.data_ptr() if bf is not None else 0, rm.data_ptr() if rm is not None else 0,
                          rv.data_ptr() if rv is not None else 0, mean.data_ptr(), rstd.data_ptr(), ws.data_ptr(),
                          float(mom), float(eps), False, 0, stats=ts[0].data_ptr() if ts is not None else 0,
                          nstat=ts[1] if ts is not None else 0)
             outs.append((wf, mean, rstd, ws))
         y = torch.empty_like(x1, memory_format=torch.channels_last)
-        mask = torch.empty(m.bn_mask_bytes(True, M, C), dtype=torch.uint8, device=x1.device)
+        mask = torch.empty(m.bn_mask_bytes(bf16, M, C), dtype=torch.uint8, device=x1.device)
         m.bn_pair_apply(dev, stream, x1.data_ptr(), outs[0][3].data_ptr(), x2.data_ptr(), outs[1][3].data_ptr(),
-                        y.data_ptr(), M, C, mask.data_ptr())
+                        y.data_ptr(), M, C, mask.data_ptr(), f32=not bf16)
         (wf1, mean1, rstd1, _), (wf2, mean2, rstd2, _) = outs
         ctx.save_for_backward(x1, x2, mask, wf1, mean1, rstd1, wf2, mean2, rstd2)
         ctx.has = (w1 is not None, b1 is not None, w2 is not None, b2 is not None)
@@ -308,7 +309,7 @@ class _BNPairFn(torch.autograd.Function):
             dg = torch.empty(C, **f32) if hw else None
             db = torch.empty(C, **f32) if hb else None
             ws = torch.empty(m.bn_workspace_floats(C), **f32)
-            m.bn_act_bwd(dev, stream, True, dy.data_ptr(), mask.data_ptr(), x.data_ptr(), 0, 0, M, C,
+            m.bn_act_bwd(dev, stream, x1.dtype == torch.bfloat16, dy.data_ptr(), mask.data_ptr(), x.data_ptr(), 0, 0, M, C,
                          wf.data_ptr() if wf is not None else 0, mean.data_ptr(), rstd.data_ptr(),
                          dg.data_ptr() if dg is not None else 0, db.data_ptr() if db is not None else 0, ws.data_ptr(),
                          True, part=p.data_ptr() if p is not None else 0, npart=npart if p is not None else 0)
@@ -317,7 +318,8 @@ class _BNPairFn(torch.autograd.Function):
         dx1 = torch.empty_like(x1, memory_format=torch.channels_last)
         dx2 = torch.empty_like(x2, memory_format=torch.channels_last)
         m.bn_pair_bwd_apply(dev, stream, dy.data_ptr(), mask.data_ptr(), x1.data_ptr(), wss[0].data_ptr(),
-                            dx1.data_ptr(), x2.data_ptr(), wss[1].data_ptr(), dx2.data_ptr(), M, C)
+                            dx1.data_ptr(), x2.data_ptr(), wss[1].data_ptr(), dx2.data_ptr(), M, C,
+                            f32=x1.dtype == torch.float32)
         (dg1, db1), (dg2, db2) = grads
         return (dx1, dg1, db1, None, None, dx2, dg2, db2, None, None, None, None, None, None, None, None, None)
 
@@ -326,7 +328,7 @@ def bn_pair(bn1: "BatchNormAct2d", x1: torch.Tensor, bn2: "BatchNormAct2d", x2: 
     """``relu(bn1(x1) + bn2(x2))`` (bn1 with ReLU, bn2 without): one fused op on the GPU
     training path (:class:`_BNPairFn`), the two modules otherwise."""
     ok = (bn1.act and not bn2.act and bn1.training and bn2.training and bn1.track_running_stats
-          and bn2.track_running_stats and _supported(x1) and x1.dtype == torch.bfloat16 and x2.shape == x1.shape
+          and bn2.track_running_stats and _supported(x1) and x2.shape == x1.shape
           and x2.is_cuda and x2.dtype in (torch.bfloat16, torch.float32))
     if not ok:
         return bn1(x1, bn2(x2))

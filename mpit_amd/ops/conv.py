@@ -1,5 +1,14 @@
 """Convolutions on the hand-written MFMA GEMMs (csrc/kernels/gemm.hip).
 
+Two compute dtypes, chosen per call from the input and the autocast state (:func:`mfma_dtype`):
+
+* bf16 (bf16 autocast / bf16 tensors): ``v_mfma_f32_32x32x16_bf16``, fp32 accumulate, bf16
+  activations; the fp32 master weights are cast once per step (:class:`WeightCastPlan`);
+* fp32 (fp32 tensors, no autocast — the reference's training precision,
+  asyncsgd/glaunch.lua:11, BiCNN/plaunch.lua:200): ``v_mfma_f32_32x32x2_f32``, exact fp32
+  products and accumulation, fp32 activations; the forward reads the fp32 master weight
+  itself, the backward-data its fp32 (tap-flipped) transpose.
+
 A stride-1 1x1 convolution over a channels_last activation is a GEMM over its [N*H*W, C]
 row-major view. Measured on MI355X (benchmarks/conv_vs_gemm.py, ResNet-50 at batch 256)
 MIOpen runs these at 100-450 TFLOP/s, and every backward-weight call also costs a zero
@@ -99,6 +108,19 @@ def _cl(x: torch.Tensor) -> torch.Tensor:
     return x if x.is_contiguous(memory_format=torch.channels_last) else x.contiguous(memory_format=torch.channels_last)
 
 
+def mfma_dtype(x: torch.Tensor):
+    """Compute dtype of the MFMA path for input ``x``: bf16 under bf16 autocast or for bf16
+    tensors, fp32 for fp32 tensors outside autocast, else None (no MFMA path)."""
+    if torch.is_autocast_enabled("cuda"):
+        return torch.bfloat16 if torch.get_autocast_dtype("cuda") == torch.bfloat16 else None
+    return x.dtype if x.dtype in (torch.bfloat16, torch.float32) else None
+
+
+def _to(x: torch.Tensor, dt) -> torch.Tensor:
+    x = _cl(x)
+    return x if x.dtype == dt else x.to(dt)
+
+
 def tile_stats_to_sums(part: torch.Tensor, M: int, N: int) -> torch.Tensor:
     """Per-128-row-tile (mean, M2) partials ([tiles][2][N]) -> [2, N] (sum, sum of squares)."""
     p = part.view(-1, 2, N).double()
@@ -108,29 +130,29 @@ def tile_stats_to_sums(part: torch.Tensor, M: int, N: int) -> torch.Tensor:
 
 
 def gemm_nt(a: torch.Tensor, b: torch.Tensor, stats: bool = False):
-    """``a[M,K] . b[N,K]^T`` in bf16 (fp32 accumulate). With ``stats`` also returns the
-    per-column ``[sum, sum of squares]`` of the result as a [2, N] fp32 tensor (from the
-    epilogue's per-tile (mean, M2) partials)."""
-    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
-        raise TypeError("gemm_nt takes bf16 operands")
+    """``a[M,K] . b[N,K]^T`` in bf16 or fp32 (fp32 accumulate; result in the operands'
+    dtype). With ``stats`` also returns the per-column ``[sum, sum of squares]`` of the
+    result as a [2, N] fp32 tensor (from the epilogue's per-tile (mean, M2) partials)."""
+    if a.dtype not in (torch.bfloat16, torch.float32) or b.dtype != a.dtype:
+        raise TypeError("gemm_nt takes two bf16 or two fp32 operands")
     if a.dim() != 2 or b.dim() != 2 or a.shape[1] != b.shape[1] or a.stride(1) != 1 or b.stride(1) != 1:
         raise ValueError("gemm_nt: a[M,K], b[N,K] with unit column stride")
     M, K = a.shape
     N = b.shape[0]
-    c = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    c = torch.empty((M, N), dtype=a.dtype, device=a.device)
     m = native()
     st = torch.empty(m.gemm_nt_stats_floats(M, N), dtype=torch.float32, device=a.device) if stats else None
     m.gemm_nt(a.device.index, _stream(a), M, N, K, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(),
-              N, st.data_ptr() if st is not None else 0)
+              N, st.data_ptr() if st is not None else 0, f32=a.dtype == torch.float32)
     if stats:
         return c, tile_stats_to_sums(st, M, N)
     return c
 
 
 def gemm_tn(y: torch.Tensor, x: torch.Tensor, out: torch.Tensor = None, beta: float = 0.0) -> torch.Tensor:
-    """``out[N,K] = beta*out + y[M,N]^T . x[M,K]`` in fp32 from bf16 operands."""
-    if y.dtype != torch.bfloat16 or x.dtype != torch.bfloat16:
-        raise TypeError("gemm_tn takes bf16 operands")
+    """``out[N,K] = beta*out + y[M,N]^T . x[M,K]`` in fp32 from bf16 or fp32 operands."""
+    if y.dtype not in (torch.bfloat16, torch.float32) or x.dtype != y.dtype:
+        raise TypeError("gemm_tn takes two bf16 or two fp32 operands")
     M, N = y.shape
     K = x.shape[1]
     if x.shape[0] != M or y.stride(1) != 1 or x.stride(1) != 1:
@@ -144,19 +166,22 @@ def gemm_tn(y: torch.Tensor, x: torch.Tensor, out: torch.Tensor = None, beta: fl
     nws = m.gemm_tn_ws_floats(dev, M, N, K) or (N * K if beta != 0.0 else 0)
     ws = torch.empty(nws, dtype=torch.float32, device=y.device) if nws else None
     m.gemm_tn(dev, _stream(y), M, N, K, y.data_ptr(), y.stride(0), x.data_ptr(), x.stride(0), out.data_ptr(),
-              ws.data_ptr() if ws is not None else 0, float(beta))
+              ws.data_ptr() if ws is not None else 0, float(beta), f32=y.dtype == torch.float32)
     return out
 
 
-def cast_transpose(w: torch.Tensor):
-    """fp32 ``w[R, C]`` -> (bf16 copy [R, C], bf16 transpose [C, R]) in one launch."""
+def cast_transpose(w: torch.Tensor, dtype=torch.bfloat16):
+    """fp32 ``w[R, C]`` -> (copy [R, C], transpose [C, R]) in ``dtype``, one launch. For fp32
+    the copy is ``w`` itself (2-D view) and only the transpose is written."""
     w2 = w.reshape(w.shape[0], -1)
     if w2.dtype != torch.float32 or not w2.is_contiguous():
         w2 = w2.float().contiguous()
     R, C = w2.shape
-    wb = torch.empty((R, C), dtype=torch.bfloat16, device=w.device)
-    wt = torch.empty((C, R), dtype=torch.bfloat16, device=w.device)
-    native().cast_transpose(w.device.index, _stream(w), w2.data_ptr(), R, C, wb.data_ptr(), wt.data_ptr())
+    f32 = dtype == torch.float32
+    wb = w2 if f32 else torch.empty((R, C), dtype=torch.bfloat16, device=w.device)
+    wt = torch.empty((C, R), dtype=dtype, device=w.device)
+    native().cast_transpose(w.device.index, _stream(w), w2.data_ptr(), R, C, 0 if f32 else wb.data_ptr(),
+                            wt.data_ptr(), f32=f32)
     return wb, wt
 
 
@@ -174,11 +199,12 @@ def _red_args(link, c: int, ntiles: int, device):
     return kw, part, part2
 
 
-def _link_of(x: torch.Tensor, pair_ok: bool = True):
-    """The BNLink of the BN layer that produced ``x``; a bn_pair link only for consumers
-    whose backward-data GEMM can run the paired reduction (``pair_ok``: the 1x1 GEMMs)."""
+def _link_of(x: torch.Tensor, dt, pair_ok: bool = True):
+    """The BNLink of the BN layer that produced ``x`` when the consumer computes in ``dt`` (the
+    BN's dtype); a bn_pair link only for consumers whose backward-data GEMM can run the
+    paired reduction (``pair_ok``: the 1x1 GEMMs)."""
     link = getattr(x, "_mpit_bnlink", None)
-    if link is None or not link.ready(x) or (link.x2 is not None and not pair_ok):
+    if link is None or not link.ready(x) or x.dtype != dt or (link.x2 is not None and not pair_ok):
         return None
     return link
 
@@ -253,22 +279,21 @@ def park_grad(x: torch.Tensor, slot: GradSlot) -> torch.Tensor:
 
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, slot=None, hold=None, link=None, wcast=None):
-        x = _cl(x)
-        if x.dtype != torch.bfloat16:
-            x = x.to(torch.bfloat16)
+    def forward(ctx, x, weight, slot=None, hold=None, link=None, wcast=None, dt=torch.bfloat16):
+        x = _to(x, dt)
+        f32 = dt == torch.float32
         n, ci, h, w = x.shape
         co = weight.shape[0]
         M = n * h * w
-        wb, wt = wcast if wcast is not None else cast_transpose(weight)
-        y = torch.empty((n, co, h, w), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+        wb, wt = wcast if wcast is not None else cast_transpose(weight, dt)
+        y = torch.empty((n, co, h, w), dtype=dt, device=x.device, memory_format=torch.channels_last)
         m = native()
         st = None
         if hold is not None:  # batch-norm statistics of y from the accumulators
             st, nt = _tile_stats(co, M, x.device)
             hold.append((st, nt))
         m.gemm_nt(x.device.index, _stream(x), M, co, ci, x.data_ptr(), ci, wb.data_ptr(), ci, y.data_ptr(), co,
-                  st.data_ptr() if st is not None else 0)
+                  st.data_ptr() if st is not None else 0, f32=f32)
         ctx.save_for_backward(x, wt)
         ctx.wshape = weight.shape
         ctx.slot = slot
@@ -278,9 +303,9 @@ class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, wt = ctx.saved_tensors
-        dy = _cl(dy)
-        if dy.dtype != torch.bfloat16:
-            dy = dy.to(torch.bfloat16)
+        dt = x.dtype
+        f32 = dt == torch.float32
+        dy = _to(dy, dt)
         n, ci, h, w = x.shape
         co = dy.shape[1]
         M = n * h * w
@@ -296,15 +321,13 @@ class _Conv1x1Fn(torch.autograd.Function):
                 nt = m.gemm_nt_tiles(M)
                 kw, part, part2 = _red_args(ctx.link, ci, nt, x.device)
             if extra is not None:  # gradient parked by the block (GradSlot): added in the epilogue
-                extra = _cl(extra)
-                if extra.dtype != torch.bfloat16:
-                    extra = extra.to(torch.bfloat16)
+                extra = _to(extra, dt)
                 if extra.shape != x.shape:
                     raise RuntimeError("GradSlot gradient does not match the convolution input")
                 m.gemm_nt(dev, s, M, ci, co, dy.data_ptr(), co, wt.data_ptr(), co, dx.data_ptr(), ci, 0,
-                          extra.data_ptr(), emask.data_ptr() if emask is not None else 0, **kw)
+                          extra.data_ptr(), emask.data_ptr() if emask is not None else 0, f32=f32, **kw)
             else:
-                m.gemm_nt(dev, s, M, ci, co, dy.data_ptr(), co, wt.data_ptr(), co, dx.data_ptr(), ci, 0, **kw)
+                m.gemm_nt(dev, s, M, ci, co, dy.data_ptr(), co, wt.data_ptr(), co, dx.data_ptr(), ci, 0, f32=f32, **kw)
             if part is not None:
                 ctx.link.publish(part, nt, dx, part2)
         if ctx.needs_input_grad[1]:
@@ -312,17 +335,13 @@ class _Conv1x1Fn(torch.autograd.Function):
             nws = m.gemm_tn_ws_floats(dev, M, co, ci)
             ws = torch.empty(nws, dtype=torch.float32, device=x.device) if nws else None
             m.gemm_tn(dev, side.cuda_stream if side is not None else s, M, co, ci, dy.data_ptr(), co, x.data_ptr(),
-                      ci, dw.data_ptr(), ws.data_ptr() if ws is not None else 0, 0.0)
+                      ci, dw.data_ptr(), ws.data_ptr() if ws is not None else 0, 0.0, f32=f32)
             _used_on(side, dy, x, dw, ws)
-        return dx, dw, None, None, None, None
+        return dx, dw, None, None, None, None, None
 
 
 def conv1x1_supported(x: torch.Tensor, weight: torch.Tensor) -> bool:
-    if not x.is_cuda or x.dim() != 4:
-        return False
-    bf16 = x.dtype == torch.bfloat16 or (torch.is_autocast_enabled("cuda")
-                                         and torch.get_autocast_dtype("cuda") == torch.bfloat16)
-    if not bf16:
+    if not x.is_cuda or x.dim() != 4 or mfma_dtype(x) is None:
         return False
     co, ci = weight.shape[0], weight.shape[1]
     return ci % 64 == 0 and co % 64 == 0 and x.shape[1] == ci
@@ -331,7 +350,7 @@ def conv1x1_supported(x: torch.Tensor, weight: torch.Tensor) -> bool:
 def conv1x1(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     """Stride-1, unpadded, bias-free 1x1 convolution (MFMA GEMM path when supported)."""
     if conv1x1_supported(x, weight):
-        return _Conv1x1Fn.apply(x, weight, None, None, None, None)
+        return _Conv1x1Fn.apply(x, weight, None, None, None, None, mfma_dtype(x))
     return F.conv2d(x, weight)
 
 
@@ -350,8 +369,9 @@ class Conv1x1(nn.Conv2d):
     def forward(self, x: torch.Tensor, slot: "GradSlot" = None) -> torch.Tensor:
         if self.fused(x):
             hold = [] if (self.emit_stats and self.training) else None
-            y = _Conv1x1Fn.apply(x, self.weight, slot, hold, _link_of(x) if torch.is_grad_enabled() else None,
-                                 WeightCastPlan.cached(self))
+            dt = mfma_dtype(x)
+            y = _Conv1x1Fn.apply(x, self.weight, slot, hold, _link_of(x, dt) if torch.is_grad_enabled() else None,
+                                 WeightCastPlan.cached(self, dt), dt)
             return _attach_stats(y, hold)
         if slot is not None:
             raise RuntimeError("GradSlot needs the MFMA path (see Conv1x1.fused)")
@@ -366,14 +386,22 @@ def _weight_nhwc(weight: torch.Tensor) -> torch.Tensor:
     return w if w.is_contiguous(memory_format=torch.channels_last) else w.contiguous(memory_format=torch.channels_last)
 
 
-def conv_weights(weight: torch.Tensor, dgrad: bool):
-    """(bf16 [Co][R][S][C], bf16 tap-flipped transpose [C][R][S][Co] or None), one launch."""
+def _as_rsc(w: torch.Tensor) -> torch.Tensor:
+    """[Co, C, R, S] channels_last fp32 weight as its [Co, R, S, C] memory view (no copy)."""
+    return w.permute(0, 2, 3, 1)
+
+
+def conv_weights(weight: torch.Tensor, dgrad: bool, dtype=torch.bfloat16):
+    """(forward weight [Co][R][S][C], tap-flipped transpose [C][R][S][Co] or None) in
+    ``dtype``, one launch. fp32: the forward weight is the master itself."""
     co, c, r, s = weight.shape
     w = _weight_nhwc(weight)
-    wb = torch.empty((co, r, s, c), dtype=torch.bfloat16, device=w.device)
-    wt = torch.empty((c, r, s, co), dtype=torch.bfloat16, device=w.device) if dgrad else None
-    native().cast_transpose(w.device.index, _stream(w), w.data_ptr(), co, c, wb.data_ptr(),
-                            wt.data_ptr() if wt is not None else 0, r * s)
+    f32 = dtype == torch.float32
+    wb = _as_rsc(w) if f32 else torch.empty((co, r, s, c), dtype=torch.bfloat16, device=w.device)
+    wt = torch.empty((c, r, s, co), dtype=dtype, device=w.device) if dgrad else None
+    if wt is not None or not f32:
+        native().cast_transpose(w.device.index, _stream(w), w.data_ptr(), co, c, 0 if f32 else wb.data_ptr(),
+                                wt.data_ptr() if wt is not None else 0, r * s, f32=f32)
     return wb, wt
 
 
@@ -390,6 +418,7 @@ def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None):
     nb, c, h, w = x.shape
     co, r, s, _ = wb.shape
     ho, wo = dz.shape[2], dz.shape[3]
+    f32 = x.dtype == torch.float32
     m = native()
     dev, st = x.device.index, _stream(x)
     dx = dw = None
@@ -402,8 +431,8 @@ def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None):
             if link is not None:
                 nt = m.gemm_nt_tiles(nb * h * w)
                 kw, part, _ = _red_args(link, c, nt, x.device)
-            m.conv_fwd(dev, st, nb, ho, wo, co, c, r, s, 1, r - 1 - pad, dz.data_ptr(), wt.data_ptr(), dx.data_ptr(),
-                       **kw)
+            m.conv_fwd(dev, st, nb, ho, wo, co, c, r, s, 1, r - 1 - pad, dz.data_ptr(), wt.data_ptr(),
+                       dx.data_ptr(), f32=f32, **kw)
             if part is not None:
                 link.publish(part, nt, dx)
         elif wt is not None:
@@ -415,11 +444,11 @@ def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None):
                 nt = m.conv_dgrad_strided_tiles(nb, h, w, c, co, r, s, stride, pad)
                 kw, part, _ = _red_args(link, c, nt, x.device)
             m.conv_dgrad_strided(dev, st, nb, h, w, c, co, r, s, stride, pad, dz.data_ptr(), wt.data_ptr(),
-                                 dx.data_ptr(), **kw)
+                                 dx.data_ptr(), f32=f32, **kw)
             if part is not None:
                 link.publish(part, nt, dx)
         else:  # MIOpen's NHWC backward-data
-            wv = wb.permute(0, 3, 1, 2)  # [Co, C, R, S] view with channels_last strides
+            wv = wb.permute(0, 3, 1, 2).to(x.dtype)  # [Co, C, R, S] view with channels_last strides
             dx = torch.ops.aten.convolution_backward(dz, x, wv, None, [stride, stride], [pad, pad], [1, 1], False,
                                                      [0, 0], 1, [True, False, False])[0]
     if ctx.needs_input_grad[1]:
@@ -427,29 +456,30 @@ def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None):
         nws = m.conv_wgrad_ws_floats(dev, nb, h, w, c, co, r, s, stride, pad)
         ws = torch.empty(nws, dtype=torch.float32, device=x.device) if nws else None
         m.conv_wgrad(dev, side.cuda_stream if side is not None else st, nb, h, w, c, co, r, s, stride, pad,
-                     dz.data_ptr(), x.data_ptr(), dw.data_ptr(), ws.data_ptr() if ws is not None else 0, 0.0)
+                     dz.data_ptr(), x.data_ptr(), dw.data_ptr(), ws.data_ptr() if ws is not None else 0, 0.0, f32=f32)
         _used_on(side, dz, x, dw, ws)
     return dx, dw
 
 
 def _bf16_cl(t: torch.Tensor) -> torch.Tensor:
-    t = _cl(t)
-    return t if t.dtype == torch.bfloat16 else t.to(torch.bfloat16)
+    return _to(t, torch.bfloat16)
 
 
 def strided_dgrad_supported(c: int, co: int, stride: int) -> bool:
     return 2 <= stride <= 4 and c % 64 == 0 and co % 32 == 0
 
 
-def strided_dgrad_weights(weight: torch.Tensor, stride: int, pad: int):
-    """(bf16 [Co][R][S][C], packed parity-class backward-data weights), one launch."""
+def strided_dgrad_weights(weight: torch.Tensor, stride: int, pad: int, dtype=torch.bfloat16):
+    """(forward weight [Co][R][S][C], packed parity-class backward-data weights) in ``dtype``,
+    one launch (fp32: the forward weight is the master itself)."""
     co, c, r, s = weight.shape
     w = _weight_nhwc(weight)
     m = native()
-    wb = torch.empty((co, r, s, c), dtype=torch.bfloat16, device=w.device)
-    wc = torch.empty(m.conv_dgrad_strided_wfloats(c, co, r, s, stride, pad), dtype=torch.bfloat16, device=w.device)
-    m.conv_dgrad_strided_weights(w.device.index, _stream(w), w.data_ptr(), co, c, r, s, stride, pad, wb.data_ptr(),
-                                 wc.data_ptr())
+    f32 = dtype == torch.float32
+    wb = _as_rsc(w) if f32 else torch.empty((co, r, s, c), dtype=torch.bfloat16, device=w.device)
+    wc = torch.empty(m.conv_dgrad_strided_wfloats(c, co, r, s, stride, pad), dtype=dtype, device=w.device)
+    m.conv_dgrad_strided_weights(w.device.index, _stream(w), w.data_ptr(), co, c, r, s, stride, pad,
+                                 0 if f32 else wb.data_ptr(), wc.data_ptr(), f32=f32)
     return wb, wc
 
 
@@ -459,8 +489,9 @@ class _ConvFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, stride: int, pad: int, bias=None, relu: bool = False, hold=None, link=None,
-                wcast=None):
-        x = _bf16_cl(x)
+                wcast=None, dt=torch.bfloat16):
+        x = _to(x, dt)
+        f32 = dt == torch.float32
         nb, c, h, w = x.shape
         co, _, r, s = weight.shape
         ho, wo = (h + 2 * pad - r) // stride + 1, (w + 2 * pad - s) // stride + 1
@@ -468,10 +499,10 @@ class _ConvFn(torch.autograd.Function):
         if wcast is not None:  # cast for this step by the model's WeightCastPlan
             wb, wt = wcast
         elif need_dx and stride > 1 and strided_dgrad_supported(c, co, stride):
-            wb, wt = strided_dgrad_weights(weight, stride, pad)
+            wb, wt = strided_dgrad_weights(weight, stride, pad, dt)
         else:
-            wb, wt = conv_weights(weight, dgrad=need_dx and stride == 1)
-        y = torch.empty((nb, co, ho, wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+            wb, wt = conv_weights(weight, need_dx and stride == 1, dt)
+        y = torch.empty((nb, co, ho, wo), dtype=dt, device=x.device, memory_format=torch.channels_last)
         b = None
         if bias is not None:
             b = bias if (bias.dtype == torch.float32 and bias.is_contiguous()) else bias.float().contiguous()
@@ -481,7 +512,7 @@ class _ConvFn(torch.autograd.Function):
             hold.append((st, nt))
         native().conv_fwd(x.device.index, _stream(x), nb, h, w, c, co, r, s, stride, pad, x.data_ptr(), wb.data_ptr(),
                           y.data_ptr(), stats=st.data_ptr() if st is not None else 0,
-                          bias=b.data_ptr() if b is not None else 0, relu=bool(relu))
+                          bias=b.data_ptr() if b is not None else 0, relu=bool(relu), f32=f32)
         ctx.save_for_backward(x, wb, wt, y if relu else None)
         ctx.geo = (stride, pad, bias is not None, bool(relu))
         ctx.link = link
@@ -491,7 +522,8 @@ class _ConvFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, wb, wt, y = ctx.saved_tensors
         stride, pad, has_bias, relu = ctx.geo
-        dy = _bf16_cl(dy)
+        dt = x.dtype
+        dy = _to(dy, dt)
         db = None
         if relu:
             nb_, co, ho, wo = dy.shape
@@ -502,24 +534,23 @@ class _ConvFn(torch.autograd.Function):
             db = torch.empty(co, dtype=torch.float32, device=dy.device) if want_db else None
             ws = torch.empty(m.relu_bias_bwd_ws_floats(co), dtype=torch.float32, device=dy.device) if want_db else None
             m.relu_bias_bwd(dy.device.index, _stream(dy), M, co, dy.data_ptr(), y.data_ptr(), dz.data_ptr(),
-                            db.data_ptr() if db is not None else 0, ws.data_ptr() if ws is not None else 0)
+                            db.data_ptr() if db is not None else 0, ws.data_ptr() if ws is not None else 0,
+                            f32=dt == torch.float32)
         else:
             dz = dy
             if has_bias and ctx.needs_input_grad[4]:
                 db = dy.float().sum(dim=(0, 2, 3))
         dx, dw = _conv_backward(ctx, x, wb, wt, dz, stride, pad, ctx.link)
-        return dx, dw, None, None, db, None, None, None, None
+        return dx, dw, None, None, db, None, None, None, None, None
 
 
 def conv_supported(x: torch.Tensor, weight: torch.Tensor) -> bool:
-    """The MFMA implicit-GEMM path takes bf16 (autocast) NHWC-able inputs with channel
-    counts that are multiples of 64 (wgrad tiles are 64 wide)."""
-    if not x.is_cuda or x.dim() != 4 or weight.dim() != 4:
+    """The MFMA implicit-GEMM path takes bf16 (autocast) or fp32 NHWC-able inputs with
+    channel counts that are multiples of 64 (wgrad tiles are 64 wide)."""
+    if not x.is_cuda or x.dim() != 4 or weight.dim() != 4 or mfma_dtype(x) is None:
         return False
-    bf16 = x.dtype == torch.bfloat16 or (torch.is_autocast_enabled("cuda")
-                                         and torch.get_autocast_dtype("cuda") == torch.bfloat16)
     co, ci = weight.shape[0], weight.shape[1]
-    return bf16 and ci % 64 == 0 and co % 64 == 0 and x.shape[1] == ci
+    return ci % 64 == 0 and co % 64 == 0 and x.shape[1] == ci
 
 
 class ConvAct2d(nn.Conv2d):
@@ -538,7 +569,7 @@ class ConvAct2d(nn.Conv2d):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.fused(x):
             return _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0], self.bias, self.act, None, None,
-                                 None)
+                                 None, mfma_dtype(x))
         y = super().forward(x)
         return F.relu(y) if self.act else y
 
@@ -558,32 +589,37 @@ class ConvNHWC(nn.Conv2d):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.fused(x):
             hold = [] if (self.emit_stats and self.training) else None
+            dt = mfma_dtype(x)
             y = _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0], None, False, hold,
-                              _link_of(x, pair_ok=False) if torch.is_grad_enabled() else None,
-                              WeightCastPlan.cached(self))
+                              _link_of(x, dt, pair_ok=False) if torch.is_grad_enabled() else None,
+                              WeightCastPlan.cached(self, dt), dt)
             return _attach_stats(y, hold)
         return super().forward(x)
 
 
 class WeightCastPlan:
-    """bf16 copies of every MFMA convolution weight of a model, made in ONE launch per step
-    (csrc/kernels/gemm.hip ``cast_batch_kernel``) instead of one cast kernel per conv.
+    """The per-step weight operands of every MFMA convolution of a model, made in ONE launch
+    per step (csrc/kernels/gemm.hip ``cast_batch_kernel``) instead of one kernel per conv.
 
-    ``run()`` casts the current fp32 master weights into persistent bf16 buffers (plain +
-    tap-flipped transposes, or the strided parity-class weights), exactly what each
-    convolution's forward would otherwise make; until ``invalidate()`` the convolutions
-    use them. The trainer brackets its forward/backward with the two calls, so a weight
-    update in between (PS pull, optimizer) is never missed; forwards outside that window
-    cast per call as before."""
+    bf16 plan (``dtype=torch.bfloat16``): ``run()`` casts the current fp32 master weights
+    into persistent bf16 buffers (plain + tap-flipped transposes, or the strided parity-class
+    weights). fp32 plan: the forward reads the master weight itself and ``run()`` writes only
+    the fp32 transposes the backward-data GEMMs read (a snapshot taken before the forward, so
+    a shard pulled into the model during the backward does not change this step's gradient).
+    Until ``invalidate()`` the convolutions use them. The trainer brackets its
+    forward/backward with the two calls, so a weight update in between (PS pull, optimizer)
+    is never missed; forwards outside that window cast per call as before."""
 
-    def __init__(self, model: nn.Module):
+    def __init__(self, model: nn.Module, dtype=torch.bfloat16):
         self.model = model
+        self.dtype = dtype
         self.valid = False
         self._build()
 
     def _build(self):
         specs, self.mods = [], []
         m = native()
+        f32 = self.dtype == torch.float32
         for mod in self.model.modules():
             kind = None
             if isinstance(mod, Conv1x1) and mod.stride == (1, 1):
@@ -598,18 +634,21 @@ class WeightCastPlan:
             if not w.is_cuda or w.dtype != torch.float32 or not w.is_contiguous(memory_format=torch.channels_last):
                 continue
             co, c, r, sw = w.shape
-            wb = torch.empty((co, r, sw, c), dtype=torch.bfloat16, device=w.device)
+            wb = _as_rsc(w) if f32 else torch.empty((co, r, sw, c), dtype=torch.bfloat16, device=w.device)
             if kind == 0:
-                wt = torch.empty((c, r, sw, co), dtype=torch.bfloat16, device=w.device)
+                wt = torch.empty((c, r, sw, co), dtype=self.dtype, device=w.device)
             elif kind == 1:
                 wt = torch.empty(m.conv_dgrad_strided_wfloats(c, co, r, sw, mod.stride[0], mod.padding[0]),
-                                 dtype=torch.bfloat16, device=w.device)
+                                 dtype=self.dtype, device=w.device)
             else:
                 wt = None
             if isinstance(mod, Conv1x1):  # the 1x1 path takes 2-D [co, ci] / [ci, co] views
-                wb, wt = wb.view(co, c), wt.view(c, co)
-            specs.append([kind, w.data_ptr(), wb.data_ptr(), wt.data_ptr() if wt is not None else 0, co, c, r, sw,
-                          mod.stride[0], mod.padding[0]])
+                wb, wt = wb.reshape(co, c), wt.view(c, co)
+            if f32 and wt is None:
+                self.mods.append((mod, w.data_ptr(), (wb, wt)))  # nothing to write
+                continue
+            specs.append([kind | (256 if f32 else 0), w.data_ptr(), 0 if f32 else wb.data_ptr(),
+                          wt.data_ptr() if wt is not None else 0, co, c, r, sw, mod.stride[0], mod.padding[0]])
             self.mods.append((mod, w.data_ptr(), (wb, wt)))
         self.njobs = len(specs)
         self.table = None
@@ -633,27 +672,27 @@ class WeightCastPlan:
         self.valid = False
 
     @staticmethod
-    def cached(mod):
-        """The (wb, wt) cast for ``mod`` by a valid plan, else None."""
+    def cached(mod, dtype=torch.bfloat16):
+        """The (wb, wt) operands for ``mod`` by a valid plan of ``dtype``, else None."""
         c = getattr(mod, "_mpit_wcast", None)
-        if c is None or not c[0].valid:
+        if c is None or not c[0].valid or c[0].dtype != dtype:
             return None
         return c[1]
 
 
 # ------------------------------------------------------------------ the 7x7 stem
 
-def _stem_pack_input(x: torch.Tensor, pad: int, hp: int, wp: int) -> torch.Tensor:
-    """[N, 3, H, W] -> zero-padded NHWC4 bf16 [N, hp, wp, 4] (one pad kernel)."""
-    v = _bf16_cl(x).permute(0, 2, 3, 1)  # NHWC view of the channels_last tensor
+def _stem_pack_input(x: torch.Tensor, pad: int, hp: int, wp: int, dt=torch.bfloat16) -> torch.Tensor:
+    """[N, 3, H, W] -> zero-padded NHWC4 [N, hp, wp, 4] in ``dt`` (one pad kernel)."""
+    v = _to(x, dt).permute(0, 2, 3, 1)  # NHWC view of the channels_last tensor
     n, h, w, c = v.shape
     return F.pad(v, (0, 4 - c, pad, wp - w - pad, pad, hp - h - pad))
 
 
-def _stem_pack_weight(weight: torch.Tensor) -> torch.Tensor:
-    """[Co, C<=4, R<=8, S<=8] -> bf16 [Co, 8, 8, 4], zero-extended."""
+def _stem_pack_weight(weight: torch.Tensor, dt=torch.bfloat16) -> torch.Tensor:
+    """[Co, C<=4, R<=8, S<=8] -> [Co, 8, 8, 4] in ``dt``, zero-extended."""
     co, c, r, s = weight.shape
-    wp = torch.zeros((co, 8, 8, 4), dtype=torch.bfloat16, device=weight.device)
+    wp = torch.zeros((co, 8, 8, 4), dtype=dt, device=weight.device)
     wp[:, :r, :s, :c] = weight.permute(0, 2, 3, 1)
     return wp
 
@@ -666,20 +705,21 @@ class _StemConvFn(torch.autograd.Function):
     of its output; backward computes the weight gradient only (the image needs none)."""
 
     @staticmethod
-    def forward(ctx, x, weight, stride: int, pad: int, hold=None):
+    def forward(ctx, x, weight, stride: int, pad: int, hold=None, dt=torch.bfloat16):
         nb, _, h, w = x.shape
         co, _, r, s = weight.shape
+        f32 = dt == torch.float32
         ho, wo = (h + 2 * pad - r) // stride + 1, (w + 2 * pad - s) // stride + 1
         hp, wp = max(h + 2 * pad, (ho - 1) * stride + 8), max(w + 2 * pad, (wo - 1) * stride + 8)
-        xp = _stem_pack_input(x, pad, hp, wp)
-        wb = _stem_pack_weight(weight)
-        y = torch.empty((nb, co, ho, wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+        xp = _stem_pack_input(x, pad, hp, wp, dt)
+        wb = _stem_pack_weight(weight, dt)
+        y = torch.empty((nb, co, ho, wo), dtype=dt, device=x.device, memory_format=torch.channels_last)
         st = None
         if hold is not None:
             st, nt = _tile_stats(co, nb * ho * wo, x.device)
             hold.append((st, nt))
         native().conv_stem_fwd(x.device.index, _stream(x), nb, hp, wp, co, ho, wo, stride, xp.data_ptr(),
-                               wb.data_ptr(), y.data_ptr(), st.data_ptr() if st is not None else 0)
+                               wb.data_ptr(), y.data_ptr(), st.data_ptr() if st is not None else 0, f32=f32)
         ctx.save_for_backward(xp)
         ctx.geo = (nb, hp, wp, co, ho, wo, stride, tuple(weight.shape))
         return y
@@ -690,17 +730,18 @@ class _StemConvFn(torch.autograd.Function):
         nb, hp, wp, co, ho, wo, stride, wshape = ctx.geo
         dw = None
         if ctx.needs_input_grad[1]:
-            dy = _bf16_cl(dy)
+            dt = xp.dtype
+            dy = _to(dy, dt)
             m = native()
             dev = xp.device.index
             dwp = torch.empty((co, 8, 8, 4), dtype=torch.float32, device=xp.device)
             nws = m.conv_stem_wgrad_ws_floats(dev, nb, ho, wo, co)
             ws = torch.empty(nws, dtype=torch.float32, device=xp.device) if nws else None
             m.conv_stem_wgrad(dev, _stream(xp), nb, hp, wp, co, ho, wo, stride, dy.data_ptr(), xp.data_ptr(),
-                              dwp.data_ptr(), ws.data_ptr() if ws is not None else 0)
+                              dwp.data_ptr(), ws.data_ptr() if ws is not None else 0, f32=dt == torch.float32)
             _, c, r, s = wshape
             dw = dwp[:, :r, :s, :c].permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
-        return None, dw, None, None, None
+        return None, dw, None, None, None, None
 
 
 class StemConv(nn.Conv2d):
@@ -714,16 +755,14 @@ class StemConv(nn.Conv2d):
 
     def fused(self, x: torch.Tensor) -> bool:
         co, c, r, s = self.weight.shape
-        bf16 = x.dtype == torch.bfloat16 or (torch.is_autocast_enabled("cuda")
-                                             and torch.get_autocast_dtype("cuda") == torch.bfloat16)
-        return (x.is_cuda and bf16 and x.dim() == 4 and not x.requires_grad and c <= 4 and r <= 8 and s <= 8
-                and co % 64 == 0 and self.dilation == (1, 1) and self.groups == 1
+        return (x.is_cuda and mfma_dtype(x) is not None and x.dim() == 4 and not x.requires_grad and c <= 4
+                and r <= 8 and s <= 8 and co % 64 == 0 and self.dilation == (1, 1) and self.groups == 1
                 and self.stride[0] == self.stride[1] and self.padding[0] == self.padding[1]
                 and os.environ.get("MPIT_MFMA_STEM", "1") != "0")
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.fused(x):
             hold = [] if (self.emit_stats and self.training) else None
-            y = _StemConvFn.apply(x, self.weight, self.stride[0], self.padding[0], hold)
+            y = _StemConvFn.apply(x, self.weight, self.stride[0], self.padding[0], hold, mfma_dtype(x))
             return _attach_stats(y, hold)
         return super().forward(x)

@@ -3,7 +3,7 @@
 The forward keeps a one-byte argmax per output element; the backward gathers, for each
 input pixel, the gradients of the windows that selected it (dx written once, no atomics,
 no zero fill). :class:`MaxPool2dNHWC` is a drop-in ``nn.MaxPool2d`` that takes this path
-for bf16 channels_last CUDA tensors with C % 8 == 0 and falls back to PyTorch otherwise.
+for bf16 / fp32 channels_last CUDA tensors with C % 8 == 0 and falls back to PyTorch otherwise.
 """
 from __future__ import annotations
 
@@ -27,7 +27,8 @@ class _MaxPoolFn(torch.autograd.Function):
         y = torch.empty((n, c, ho, wo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
         idx = torch.empty((n, ho, wo, c), dtype=torch.uint8, device=x.device)
         native().maxpool_fwd(x.device.index, _stream(x), n, h, w, c, k, stride, pad, x.data_ptr(), y.data_ptr(),
-                             idx.data_ptr())
+                             idx.data_ptr(), f32=x.dtype == torch.float32)
+        ctx.dt = x.dtype
         ctx.save_for_backward(idx)
         ctx.geo = (n, c, h, w, k, stride, pad)
         return y
@@ -36,13 +37,13 @@ class _MaxPoolFn(torch.autograd.Function):
     def backward(ctx, dy):
         (idx,) = ctx.saved_tensors
         n, c, h, w, k, stride, pad = ctx.geo
-        if dy.dtype != torch.bfloat16:
-            dy = dy.to(torch.bfloat16)
+        if dy.dtype != ctx.dt:
+            dy = dy.to(ctx.dt)
         if not dy.is_contiguous(memory_format=torch.channels_last):
             dy = dy.contiguous(memory_format=torch.channels_last)
-        dx = torch.empty((n, c, h, w), dtype=torch.bfloat16, device=dy.device, memory_format=torch.channels_last)
+        dx = torch.empty((n, c, h, w), dtype=ctx.dt, device=dy.device, memory_format=torch.channels_last)
         native().maxpool_bwd(dy.device.index, _stream(dy), n, h, w, c, k, stride, pad, dy.data_ptr(), idx.data_ptr(),
-                             dx.data_ptr())
+                             dx.data_ptr(), f32=ctx.dt == torch.float32)
         return dx, None, None, None
 
 
@@ -51,11 +52,11 @@ def _int(v):
 
 
 class MaxPool2dNHWC(nn.MaxPool2d):
-    """``nn.MaxPool2d(k, stride, padding)`` with the HIP path for bf16 NHWC tensors."""
+    """``nn.MaxPool2d(k, stride, padding)`` with the HIP path for bf16 / fp32 NHWC tensors."""
 
     def fused(self, x: torch.Tensor) -> bool:
         k, s, p = _int(self.kernel_size), _int(self.stride), _int(self.padding)
-        return (x.is_cuda and x.dim() == 4 and x.dtype == torch.bfloat16 and x.shape[1] % 8 == 0
+        return (x.is_cuda and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float32) and x.shape[1] % 8 == 0
                 and _int(self.dilation) == 1 and not self.ceil_mode and not self.return_indices
                 and 2 * p <= k <= 15 and self.kernel_size in (k, (k, k)) and self.stride in (s, (s, s))
                 and self.padding in (p, (p, p)))

@@ -114,7 +114,7 @@ class Trainer:
         if self.on_gpu and cfg.extra.get("batched_weight_casts", True):
             from .ops.conv import WeightCastPlan
 
-            plan = WeightCastPlan(self.model)
+            plan = WeightCastPlan(self.model, torch.bfloat16 if cfg.amp else torch.float32)
             self.wcast = plan if plan.njobs else None
         self.steps = 0
 

@@ -1,0 +1,292 @@
+"""The fp32 training path (the reference's precision: asyncsgd/glaunch.lua:11 trains
+CudaTensors, BiCNN/plaunch.lua:200 likewise) on the hand-written gfx950 kernels:
+``v_mfma_f32_32x32x2_f32`` GEMMs / implicit-GEMM convolutions (csrc/kernels/gemm.hip),
+fp32 fused BN (bn_act.hip) and max pooling (pool.hip).
+
+Every GEMM-shaped op is held to at most 2x the error of PyTorch's own fp32 op (rocBLAS /
+MIOpen) against an fp64 reference of the same math, computed on the CPU."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from mpit_amd.ops import conv as C
+
+gpu = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-300)).item()
+
+
+def _cl(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+def test_mfma_dtype_selection_cpu():
+    x = torch.randn(2, 64, 4, 4)
+    assert C.mfma_dtype(x) == torch.float32
+    assert C.mfma_dtype(x.to(torch.bfloat16)) == torch.bfloat16
+    assert C.mfma_dtype(x.half()) is None
+    # CPU tensors never take the MFMA path
+    assert not C.conv_supported(x, torch.randn(64, 64, 3, 3))
+
+
+@gpu
+@pytest.mark.parametrize("M,N,K", [(128, 64, 64), (1000, 192, 128), (4096, 256, 512), (333, 64, 1024),
+                                   (12544, 512, 2048), (50176, 128, 576)])
+def test_gemm_nt_fp32_vs_fp64(M, N, K):
+    torch.manual_seed(M + N + K)
+    a = torch.randn(M, K, device="cuda")
+    b = torch.randn(N, K, device="cuda") * 0.05
+    ref = a.double().cpu() @ b.double().cpu().t()
+    c = C.gemm_nt(a, b)
+    assert c.dtype == torch.float32 and c.shape == (M, N)
+    lib = a @ b.t()
+    e, el = _rel(c, ref), _rel(lib, ref)
+    assert e <= 2.0 * el + 1e-9, (e, el)
+    assert e < 2e-6
+
+
+@gpu
+@pytest.mark.parametrize("M,N,K", [(256, 64, 64), (1000, 128, 192)])
+def test_gemm_nt_fp32_stats(M, N, K):
+    torch.manual_seed(1)
+    a, b = torch.randn(M, K, device="cuda"), torch.randn(N, K, device="cuda") * 0.05
+    c, st = C.gemm_nt(a, b, stats=True)
+    cd = c.double()
+    torch.testing.assert_close(st[0].double(), cd.sum(0), rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(st[1].double(), (cd * cd).sum(0), rtol=1e-5, atol=1e-4)
+
+
+@gpu
+@pytest.mark.parametrize("M,N,K", [(64, 64, 64), (1000, 64, 128), (4096, 128, 128), (200704, 256, 64),
+                                   (12544, 512, 2048), (5000, 192, 320)])
+def test_gemm_tn_fp32_vs_fp64(M, N, K):
+    torch.manual_seed(M % 97 + N + K)
+    y, x = torch.randn(M, N, device="cuda"), torch.randn(M, K, device="cuda")
+    ref = y.double().cpu().t() @ x.double().cpu()
+    out = C.gemm_tn(y, x)
+    lib = y.t() @ x
+    e, el = _rel(out, ref), _rel(lib, ref)
+    assert e <= 2.0 * el + 1e-9, (e, el)
+    base = torch.randn(N, K, device="cuda")
+    out2 = C.gemm_tn(y, x, out=base.clone(), beta=1.0)
+    assert _rel(out2, ref + base.double().cpu()) < 4 * el + 1e-7
+
+
+@gpu
+def test_cast_transpose_fp32_taps():
+    w = _cl(torch.randn(128, 64, 3, 3, device="cuda"))
+    wb, wt = C.conv_weights(w, dgrad=True, dtype=torch.float32)
+    ref = w.permute(0, 2, 3, 1)  # [Co][R][S][C]
+    assert wb.data_ptr() == w.data_ptr() and torch.equal(wb, ref)
+    assert wt.dtype == torch.float32
+    assert torch.equal(wt, ref.flip(1, 2).permute(3, 1, 2, 0).contiguous())
+    wb2, wt2 = C.cast_transpose(torch.randn(192, 320, device="cuda"), torch.float32)
+    assert torch.equal(wt2, wb2.t().contiguous())
+
+
+def _conv_case(n, ci, co, hw, k, stride, mod_cls):
+    torch.manual_seed(n * ci + co + k + stride)
+    pad = k // 2
+    if mod_cls is C.Conv1x1:
+        mod = C.Conv1x1(ci, co)
+    else:
+        mod = C.ConvNHWC(ci, co, k, stride=stride, padding=pad)
+    mod = mod.cuda().to(memory_format=torch.channels_last)
+    x = _cl(torch.randn(n, ci, hw, hw, device="cuda"))
+    x1 = x.clone().requires_grad_(True)
+    y1 = mod(x1)
+    assert y1.dtype == torch.float32
+    g = torch.randn_like(y1)
+    y1.backward(g)
+    ours = (y1.detach(), x1.grad, mod.weight.grad)
+    # PyTorch fp32 (MIOpen) and fp64 (CPU) references
+    w = mod.weight.detach()
+
+    def run(dev, dt):
+        xx = x.detach().to(dev, dt).clone().requires_grad_(True)
+        ww = w.to(dev, dt).clone().requires_grad_(True)
+        yy = F.conv2d(xx, ww, stride=mod.stride, padding=mod.padding)
+        yy.backward(g.to(dev, dt))
+        return yy.detach(), xx.grad, ww.grad
+
+    lib = run("cuda", torch.float32)
+    ref = run("cpu", torch.float64)
+    return ours, lib, ref
+
+
+@gpu
+@pytest.mark.parametrize("n,ci,co,hw,k,stride", [(2, 64, 64, 28, 3, 1), (2, 128, 128, 28, 3, 2),
+                                                 (2, 256, 256, 14, 3, 1), (2, 64, 128, 9, 3, 2),
+                                                 (2, 128, 64, 13, 5, 1), (2, 256, 512, 14, 1, 2),
+                                                 (2, 64, 64, 12, 3, 3)])
+def test_conv_fp32_within_2x_of_pytorch_fp32(n, ci, co, hw, k, stride):
+    """fwd, dgrad (stride 1 and the strided parity classes), wgrad on v_mfma_f32_32x32x2_f32."""
+    ours, lib, ref = _conv_case(n, ci, co, hw, k, stride, C.ConvNHWC)
+    for name, a, b, r in zip(("y", "dx", "dw"), ours, lib, ref):
+        e, el = _rel(a, r), _rel(b, r)
+        assert e <= 2.0 * el + 1e-9, (name, e, el)
+
+
+@gpu
+@pytest.mark.parametrize("n,ci,co,hw", [(4, 64, 256, 14), (2, 256, 64, 9), (3, 128, 128, 7)])
+def test_conv1x1_fp32_within_2x_of_pytorch_fp32(n, ci, co, hw):
+    ours, lib, ref = _conv_case(n, ci, co, hw, 1, 1, C.Conv1x1)
+    for name, a, b, r in zip(("y", "dx", "dw"), ours, lib, ref):
+        e, el = _rel(a, r), _rel(b, r)
+        assert e <= 2.0 * el + 1e-9, (name, e, el)
+
+
+@gpu
+def test_stem_fp32():
+    torch.manual_seed(5)
+    mod = C.StemConv(3, 64, 7, 2, 3).cuda().to(memory_format=torch.channels_last)
+    x = _cl(torch.randn(2, 3, 64, 64, device="cuda"))
+    assert mod.fused(x)
+    y = mod(x)
+    assert y.dtype == torch.float32
+    g = torch.randn_like(y)
+    y.backward(g)
+    w = mod.weight.detach()
+    xx = x.double().cpu()
+    ww = w.double().cpu().requires_grad_(True)
+    yr = F.conv2d(xx, ww, stride=2, padding=3)
+    yr.backward(g.double().cpu())
+    xl = x.clone()
+    wl = w.clone().requires_grad_(True)
+    yl = F.conv2d(xl, wl, stride=2, padding=3)
+    yl.backward(g)
+    assert _rel(y, yr) <= 2 * _rel(yl, yr) + 1e-9
+    assert _rel(mod.weight.grad, ww.grad) <= 2 * _rel(wl.grad, ww.grad) + 1e-9
+
+
+@gpu
+def test_maxpool_fp32_exact():
+    from mpit_amd.ops.pool import MaxPool2dNHWC
+
+    torch.manual_seed(2)
+    x = _cl(torch.randn(2, 64, 17, 17, device="cuda")).requires_grad_(True)
+    p = MaxPool2dNHWC(3, stride=2, padding=1)
+    assert p.fused(x)
+    y = p(x)
+    x2 = x.detach().clone().requires_grad_(True)
+    y2 = F.max_pool2d(x2, 3, 2, 1)
+    assert torch.equal(y, y2)
+    g = torch.randn_like(y)
+    y.backward(g)
+    y2.backward(g)
+    torch.testing.assert_close(x.grad, x2.grad, rtol=1e-6, atol=1e-6)
+
+
+def _ref_block(blk, x):
+    """The bottleneck's math on plain PyTorch ops in x's dtype."""
+    def bn(mod, t):
+        return F.batch_norm(t, None, None, mod.weight.to(t.dtype), mod.bias.to(t.dtype), training=True, eps=mod.eps)
+
+    def conv(mod, t):
+        return F.conv2d(t, mod.weight.to(t.dtype), stride=mod.stride, padding=mod.padding)
+
+    out = F.relu(bn(blk.bn1, conv(blk.conv1, x)))
+    out = F.relu(bn(blk.bn2, conv(blk.conv2, out)))
+    out = bn(blk.bn3, conv(blk.conv3, out))
+    idt = x if blk.downsample is None else bn(blk.downsample[1], conv(blk.downsample[0], x))
+    return F.relu(out + idt)
+
+
+@gpu
+@pytest.mark.parametrize("inp,planes,stride", [(256, 64, 1), (256, 128, 2)])
+def test_bottleneck_fp32_vs_fp64(inp, planes, stride):
+    """A whole fused bottleneck block in fp32 (GEMM-epilogue BN statistics and backward
+    reductions, parked shortcut gradients, bn_pair) against fp64 on the CPU: within 2x of
+    the same block on PyTorch's fp32 ops."""
+    from mpit_amd.models.resnet import Bottleneck, conv1x1
+    from mpit_amd.ops.bn import BatchNormAct2d
+
+    torch.manual_seed(inp + planes + stride)
+    down = None
+    if stride != 1 or inp != planes * 4:
+        down = torch.nn.Sequential(conv1x1(inp, planes * 4, stride), BatchNormAct2d(planes * 4, act=False))
+    blk = Bottleneck(inp, planes, stride, down).cuda().to(memory_format=torch.channels_last)
+    for m in blk.modules():
+        if isinstance(m, BatchNormAct2d):
+            m.weight.data.uniform_(0.5, 1.5)
+            m.bias.data.uniform_(-0.2, 0.2)
+    x = _cl(torch.randn(4, inp, 14, 14, device="cuda"))
+    x1 = x.clone().requires_grad_(True)
+    y1 = blk(x1)
+    assert y1.dtype == torch.float32
+    g = torch.randn(y1.shape, device="cuda")
+    y1.backward(g)
+    ours = {n: p.grad.detach().clone() for n, p in blk.named_parameters()}
+    ours.update(y=y1.detach(), dx=x1.grad)
+    blk.zero_grad(set_to_none=True)
+    x3 = x.clone().requires_grad_(True)
+    y3 = _ref_block(blk, x3)
+    y3.backward(g)
+    lib = {n: p.grad.detach().clone() for n, p in blk.named_parameters()}
+    lib.update(y=y3.detach(), dx=x3.grad)
+    blk.zero_grad(set_to_none=True)
+    bd = blk.double().cpu()
+    x2 = x.double().cpu().requires_grad_(True)
+    y2 = _ref_block(bd, x2)
+    y2.backward(g.double().cpu())
+    ref = {n: p.grad.detach().clone() for n, p in bd.named_parameters()}
+    ref.update(y=y2.detach(), dx=x2.grad)
+    for k in ref:
+        e, el = _rel(ours[k], ref[k]), _rel(lib[k], ref[k])
+        assert e <= 2.0 * el + 1e-7, (k, e, el)
+
+
+@gpu
+def test_weight_cast_plan_fp32():
+    """The fp32 plan writes exactly the per-call fp32 transposes and forwards read the master."""
+    from mpit_amd.models.resnet import Bottleneck, conv1x1
+    from mpit_amd.ops.bn import BatchNormAct2d
+
+    torch.manual_seed(3)
+    down = torch.nn.Sequential(conv1x1(256, 512, 2), BatchNormAct2d(512, act=False))
+    net = torch.nn.Sequential(Bottleneck(256, 128, 2, down), Bottleneck(512, 128)).cuda().to(
+        memory_format=torch.channels_last)
+    plan = C.WeightCastPlan(net, torch.float32)
+    plan.run()
+    for mod, _, (wb, wt) in plan.mods:
+        w = mod.weight
+        assert wb.data_ptr() == w.data_ptr()
+        if isinstance(mod, C.Conv1x1):
+            _, rt = C.cast_transpose(w, torch.float32)
+        elif mod.stride[0] > 1 and C.strided_dgrad_supported(w.shape[1], w.shape[0], mod.stride[0]):
+            _, rt = C.strided_dgrad_weights(w, mod.stride[0], mod.padding[0], torch.float32)
+        elif mod.stride[0] > 1:
+            rt = None
+        else:
+            _, rt = C.conv_weights(w, True, torch.float32)
+        assert (wt is None) == (rt is None)
+        if wt is not None:
+            assert torch.equal(wt.reshape(-1), rt.reshape(-1))
+    x = _cl(torch.randn(2, 256, 14, 14, device="cuda"))
+    y1 = net(x)
+    plan.invalidate()
+    y2 = net(x)
+    assert torch.equal(y1, y2)
+
+
+@gpu
+def test_resnet50_fp32_step_runs_native():
+    """One fp32 ResNet-50 forward/backward: every convolution on the MFMA kernels (no MIOpen
+    conv), finite loss and gradients."""
+    from mpit_amd.models.resnet import resnet50
+
+    torch.manual_seed(0)
+    net = resnet50(num_classes=10).cuda().to(memory_format=torch.channels_last)
+    convs = [m for m in net.modules() if isinstance(m, torch.nn.Conv2d)]
+    x = _cl(torch.randn(4, 3, 64, 64, device="cuda"))
+    assert net.conv1.fused(x)
+    out = net(x)
+    assert out.dtype == torch.float32
+    loss = F.cross_entropy(out, torch.randint(0, 10, (4,), device="cuda"))
+    loss.backward()
+    assert torch.isfinite(loss)
+    for m in convs:
+        assert m.weight.grad is not None and torch.isfinite(m.weight.grad).all()

@@ -7,27 +7,63 @@ the mpit_amd parameter server on 1/2/4/8 MI355X (BASELINE.json).
         --master-port 29500 bench.py --gpus 8 --steps 20 --warmup 5
 
 One process per GPU. Every rank trains a ResNet-50 replica on a synthetic ImageNet batch
-(random bf16 images, random labels, random-init weights) AND serves one shard of the
-flat parameter vector (co-located sharded parameter servers). Each step: forward +
-backward (bf16 autocast, channels_last), fused Downpour scale into the push window, push
-of every gradient shard to its server + pull of every refreshed shard (one fused HIP
-kernel per shard reading / writing the worker's HBM over xGMI), wait. Weak scaling: the
-per-GPU batch is fixed. The timed region is exactly `--steps` full steps bracketed by a
-barrier + device synchronize on both sides; the reported time is the max over ranks.
+(random images, random labels, random-init weights) AND serves one shard of the flat
+parameter vector (co-located sharded parameter servers). Each step: forward + backward,
+fused Downpour scale into the push window, push of every gradient shard to its server +
+pull of every refreshed shard (overlapped with the backward, shard by shard), wait. Weak
+scaling: the per-GPU batch is fixed. The timed region is exactly ``--steps`` full steps
+bracketed by a barrier + device synchronize on both sides; the reported time is the max
+over ranks.
+
+Precision: the headline is **fp32** — the reference trains fp32 Float/CudaTensors
+(asyncsgd/glaunch.lua:11, BiCNN/plaunch.lua:200) — with fp32 weights, activations and
+gradients on the hand-written v_mfma_f32_32x32x2_f32 kernels. bf16 autocast (fp32 master
+weights) is reported as the secondary field ``secondary.bf16_autocast`` of the same job.
+
+Also reported, outside the timed region (``--no-secondary`` skips them):
+* ``ps_check``: after the run every worker pulls every shard again and the exact bit-sums
+  of each shard must agree between all workers and the owning server (exit status 3 if
+  not); ``world`` / ``rccl``: the ranks and the collective backend actually seen;
+* at N > 1: ``secondary.dedicated``: the same step in BASELINE config 2's topology (1
+  dedicated pserver + N-1 workers); ``secondary.ps_pingpong``: the reference's
+  asyncsgd/ptest.lua instrument (640 MiB pull + push, bi-directional GB/s);
+  ``secondary.allreduce``: test/testreduceall.lua's 40 MiB Allreduce time.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
+import time
 
 METRIC = "images/sec (whole node) ResNet-50 async-SGD at 1/2/4/8 MI355X"
 _REPO = os.path.dirname(os.path.abspath(__file__))
 # MIOpen find / perf databases are kept in-tree (miopen_db/) so a fresh box reuses the
-# algorithm choices of earlier runs instead of re-searching every convolution.
+# algorithm choices of earlier runs (only the fc layer and fallbacks still reach MIOpen).
 os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(_REPO, "miopen_db"))
 os.environ.setdefault("MIOPEN_CUSTOM_CACHE_DIR", os.path.join(_REPO, "miopen_db", "kcache"))
+
+
+def _par(a, tr, nworkers) -> str:
+    par = {"downpour": "async-ps", "eamsgd": "easgd-ps", "easgd": "easgd-ps", "msgd": "local",
+           "allreduce": "dp"}[a.optimizer]
+    if a.optimizer not in ("allreduce", "msgd"):
+        return par + f"-{tr.cfg.topology}-{len(tr.sranks)}srv-{nworkers}wrk"
+    return par + str(a.gpus)
+
+
+def _make(a, mp_train, amp: bool, topology: str, servers: int, ps_id: int):
+    nw_world = int(os.environ.get("WORLD_SIZE", "1"))
+    nw = nw_world if topology == "colocated" else max(1, nw_world - servers)
+    mva = 0.9 / max(1, nw_world) if a.optimizer in ("eamsgd", "easgd") else 0.0
+    lr = a.lr / max(1, nw) if a.optimizer == "downpour" else a.lr
+    cfg = mp_train.TrainConfig(model=a.model, batch=a.batch, optimizer=a.optimizer, topology=topology,
+                               servers=servers, su=a.su, lr=lr, mva=mva, mom=0.0, amp=amp,
+                               channels_last=not a.no_channels_last, datapath=a.datapath, staleness=a.staleness,
+                               wire_dtype=a.wire, extra={"ps_id": ps_id})
+    return mp_train.Trainer(cfg)
 
 
 def main(argv=None) -> int:
@@ -47,12 +83,16 @@ def main(argv=None) -> int:
     ap.add_argument("--datapath", type=int, default=2)
     ap.add_argument("--staleness", type=int, default=-1, help="bounded staleness (SSP); -1 = fully async")
     ap.add_argument("--wire", default="fp32", choices=["fp32", "bf16"], help="EASGD elastic-difference dtype")
-    ap.add_argument("--no-amp", action="store_true")
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="headline compute precision (fp32 = the reference's; bf16 = autocast, fp32 master)")
+    ap.add_argument("--no-amp", action="store_true", help="alias of --dtype fp32 (kept for old scripts)")
+    ap.add_argument("--no-secondary", action="store_true", help="headline only")
     ap.add_argument("--no-channels-last", action="store_true")
     ap.add_argument("--miopen-find", action="store_true",
-                    help="exhaustive MIOpen algorithm search (measured: same steady-state speed as the "
-                         "heuristics for ResNet-50 bf16 NHWC on MI355X, but minutes of warm-up)")
+                    help="exhaustive MIOpen algorithm search for what still runs on MIOpen (the fc layer)")
     a = ap.parse_args(argv)
+    if a.no_amp:
+        a.dtype = "fp32"
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != a.gpus:
@@ -64,36 +104,58 @@ def main(argv=None) -> int:
 
     torch.backends.cudnn.benchmark = a.miopen_find
     import mpit_amd as mp
-    from mpit_amd.train import TrainConfig, Trainer, timed_steps
-
-    mp.Init()
-    mva = 0.9 / max(1, a.gpus) if a.optimizer in ("eamsgd", "easgd") else 0.0
-    nw = a.gpus if a.topology == "colocated" else max(1, a.gpus - a.servers)
-    lr = a.lr / max(1, nw) if a.optimizer == "downpour" else a.lr
-    cfg = TrainConfig(model=a.model, batch=a.batch, optimizer=a.optimizer, topology=a.topology, servers=a.servers,
-                      su=a.su, lr=lr, mva=mva, mom=0.0, amp=not a.no_amp, channels_last=not a.no_channels_last,
-                      datapath=a.datapath, staleness=a.staleness, wire_dtype=a.wire)
-    tr = Trainer(cfg)
-    secs, loss = timed_steps(tr, a.steps, a.warmup)
-    nworkers = len(tr.cranks)
+    from mpit_amd import train as mp_train
     from mpit_amd.models.cnn import INPUT_SHAPES
 
+    mp.Init()
+    W = mp.COMM_WORLD()
+    amp = a.dtype == "bf16"
+    tr = _make(a, mp_train, amp, a.topology, a.servers, 0)
+    secs, loss = mp_train.timed_steps(tr, a.steps, a.warmup)
+    nworkers = len(tr.cranks)
     shape = INPUT_SHAPES.get(a.model, (3, 224, 224))
-    images = a.steps * a.batch * nworkers
-    value = images / secs
-    import math
-
+    value = a.steps * a.batch * nworkers / secs
     lossv = float(loss.float().item()) if loss is not None else None
     if lossv is not None and not math.isfinite(lossv):
         lossv = None  # keep the line strict JSON
+    par = _par(a, tr, nworkers)
+    secondary = {}
+    t_sec = time.perf_counter()
+    sec_steps, sec_warm = max(3, min(a.steps, 10)), 2
+    if not a.no_secondary and tr.on_gpu:
+        # the other precision on the same replicas / PS (bf16 autocast when the headline is fp32)
+        tr.set_amp(not amp)
+        s2, _ = mp_train.timed_steps(tr, sec_steps, sec_warm)
+        secondary["bf16_autocast" if not amp else "fp32"] = {
+            "value": round(sec_steps * a.batch * nworkers / s2, 2), "unit": "images/sec",
+            "ms_per_step": round(1000.0 * s2 / sec_steps, 3), "steps": sec_steps, "warmup": sec_warm,
+            "dtype": "bf16" if not amp else "fp32", "parallelism": par}
+        tr.set_amp(amp)
+    check = tr.verify_ps() if (tr.pc is not None or tr.ps_server is not None) else None
     tr.stop()
-    if tr.rank == 0:
-        par = {"downpour": "async-ps", "eamsgd": "easgd-ps", "easgd": "easgd-ps", "msgd": "local",
-               "allreduce": "dp"}[a.optimizer]
-        if a.optimizer != "allreduce" and a.optimizer != "msgd":
-            par += f"-{a.topology}-{len(tr.sranks)}srv-{nworkers}wrk"
-        else:
-            par += str(a.gpus)
+    st = mp.runtime.state()
+    rccl = None
+    if world > 1 and tr.on_gpu:
+        rccl = bool(W._use_rccl(torch.zeros(1, device=tr.device)))
+    if not a.no_secondary and world > 1 and a.optimizer != "allreduce":
+        from mpit_amd.instruments import allreduce_time, ps_pingpong
+
+        try:
+            # BASELINE config 2: one dedicated pserver, N-1 workers (second PS instance)
+            td = _make(a, mp_train, amp, "dedicated", 1, 1)
+            sd, _ = mp_train.timed_steps(td, sec_steps, sec_warm)
+            nwd = len(td.cranks)
+            cd = td.verify_ps()
+            td.stop()
+            secondary["dedicated"] = {"value": round(sec_steps * a.batch * nwd / sd, 2), "unit": "images/sec",
+                                      "ms_per_step": round(1000.0 * sd / sec_steps, 3), "steps": sec_steps,
+                                      "dtype": a.dtype, "parallelism": _par(a, td, nwd), "ps_check": cd}
+            del td
+            secondary["ps_pingpong"] = ps_pingpong(640.0, iters=100, warmup=2, ps_id=7, time_budget_s=8.0)
+            secondary["allreduce"] = allreduce_time(10.0, iters=10)
+        except Exception as e:  # secondary fields never take the headline down
+            secondary["error"] = f"{type(e).__name__}: {e}"
+    if W.Get_rank() == 0:
         out = {
             "metric": METRIC if (a.model == "resnet50" and a.optimizer == "downpour") else
                       f"images/sec (whole node) {a.model} {a.optimizer}",
@@ -106,15 +168,20 @@ def main(argv=None) -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16" if (tr.on_gpu and not a.no_amp) else "fp32",
+            "dtype": "fp32" if not (tr.on_gpu and amp) else "bf16",
             "data": f"synthetic (random images {shape[0]}x{shape[1]}x{shape[2]}, random labels, random-init weights)",
             "config": {"model": a.model, "global_batch": a.batch * nworkers, "seq_len": None, "image_size": shape[-1],
                        "parallelism": par, "optimizer": a.optimizer, "su": a.su, "per_gpu_batch": a.batch,
                        "master_weights": "fp32", "loss_last": lossv},
+            "world": st.world, "shared_devices": st.shared_devices, "rccl": rccl,
+            "ps_check": check,
+            "secondary": secondary,
+            "secondary_s": round(time.perf_counter() - t_sec, 2),
         }
         print(json.dumps(out), flush=True)
+    ok = check is None or check["ok"]
     mp.Finalize()
-    return 0
+    return 0 if ok else 3
 
 
 if __name__ == "__main__":

@@ -1,8 +1,11 @@
 """Time the MFMA GEMM / implicit-GEMM conv kernels on one shape (for rocprofv3 counter
-runs and tile experiments).
+runs and tile experiments), bf16 or fp32 (``--f32``: v_mfma_f32_32x32x2_f32).
 
-    python benchmarks/gemm_probe.py nt M N K [iters]
-    python benchmarks/gemm_probe.py conv N H W C Co R stride [iters]
+    python benchmarks/gemm_probe.py [--f32] nt M N K [iters]
+    python benchmarks/gemm_probe.py [--f32] tn M N K [iters]
+    python benchmarks/gemm_probe.py [--f32] conv N H W C Co R stride [iters]
+    python benchmarks/gemm_probe.py [--f32] wgrad N H W C Co R stride [iters]
+    python benchmarks/gemm_probe.py [--f32] dgrad N H W C Co R 1 [iters]      (stride-1 backward-data)
 """
 import json
 import os
@@ -30,28 +33,56 @@ def timeit(fn, it):
 def main():
     m = native()
     st = torch.cuda.current_stream().cuda_stream
-    kind = sys.argv[1]
-    if kind == "nt":
-        M, N, K = map(int, sys.argv[2:5])
-        it = int(sys.argv[5]) if len(sys.argv) > 5 else 50
-        a = torch.randn(M, K, device="cuda").to(torch.bfloat16)
-        b = (torch.randn(N, K, device="cuda") * 0.05).to(torch.bfloat16)
-        c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-        ms = timeit(lambda: m.gemm_nt(0, st, M, N, K, a.data_ptr(), K, b.data_ptr(), K, c.data_ptr(), N, 0), it)
+    args = sys.argv[1:]
+    f32 = "--f32" in args
+    args = [a for a in args if a != "--f32"]
+    dt = torch.float32 if f32 else torch.bfloat16
+    es = 4 if f32 else 2
+    kind = args[0]
+    if kind in ("nt", "tn"):
+        M, N, K = map(int, args[1:4])
+        it = int(args[4]) if len(args) > 4 else 50
+        if kind == "nt":
+            a = torch.randn(M, K, device="cuda").to(dt)
+            b = (torch.randn(N, K, device="cuda") * 0.05).to(dt)
+            c = torch.empty(M, N, device="cuda", dtype=dt)
+            ms = timeit(lambda: m.gemm_nt(0, st, M, N, K, a.data_ptr(), K, b.data_ptr(), K, c.data_ptr(), N, 0,
+                                          f32=f32), it)
+            by = es * (M * K + N * K + M * N)
+        else:
+            y = torch.randn(M, N, device="cuda").to(dt)
+            x = torch.randn(M, K, device="cuda").to(dt)
+            out = torch.empty(N, K, device="cuda")
+            nws = m.gemm_tn_ws_floats(0, M, N, K)
+            ws = torch.empty(max(1, nws), device="cuda")
+            ms = timeit(lambda: m.gemm_tn(0, st, M, N, K, y.data_ptr(), N, x.data_ptr(), K, out.data_ptr(),
+                                          ws.data_ptr(), 0.0, f32=f32), it)
+            by = es * (M * K + M * N) + 4 * N * K
         fl = 2.0 * M * N * K
-        by = 2.0 * (M * K + N * K + M * N)
     else:
-        Nb, H, W, C, Co, R, S = map(int, sys.argv[2:9])
-        it = int(sys.argv[9]) if len(sys.argv) > 9 else 50
+        Nb, H, W, C, Co, R, S = map(int, args[1:8])
+        it = int(args[8]) if len(args) > 8 else 50
         pad = R // 2
-        x = torch.randn(Nb, H, W, C, device="cuda").to(torch.bfloat16)
-        w = (torch.randn(Co, R, R, C, device="cuda") * 0.05).to(torch.bfloat16)
         Ho, Wo = (H + 2 * pad - R) // S + 1, (W + 2 * pad - R) // S + 1
-        y = torch.empty(Nb, Ho, Wo, Co, device="cuda", dtype=torch.bfloat16)
-        ms = timeit(lambda: m.conv_fwd(0, st, Nb, H, W, C, Co, R, R, S, pad, x.data_ptr(), w.data_ptr(),
-                                       y.data_ptr()), it)
+        x = torch.randn(Nb, H, W, C, device="cuda").to(dt)
+        w = (torch.randn(Co, R, R, C, device="cuda") * 0.05).to(dt)
+        y = torch.randn(Nb, Ho, Wo, Co, device="cuda").to(dt)
+        if kind == "conv":
+            ms = timeit(lambda: m.conv_fwd(0, st, Nb, H, W, C, Co, R, R, S, pad, x.data_ptr(), w.data_ptr(),
+                                           y.data_ptr(), f32=f32), it)
+        elif kind == "dgrad":  # stride-1 backward-data = forward conv of dy with the transposed weight
+            wt = (torch.randn(C, R, R, Co, device="cuda") * 0.05).to(dt)
+            dx = torch.empty_like(x)
+            ms = timeit(lambda: m.conv_fwd(0, st, Nb, Ho, Wo, Co, C, R, R, 1, R - 1 - pad, y.data_ptr(),
+                                           wt.data_ptr(), dx.data_ptr(), f32=f32), it)
+        else:
+            dw = torch.empty(Co, R, R, C, device="cuda")
+            nws = m.conv_wgrad_ws_floats(0, Nb, H, W, C, Co, R, R, S, pad)
+            ws = torch.empty(max(1, nws), device="cuda")
+            ms = timeit(lambda: m.conv_wgrad(0, st, Nb, H, W, C, Co, R, R, S, pad, y.data_ptr(), x.data_ptr(),
+                                             dw.data_ptr(), ws.data_ptr(), 0.0, f32=f32), it)
         fl = 2.0 * Nb * Ho * Wo * Co * R * R * C
-        by = 2.0 * (x.numel() + w.numel() + y.numel())
+        by = es * (x.numel() + w.numel() + y.numel())
     print(json.dumps({"args": sys.argv[1:], "ms": round(ms, 4), "tflops": round(fl / ms / 1e9, 1),
                       "hbm_tbs": round(by / ms / 1e9, 2)}), flush=True)
 

@@ -9,20 +9,18 @@ First half of the ranks serve, second half are clients (ptest.lua:20-26), or
 iteration; the reported number is that bi-directional volume per second per client, and
 summed over clients. ``--straggle`` adds ``(rank+1-size/2)^2`` extra elementwise passes per
 iteration on each client (ptest2.lua:66-70) to show the asynchronous server is not held
-back by slow clients.
+back by slow clients. The measurement itself is mpit_amd.instruments.ps_pingpong.
 """
 import argparse
 import json
 import os
 import sys
-import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-import torch
 
 import mpit_amd as mp
+from mpit_amd.instruments import ps_pingpong
 from mpit_amd.launch import colocated, half_half
-from mpit_amd.parallel.ps import PClient, PServer, ServerOpt
 
 
 def main():
@@ -36,50 +34,11 @@ def main():
     a = ap.parse_args()
     mp.Init()
     W = mp.COMM_WORLD()
-    rank, size = W.Get_rank(), W.Get_size()
-    dev = mp.runtime.device() or torch.device("cpu")
+    size = W.Get_size()
     servers, clients, _ = colocated(size) if (a.colocated or size == 1) else half_half(size)
-    plong = int(a.mib * (1 << 20)) // 4
-    conf = dict(rank=rank, sranks=servers, cranks=clients, plong=plong, opt=ServerOpt("sum"), datapath=a.datapath)
-    srv = None
-    if rank in servers:
-        srv = PServer(conf)
-        srv.start(block=rank not in clients)
-    res = None
-    if rank in clients:
-        p = torch.zeros(plong, device=dev)
-        g = torch.full((plong,), 1e-6, device=dev)
-        pc = PClient(conf).start(p, g)
-        extra = max(0, (rank + 1 - size // 2)) ** 2 if a.straggle else 0
-        scratch = torch.zeros(1 << 20, device=dev)
-        for _ in range(a.warmup):
-            pc.async_recv_param()
-            pc.async_send_grad()
-            pc.wait()
-        if dev.type == "cuda":
-            torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(a.iters):
-            for _ in range(extra):
-                scratch.mul_(1.0001)
-            pc.async_recv_param()
-            pc.async_send_grad()
-            pc.wait()
-        if dev.type == "cuda":
-            torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
-        gbps = 2 * plong * 4 * a.iters / dt / 1e9
-        res = dict(rank=rank, seconds=round(dt, 4), GBps_bidir=round(gbps, 2), ms_per_iter=round(1000 * dt / a.iters, 3),
-                   extra_passes=extra)
-        pc.stop()
-    allr = W.allgather_obj(res)
-    if srv is not None and rank in clients:
-        srv.wait_done()
-    if rank == 0:
-        rs = [r for r in allr if r]
-        print(json.dumps({"benchmark": "ps_pingpong", "payload_MiB": a.mib, "iters": a.iters, "servers": len(servers),
-                          "clients": len(clients), "device": str(dev), "per_client": rs,
-                          "aggregate_GBps_bidir": round(sum(r["GBps_bidir"] for r in rs), 2)}), flush=True)
+    r = ps_pingpong(a.mib, a.iters, a.warmup, servers, clients, straggle=a.straggle, datapath=a.datapath)
+    if W.Get_rank() == 0:
+        print(json.dumps(dict(benchmark="ps_pingpong", **r)), flush=True)
     mp.Finalize()
 
 

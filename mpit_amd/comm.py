@@ -14,6 +14,7 @@ Transport is chosen by the tensor's device inside one native core (SURVEY §7.4 
 """
 from __future__ import annotations
 
+import os
 import threading
 from typing import Callable, List, Optional, Sequence
 
@@ -336,6 +337,8 @@ def _loc(better):
     return f
 
 
+# built-in ops that act element by element (safe to apply to any chunk of a buffer)
+_ELEMENTWISE_OPS = {"SUM", "PROD", "MAX", "MIN", "LAND", "BAND", "LOR", "BOR", "LXOR", "BXOR"}
 SUM = Op(lambda a, b: a + b, name="SUM")
 PROD = Op(lambda a, b: a * b, name="PROD")
 MAX = Op(torch.maximum, name="MAX")
@@ -594,10 +597,17 @@ class Comm:
         return self._irecv(buf, source, tag, self._cctx())
 
     def _use_rccl(self, t: torch.Tensor) -> bool:
-        if not t.is_cuda or self.Get_size() == 1:
+        """Run this collective through torch.distributed: RCCL for HBM tensors when every
+        rank owns its GPU; gloo for host tensors only when MPIT_DIST_HOST=1 (the shm
+        point-to-point algorithms below are the default host path; the switch exists so
+        CPU tests exercise the torch.distributed branch and its Request(work=...))."""
+        if self.Get_size() == 1:
             return False
         st = _rt.state()
-        if st.shared_devices:
+        if t.is_cuda:
+            if st.shared_devices:
+                return False
+        elif os.environ.get("MPIT_DIST_HOST") != "1":
             return False
         import torch.distributed as dist
 
@@ -605,10 +615,15 @@ class Comm:
             return False
         if self._pg is None and not self._pg_tried:
             self._pg_tried = True
-            if len(self._ranks) == st.world:
+            # torch.distributed only for communicators over every rank in world order (WORLD,
+            # its Dup, an all-ranks Split keyed by rank): the torch group's rank order is
+            # then the communicator's. Sub-communicators run on the native point-to-point
+            # engine (IPC peer copies over xGMI for HBM tensors): torch's locally
+            # synchronised sub-groups deadlock when two of them overlap in a rank
+            # (reproduced with gloo: [0,2] then [1,2]), and communicator creation is not
+            # collective over WORLD, so world-synchronised groups cannot be made either.
+            if list(self._ranks) == list(range(st.world)):
                 self._pg = dist.group.WORLD
-            else:
-                self._pg = dist.new_group(self._ranks, use_local_synchronization=True)
         return self._pg is not None
 
     # ---------------------------------------------------------------- collectives
@@ -720,12 +735,43 @@ class Comm:
                 dst.copy_(src)
             dist.all_reduce(dst, op=_rccl_op(op), group=self._pg)
             return recvbuf
+        if op.name in _ELEMENTWISE_OPS and n > 2 and src.numel() >= 64 * n:
+            if dst.data_ptr() != src.data_ptr():
+                dst.copy_(src)
+            self._ring_allreduce(dst, op)
+            return recvbuf
         tmp = torch.empty_like(src)
         self.Reduce(src, tmp, op, 0)
         if self.Get_rank() == 0:
             dst.copy_(tmp)
         self.Bcast(dst, 0)
         return recvbuf
+
+    def _ring_allreduce(self, buf: torch.Tensor, op: Op):
+        """Ring reduce-scatter + all-gather over the point-to-point layer (commutative
+        ops): every rank sends and receives 2(n-1)/n of the buffer, with both of its
+        neighbour links busy every step, instead of a binomial reduce + broadcast that
+        moves the whole buffer log2(n) times through the root."""
+        n, r = self.Get_size(), self.Get_rank()
+        m = buf.numel()
+        bounds = [m * k // n for k in range(n + 1)]
+        chunk = [buf[bounds[k]: bounds[k + 1]] for k in range(n)]
+        tmp = torch.empty(max(bounds[k + 1] - bounds[k] for k in range(n)), dtype=buf.dtype, device=buf.device)
+        right, left = (r + 1) % n, (r - 1) % n
+        for s in range(n - 1):  # reduce-scatter: rank r ends owning chunk (r + 1) % n
+            si, ri = (r - s) % n, (r - s - 1) % n
+            t = tmp[: chunk[ri].numel()]
+            rq = self._crecv(t, left, 10)
+            sq = self._csend(chunk[si], right, 10)
+            rq.Wait()
+            chunk[ri].copy_(op(chunk[ri], t))
+            sq.Wait()
+        for s in range(n - 1):  # all-gather of the reduced chunks
+            si, ri = (r + 1 - s) % n, (r - s) % n
+            rq = self._crecv(chunk[ri], left, 11)
+            sq = self._csend(chunk[si], right, 11)
+            rq.Wait()
+            sq.Wait()
 
     def Iallreduce(self, sendbuf, recvbuf=None, op: Op = SUM) -> Request:
         """Non-blocking all-reduce (mpifuncs.c:1357). RCCL work handle on HBM tensors,

@@ -7,13 +7,16 @@ config 3 asks for one ("ResNet-50 sync all-reduce DP=8 over xGMI").
 Design for MI355X: the model's gradients are views into ONE flat fp32 buffer
 (:class:`~mpit_amd.utils.flat.FlatParams`), so a bucket is just a contiguous slice of it —
 no pack/unpack copies. Buckets are formed in reverse parameter order (the order backward
-produces gradients) with a size target of ``bucket_mb`` (default 64 MB: few, large RCCL
-calls; each 8-GPU ring all-reduce moves 2·(N-1)/N of the bucket over every xGMI link, so
-large buckets keep the per-call latency off the critical path). A post-accumulate-grad
-hook counts finished parameters per bucket and launches the bucket's non-blocking
-all-reduce (RCCL on its own stream) as soon as it is complete, so communication overlaps
-the rest of backward. ``finish()`` waits for the outstanding buckets; the 1/N averaging is
-fused into the optimizer kernel (``gscale``).
+produces gradients). Sizing for xGMI: an 8-GPU ring all-reduce moves 2·(N-1)/N of a bucket
+over each of the 7 point-to-point links at ~153 GB/s, so a 25 MB bucket costs ~0.3 ms of
+link time and ~10 µs of launch latency — large enough to stay bandwidth-bound, small
+enough that ResNet-50's 102 MB of gradients makes 4-5 buckets which overlap the backward.
+The first bucket (the last layers, complete first) is capped at ``first_bucket_mb`` so the
+first all-reduce starts after a few layers of backward instead of a quarter of it. A
+post-accumulate-grad hook counts finished parameters per bucket and launches the bucket's
+non-blocking all-reduce (RCCL on its own stream) as soon as it is complete. ``finish()``
+waits for the outstanding buckets; the 1/N averaging is fused into the optimizer kernel
+(``gscale``).
 """
 from __future__ import annotations
 
@@ -26,17 +29,20 @@ from ..utils.flat import FlatParams
 
 
 class BucketedAllreduce:
-    def __init__(self, model: torch.nn.Module, flat: FlatParams, bucket_mb: float = 64.0, comm: Optional[Comm] = None):
+    def __init__(self, model: torch.nn.Module, flat: FlatParams, bucket_mb: float = 25.0, comm: Optional[Comm] = None,
+                 first_bucket_mb: float = 4.0):
         self.comm = comm or COMM_WORLD()
         self.flat = flat
-        cap = int(bucket_mb * (1 << 20)) // flat.grad.element_size()
+        es = flat.grad.element_size()
+        cap = int(bucket_mb * (1 << 20)) // es
+        first = min(cap, int(first_bucket_mb * (1 << 20)) // es) if first_bucket_mb > 0 else cap
         order = list(range(len(flat.params)))[::-1]  # backward order
         self.buckets: List[tuple] = []  # (lo, hi) element range in the flat buffer
         self.bucket_of: Dict[int, int] = {}
         starts, n = [], 0  # first flat offset of each bucket, walking backward order
         for i in order:
             n += flat.params[i].numel()
-            if n >= cap:
+            if n >= (first if not starts else cap):
                 starts.append(flat.offsets[i])
                 n = 0
         if not starts or starts[-1] != 0:

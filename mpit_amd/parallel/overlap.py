@@ -12,9 +12,12 @@ the update and write the refreshed shard back while the backward of the earlier 
 is still running, so only the last shard's round trip is left to wait for.
 
 Safe because a shard is pushed only after every kernel that reads its parameters in
-this step has been queued ahead of the gate: the convolutions and the classifier run on
-bf16 copies made in the forward, and a BN layer reads its fp32 gamma before it emits its
-gradient.
+this step has been queued ahead of the gate: the convolutions' backward-data GEMMs read
+the per-step weight copies made before the forward (bf16 casts, or the fp32 transposes of
+an fp32 step — ops/conv.py WeightCastPlan), a layer's other parameter reads (the
+classifier's grad_input, a BN layer's gamma) are issued by the same autograd node that
+emits their gradients, i.e. before the shard can complete. tests/test_overlap.py checks
+the overlapped parameters against the non-overlapped ones bit for bit on the GPU.
 """
 from __future__ import annotations
 

@@ -51,7 +51,7 @@ class TrainConfig:
     wire_dtype: str = "fp32"  # "bf16": EASGD elastic differences cross xGMI in bf16
     server_rule: Optional[ServerOpt] = None
     seed: int = 1234
-    bucket_mb: float = 64.0  # allreduce bucket size
+    bucket_mb: float = 25.0  # allreduce bucket size (parallel/ddp.py sizing note)
     extra: dict = field(default_factory=dict)
 
 
@@ -151,7 +151,7 @@ class Trainer:
         # pushed by Downpour stay fp32 (they are summed into the fp32 master shard)
         wire = torch.bfloat16 if (c.wire_dtype == "bf16" and c.optimizer in ("eamsgd", "easgd")) else torch.float32
         conf = dict(rank=self.rank, sranks=self.sranks, cranks=self.cranks, plong=self.plong, opt=rule,
-                    datapath=c.datapath, staleness=c.staleness, grad_dtype=wire)
+                    datapath=c.datapath, staleness=c.staleness, grad_dtype=wire, ps_id=int(c.extra.get("ps_id", 0)))
         if self.is_server:
             self.ps_server = PServer(conf)
             self.ps_server.start(block=False)
@@ -219,6 +219,61 @@ class Trainer:
             raise ValueError(f"unknown optimizer {c.optimizer!r}")
         self.steps += 1
         return fx
+
+    def set_amp(self, amp: bool):
+        """Switch the compute precision between steps: bf16 autocast (``amp``) or fp32. The
+        parameters, the PS and the optimizer state are untouched; the synthetic batch and
+        the per-step weight plan follow the new dtype."""
+        if amp == self.cfg.amp:
+            return
+        self.cfg.amp = amp
+        if self.on_gpu:
+            self.x = self.x.to(torch.bfloat16 if amp else torch.float32)
+            if self.wcast is not None:
+                from .ops.conv import WeightCastPlan
+
+                plan = WeightCastPlan(self.model, torch.bfloat16 if amp else torch.float32)
+                self.wcast = plan if plan.njobs else None
+
+    def verify_ps(self) -> dict:
+        """Post-run consistency check of the parameter server (bench.py at N > 1).
+
+        Every worker pulls every shard once more after all pushes are done (barrier), then
+        each shard's bits are summed exactly (int64 sum of the fp32 words) on the worker's
+        pulled copy and on the server that owns it; the sums must be identical on every
+        rank. Returns {"ok", "shards", "workers", "mismatches"} on every rank."""
+        from .parallel.ps import shard_ranges
+
+        W = COMM_WORLD()
+        self.sync()
+        self.barrier()
+        if self.pc is not None:
+            self.pc.async_recv_param()
+            self.pc.wait()
+        self.sync()
+        self.barrier()
+
+        def bits(t):
+            return int(t.detach().reshape(-1).view(torch.int32).to(torch.int64).sum().item())
+
+        mine = {"rank": self.rank, "worker": None, "server": None}
+        if self.pc is not None and self.sranks:
+            rx = self.pc.rx
+            mine["worker"] = [bits(rx[o:o + n]) for (o, n) in shard_ranges(self.plong, len(self.sranks))]
+        if self.ps_server is not None:
+            self.ps_server.native.sync()
+            mine["server"] = bits(self.ps_server.p)
+        allv = W.allgather_obj(mine)
+        srv = {v["rank"]: v["server"] for v in allv if v["server"] is not None}
+        bad = []
+        for v in allv:
+            if v["worker"] is None:
+                continue
+            for k, s in enumerate(self.sranks):
+                if v["worker"][k] != srv.get(s):
+                    bad.append((v["rank"], s))
+        return {"ok": not bad and len(srv) == len(self.sranks), "shards": len(self.sranks),
+                "workers": sum(v["worker"] is not None for v in allv), "mismatches": bad[:8]}
 
     def run_server(self):
         """Block a dedicated server rank until all workers sent stop."""

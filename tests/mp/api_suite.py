@@ -118,8 +118,14 @@ W.Allreduce(a, a, mp.SUM)
 assert torch.all(a == n * (n + 1) / 2)
 ia = torch.full((1000,), 2.0, device=dev)
 req = W.Iallreduce(ia, ia, mp.SUM)
+if req._work is not None and r == 0:
+    print("DIST_WORK_REQUEST", flush=True)  # the torch.distributed branch (RCCL / gloo) ran
 req.Wait()
 assert req.Test() and torch.all(ia == 2.0 * n)
+# ring all-reduce (host point-to-point path for n > 2): odd length, every element checked
+big = torch.arange(100003, dtype=torch.float64, device=dev) * (r + 1)
+W.Allreduce(big, big, mp.SUM)
+assert torch.equal(big, torch.arange(100003, dtype=torch.float64, device=dev) * (n * (n + 1) / 2))
 ok("allreduce_iallreduce")
 
 # ---- reductions: MAX MIN PROD LAND BOR MAXLOC MINLOC, Reduce to root, user op

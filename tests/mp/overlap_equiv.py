@@ -1,0 +1,47 @@
+"""Downpour with the ShardPusher overlap (shards pushed and refreshed shards pulled into the
+model while the backward of earlier layers still runs, parallel/overlap.py) must produce
+bit-identical parameters to the non-overlapped path (push + pull after the backward).
+
+Run under torch.distributed.run with 3 ranks: 2 dedicated servers, 1 worker. For each
+precision (fp32, bf16 autocast) two PS instances train the same model from the same init on
+the same data, one with overlap, one without; the final pulled parameters are compared
+bit for bit (int64 sums of the fp32 words and an exact tensor compare on the worker)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import torch
+
+import mpit_amd as mp
+from mpit_amd.train import TrainConfig, Trainer, timed_steps
+
+model = os.environ.get("T_MODEL", "resnet18")
+steps = int(os.environ.get("T_STEPS", "4"))
+mp.Init()
+W = mp.COMM_WORLD()
+results = {}
+ps_id = 0
+for amp in (False, True):
+    finals = {}
+    for overlap in (True, False):
+        tr = Trainer(TrainConfig(model=model, batch=8, num_classes=10, optimizer="downpour", topology="dedicated",
+                                 servers=2, lr=0.05, amp=amp,
+                                 extra={"ps_id": ps_id, "overlap_push": overlap}))
+        ps_id += 1
+        if tr.is_worker:
+            assert ("pusher" in tr.opt_config) == overlap
+        timed_steps(tr, steps, 0)
+        chk = tr.verify_ps()
+        assert chk["ok"], chk
+        if tr.is_worker:
+            finals[overlap] = tr.flat.flat.detach().clone()
+        tr.stop()
+    if finals:
+        a, b = finals[True], finals[False]
+        same = bool(torch.equal(a.view(torch.int32), b.view(torch.int32)))
+        diff = float((a - b).abs().max())
+        results["bf16" if amp else "fp32"] = (same, diff)
+allr = [r for r in W.allgather_obj(results) if r]
+if W.Get_rank() == 0:
+    print("RESULT", allr, flush=True)
+mp.Finalize()

@@ -42,6 +42,20 @@ def test_api_suite_cpu(n):
     assert "ALL_DONE" in out
 
 
+@pytest.mark.parametrize("n", [2, 3])
+def test_api_suite_cpu_torch_distributed_branch(n):
+    """Every host collective through torch.distributed (gloo) instead of the shm
+    point-to-point algorithms: the branch HBM tensors take with RCCL on a multi-GPU node —
+    Iallreduce's Request(work=...), all_gather_into_tensor, all_to_all_single,
+    reduce_scatter_tensor, broadcast / reduce — runs here at least once; sub-communicators
+    stay on the point-to-point engine (comm.py Comm._use_rccl)."""
+    out = run_ranks("api_suite.py", n, {"MPIT_CPU_ONLY": "1", "MPIT_DIST_HOST": "1"}, timeout=300)
+    for c in CHECKS:
+        assert f"OK {c}" in out, (c, out[-3000:])
+    assert "ALL_DONE" in out
+    assert "DIST_WORK_REQUEST" in out
+
+
 @pytest.mark.gpu
 def test_api_suite_gpu_two_ranks_one_device():
     out = run_ranks("api_suite.py", 2, {"T_DEVICE": "cuda"}, timeout=300)

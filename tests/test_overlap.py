@@ -1,6 +1,12 @@
 """ShardPusher (parallel/overlap.py): shard-by-shard Downpour pushes from inside the
-backward. Checked on CPU against the one-shot gather of every gradient."""
+backward. Checked on CPU against the one-shot gather of every gradient, and on the GPU
+(real pulls landing mid-backward) against the non-overlapped path, bit for bit."""
+import re
+
+import pytest
 import torch
+
+from mp_util import run_ranks
 
 from mpit_amd.models import get_model
 from mpit_amd.parallel.overlap import ShardPusher
@@ -55,3 +61,18 @@ def test_shard_pusher_matches_one_shot_gather():
         torch.testing.assert_close(pc.tx[off:off + p.numel()].view_as(g), a * g)
         assert p.grad is None
     pusher.close()
+
+
+@pytest.mark.gpu
+def test_overlap_equals_non_overlapped_on_gpu_three_ranks():
+    """1 worker + 2 dedicated servers on the box's GPU: ResNet-18 Downpour steps with the
+    refreshed shards written into the model during the backward give exactly the parameters
+    of pushing / pulling after the backward, in fp32 and in bf16 autocast."""
+    out = run_ranks("overlap_equiv.py", 3, {"MPIT_WGRAD_STREAM": "force"}, timeout=400)
+    m = re.search(r"RESULT (.*)", out)
+    assert m, out[-3000:]
+    res = eval(m.group(1))
+    assert len(res) == 1, res
+    for prec in ("fp32", "bf16"):
+        same, diff = res[0][prec]
+        assert same, (prec, diff)

@@ -114,6 +114,48 @@ __device__ __forceinline__ float rnd(float v) {
   else return v;
 }
 
+// fp32 GEMMs on the bf16 matrix cores ("bf16x6", FM = 1): every fp32 operand is split
+// exactly into three bf16 terms, x = h + m + l (round-to-nearest h = bf16(x), m =
+// bf16(x - h), l = bf16(x - h - m); for normal numbers the three carry all 24 significant
+// bits), and a product is the sum of the six partial products whose order sum is <= 2:
+// hh + (hm + mh + mm + hl + lh). The dropped ml, lm, ll are below 2^-25 relative, and
+// bf16 x bf16 products are exact in the fp32 accumulators, so the result carries fp32
+// accuracy at 6 bf16 MFMAs per product (2.5 PF / 6 = 417 TF peak, against 157 TF for the
+// fp32-input MFMA). hh accumulates in its own registers, the five small terms in a second
+// set, so the big running sum is rounded once per 16-deep MFMA, not six times.
+__device__ __forceinline__ void split3(const float (&v)[8], bf16x8& h, bf16x8& m, bf16x8& l) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const __bf16 hb = static_cast<__bf16>(v[e]);
+    const float r1 = v[e] - static_cast<float>(hb);
+    const __bf16 mb = static_cast<__bf16>(r1);
+    const float r2 = r1 - static_cast<float>(mb);
+    h[e] = hb;
+    m[e] = mb;
+    l[e] = static_cast<__bf16>(r2);
+  }
+}
+template <int TM, int TN>
+__device__ __forceinline__ void mfma_x3(f32x16 (&hi)[TM][TN], f32x16 (&lo)[TM][TN], const bf16x8 (&ah)[TM],
+                                        const bf16x8 (&am)[TM], const bf16x8 (&al)[TM], const bf16x8 (&bh)[TN],
+                                        const bf16x8 (&bm)[TN], const bf16x8 (&bl)[TN], bool swap) {
+  // swap: D = B.A^T (the NT kernel's lane -> row-of-C layout), else D = A.B^T
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const bf16x8 &x0 = swap ? bh[j] : ah[i], &y0 = swap ? ah[i] : bh[j];
+      const bf16x8 &x1 = swap ? bm[j] : am[i], &y1 = swap ? am[i] : bm[j];
+      const bf16x8 &x2 = swap ? bl[j] : al[i], &y2 = swap ? al[i] : bl[j];
+      hi[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x0, y0, hi[i][j], 0, 0, 0);
+      lo[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, y0, lo[i][j], 0, 0, 0);
+      lo[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x0, y1, lo[i][j], 0, 0, 0);
+      lo[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x1, y1, lo[i][j], 0, 0, 0);
+      lo[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x2, y0, lo[i][j], 0, 0, 0);
+      lo[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(x0, y2, lo[i][j], 0, 0, 0);
+    }
+}
+
 // NHWC convolution geometry for the implicit-GEMM (CONV) kernel variants
 struct ConvGeo {
   int H, W, C;     // input image
@@ -225,7 +267,7 @@ __device__ __forceinline__ int xcd_tile(int bid, int nb) {
 // the tile about to be used (a __syncthreads() would drain the whole ring). The LDS image
 // is lane-linear per wave instruction (16 rows x 64 B); the swizzle is applied on the
 // global source address.
-template <typename T, int BM, int BN, int STAGES, int EPI, bool CONV>
+template <typename T, int BM, int BN, int STAGES, int EPI, bool CONV, int FM = 0>
 __global__ __launch_bounds__(256, sizeof(T) == 4 ? 2 : (BM == 256 ? (BN == 256 ? 1 : 2) : (STAGES == 2 ? (CONV || EPI == 3 ? 4 : 5) : 2))) void gemm_nt_kernel(const T* __restrict__ A, int64_t lda,
                                                          const T* __restrict__ B, int64_t ldb,
                                                          T* C, int64_t ldc, int64_t M, int N, int K,
@@ -319,7 +361,8 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? 2 : (BM == 256 ? (BN == 256 ?
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
 
-  // fp32: the running chain of the current block of tiles (see the MFMA loop)
+  // fp32: the running chain of the current block of tiles (native fp32 MFMA, see the MFMA
+  // loop) or the small-term accumulators of the split products (FM = 1)
   f32x16 tacc[F32 ? TM : 1][F32 ? TN : 1];
 #pragma unroll
   for (int i = 0; i < (F32 ? TM : 1); ++i)
@@ -361,6 +404,25 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? 2 : (BM == 256 ? (BN == 256 ?
         const int r = wn * WN + j * 32 + fr;
         bfg[j][0] = *reinterpret_cast<const float4*>(Bs + r * BK + swzk<BKB>(r, 2 * fh) * 4);
         bfg[j][1] = *reinterpret_cast<const float4*>(Bs + r * BK + swzk<BKB>(r, 2 * fh + 1) * 4);
+      }
+      if constexpr (FM == 1) {
+        // bf16x6: the lane's 8 floats of a row are exactly the k = 8fh + j operand of one
+        // v_mfma_f32_32x32x16_bf16 over the 16-deep tile; split each fragment in registers
+        bf16x8 ah[TM], am[TM], al[TM], bh[TN], bm[TN], bl[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const float v[8] = {af[i][0].x, af[i][0].y, af[i][0].z, af[i][0].w,
+                              af[i][1].x, af[i][1].y, af[i][1].z, af[i][1].w};
+          split3(v, ah[i], am[i], al[i]);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const float v[8] = {bfg[j][0].x, bfg[j][0].y, bfg[j][0].z, bfg[j][0].w,
+                              bfg[j][1].x, bfg[j][1].y, bfg[j][1].z, bfg[j][1].w};
+          split3(v, bh[j], bm[j], bl[j]);
+        }
+        mfma_x3<TM, TN>(acc, tacc, ah, am, al, bh, bm, bl, true);
+        continue;
       }
       auto el = [](const float4 (&q)[2], int s) -> float {
         const float4& h = q[s >> 2];
@@ -445,6 +507,13 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? 2 : (BM == 256 ? (BN == 256 ?
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfg[j], af[i], acc[i][j], 0, 0, 0);
     }
     }
+  }
+
+  if constexpr (F32 && FM == 1) {  // hh + the five small terms
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] += tacc[i][j];
   }
 
   // ---- epilogue, phase A: accumulators (+ bias, ReLU) -> T tile in LDS. Lane holds
@@ -693,7 +762,7 @@ __device__ __forceinline__ int tswz(int row, int ch) {
   else return ch ^ (((row >> 1) & 1) << 2);
 }
 
-template <typename T, int TBN, int TBK, int STAGES, bool CONV>
+template <typename T, int TBN, int TBK, int STAGES, bool CONV, int FM = 0>
 __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y, int64_t ldy,
                                                          const T* __restrict__ X, int64_t ldx,
                                                          float* __restrict__ part, int64_t M, int N, int K,
@@ -818,6 +887,14 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y
   const int h = g >> 1;
   const int cbase = 2 * (g & 1) + (p >> 1), cbyte = 4 * (p & 1);  // chunk / element offset in it
   const int fr = lane & 31, fh = lane >> 5;
+  // fp32 split products (FM = 1): the small-term accumulators
+  f32x16 lacc[F32 ? TM : 1][F32 ? TN : 1];
+#pragma unroll
+  for (int i = 0; i < (F32 ? TM : 1); ++i)
+#pragma unroll
+    for (int j = 0; j < (F32 ? TN : 1); ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) lacc[i][j][v] = 0.f;
 
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
@@ -842,7 +919,32 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y
       __syncthreads();
     }
     if (st + STAGES - 1 < nsteps) issue(st + STAGES - 1, int((st + STAGES - 1) % STAGES));
-    if constexpr (F32) {
+    if constexpr (F32 && FM == 1) {
+      // bf16x6 (see split3): lane (fr, fh) of a 16-row step holds Y[16kk + 8fh + j][n0' + fr]
+      // and X[16kk + 8fh + j][k0' + fr], j = 0..7 — the k = 8fh + j operands of one
+      // v_mfma_f32_32x32x16_bf16, read down a column (ds_read_b32, 32 consecutive floats
+      // per half-wave: conflict-free) and split in registers
+#pragma unroll
+      for (int kk = 0; kk < kRows / 16; ++kk) {
+        const int r0 = 16 * kk + 8 * fh;
+        bf16x8 ah[TM], am[TM], al[TM], bh[TN], bm[TN], bl[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          float v[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = Ys[(r0 + e) * TBN + wn * WN + i * 32 + fr];
+          split3(v, ah[i], am[i], al[i]);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          float v[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = Xs[(r0 + e) * TBK + wk * WK + j * 32 + fr];
+          split3(v, bh[j], bm[j], bl[j]);
+        }
+        mfma_x3<TM, TN>(acc, lacc, ah, am, al, bh, bm, bl, false);
+      }
+    } else if constexpr (F32) {
       // v_mfma_f32_32x32x2_f32: lane (fr, fh) supplies Y[row][n0' + fr] and X[row][k0' + fr]
       // of row 2s + fh in step s (32 consecutive floats per half-wave: ds_read_b32, no
       // conflicts). Each staged step is one fresh 32-long fmaf chain folded into acc (blocked
@@ -896,6 +998,12 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
     }
     }
+  }
+  if constexpr (F32 && FM == 1) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] += lacc[i][j];
   }
   // D[n][k]: column k = lane&31, row n = (v&3) + 8*(v>>2) + 4*(lane>>5)
   float* out = part + int64_t(split) * N * K;
@@ -1070,6 +1178,16 @@ static int nt_tile_config(int N, int K, bool conv, int cin_conv, bool f32) {
   return cfg;
 }
 
+// fp32 GEMM mode: 1 = bf16x6 split products on the bf16 MFMA (default), 0 = the fp32-input
+// MFMA (exact fmaf chains, 1/2.7 of the split path's peak). MPIT_F32_MFMA=native selects 0.
+static int f32_mode() {
+  static const int m = [] {
+    const char* e = std::getenv("MPIT_F32_MFMA");
+    return e && std::string(e) == "native" ? 0 : 1;
+  }();
+  return m;
+}
+
 template <typename T>
 static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B,
                         int64_t ldb, uintptr_t C, int64_t ldc, uintptr_t cin, uintptr_t cmask, const ConvGeo* geo,
@@ -1123,11 +1241,20 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
                                                reinterpret_cast<const void*>(&gemm_nt_kernel<T, BM, BN, ST, EPI, CONV>), \
                                                hipFuncAttributeMaxDynamicSharedMemorySize, int(shm)),                \
                                            "hipFuncSetAttribute"),                                                   \
+                                 hip_check(hipFuncSetAttribute(                                                      \
+                                               reinterpret_cast<const void*>(                                        \
+                                                   &gemm_nt_kernel<T, BM, BN, ST, EPI, CONV, F32 ? 1 : 0>),          \
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, int(shm)),                \
+                                           "hipFuncSetAttribute"),                                                   \
                                  true);                                                                              \
       (void)opted;                                                                                                   \
     }                                                                                                                \
-    hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, ST, EPI, CONV>), dim3(unsigned(nb)), dim3(256), shm, s, a,       \
-                       lda, b, ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g);                             \
+    if (F32 && f32_mode() == 1)                                                                                    \
+      hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, ST, EPI, CONV, F32 ? 1 : 0>), dim3(unsigned(nb)), dim3(256), shm, \
+                         s, a, lda, b, ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g);                          \
+    else                                                                                                           \
+      hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, ST, EPI, CONV>), dim3(unsigned(nb)), dim3(256), shm, s, a,     \
+                         lda, b, ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g);                           \
   } while (0)
 #define MPIT_NT_LAUNCH2(BM, BN, ST, CONV)                                                         \
   do {                                                                                              \
@@ -1284,7 +1411,13 @@ static void launch_tn_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
 #define MPIT_TN_LAUNCH1(A, B, ST)                                                                                  \
   do {                                                                                                             \
     const size_t shm = size_t(ST) * kRows * (tbn + tbk) * sizeof(T);                                             \
-    if (geo)                                                                                                       \
+    if (geo && F32 && f32_mode() == 1)                                                                           \
+      hipLaunchKernelGGL((gemm_tn_kernel<T, A, B, ST, true, F32 ? 1 : 0>), grid, dim3(256), shm, s, y, ldy, x,     \
+                         ldx, part, M, N, K, rps, ntk, ntiles, g);                                                 \
+    else if (F32 && f32_mode() == 1)                                                                               \
+      hipLaunchKernelGGL((gemm_tn_kernel<T, A, B, ST, false, F32 ? 1 : 0>), grid, dim3(256), shm, s, y, ldy, x,    \
+                         ldx, part, M, N, K, rps, ntk, ntiles, g);                                                 \
+    else if (geo)                                                                                                  \
       hipLaunchKernelGGL((gemm_tn_kernel<T, A, B, ST, true>), grid, dim3(256), shm, s, y, ldy, x, ldx, part, M, N, \
                          K, rps, ntk, ntiles, g);                                                                  \
     else                                                                                                           \

@@ -365,7 +365,8 @@ PYBIND11_MODULE(_mpit, m) {
       .def("send_grad", [](PSClient& c, uintptr_t s, bool pull) { c.send_grad(S(s), pull); })
       .def("send_grad_to", [](PSClient& c, uintptr_t s, int k, bool pull) { c.send_grad_to(S(s), k, pull); })
       .def("recv_param", [](PSClient& c, uintptr_t s) { c.recv_param(S(s)); })
-      .def("send_param", [](PSClient& c, uintptr_t s) { c.send_param(S(s)); })
+      .def("send_param", [](PSClient& c, uintptr_t s, bool from_rx) { c.send_param(S(s), from_rx); },
+           py::arg("stream"), py::arg("from_rx") = false)
       .def("stop", &PSClient::stop, py::call_guard<py::gil_scoped_release>())
       .def("wait", &PSClient::wait, py::call_guard<py::gil_scoped_release>())
       .def("test", &PSClient::test)

@@ -65,7 +65,7 @@ void Engine::shutdown() {
     }
     {
       std::lock_guard<std::mutex> g(ipc_mu_);
-      for (auto& kv : ipc_cache_) hipIpcCloseMemHandle(kv.second);
+      for (auto& kv : ipc_cache_) hipIpcCloseMemHandle(kv.second.ptr);
       ipc_cache_.clear();
     }
     if (stream_) hipStreamDestroy(stream_);
@@ -145,16 +145,59 @@ void Engine::export_ptr(const void* p, hipIpcMemHandle_t* h, int64_t* offset, in
   if (alloc_bytes) *alloc_bytes = int64_t(sz);
 }
 
-void* Engine::open_ipc(int owner_rank, const hipIpcMemHandle_t& h) {
+void Engine::export_cached(const void* p, hipIpcMemHandle_t* h, int64_t* offset) {
+  hipDeviceptr_t base = nullptr;
+  size_t sz = 0;
+  hipc(hipMemGetAddressRange(&base, &sz, const_cast<void*>(p)), "hipMemGetAddressRange");
+  uint64_t id = 0;
+  hipc(hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, reinterpret_cast<hipDeviceptr_t>(const_cast<void*>(p))),
+       "hipPointerGetAttribute(BUFFER_ID)");
+  *offset = int64_t(reinterpret_cast<const uint8_t*>(p) - reinterpret_cast<const uint8_t*>(base));
+  std::lock_guard<std::mutex> g(export_mu_);
+  auto it = export_cache_.find(id);
+  if (it != export_cache_.end() && it->second.second == reinterpret_cast<uintptr_t>(base)) {
+    *h = it->second.first;
+    return;
+  }
+  hipc(hipIpcGetMemHandle(h, base), "hipIpcGetMemHandle");
+  if (export_cache_.size() > 4096) export_cache_.clear();  // bounded; entries are cheap to redo
+  export_cache_[id] = {*h, reinterpret_cast<uintptr_t>(base)};
+}
+
+void* Engine::open_ipc(int owner_rank, const hipIpcMemHandle_t& h, bool permanent) {
   std::string key(reinterpret_cast<const char*>(&h), sizeof(h));
   std::lock_guard<std::mutex> g(ipc_mu_);
   auto it = ipc_cache_.find({owner_rank, key});
-  if (it != ipc_cache_.end()) return it->second;
+  if (it != ipc_cache_.end()) {
+    it->second.last_use = ++ipc_tick_;
+    it->second.inflight += permanent ? kPinned : 1;
+    return it->second.ptr;
+  }
+  if (ipc_cache_.size() >= kIpcCacheMax) {  // close the least recently used idle mapping
+    auto victim = ipc_cache_.end();
+    for (auto v = ipc_cache_.begin(); v != ipc_cache_.end(); ++v)
+      if (v->second.inflight == 0 && (victim == ipc_cache_.end() || v->second.last_use < victim->second.last_use))
+        victim = v;
+    if (victim != ipc_cache_.end()) {
+      hipIpcCloseMemHandle(victim->second.ptr);
+      ipc_cache_.erase(victim);
+    }
+  }
   hipc(hipSetDevice(device_), "hipSetDevice");
   void* p = nullptr;
   hipc(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle");
-  ipc_cache_[{owner_rank, key}] = p;
+  IpcMapping mp;
+  mp.ptr = p;
+  mp.last_use = ++ipc_tick_;
+  mp.inflight = permanent ? kPinned : 1;
+  ipc_cache_[{owner_rank, key}] = mp;
   return p;
+}
+
+void Engine::release_ipc(int owner_rank, const std::string& key) {
+  std::lock_guard<std::mutex> g(ipc_mu_);
+  auto it = ipc_cache_.find({owner_rank, key});
+  if (it != ipc_cache_.end() && it->second.inflight > 0) --it->second.inflight;
 }
 
 // --------------------------------------------------------------------------- p2p API
@@ -308,9 +351,23 @@ void Engine::deliver_locked(Incoming& in) {
   }
   if (!in.data.empty() && n > 0) {
     if (r->rdev) {
+      // host payload into HBM: the copy completes (and the request finishes, the sync-send
+      // ack goes out) on the progress thread's copy poll — no stream synchronise under mu_,
+      // which would stall every other message until the copy landed
       hipc(hipSetDevice(device_), "hipSetDevice");
-      hipc(hipMemcpyAsync(r->rbuf, in.data.data(), size_t(n), hipMemcpyHostToDevice, stream_), "hipMemcpyAsync(H2D)");
-      hipc(hipStreamSynchronize(stream_), "hipStreamSynchronize");
+      auto keep = std::make_shared<std::vector<uint8_t>>(std::move(in.data));
+      hipc(hipMemcpyAsync(r->rbuf, keep->data(), size_t(n), hipMemcpyHostToDevice, stream_), "hipMemcpyAsync(H2D)");
+      hipEvent_t ev;
+      hipc(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+      hipc(hipEventRecord(ev, stream_), "hipEventRecord");
+      r->st.source = h.src;
+      r->st.tag = h.tag;
+      r->st.count = n;
+      bytes_recv_.fetch_add(n, std::memory_order_relaxed);
+      PendingCopy pc{ev, r, (h.flags & MF_SYNC) ? h.src : -1, h.aux1, [keep] {}};
+      std::lock_guard<std::mutex> g(copy_mu_);
+      copies_.push_back(std::move(pc));
+      return;
     } else if (r->rbuf != in.data.data()) {
       std::memcpy(r->rbuf, in.data.data(), size_t(n));
     }
@@ -347,20 +404,27 @@ void Engine::start_dev_pull_locked(Incoming& in) {
   }
   hipc(hipSetDevice(device_), "hipSetDevice");
   const void* remote;
+  std::string ipc_key;
   if (h.src == rank_) {
     remote = reinterpret_cast<const void*>(h.aux2);
   } else {
     hipIpcMemHandle_t hd;
     std::memcpy(&hd, h.data, sizeof(hd));
-    remote = static_cast<const uint8_t*>(open_ipc(h.src, hd)) + h.aux0;
+    ipc_key.assign(reinterpret_cast<const char*>(&hd), sizeof(hd));
+    remote = static_cast<const uint8_t*>(open_ipc(h.src, hd, false)) + h.aux0;
   }
   if (n > 0) hipc(hipMemcpyAsync(r->rbuf, remote, size_t(n), hipMemcpyDefault, stream_), "hipMemcpyAsync(pull)");
   hipEvent_t ev;
   hipc(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
   hipc(hipEventRecord(ev, stream_), "hipEventRecord");
   bytes_recv_.fetch_add(n, std::memory_order_relaxed);
+  PendingCopy pc{ev, r, h.src, h.aux1, nullptr};
+  if (!ipc_key.empty()) {
+    pc.ipc_owner = h.src;
+    pc.ipc_key = std::move(ipc_key);
+  }
   std::lock_guard<std::mutex> g(copy_mu_);
-  copies_.push_back(PendingCopy{ev, r, h.src, h.aux1, nullptr});
+  copies_.push_back(std::move(pc));
 }
 
 void Engine::on_header_locked(int src, const Msg& h) {
@@ -474,7 +538,7 @@ bool Engine::progress_sends_locked() {
             hipIpcMemHandle_t hd;
             int64_t off = 0;
             hipc(hipSetDevice(device_), "hipSetDevice");
-            export_ptr(r->sbuf, &hd, &off, nullptr);
+            export_cached(r->sbuf, &hd, &off);
             std::memcpy(m.data, &hd, sizeof(hd));
             m.aux0 = off;
           }
@@ -544,6 +608,7 @@ bool Engine::progress_copies() {
   if (done.empty()) return false;
   for (auto& c : done) {
     hipEventDestroy(c.ev);
+    if (c.ipc_owner >= 0) release_ipc(c.ipc_owner, c.ipc_key);
     if (c.req) {
       std::lock_guard<std::mutex> g(mu_);
       if (c.ack_to >= 0) {

@@ -87,6 +87,14 @@ struct PendingCopy {  // an outstanding hipMemcpyAsync whose completion finishes
   int ack_to = -1;      // rank to send MK_ACK to on completion (rendezvous)
   int64_t ack_id = 0;
   std::function<void()> then;  // optional continuation (runs on the progress thread)
+  int ipc_owner = -1;          // an IPC mapping the copy reads (released on completion)
+  std::string ipc_key;
+};
+
+struct IpcMapping {  // an opened peer allocation (receiver side)
+  void* ptr = nullptr;
+  uint64_t last_use = 0;
+  int64_t inflight = 0;  // copies reading it; permanent (window) mappings hold kPinned
 };
 
 class Engine {
@@ -131,7 +139,13 @@ class Engine {
   hipStream_t comm_stream() const { return stream_; }
   // IPC helpers (also used by windows)
   static void export_ptr(const void* p, hipIpcMemHandle_t* h, int64_t* offset, int64_t* alloc_bytes);
-  void* open_ipc(int owner_rank, const hipIpcMemHandle_t& h);
+  // export with a per-allocation handle cache (keyed by the allocation's unique buffer id,
+  // so a recycled address range never reuses a stale handle)
+  void export_cached(const void* p, hipIpcMemHandle_t* h, int64_t* offset);
+  // open (or reuse) a peer allocation. permanent: a window mapping, never evicted;
+  // otherwise the caller holds it for one copy and returns it with release_ipc
+  void* open_ipc(int owner_rank, const hipIpcMemHandle_t& h, bool permanent = true);
+  void release_ipc(int owner_rank, const std::string& key);
 
   // statistics
   int64_t bytes_sent() const { return bytes_sent_.load(); }
@@ -186,7 +200,14 @@ class Engine {
   int next_hook_ = 1;
 
   std::mutex ipc_mu_;
-  std::map<std::pair<int, std::string>, void*> ipc_cache_;
+  std::map<std::pair<int, std::string>, IpcMapping> ipc_cache_;
+  uint64_t ipc_tick_ = 0;
+  // LRU bound on transient peer mappings: a mapping keeps the exporter's (possibly freed
+  // and recycled) allocation alive, so idle ones are closed once the cache is full
+  static constexpr size_t kIpcCacheMax = 256;
+  static constexpr int64_t kPinned = int64_t(1) << 40;
+  std::mutex export_mu_;
+  std::unordered_map<uint64_t, std::pair<hipIpcMemHandle_t, uintptr_t>> export_cache_;  // buffer id -> (handle, base)
 
   std::atomic<int64_t> bytes_sent_{0}, bytes_recv_{0}, msgs_sent_{0};
   std::atomic<uint64_t> activity_{0};

@@ -32,6 +32,7 @@ PSServer::PSServer(Engine& eng, int ps_id, Window& rx, Window& tx, std::vector<i
       p_(reinterpret_cast<void*>(p)),
       inbox_(reinterpret_cast<void*>(inbox)),
       rule_(rule),
+      lr_(rule.lr),
       datapath_(datapath),
       staleness_(staleness),
       grad_bf16_(grad_bf16),
@@ -120,7 +121,7 @@ void PSServer::on_msg(const Msg& m) {
                      (long long)m.aux0, (long long)m.aux1, (long long)off_, (long long)len_);
       break;
     case kTagParam:
-      do_param(m.src);
+      do_param(m.src, (m.aux0 & kPsFromRx) != 0);
       if (init_rank_ >= 0 && m.src == init_rank_) {
         init_rank_ = -1;
         std::vector<Msg> later;
@@ -183,7 +184,8 @@ void PSServer::apply_rule(const void* g, void* out) {
     if (int(k) < need[rule_.kind]) ptrs.push_back(P(st_[k]));
   }
   if (out) ptrs.push_back(P(out));
-  const ServerRule& r = rule_;
+  ServerRule r = rule_;  // progress thread only; lr may be changed concurrently (set_lr)
+  r.lr = lr_.load(std::memory_order_relaxed);
   switch (r.kind) {
     case 0:
       ew_update(kApply, v, dev, stream_, len_, ptrs, bf, {r.a});
@@ -218,15 +220,17 @@ void PSServer::apply_rule(const void* g, void* out) {
   version_.fetch_add(1);
 }
 
-void PSServer::do_param(int c) {
+void PSServer::do_param(int c, bool from_rx) {
   const int m = member_of(c);
-  const int64_t es = grad_bf16_ ? 2 : 4;
-  const uint8_t* src = reinterpret_cast<const uint8_t*>(tx_.remote_ptr(m)) + off_ * es;
-  if (!device_ && tx_.remote_device(m)) throw std::runtime_error("mpit: host server cannot read a device tx window");
+  const Window& w = from_rx ? rx_ : tx_;  // rx is always fp32
+  const bool bf = grad_bf16_ && !from_rx;
+  const int64_t es = bf ? 2 : 4;
+  const uint8_t* src = reinterpret_cast<const uint8_t*>(w.remote_ptr(m)) + off_ * es;
+  if (!device_ && w.remote_device(m)) throw std::runtime_error("mpit: host server cannot read a device window");
   if (device_) hipp(hipSetDevice(eng_.device()), "hipSetDevice");
-  // p (fp32) = tx shard (fp32 | bf16): one copy / cast kernel, or a host loop
+  // p (fp32) = pushed shard (fp32 | bf16): one copy / cast kernel, or a host loop
   ew_update(kCopy, 0, device_ ? eng_.device() : -1, stream_, len_,
-            {reinterpret_cast<uintptr_t>(p_), reinterpret_cast<uintptr_t>(src)}, grad_bf16_ ? 2u : 0u, {1.f});
+            {reinterpret_cast<uintptr_t>(p_), reinterpret_cast<uintptr_t>(src)}, bf ? 2u : 0u, {1.f});
   {
     std::lock_guard<std::mutex> g(mu_);
     ++stats_.param_pushes;
@@ -389,7 +393,7 @@ ServerStats PSServer::stats() const {
   return stats_;
 }
 
-void PSServer::set_lr(float lr) { rule_.lr = lr; }
+void PSServer::set_lr(float lr) { lr_.store(lr, std::memory_order_relaxed); }
 
 void PSServer::sync() {
   if (device_) {
@@ -490,10 +494,10 @@ void PSClient::recv_param(hipStream_t s) {
   });
 }
 
-void PSClient::send_param(hipStream_t s) {
+void PSClient::send_param(hipStream_t s, bool from_rx) {
   pending_.fetch_add(int64_t(servers_.size()));
-  gate(s, [this] {
-    for (int srv : servers_) eng_.send_am(srv, ps_am_id(ps_id_, kTagParam), nullptr, 0);
+  gate(s, [this, from_rx] {
+    for (int srv : servers_) eng_.send_am(srv, ps_am_id(ps_id_, kTagParam), nullptr, 0, from_rx ? kPsFromRx : 0);
   });
 }
 

@@ -52,7 +52,10 @@ enum PsTag : int {
   kTagParamTail = 7,
   kTagGradTail = 8,
 };
-enum PsFlags : int64_t { kPsWithPull = 1 };
+// kPsWithPull (tag 2): reply with the refreshed shard; kPsFromRx (tag 4): the pushed
+// parameters are in the client's fp32 rx window, not its tx window (an EASGD client whose
+// wire is bf16 initialises the shards with exact fp32 weights).
+enum PsFlags : int64_t { kPsWithPull = 1, kPsFromRx = 2 };
 
 inline int ps_am_id(int ps_id, int tag) { return 4096 + ps_id * 16 + tag; }
 
@@ -89,7 +92,7 @@ class PSServer {
 
  private:
   void on_msg(const Msg& m);
-  void do_param(int c);
+  void do_param(int c, bool from_rx = false);
   void do_grad(int c, bool pull);
   void do_pull(int c);
   void apply_rule(const void* g, void* out);
@@ -111,6 +114,7 @@ class PSServer {
   std::vector<void*> st_;
   void* inbox_;
   ServerRule rule_;
+  std::atomic<float> lr_;  // rule_.lr, changed by set_lr from the caller's thread while the progress thread runs
   int datapath_;
   int64_t staleness_;
   bool grad_bf16_;
@@ -148,7 +152,7 @@ class PSClient {
   void send_grad_to(hipStream_t s, int k, bool with_pull);
   void recv_param(hipStream_t s);  // tag 5 header -> tag 3 once the shard landed in rx;
                                    // gated on s when rx is still being read there
-  void send_param(hipStream_t s);
+  void send_param(hipStream_t s, bool from_rx = false);
   void stop();
   void wait();             // until every outstanding reply arrived (GIL released)
   bool test() const { return pending_.load() == 0; }

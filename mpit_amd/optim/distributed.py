@@ -139,6 +139,10 @@ def eamsgd(opfunc, w, config, state=None):
 
     def localupdate(sug=None):
         if lr == 0:
+            # no local step (and no pversion increment), but the elastic correction still
+            # applies: w -= sug (asyncsgd/optim-eamsgd.lua:69-70 runs it whatever the lr)
+            if sug is not None:
+                ops.axpby_(w, sug, -1.0, 1.0)
             return
         pv = state["pversion"]
         vt = None

@@ -96,8 +96,12 @@ class ShardPusher:
                 continue
             p = self.params[i]
             g = p.grad
-            if g is None:  # unused this step: its slice of the push window is zero
-                self.pc.tx[self.flat.offsets[i]: self.flat.offsets[i] + p.numel()].zero_()
+            if g is None:  # unused this step: no gradient, but weight decay still applies
+                sl = slice(self.flat.offsets[i], self.flat.offsets[i] + p.numel())
+                if self.aux is not None and self.b != 0.0:  # a*0 + b*aux (optim-downpour.lua:24)
+                    torch.mul(self.aux[sl], self.b, out=self.pc.tx[sl])
+                else:
+                    self.pc.tx[sl].zero_()
             else:
                 if g.dim() == 4 and self.flat.channels_last:
                     g = g.contiguous(memory_format=torch.channels_last)

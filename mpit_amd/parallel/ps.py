@@ -347,8 +347,16 @@ class PClient:
 
     def async_send_param(self, src: Optional[torch.Tensor] = None):
         """Push parameters (``src``, default the bound parameter tensor) to the servers,
-        which overwrite their shards (tag 4, acked with tag 7)."""
-        self._stage_out(self._user_p if src is None else src)
+        which overwrite their shards (tag 4, acked with tag 7). With a bf16 push window the
+        parameters travel through the fp32 rx window instead (staged there when ``src`` is
+        another tensor), so the shards get the exact fp32 values (BiCNN/pserver.lua:272-278)."""
+        src = self._user_p if src is None else src
+        if self.grad_dtype == torch.bfloat16:
+            if src is not None and src.data_ptr() != self.rx.data_ptr():
+                self.rx.copy_(src.reshape(-1))
+            self.native.send_param(self._stream(), True)
+            return
+        self._stage_out(src)
         self.native.send_param(self._stream())
 
     def ping(self, nb: Optional[int] = None):

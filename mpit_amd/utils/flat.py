@@ -119,6 +119,12 @@ class StolenGrads:
         srcs, offs, ns = self._table()
         if len(srcs) < len(self.flat.params):
             dst.zero_()
+            if aux is not None and b != 0.0:
+                # parameters without a gradient this step still get the weight-decay term:
+                # the reference adds l2wd*w to the whole dfdx (asyncsgd/optim-downpour.lua:24)
+                for p, off in zip(self.flat.params, self.flat.offsets):
+                    if p.grad is None:
+                        torch.mul(aux[off: off + p.numel()], b, out=dst[off: off + p.numel()])
         gather_scale_(dst, srcs, offs, ns, a, aux, b)
         for p in self.flat.params:
             p.grad = None

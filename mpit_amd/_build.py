@@ -6,7 +6,12 @@ the HIP headers; one shared object links them with libamdhip64. No torch headers
 involved, so a clean build takes well under a minute on 8 cores and cross-compiles on a
 machine without a GPU. Objects are rebuilt only when a source or header is newer.
 
-Usage: ``python -m mpit_amd._build [-j N] [--force]``
+Usage: ``python -m mpit_amd._build [-j N] [--force] [--sanitize address|thread]``
+
+``--sanitize`` builds a host-sanitized variant into ``build/san_<kind>/`` (ASan / TSan on
+the host code: the runtime in csrc/core and the host side of the kernel files, the device
+code untouched), loaded instead of the in-tree module when ``MPIT_NATIVE_SO`` names it;
+scripts/sanitize.sh runs the multi-process suites under both (CPU, MPIT_CPU_ONLY=1).
 """
 from __future__ import annotations
 
@@ -51,20 +56,27 @@ def _headers() -> list[str]:
     return glob.glob(os.path.join(CSRC, "**", "*.h"), recursive=True)
 
 
-def _jobs() -> list[tuple[str, str, list[str]]]:
+def _san_flags(san):
+    return [f"-fsanitize={san}", "-fno-omit-frame-pointer", "-g"] if san else []
+
+
+def _jobs(san=None, build_dir=BUILD) -> list[tuple[str, str, list[str]]]:
     jobs = []
     hipcc = os.path.join(ROCM, "bin", "hipcc")
     clang = os.path.join(ROCM, "llvm", "bin", "clang++")
     if not os.path.exists(clang):
         clang = os.path.join(ROCM, "bin", "amdclang++")
+    # hipcc lines: the sanitizer applies to the host compilation only (-Xarch_host before
+    # each -fsanitize=), the gfx950 device code is built as usual
+    kflags = [f for x in _san_flags(san) for f in (["-Xarch_host", x] if x.startswith("-fsanitize") else [x])]
     for src in sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip"))):
-        obj = os.path.join(BUILD, "k_" + os.path.basename(src) + ".o")
-        cmd = [hipcc, f"--offload-arch={ARCH}", "-munsafe-fp-atomics"] + _common_flags() + ["-c", src, "-o", obj]
+        obj = os.path.join(build_dir, "k_" + os.path.basename(src) + ".o")
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-munsafe-fp-atomics"] + _common_flags() + kflags + ["-c", src, "-o", obj]
         jobs.append((src, obj, cmd))
     host_srcs = sorted(glob.glob(os.path.join(CSRC, "core", "*.cpp"))) + [os.path.join(CSRC, "bindings.cpp")]
     for src in host_srcs:
-        obj = os.path.join(BUILD, "h_" + os.path.basename(src) + ".o")
-        cmd = [clang, "-x", "c++"] + _common_flags() + [
+        obj = os.path.join(build_dir, "h_" + os.path.basename(src) + ".o")
+        cmd = [clang, "-x", "c++"] + _common_flags() + _san_flags(san) + [
             f"-I{_pybind_include()}",
             f"-I{sysconfig.get_paths()['include']}",
             "-fvisibility=hidden",
@@ -84,10 +96,14 @@ def _stale(src: str, obj: str, hdr_mtime: float) -> bool:
     return os.path.getmtime(src) > t or hdr_mtime > t
 
 
-def build(jobs: int = 8, force: bool = False, verbose: bool = False) -> str:
-    os.makedirs(BUILD, exist_ok=True)
+def build(jobs: int = 8, force: bool = False, verbose: bool = False, sanitize: str = None) -> str:
+    build_dir = BUILD if not sanitize else os.path.join(ROOT, "build", f"obj_{sanitize}")
+    target = TARGET if not sanitize else os.path.join(ROOT, "build", f"san_{sanitize}", "_mpit" + EXT)
+    os.makedirs(build_dir, exist_ok=True)
+    os.makedirs(os.path.dirname(target), exist_ok=True)
     hdr_mtime = max([os.path.getmtime(h) for h in _headers()] + [0.0])
-    todo = [(s, o, c) for (s, o, c) in _jobs() if force or _stale(s, o, hdr_mtime)]
+    all_jobs = _jobs(sanitize, build_dir)
+    todo = [(s, o, c) for (s, o, c) in all_jobs if force or _stale(s, o, hdr_mtime)]
 
     def run(job):
         src, obj, cmd = job
@@ -102,11 +118,14 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = False) -> str:
         for src in ex.map(run, todo):
             if verbose:
                 print("built", os.path.relpath(src, ROOT), flush=True)
-    objs = [o for (_, o, _) in _jobs()]
+    objs = [o for (_, o, _) in all_jobs]
     newest = max(os.path.getmtime(o) for o in objs)
-    if force or todo or not os.path.exists(TARGET) or os.path.getmtime(TARGET) < newest:
+    if force or todo or not os.path.exists(target) or os.path.getmtime(target) < newest:
         hipcc = os.path.join(ROCM, "bin", "hipcc")
-        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", TARGET] + objs + [
+        # sanitized variant: the shared sanitizer runtime comes from LD_PRELOAD (Python is not
+        # instrumented), the module only references it
+        san = ["-Xarch_host", f"-fsanitize={sanitize}", "-shared-libsan"] if sanitize else []
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC"] + san + ["-o", target] + objs + [
             f"-L{ROCM}/lib",
             "-lamdhip64",
             "-lrt",
@@ -118,7 +137,7 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = False) -> str:
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed\n{r.stdout}\n{r.stderr}")
-    return TARGET
+    return target
 
 
 def main(argv=None) -> int:
@@ -126,8 +145,9 @@ def main(argv=None) -> int:
     ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 1))
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-v", action="store_true")
+    ap.add_argument("--sanitize", choices=["address", "thread"], default=None)
     a = ap.parse_args(argv)
-    print(build(a.j, a.force, a.v))
+    print(build(a.j, a.force, a.v, a.sanitize))
     return 0
 
 

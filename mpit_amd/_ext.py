@@ -21,6 +21,16 @@ def native():
     with _lock:
         if _mod is not None:
             return _mod
+        so = os.environ.get("MPIT_NATIVE_SO")
+        if so:  # an explicitly built variant (e.g. the sanitizer builds of _build.py)
+            import importlib.util
+            import sys
+
+            spec = importlib.util.spec_from_file_location("mpit_amd._mpit", so)
+            _mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(_mod)
+            sys.modules["mpit_amd._mpit"] = _mod
+            return _mod
         try:
             _mod = importlib.import_module("mpit_amd._mpit")
         except ImportError:

@@ -351,6 +351,8 @@ PYBIND11_MODULE(_mpit, m) {
       .def("done", &PSServer::done)
       .def("wait_done", &PSServer::wait_done, py::call_guard<py::gil_scoped_release>())
       .def("version", &PSServer::version)
+      .def("step", &PSServer::step)
+      .def("set_counters", &PSServer::set_counters)
       .def("set_lr", &PSServer::set_lr)
       .def("sync", &PSServer::sync, py::call_guard<py::gil_scoped_release>())
       .def("stats", [](PSServer& s) {

@@ -1,4 +1,5 @@
 #include "ps.h"
+#include "trace.h"
 
 #include <cmath>
 #include <cstdio>
@@ -195,19 +196,19 @@ void PSServer::apply_rule(const void* g, void* out) {
       break;
     case 2: {  // BiCNN/pserver.lua:147-154: bias correction on floor(t/stepDiv)+1
       ++t_;
-      const double k = double(t_ / std::max<int64_t>(1, r.step_div) + 1);
+      const double k = double(t_.load() / std::max<int64_t>(1, r.step_div) + 1);
       const double lr_t = r.lr * std::sqrt(1.0 - std::pow(double(r.b2), k)) / (1.0 - std::pow(double(r.b1), k));
       ew_update(kAdam, v, dev, stream_, len_, ptrs, bf, {r.b1, r.b2, r.eps, float(lr_t)});
       break;
     }
     case 3: {  // BiCNN/pserver.lua:163-170
       ++t_;
-      const double lr_t = r.lr / (1.0 - std::pow(double(r.b1), double(t_)));
+      const double lr_t = r.lr / (1.0 - std::pow(double(r.b1), double(t_.load())));
       ew_update(kAdamax, v, dev, stream_, len_, ptrs, bf, {r.b1, r.b2, r.eps, float(lr_t)});
       break;
     }
     case 4: {  // BiCNN/pserver.lua:177-182
-      const float clr = float(r.lr / (1.0 + double(t_) * r.lrd));
+      const float clr = float(r.lr / (1.0 + double(t_.load()) * r.lrd));
       ++t_;
       ew_update(kAdagrad, v, dev, stream_, len_, ptrs, bf, {r.eps, clr});
       break;
@@ -221,6 +222,7 @@ void PSServer::apply_rule(const void* g, void* out) {
 }
 
 void PSServer::do_param(int c, bool from_rx) {
+  TraceRange tr("ps_server_param");
   const int m = member_of(c);
   const Window& w = from_rx ? rx_ : tx_;  // rx is always fp32
   const bool bf = grad_bf16_ && !from_rx;
@@ -255,6 +257,7 @@ void PSServer::copy_out(int c) {
 }
 
 void PSServer::do_pull(int c) {
+  TraceRange tr("ps_server_pull");
   const int ci = client_index(c);
   if (pipelined(ci, c)) {
     // snapshot the shard in update order on stream_, push it over the client's link
@@ -285,6 +288,7 @@ void PSServer::do_pull(int c) {
 }
 
 void PSServer::do_grad(int c, bool pull) {
+  TraceRange tr(pull ? "ps_server_update+pull" : "ps_server_update");
   const int m = member_of(c);
   const int64_t es = grad_bf16_ ? 2 : 4;
   const void* g = reinterpret_cast<const uint8_t*>(tx_.remote_ptr(m)) + off_ * es;

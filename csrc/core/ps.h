@@ -87,6 +87,12 @@ class PSServer {
   void wait_done();
   ServerStats stats() const;
   int64_t version() const { return version_.load(); }
+  // rule step counter and update version, saved / restored by checkpoints (quiescent server)
+  int64_t step() const { return t_.load(); }
+  void set_counters(int64_t step, int64_t version) {
+    t_.store(step);
+    version_.store(version);
+  }
   void set_lr(float lr);
   void sync();  // wait for all queued server work
 
@@ -133,7 +139,7 @@ class PSServer {
   std::atomic<int64_t> version_{0};
   int init_rank_;                 // client whose parameter push initialises the shard (-1: ready)
   std::vector<Msg> backlog_;      // grads / pulls that arrived before that push
-  int64_t t_ = 0;  // rule step counter (adam / adamax / adagrad / adadelta)
+  std::atomic<int64_t> t_{0};  // rule step counter (adam / adamax / adagrad / adadelta)
   std::vector<int64_t> clock_;  // pushes received per client (SSP)
   std::deque<int> deferred_;     // clients whose pull waits for stragglers
   mutable std::mutex mu_;

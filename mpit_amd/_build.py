@@ -130,6 +130,7 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = False, sanitize: s
             "-lamdhip64",
             "-lrt",
             "-lpthread",
+            "-ldl",
             f"-Wl,-rpath,{ROCM}/lib",
         ]
         if verbose:

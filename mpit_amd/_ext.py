@@ -6,7 +6,9 @@ fails loudly, so a GPU run can never silently measure an eager/PyTorch path.
 from __future__ import annotations
 
 import importlib
+import importlib.util
 import os
+import sys
 import threading
 
 _lock = threading.Lock()
@@ -23,9 +25,6 @@ def native():
             return _mod
         so = os.environ.get("MPIT_NATIVE_SO")
         if so:  # an explicitly built variant (e.g. the sanitizer builds of _build.py)
-            import importlib.util
-            import sys
-
             spec = importlib.util.spec_from_file_location("mpit_amd._mpit", so)
             _mod = importlib.util.module_from_spec(spec)
             spec.loader.exec_module(_mod)

@@ -28,6 +28,7 @@ import torch
 
 from ..ops.conv import WgradStream
 from ..ops.fused import gather_scale_
+from ..utils import trace as _trace
 
 
 # MPIT_PUSH_ON_SIDE=1: gather + push gate on the side stream instead of joining it. Measured
@@ -115,7 +116,8 @@ class ShardPusher:
                     g.record_stream(side)
             self.gathered[i] = True
         if srcs:
-            gather_scale_(self.pc.tx, srcs, offs, ns, self.a, self.aux, self.b)
+            with _trace.range(f"gather_shard{k}"):
+                gather_scale_(self.pc.tx, srcs, offs, ns, self.a, self.aux, self.b)
         for i in self.members[k]:
             self.params[i].grad = None  # the caching allocator orders reuse on the stream
         self.pc.async_send_grad_shard(k, pull=True)

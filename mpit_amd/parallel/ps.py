@@ -31,6 +31,7 @@ import torch
 from .. import runtime as _rt
 from .._ext import native
 from ..comm import Comm
+from ..utils import trace as _trace
 from ..window import host_view
 
 TAGS = dict(recv_init=1, recv_grad=2, send_param=3, recv_param=4, recv_header=5, recv_stop=6,
@@ -247,14 +248,19 @@ class PServer:
         self.native.sync()
         return {"offset": self.offset, "size": self.size, "p": self.p.detach().cpu(),
                 "state": [t.detach().cpu() for t in self.opt_state], "version": self.native.version(),
-                "rule": self.opt.rule}
+                "step": self.native.step(), "rule": self.opt.rule}
 
     def load_state_dict(self, sd: dict):
+        """Restore a quiescent server (no client message in flight): shard, rule state and
+        the rule's step counter (Adam's bias correction) / update version."""
         self.native.sync()
         assert sd["offset"] == self.offset and sd["size"] == self.size, "checkpoint shard mismatch"
         self.p.copy_(sd["p"])
         for t, s in zip(self.opt_state, sd["state"]):
             t.copy_(s)
+        self.native.set_counters(int(sd.get("step", 0)), int(sd.get("version", 0)))
+        if self.p.is_cuda:
+            torch.cuda.synchronize(self.p.device)
 
 
 # ------------------------------------------------------------------ client
@@ -330,6 +336,7 @@ class PClient:
         """Push the gradient buffer to every server; ``pull=True`` also asks each server
         to write its refreshed shard back (fused push+pull, one kernel per shard)."""
         self._stage_out(self._user_g)
+        _trace.mark("ps_push+pull" if pull else "ps_push")
         self.native.send_grad(self._stream(), bool(pull))
         if pull:
             self._pull_pending = True
@@ -337,11 +344,13 @@ class PClient:
     def async_send_grad_shard(self, k: int, pull: bool = False):
         """Push shard ``k`` (index into ``sranks``) of the gradient buffer only, gated on
         the work queued so far on the current stream (see parallel/overlap.py)."""
+        _trace.mark(f"ps_push_shard{k}")
         self.native.send_grad_to(self._stream(), int(k), bool(pull))
         if pull:
             self._pull_pending = True
 
     def async_recv_param(self):
+        _trace.mark("ps_pull")
         self.native.recv_param(self._stream())
         self._pull_pending = True
 
@@ -365,7 +374,8 @@ class PClient:
         return self.native.pending()
 
     def wait(self):
-        self.native.wait()
+        with _trace.range("ps_wait"):
+            self.native.wait()
         if self._pull_pending:
             self._pull_pending = False
             if self._user_p is not None and self._user_p.data_ptr() != self.rx.data_ptr():

@@ -28,6 +28,7 @@ from .models import get_model
 from .models.cnn import INPUT_SHAPES
 from .optim import distributed as dopt
 from .parallel.ps import PClient, PServer, ServerOpt
+from .utils import trace as _trace
 from .utils.flat import FlatParams
 
 
@@ -179,14 +180,17 @@ class Trainer:
         if self.wcast is not None:  # the weights as they are now, for this forward/backward only
             self.wcast.run()
         try:
-            if self.on_gpu and self.cfg.amp:
-                with torch.autocast("cuda", dtype=torch.bfloat16):
+            with _trace.range("fwd"):
+                if self.on_gpu and self.cfg.amp:
+                    with torch.autocast("cuda", dtype=torch.bfloat16):
+                        out = self.model(self.x)
+                    loss = F.cross_entropy(out.float(), self.y)
+                else:
                     out = self.model(self.x)
-                loss = F.cross_entropy(out.float(), self.y)
-            else:
-                out = self.model(self.x)
-                loss = F.nll_loss(out, self.y) if self.cfg.model in ("cnn7", "lenet") else F.cross_entropy(out, self.y)
-            loss.backward()
+                    loss = (F.nll_loss(out, self.y) if self.cfg.model in ("cnn7", "lenet")
+                            else F.cross_entropy(out, self.y))
+            with _trace.range("bwd"):
+                loss.backward()
         finally:
             if self.wcast is not None:
                 self.wcast.invalidate()
@@ -202,6 +206,10 @@ class Trainer:
 
     def step(self):
         """One training step of this worker; returns the loss tensor (not synced)."""
+        with _trace.range("step"):
+            return self._step()
+
+    def _step(self):
         c = self.cfg
         w = self.flat.flat
         if c.optimizer == "allreduce":
@@ -219,6 +227,59 @@ class Trainer:
             raise ValueError(f"unknown optimizer {c.optimizer!r}")
         self.steps += 1
         return fx
+
+    # ------------------------------------------------------------------ checkpoint / resume
+    def save_checkpoint(self, directory: str) -> str:
+        """Collective: every rank writes its part of the job's state at a quiescent point
+        (after a barrier every push of every worker has been applied and acked): workers
+        their flat parameters, model buffers, local optimizer state and RNG states;
+        server ranks their shard, server optimizer state and rule counters
+        (utils/checkpoint.py). The reference saves only worker models / the tester's
+        parameters (asyncsgd/goot.lua:246-254, BiCNN/bicnn.lua:590-594)."""
+        from .utils import checkpoint
+
+        self.sync()
+        self.barrier()
+        for m in self.model.modules():
+            if hasattr(m, "sync_num_batches_tracked"):
+                m.sync_num_batches_tracked()
+        extra = {"steps": self.steps, "rng_cpu": torch.get_rng_state(),
+                 "buffers": {n: b.detach().cpu() for n, b in self.model.named_buffers()}}
+        if self.on_gpu:
+            extra["rng_cuda"] = torch.cuda.get_rng_state(self.device)
+        path = checkpoint.save(directory, self.steps, self.rank, self.flat if self.is_worker else None,
+                               self.state if self.is_worker else None, self.ps_server, extra)
+        self.barrier()
+        return path
+
+    def load_checkpoint(self, directory: str, path: Optional[str] = None) -> dict:
+        """Collective: restore what :meth:`save_checkpoint` wrote (this rank's latest file in
+        ``directory`` unless ``path``). Call right after construction: the barrier first
+        lets the servers finish the first client's initial parameter push, which the
+        restored shards then replace."""
+        from .utils import checkpoint
+
+        self.sync()
+        self.barrier()
+        path = path or checkpoint.latest(directory, self.rank)
+        if path is None:
+            raise FileNotFoundError(f"no checkpoint of rank {self.rank} in {directory}")
+        obj = checkpoint.load(path, flat=self.flat if self.is_worker else None,
+                              opt_state=self.state if self.is_worker else None, server=self.ps_server)
+        ex = obj.get("extra", {})
+        bufs = dict(self.model.named_buffers())
+        with torch.no_grad():
+            for n, v in ex.get("buffers", {}).items():
+                if n in bufs:
+                    bufs[n].copy_(v.to(bufs[n].device))
+        if "rng_cpu" in ex:
+            torch.set_rng_state(ex["rng_cpu"])
+        if self.on_gpu and "rng_cuda" in ex:
+            torch.cuda.set_rng_state(ex["rng_cuda"], self.device)
+        self.steps = int(ex.get("steps", obj.get("step", 0)))
+        self.sync()
+        self.barrier()
+        return obj
 
     def set_amp(self, amp: bool):
         """Switch the compute precision between steps: bf16 autocast (``amp``) or fp32. The

@@ -98,8 +98,35 @@ def load_files(embedding: str, train: str, label2answer: str, valid: Optional[st
     return d
 
 
+def save_binary(d: QAData, path: str) -> None:
+    """Prepared-data cache (the reference's ``-preloadBinary`` files written from
+    prepareData.lua's tables, BiCNN/plaunch.lua:218-229): one file of plain containers +
+    one tensor, loadable with ``torch.load(weights_only=True)`` (nothing executes)."""
+    torch.save({
+        "version": 1, "emb_dim": d.emb_dim, "conv_width": d.conv_width,
+        "words": list(d.word2idx.keys()), "ids": list(d.word2idx.values()),
+        "vectors": torch.tensor(d.vectors, dtype=torch.float32) if d.vectors else torch.zeros(0, d.emb_dim),
+        "train": [[list(l), list(q), list(a)] for l, q, a in d.train],
+        "valid": [[list(l), list(q), list(p)] for l, q, p in d.valid],
+        "tests": [[[list(l), list(q), list(p)] for l, q, p in t] for t in d.tests],
+        "answer_labels": list(d.answers.keys()), "answer_ids": list(d.answers.values()),
+    }, path)
+
+
+def load_binary(path: str) -> QAData:
+    s = torch.load(path, weights_only=True)
+    d = QAData(emb_dim=int(s["emb_dim"]), conv_width=int(s["conv_width"]))
+    d.word2idx = dict(zip(s["words"], s["ids"]))
+    d.vectors = s["vectors"].tolist()
+    d.train = [tuple(x) for x in s["train"]]
+    d.valid = [tuple(x) for x in s["valid"]]
+    d.tests = [[tuple(x) for x in t] for t in s["tests"]]
+    d.answers = dict(zip(s["answer_labels"], s["answer_ids"]))
+    return d
+
+
 def synthetic_qa(n_answers: int = 200, n_train: int = 2000, n_valid: int = 200, vocab: int = 2000, pool: int = 20,
-                 emb_dim: int = 100, conv_width: int = 2, seed: int = 1) -> QAData:
+                 emb_dim: int = 100, conv_width: int = 2, seed: int = 1, n_tests: int = 2) -> QAData:
     """Answers are random word sequences; a question shares 3 "key" words with its answer
     plus noise words, so GESD ranking is learnable."""
     rng = random.Random(seed)
@@ -117,8 +144,14 @@ def synthetic_qa(n_answers: int = 200, n_train: int = 2000, n_valid: int = 200, 
     for _ in range(n_train):
         lab = rng.randrange(n_answers)
         d.train.append(([lab], d.encode(question(lab), rng), d.answers[lab]))
-    for _ in range(n_valid):
-        lab = rng.randrange(n_answers)
-        cands = list({lab} | set(rng.sample(range(n_answers), pool - 1)))
-        d.valid.append(([lab], d.encode(question(lab), rng), cands))
+    def eval_set():
+        out = []
+        for _ in range(n_valid):
+            lab = rng.randrange(n_answers)
+            cands = list({lab} | set(rng.sample(range(n_answers), pool - 1)))
+            out.append(([lab], d.encode(question(lab), rng), cands))
+        return out
+
+    d.valid = eval_set()
+    d.tests = [eval_set() for _ in range(n_tests)]  # stand-ins for test1 / test2
     return d

@@ -8,11 +8,12 @@ Embedding(V, 100) -> Linear(100, 200) -> Tanh -> Conv1d(200, 3000, k=2) -> max o
 negative (BiCNN/bicnn.lua:87-116 — with tied weights the two are identical functions of
 the same question, kept for parity).
 
-MI355X adaptation: the reference runs one (question, answer) pair at a time with
-data-dependent negative sampling; here a batch of padded sequences is encoded at once
-(max-over-time masks the padding) and the hardest of ``num_neg`` sampled negatives is
-used per question, which is the batched form of "sample until a margin violation"
-(BiCNN/bicnn.lua:279-420).
+MI355X adaptation: the reference runs one (question, answer) pair at a time; here a batch
+of padded sequences is encoded at once (max-over-time masks the padding). Negative
+sampling keeps the reference's semantics — per example, the first margin-violating draw
+within ``maxnegsample`` (:func:`first_violations`, BiCNN/bicnn.lua:321-374) — with the
+draws encoded in batched windows; :func:`margin_ranking_loss` is the cheaper
+hardest-of-k alternative.
 """
 from __future__ import annotations
 
@@ -70,8 +71,10 @@ class BiCNN(nn.Module):
         c = self.conv(h.transpose(1, 2))  # [B, F, T-k+1]
         k = self.conv.kernel_size[0]
         valid = (tok != self.pad_idx)
-        # a window is valid when its first token is not padding (sentences are left-aligned)
-        vw = valid[:, : c.shape[-1]].unsqueeze(1)
+        # a window is valid when its LAST token is not padding (sentences are left-aligned,
+        # so every token of the window is then a real one): exactly the windows of the
+        # unpadded sentence
+        vw = valid[:, k - 1:].unsqueeze(1)
         c = c.masked_fill(~vw, float("-inf"))
         m = c.max(dim=-1).values
         m = torch.nan_to_num(m, neginf=0.0)
@@ -93,6 +96,77 @@ def margin_ranking_loss(s_pos, s_neg, margin: float = 0.009):
     (BiCNN/bicnn.lua:121, :279-420)."""
     hard = s_neg.max(dim=-1).values
     return F.relu(margin - s_pos + hard).mean()
+
+
+def draw_negatives(rng, n_answers: int, positives, maxneg: int) -> list:
+    """The reference's per-example draw sequence: uniform labels with the example's
+    positives rejected, ``maxneg`` draws (BiCNN/bicnn.lua:322-333; labels are 0-based
+    here). Drawn up front so the scan below can batch the encodes."""
+    pos = set(positives)
+    if len(pos) >= n_answers:
+        return []
+    out = []
+    while len(out) < maxneg:
+        x = rng.randrange(n_answers)
+        if x not in pos:
+            out.append(x)
+    return out
+
+
+@torch.no_grad()
+def first_violations(model: "BiCNN", eq: torch.Tensor, s_pos: torch.Tensor, draws: list, answers,
+                     margin: float, pad_fn, chunk: int = 8) -> list:
+    """Parity negative sampling (BiCNN/bicnn.lua:321-374): for every example ``i`` scan its
+    draw sequence ``draws[i]`` in order and return the first negative label whose
+    similarity violates the margin (``s_pos - s_neg < margin``), or ``None`` when all
+    ``maxnegsample`` draws satisfy it (the reference then skips the example: ``goto
+    continue``).
+
+    The reference encodes one negative at a time; here the next draws of every
+    still-unresolved example are encoded in one batched pass (unique labels only, the
+    window doubling from ``chunk`` each round), so the scan costs O(log maxnegsample)
+    batched encodes instead of one tiny encode per draw. The selected label is the
+    sequential scan's: the first violating draw in draw order.
+    """
+    b = eq.shape[0]
+    chosen = [None] * b
+    live = [i for i in range(b) if draws[i]]
+    start, width = 0, chunk
+    maxlen = max((len(d) for d in draws), default=0)
+    dev = eq.device
+    while live and start < maxlen:
+        seqs = [draws[i][start: start + width] for i in live]
+        labs = sorted({x for s in seqs for x in s})
+        if not labs:
+            break
+        emb = model.encode(pad_fn([answers[x] for x in labs]).to(dev))
+        row = {x: j for j, x in enumerate(labs)}
+        w = max(len(s) for s in seqs)
+        idx = torch.tensor([[row[x] for x in s] + [0] * (w - len(s)) for s in seqs], device=dev)
+        valid = torch.tensor([[1] * len(s) + [0] * (w - len(s)) for s in seqs], device=dev, dtype=torch.bool)
+        li = torch.tensor(live, device=dev)
+        sn = gesd(eq[li].unsqueeze(1).expand(-1, w, -1), emb[idx])  # [n_live, w]
+        viol = ((s_pos[li].unsqueeze(1) - sn) < margin) & valid
+        has = viol.any(1).tolist()
+        first = viol.to(torch.int32).argmax(1).tolist()
+        nxt = []
+        for k, i in enumerate(live):
+            if has[k]:
+                chosen[i] = seqs[k][first[k]]
+            else:
+                nxt.append(i)
+        live = nxt
+        start += width
+        width *= 2
+    return chosen
+
+
+def parity_loss(model: "BiCNN", q, a_pos, a_neg, margin: float):
+    """Summed MarginRankingCriterion over the selected (violating) examples — the
+    reference accumulates ``f = f + currErr`` and the gradients of every example of the
+    batch without averaging (BiCNN/bicnn.lua:376-397)."""
+    sp, sn = model(q, a_pos, a_neg.unsqueeze(1))
+    return F.relu(margin - sp + sn[:, 0]).sum()
 
 
 @register("bicnn")

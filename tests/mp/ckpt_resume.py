@@ -15,6 +15,10 @@ import mpit_amd as mp
 from mpit_amd.parallel.ps import ServerOpt
 from mpit_amd.train import TrainConfig, Trainer
 
+# bitwise equality needs deterministic library kernels: cnn7's convolutions run on MIOpen,
+# whose default backward-weight solvers may reduce with atomics
+torch.backends.cudnn.deterministic = True
+torch.backends.cudnn.benchmark = False
 opt = os.environ.get("T_OPT", "downpour")
 topo = os.environ.get("T_TOPO", "dedicated")
 mp.Init()

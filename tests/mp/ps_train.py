@@ -27,9 +27,12 @@ if tr.pc is not None and opt == "downpour":
 cs = torch.tensor([float(tr.flat.flat.double().sum())], dtype=torch.float64)
 allcs = torch.zeros(mp.get_size(), dtype=torch.float64)
 mp.COMM_WORLD().Allgather(cs, allcs)
+ls = torch.tensor([float(loss) if loss is not None else float("nan")], dtype=torch.float64)
+all_loss = torch.zeros(mp.get_size(), dtype=torch.float64)
+mp.COMM_WORLD().Allgather(ls, all_loss)
 stats = tr.ps_server.stats() if tr.ps_server is not None else {}
 tr.stop()
 if mp.get_rank() == 0:
     print(f"RESULT opt={opt} topo={topo} secs={secs:.4f} loss={float(loss) if loss is not None else -1:.4f} "
-          f"checksums={allcs.tolist()} stats={stats}", flush=True)
+          f"checksums={allcs.tolist()} losses={all_loss.tolist()} stats={stats}", flush=True)
 mp.Finalize()

@@ -50,3 +50,16 @@ def test_sync_allreduce_dp_cpu():
     cs = eval(re.search(r"checksums=(\[.*?\])", r).group(1))
     # synchronous DP keeps every replica bit-identical
     assert max(cs) == min(cs), cs
+
+
+def test_baseline_config1_lenet_easgd_dedicated_cpu():
+    """BASELINE.json config 1: LeNet EASGD, one dedicated parameter server + one worker, on
+    the CPU (asyncsgd/mlaunch.lua's 2-rank layout)."""
+    r = _result(run_ranks("ps_train.py", 2, {"MPIT_CPU_ONLY": "1", "T_MODEL": "lenet", "T_OPT": "eamsgd",
+                                             "T_TOPO": "dedicated", "T_STEPS": "8"}))
+    assert "opt=eamsgd topo=dedicated" in r
+    losses = [float(x) for x in re.search(r"losses=\[(.*?)\]", r).group(1).split(",")]
+    assert losses[1] == losses[1] and 0 < losses[1] < 10, r  # rank 1 trains
+    stats = eval(re.search(r"stats=(\{.*\})", r).group(1))
+    assert stats, r  # rank 0 is the dedicated server
+    assert stats["grads"] + stats.get("params", 0) >= 1, stats

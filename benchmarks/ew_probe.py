@@ -1,6 +1,11 @@
 """Bandwidth of the fused update kernels (csrc/kernels/ew.h engine) on PS-sized shards.
 
     python benchmarks/ew_probe.py [n_millions ...]
+
+Each case is captured 20 times into one HIP graph and the graph is replayed, so the
+number is device time (a Python-issued launch costs more host time than a 3.2 M-element
+kernel runs: timing eager calls measures the launcher, not the kernel). The parameter
+server issues these kernels from its native progress thread, not from Python.
 """
 import json
 import os
@@ -12,17 +17,25 @@ import torch
 from mpit_amd import ops
 
 
-def timeit(fn, it=30):
-    for _ in range(3):
-        fn()
+def timeit(fn, per_graph=20, reps=10):
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        for _ in range(3):
+            fn()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(per_graph):
+            fn()
+    g.replay()
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
-    for _ in range(it):
-        fn()
+    for _ in range(reps):
+        g.replay()
     e.record()
     torch.cuda.synchronize()
-    return s.elapsed_time(e) / it
+    return s.elapsed_time(e) / (reps * per_graph)
 
 
 for nm in [float(a) for a in sys.argv[1:]] or [25.6, 3.2]:
@@ -38,5 +51,6 @@ for nm in [float(a) for a in sys.argv[1:]] or [25.6, 3.2]:
     }
     for name, (fn, bpe) in cases.items():
         ms = timeit(fn)
-        print(json.dumps({"n": n, "op": name, "us": round(ms * 1e3, 1), "tb_s": round(n * bpe / ms / 1e9, 2)}),
-              flush=True)
+        print(json.dumps({"n": n, "op": name, "us": round(ms * 1e3, 2), "tb_s": round(n * bpe / ms / 1e9, 2),
+                          "unroll": os.environ.get("MPIT_EW_UNROLL", "auto"),
+                          "grid": os.environ.get("MPIT_EW_GRID", "auto")}), flush=True)

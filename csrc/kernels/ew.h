@@ -8,10 +8,13 @@
 //
 // Design (cdna_hip_programming.md Guideline 11/13, Appendix B "Element-wise"):
 //   * 256-thread blocks (4 wave64s), 16-B per lane per array (float4 / 4×bf16 in 8 B),
-//     UNROLL independent float4 per array in flight per thread (ILP for HBM latency).
-//   * tile = 256 lanes × 4 elems × UNROLL; lane t of tile u reads base+u*1024+4t so
+//     U independent float4 per array in flight per thread (ILP for HBM latency).
+//   * tile = 256 lanes × 4 elems × U; lane t of tile u reads base+u*1024+4t so
 //     every wave-instruction is a fully coalesced 1 KiB access.
-//   * grid = min(tiles, 2048) (8 blocks/CU × 256 CUs) and grid-stride beyond that.
+//   * U and the grid follow the shard size (pick_shape): a PS shard of an 8-way sharded
+//     ResNet-50 (3.2 M elements, ~5 us of traffic) needs every CU busy from the first
+//     wave, so small shards get U = 1 and one tile per block (up to 8 blocks per CU
+//     resident at once); large ones U = 4 with a grid-stride over 2 waves of 2048 blocks.
 //   * arrays may be fp32 or bf16 (per-array bit in the BF mask); math is fp32.
 //   * read-only arrays are never stored, write-only arrays are never loaded, so the
 //     HBM bytes equal the "fused B/elem" column of SURVEY §2.7.
@@ -20,6 +23,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -84,10 +88,9 @@ MPIT_HD void store1(void* base, int64_t i, float v) {
 }
 
 constexpr int kBlock = 256;
-constexpr int kUnroll = 2;
 constexpr int kMaxGrid = 2048;
 
-template <int NA, uint32_t RD, uint32_t WR, uint32_t BF, class F>
+template <int NA, uint32_t RD, uint32_t WR, uint32_t BF, int kUnroll, class F>
 __global__ __launch_bounds__(kBlock) void ew_vec_kernel(Arrays<NA> a, int64_t n, F f) {
   const int64_t n4 = n >> 2;
   const int64_t tile = int64_t(kBlock) * kUnroll;
@@ -204,6 +207,16 @@ void run_host(const Arrays<NA>& a, int64_t n, const F& f) {
   for (auto& x : th) x.join();
 }
 
+// (unroll, grid cap) for n4 float4 groups; MPIT_EW_UNROLL / MPIT_EW_GRID override (A/B).
+inline void pick_shape(int64_t n4, int& unroll, int64_t& cap) {
+  static const int env_u = [] { const char* e = std::getenv("MPIT_EW_UNROLL"); return e ? std::atoi(e) : 0; }();
+  static const int64_t env_g = [] { const char* e = std::getenv("MPIT_EW_GRID"); return e ? std::atoll(e) : 0; }();
+  unroll = n4 <= (int64_t(1) << 21) ? 1 : (n4 <= (int64_t(1) << 23) ? 2 : 4);
+  cap = n4 <= (int64_t(1) << 21) ? int64_t(1) << 30 : kMaxGrid;
+  if (env_u == 1 || env_u == 2 || env_u == 4) unroll = env_u;
+  if (env_g > 0) cap = env_g;
+}
+
 // dev < 0: host; otherwise launch on `stream` (which belongs to the current device).
 template <int NA, uint32_t RD, uint32_t WR, uint32_t BF, class F>
 void run_ew(const Arrays<NA>& a, int64_t n, const F& f, int dev, hipStream_t stream) {
@@ -220,9 +233,17 @@ void run_ew(const Arrays<NA>& a, int64_t n, const F& f, int dev, hipStream_t str
   }
   if (aligned) {
     const int64_t n4 = n >> 2;
-    const int64_t tile = int64_t(kBlock) * kUnroll;
-    int64_t grid = std::max<int64_t>(1, std::min<int64_t>((n4 + tile - 1) / tile, kMaxGrid));
-    hipLaunchKernelGGL((ew_vec_kernel<NA, RD, WR, BF, F>), dim3(grid), dim3(kBlock), 0, stream, a, n, f);
+    int unroll;
+    int64_t cap;
+    pick_shape(n4, unroll, cap);
+    const int64_t tile = int64_t(kBlock) * unroll;
+    int64_t grid = std::max<int64_t>(1, std::min<int64_t>((n4 + tile - 1) / tile, cap));
+    if (unroll == 1)
+      hipLaunchKernelGGL((ew_vec_kernel<NA, RD, WR, BF, 1, F>), dim3(grid), dim3(kBlock), 0, stream, a, n, f);
+    else if (unroll == 2)
+      hipLaunchKernelGGL((ew_vec_kernel<NA, RD, WR, BF, 2, F>), dim3(grid), dim3(kBlock), 0, stream, a, n, f);
+    else
+      hipLaunchKernelGGL((ew_vec_kernel<NA, RD, WR, BF, 4, F>), dim3(grid), dim3(kBlock), 0, stream, a, n, f);
   } else {
     int64_t grid = std::max<int64_t>(1, std::min<int64_t>((n + kBlock - 1) / kBlock, kMaxGrid));
     hipLaunchKernelGGL((ew_scalar_kernel<NA, RD, WR, BF, F>), dim3(grid), dim3(kBlock), 0, stream, a, n, f);

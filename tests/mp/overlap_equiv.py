@@ -15,6 +15,9 @@ import torch
 import mpit_amd as mp
 from mpit_amd.train import TrainConfig, Trainer, timed_steps
 
+# bitwise comparison: layers still on MIOpen (the classifier) must pick deterministic solvers
+torch.backends.cudnn.deterministic = True
+torch.backends.cudnn.benchmark = False
 model = os.environ.get("T_MODEL", "resnet18")
 steps = int(os.environ.get("T_STEPS", "4"))
 mp.Init()
@@ -35,12 +38,17 @@ for amp in (False, True):
         assert chk["ok"], chk
         if tr.is_worker:
             finals[overlap] = tr.flat.flat.detach().clone()
+            names = [(n, off, p.numel()) for (n, p), off in zip(tr.model.named_parameters(), tr.flat.offsets)]
         tr.stop()
     if finals:
         a, b = finals[True], finals[False]
         same = bool(torch.equal(a.view(torch.int32), b.view(torch.int32)))
         diff = float((a - b).abs().max())
         results["bf16" if amp else "fp32"] = (same, diff)
+        if not same:  # which parameters differ (diagnostics)
+            bad = [(n, float((a[o:o + k] - b[o:o + k]).abs().max())) for n, o, k in names
+                   if not torch.equal(a[o:o + k], b[o:o + k])]
+            print(f"DIFF {'bf16' if amp else 'fp32'} {len(bad)}/{len(names)}: {bad[:12]}", flush=True)
 allr = [r for r in W.allgather_obj(results) if r]
 if W.Get_rank() == 0:
     print("RESULT", allr, flush=True)

@@ -123,17 +123,36 @@ __device__ __forceinline__ float rnd(float v) {
 // accuracy at 6 bf16 MFMAs per product (2.5 PF / 6 = 417 TF peak, against 157 TF for the
 // fp32-input MFMA). hh accumulates in its own registers, the five small terms in a second
 // set, so the big running sum is rounded once per 16-deep MFMA, not six times.
+//
+// The split runs on element pairs so every step is one packed instruction: v_cvt_pk_bf16_f32
+// rounds two floats into one dword, the rounded pair is unpacked by a shift and a mask, and
+// v_pk_add_f32 forms both residuals — 9 VALU per pair (4.5 per element) and the bf16 planes
+// come out as whole dwords of the MFMA operand registers (no element inserts).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint32_t pk_bf16(f32x2 x) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(x, bf16x2));
+}
+__device__ __forceinline__ f32x2 unpk_bf16(uint32_t u) {
+  return f32x2{__builtin_bit_cast(float, u << 16), __builtin_bit_cast(float, u & 0xffff0000u)};
+}
 __device__ __forceinline__ void split3(const float (&v)[8], bf16x8& h, bf16x8& m, bf16x8& l) {
+  u32x4 hu, mu, lu;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const __bf16 hb = static_cast<__bf16>(v[e]);
-    const float r1 = v[e] - static_cast<float>(hb);
-    const __bf16 mb = static_cast<__bf16>(r1);
-    const float r2 = r1 - static_cast<float>(mb);
-    h[e] = hb;
-    m[e] = mb;
-    l[e] = static_cast<__bf16>(r2);
+  for (int p = 0; p < 4; ++p) {
+    const f32x2 x = {v[2 * p], v[2 * p + 1]};
+    const uint32_t hp = pk_bf16(x);
+    const f32x2 r = x - unpk_bf16(hp);
+    const uint32_t mp = pk_bf16(r);
+    const f32x2 q = r - unpk_bf16(mp);
+    hu[p] = hp;
+    mu[p] = mp;
+    lu[p] = pk_bf16(q);
   }
+  h = __builtin_bit_cast(bf16x8, hu);
+  m = __builtin_bit_cast(bf16x8, mu);
+  l = __builtin_bit_cast(bf16x8, lu);
 }
 template <int TM, int TN>
 __device__ __forceinline__ void mfma_x3(f32x16 (&hi)[TM][TN], f32x16 (&lo)[TM][TN], const bf16x8 (&ah)[TM],
@@ -202,7 +221,11 @@ __device__ __forceinline__ int swzk(int row, int chunk) {
 
 // bytes of one staged row of gemm_nt: the 256x256 tile (1 block/CU) stages 128-B rows
 // (64 bf16: 16 MFMAs per wave between fragment refills, half the barriers per FLOP)
-__host__ __device__ constexpr int nt_bkb(int BM, int BN) { return BM == 256 && BN == 256 ? 128 : 64; }
+// fp32 bf16x6 with FM = 3 stages 32-deep k-tiles (128-B rows of 32 floats: two k16 MFMA steps
+// per barrier) instead of FM = 1's 16-deep ones.
+__host__ __device__ constexpr int nt_bkb(int BM, int BN, int FM = 0) {
+  return (BM == 256 && BN == 256) || FM == 3 ? 128 : 64;
+}
 
 typedef __attribute__((address_space(3))) void lds_void;
 
@@ -268,7 +291,7 @@ __device__ __forceinline__ int xcd_tile(int bid, int nb) {
 // is lane-linear per wave instruction (16 rows x 64 B); the swizzle is applied on the
 // global source address.
 template <typename T, int BM, int BN, int STAGES, int EPI, bool CONV, int FM = 0>
-__global__ __launch_bounds__(256, sizeof(T) == 4 ? 2 : (BM == 256 ? (BN == 256 ? 1 : 2) : (STAGES == 2 ? (CONV || EPI == 3 ? 4 : 5) : 2))) void gemm_nt_kernel(const T* __restrict__ A, int64_t lda,
+__global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : 2) : (BM == 256 ? (BN == 256 ? 1 : 2) : (STAGES == 2 ? (CONV || EPI == 3 ? 4 : 5) : 2))) void gemm_nt_kernel(const T* __restrict__ A, int64_t lda,
                                                          const T* __restrict__ B, int64_t ldb,
                                                          T* C, int64_t ldc, int64_t M, int N, int K,
                                                          int ntn, EpiArgs ep, const T* Cin,
@@ -278,14 +301,14 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? 2 : (BM == 256 ? (BN == 256 ?
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 32, TN = WN / 32;
   constexpr int EPC = epc<T>();                          // elements per 16-B chunk
-  constexpr int BKB = nt_bkb(BM, BN), BK = BKB / int(sizeof(T));
+  constexpr int BKB = nt_bkb(BM, BN, FM), BK = BKB / int(sizeof(T));
   constexpr int CPK = BKB / 16, RPI = 64 / CPK;          // 16-B chunks per row, rows per glds
   constexpr int IA = BM / RPI / NW, IB = BN / RPI / NW;  // glds instructions per wave per tile
   constexpr int NI = IA + IB;
   constexpr int TILE = (BM + BN) * BK;  // elements per stage
   constexpr bool F32 = sizeof(T) == 4;
   static_assert(IA >= 1 && IB >= 1, "tile too small");
-  static_assert(!F32 || BKB == 64, "fp32 tiles stage 64-B rows");
+  static_assert(!F32 || BKB == 64 || FM == 3, "fp32 tiles stage 64-B rows (FM 3: 128-B)");
   extern __shared__ __attribute__((aligned(16))) uint16_t smem_raw[];
   T* smem = reinterpret_cast<T*>(smem_raw);
   const T* zline = reinterpret_cast<const T*>(g_zero_line);
@@ -387,7 +410,33 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? 2 : (BM == 256 ? (BN == 256 ?
     if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
     const T* As = smem + (kt % STAGES) * TILE;
     const T* Bs = As + BM * BK;
-    if constexpr (F32) {
+    if constexpr (F32 && (FM == 1 || FM == 3)) {
+      // bf16x6: the lane's 8 floats of a row in k16 step kk (chunks 4kk + 2fh, +1 of the row)
+      // are exactly the k = 8fh + j operand of one v_mfma_f32_32x32x16_bf16; split each
+      // fragment in registers
+#pragma unroll
+      for (int kk = 0; kk < BK / 16; ++kk) {
+        bf16x8 ah[TM], am[TM], al[TM], bh[TN], bm[TN], bl[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int r = wm * WM + i * 32 + fr;
+          const float4 x0 = *reinterpret_cast<const float4*>(As + r * BK + swzk<BKB>(r, 4 * kk + 2 * fh) * 4);
+          const float4 x1 = *reinterpret_cast<const float4*>(As + r * BK + swzk<BKB>(r, 4 * kk + 2 * fh + 1) * 4);
+          const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+          split3(v, ah[i], am[i], al[i]);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int r = wn * WN + j * 32 + fr;
+          const float4 x0 = *reinterpret_cast<const float4*>(Bs + r * BK + swzk<BKB>(r, 4 * kk + 2 * fh) * 4);
+          const float4 x1 = *reinterpret_cast<const float4*>(Bs + r * BK + swzk<BKB>(r, 4 * kk + 2 * fh + 1) * 4);
+          const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+          split3(v, bh[j], bm[j], bl[j]);
+        }
+        mfma_x3<TM, TN>(acc, tacc, ah, am, al, bh, bm, bl, true);
+      }
+      continue;
+    } else if constexpr (F32) {
       // v_mfma_f32_32x32x2_f32: lane (fr, fh) supplies A[row fr][k] and B[col fr][k] of one
       // k per instruction. The 16-deep tile is split by lane half: half fh runs k = 8fh + s
       // in step s (any bijection onto the tile's k works when A and B use the same one), so
@@ -404,25 +453,6 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? 2 : (BM == 256 ? (BN == 256 ?
         const int r = wn * WN + j * 32 + fr;
         bfg[j][0] = *reinterpret_cast<const float4*>(Bs + r * BK + swzk<BKB>(r, 2 * fh) * 4);
         bfg[j][1] = *reinterpret_cast<const float4*>(Bs + r * BK + swzk<BKB>(r, 2 * fh + 1) * 4);
-      }
-      if constexpr (FM == 1) {
-        // bf16x6: the lane's 8 floats of a row are exactly the k = 8fh + j operand of one
-        // v_mfma_f32_32x32x16_bf16 over the 16-deep tile; split each fragment in registers
-        bf16x8 ah[TM], am[TM], al[TM], bh[TN], bm[TN], bl[TN];
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const float v[8] = {af[i][0].x, af[i][0].y, af[i][0].z, af[i][0].w,
-                              af[i][1].x, af[i][1].y, af[i][1].z, af[i][1].w};
-          split3(v, ah[i], am[i], al[i]);
-        }
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const float v[8] = {bfg[j][0].x, bfg[j][0].y, bfg[j][0].z, bfg[j][0].w,
-                              bfg[j][1].x, bfg[j][1].y, bfg[j][1].z, bfg[j][1].w};
-          split3(v, bh[j], bm[j], bl[j]);
-        }
-        mfma_x3<TM, TN>(acc, tacc, ah, am, al, bh, bm, bl, true);
-        continue;
       }
       auto el = [](const float4 (&q)[2], int s) -> float {
         const float4& h = q[s >> 2];
@@ -509,7 +539,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? 2 : (BM == 256 ? (BN == 256 ?
     }
   }
 
-  if constexpr (F32 && FM == 1) {  // hh + the five small terms
+  if constexpr (F32 && FM != 0) {  // hh + the five small terms
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1166,7 +1196,15 @@ static int nt_tile_config(int N, int K, bool conv, int cin_conv, bool f32) {
     const std::string v(e);
     return v == "256" ? 2 : v == "256x128" ? 1 : v == "128" ? 0 : -1;
   }();
-  if (f32) return 0;
+  if (f32) {
+    // MPIT_F32_TILE=256x128: 256 x 128 blocks (1 per CU, 128 x 64 per wave) for the bf16x6
+    // fp32 GEMMs, whose 6 MFMAs per product make them compute-bound
+    static const int f32_forced = [] {
+      const char* e = std::getenv("MPIT_F32_TILE");
+      return e && std::string(e) == "256x128" ? 1 : 0;
+    }();
+    return f32_forced == 1 && N % 128 == 0 ? 1 : 0;
+  }
   int cfg = forced >= 0 ? forced : 0;
   // Measured (profiles/gemm_big_tile_ab_r01.jsonl, gemm_bk64_128tile_ab_r01.jsonl): 256x256
   // (BK 64) beats 128x128 on large square GEMMs (8192^3: 944 vs 611 TFLOP/s) and 256x128 on
@@ -1224,37 +1262,57 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
   const auto* bs = reinterpret_cast<const float*>(bias);
   const int rl = relu ? 1 : 0;
   const ConvGeo g = geo ? *geo : ConvGeo{};
-  const int nk = K / nt_bk_of<T>();
+  // fp32 variant: 0 native fp32 MFMA, 1 bf16x6 on 16-deep k-tiles, 3 bf16x6 on 32-deep ones
+  // (MPIT_F32_BK=32; needs K and the conv's channels to be multiples of 32)
+  static const int f32_bk = [] {
+    const char* e = std::getenv("MPIT_F32_BK");
+    return e && std::atoi(e) == 32 ? 32 : 16;
+  }();
+  const int fm = !F32 || f32_mode() != 1 ? 0
+                 : (f32_bk == 32 && K % 32 == 0 && (!geo || (geo->C % 32 == 0 && !geo->pitch)) ? 3 : 1);
+  const int nk = K / (fm == 3 ? 32 : nt_bk_of<T>());
   // MPIT_GEMM_STAGES caps the ring depth (A/B measurements). fp32: the 64 KB epilogue tile
-  // of a 128x128 block holds a 4-deep ring for free.
+  // of a 128x128 block holds a 4-deep 16-deep ring (or a 2-deep 32-deep one) for free.
   static const int max_stages = [] {
     const char* e = std::getenv("MPIT_GEMM_STAGES");
     return e ? std::max(2, std::min(4, std::atoi(e))) : 2;
   }();
-  const int cap = F32 && N % 128 == 0 ? 4 : max_stages;
+  static const int f32_stages = [] {
+    const char* e = std::getenv("MPIT_F32_STAGES");
+    return e ? std::max(2, std::min(4, std::atoi(e))) : 0;
+  }();
+  int cap = F32 && N % 128 == 0 ? (fm == 3 ? 2 : 4) : max_stages;
+  if (F32 && f32_stages) cap = f32_stages;
   const int stages = std::min(cap, nk >= 4 ? 4 : (nk == 3 ? 3 : 2));
   // (kernel templates are named at a non-template call site so their host stubs are emitted)
+#define MPIT_NT_OPT_IN(BM, BN, ST, EPI, CONV, FMV)                                                                 \
+  do {                                                                                                             \
+    static const bool opted = (hip_check(hipFuncSetAttribute(reinterpret_cast<const void*>(                       \
+                                                             &gemm_nt_kernel<T, BM, BN, ST, EPI, CONV, FMV>),     \
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize, int(shm)),    \
+                                     "hipFuncSetAttribute"),                                                       \
+                               true);                                                                              \
+    (void)opted;                                                                                                   \
+  } while (0)
 #define MPIT_NT_LAUNCH1(BM, BN, ST, EPI, CONV)                                                                       \
   do {                                                                                                             \
-    if (shm > 65536) { /* beyond the default dynamic-LDS cap: opt in once per instantiation */                    \
-      static const bool opted = (hip_check(hipFuncSetAttribute(                                                      \
-                                               reinterpret_cast<const void*>(&gemm_nt_kernel<T, BM, BN, ST, EPI, CONV>), \
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, int(shm)),                \
-                                           "hipFuncSetAttribute"),                                                   \
-                                 hip_check(hipFuncSetAttribute(                                                      \
-                                               reinterpret_cast<const void*>(                                        \
-                                                   &gemm_nt_kernel<T, BM, BN, ST, EPI, CONV, F32 ? 1 : 0>),          \
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, int(shm)),                \
-                                           "hipFuncSetAttribute"),                                                   \
-                                 true);                                                                              \
-      (void)opted;                                                                                                   \
-    }                                                                                                                \
-    if (F32 && f32_mode() == 1)                                                                                    \
-      hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, ST, EPI, CONV, F32 ? 1 : 0>), dim3(unsigned(nb)), dim3(256), shm, \
-                         s, a, lda, b, ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g);                          \
-    else                                                                                                           \
-      hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, ST, EPI, CONV>), dim3(unsigned(nb)), dim3(256), shm, s, a,     \
-                         lda, b, ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g);                           \
+    if constexpr (F32) {                                                                                           \
+      if (fm == 3) {                                                                                               \
+        if (shm > 65536) MPIT_NT_OPT_IN(BM, BN, ST, EPI, CONV, 3);                                                  \
+        hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, ST, EPI, CONV, 3>), dim3(unsigned(nb)), dim3(256), shm, s, a, \
+                           lda, b, ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g);                               \
+        break;                                                                                                     \
+      }                                                                                                            \
+      if (fm == 1) {                                                                                               \
+        if (shm > 65536) MPIT_NT_OPT_IN(BM, BN, ST, EPI, CONV, 1);                                                  \
+        hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, ST, EPI, CONV, 1>), dim3(unsigned(nb)), dim3(256), shm, s, a, \
+                           lda, b, ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g);                               \
+        break;                                                                                                     \
+      }                                                                                                            \
+    }                                                                                                              \
+    if (shm > 65536) MPIT_NT_OPT_IN(BM, BN, ST, EPI, CONV, 0);                                                      \
+    hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, ST, EPI, CONV>), dim3(unsigned(nb)), dim3(256), shm, s, a, lda, b, \
+                       ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g);                                           \
   } while (0)
 #define MPIT_NT_LAUNCH2(BM, BN, ST, CONV)                                                         \
   do {                                                                                              \
@@ -1270,13 +1328,19 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
     const int64_t nb = mtn * ntn;                                                                              \
     if (nb > INT32_MAX) throw std::invalid_argument("gemm_nt: too many tiles");                               \
     /* LDS: the k-tile ring, reused by the epilogue's output tile and reduction table */                      \
-    const size_t shm = std::max({size_t(ST) * (BM + BN) * size_t(nt_bkb(BM, BN)),                              \
+    const size_t shm = std::max({size_t(ST) * (BM + BN) * size_t(nt_bkb(BM, BN, fm)),                          \
                                  size_t(BM) * BN * sizeof(T), size_t(256) * 8 * 3 * sizeof(float)});          \
     if (geo) MPIT_NT_LAUNCH2(BM, BN, ST, true);                                                           \
     else MPIT_NT_LAUNCH2(BM, BN, ST, false);                                                              \
   } while (0)
   const int tcfg = nt_tile_config(N, K, geo != nullptr, geo ? geo->C : 0, F32);
-  if constexpr (!F32) {
+  if constexpr (F32) {
+    if (tcfg == 1) {
+      MPIT_NT_LAUNCH(256, 128, 3);
+      hip_check(hipGetLastError(), "gemm_nt launch");
+      return;
+    }
+  } else {
     if (tcfg == 2) {
       MPIT_NT_LAUNCH(256, 256, 2);  // 2 x 64-deep stages = the 128 KB epilogue tile
       hip_check(hipGetLastError(), "gemm_nt launch");
@@ -1300,6 +1364,7 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
 #undef MPIT_NT_LAUNCH
 #undef MPIT_NT_LAUNCH2
 #undef MPIT_NT_LAUNCH1
+#undef MPIT_NT_OPT_IN
   hip_check(hipGetLastError(), "gemm_nt launch");
 }
 

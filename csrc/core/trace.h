@@ -1,7 +1,8 @@
 // roctx ranges from the native runtime (the server's progress thread: shard updates, pulls,
 // parameter pushes), so rocprofv3 --marker-trace shows the parameter server next to the
-// Python-side ranges of mpit_amd/utils/trace.py. libroctx64 is opened at run time and only
-// when MPIT_TRACE=1: no link dependency, nothing done otherwise.
+// Python-side ranges of mpit_amd/utils/trace.py. The roctx library is opened at run time and
+// only when MPIT_TRACE=1: no link dependency, nothing done otherwise. rocprofv3 intercepts
+// the rocprofiler-sdk roctx library (ROCm 7); the legacy libroctx64 is the fallback.
 #pragma once
 #include <dlfcn.h>
 
@@ -18,8 +19,10 @@ struct Roctx {
       Roctx x;
       const char* e = std::getenv("MPIT_TRACE");
       if (!e || std::strcmp(e, "1") != 0) return x;
-      void* h = dlopen("libroctx64.so", RTLD_NOW | RTLD_GLOBAL);
-      if (!h) h = dlopen("/opt/rocm/lib/libroctx64.so", RTLD_NOW | RTLD_GLOBAL);
+      void* h = nullptr;
+      for (const char* n : {"librocprofiler-sdk-roctx.so.1", "/opt/rocm/lib/librocprofiler-sdk-roctx.so.1",
+                            "libroctx64.so", "/opt/rocm/lib/libroctx64.so"})
+        if (!h) h = dlopen(n, RTLD_NOW | RTLD_GLOBAL);
       if (!h) return x;
       x.push = reinterpret_cast<int (*)(const char*)>(dlsym(h, "roctxRangePushA"));
       x.pop = reinterpret_cast<int (*)()>(dlsym(h, "roctxRangePop"));

@@ -1263,10 +1263,11 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
   const int rl = relu ? 1 : 0;
   const ConvGeo g = geo ? *geo : ConvGeo{};
   // fp32 variant: 0 native fp32 MFMA, 1 bf16x6 on 16-deep k-tiles, 3 bf16x6 on 32-deep ones
-  // (MPIT_F32_BK=32; needs K and the conv's channels to be multiples of 32)
+  // (default where K and the conv's channels are multiples of 32; MPIT_F32_BK=16 forces 1).
+  // Same-box ResNet-50 fp32 bench: 32-deep 4075 vs 16-deep 4016 img/s (profiles/gemm_fp32_variants_ab_r02.md)
   static const int f32_bk = [] {
     const char* e = std::getenv("MPIT_F32_BK");
-    return e && std::atoi(e) == 32 ? 32 : 16;
+    return e && std::atoi(e) == 16 ? 16 : 32;
   }();
   const int fm = !F32 || f32_mode() != 1 ? 0
                  : (f32_bk == 32 && K % 32 == 0 && (!geo || (geo->C % 32 == 0 && !geo->pitch)) ? 3 : 1);

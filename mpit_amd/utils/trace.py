@@ -1,7 +1,8 @@
 """Tracing and timing: roctx ranges visible in rocprofv3 traces, plus wall-clock
 accumulators (the reference's ``tm`` tables, asyncsgd/goot.lua:24-26, BiCNN/bicnn.lua:17-28).
 
-``range("name")`` emits roctxRangePushA/Pop through libroctx64 when it is present and
+``range("name")`` emits roctxRangePushA/Pop through the rocprofiler-sdk roctx library (the
+one rocprofv3 ``--marker-trace`` intercepts on ROCm 7; libroctx64 as fallback) when it is present and
 tracing is enabled (``MPIT_TRACE=1`` or ``Pcontrol(1)``); it is a no-op otherwise.
 ``Timers`` accumulate seconds per key; ``device=True`` timers synchronise the GPU first
 so they measure device time, not launch time.
@@ -22,7 +23,8 @@ def _roctx():
     global _lib
     if _lib is None:
         _lib = False
-        for name in ("libroctx64.so", "/opt/rocm/lib/libroctx64.so"):
+        for name in ("librocprofiler-sdk-roctx.so.1", "/opt/rocm/lib/librocprofiler-sdk-roctx.so.1",
+                     "libroctx64.so", "/opt/rocm/lib/libroctx64.so"):
             try:
                 lib = ctypes.CDLL(name)
                 lib.roctxRangePushA.argtypes = [ctypes.c_char_p]

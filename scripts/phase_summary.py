@@ -37,7 +37,9 @@ def main():
         ranges[(pid, name)].append((s, e))
     kern = collections.defaultdict(list)
     for r in _rows(a.dir, "*kernel_trace.csv"):
-        pid = r.get("Process_Id") or r.get("Pid") or "?"
+        # rocprofv3's kernel trace has no process column: one traced process per output
+        # file name (-o name_%pid%) or all kernels of the single traced process
+        pid = r.get("Process_Id") or r.get("Pid") or "*"
         kern[pid].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Kernel_Name", "")))
     lines = ["# Phase breakdown (roctx ranges, host time)", "",
              f"Source: rocprofv3 --marker-trace --kernel-trace; first {a.skip} occurrences of each range skipped.", "",
@@ -57,10 +59,11 @@ def main():
         if len(v) < 2:
             continue
         lo, hi = v[0][0], v[-1][1]
-        ks = [k for k in kern.get(pid, []) if lo <= k[0] < hi]
+        ks = [k for k in kern.get(pid, kern.get("*", [])) if lo <= k[0] < hi]
         agg = collections.Counter()
         for s, e, n in ks:
-            agg[n.split("(")[0][-60:]] += (e - s) / 1e6
+            base = n.replace("void ", "").replace("mpit::(anonymous namespace)::", "").replace("at::native::", "")
+            agg[base.split("<")[0].split("(")[0][:40]] += (e - s) / 1e6
         n = len(v)
         top = ", ".join(f"{k} {t / n:.2f}" for k, t in agg.most_common(5))
         lines.append(f"| {pid} | {n} | {(hi - lo) / 1e6 / n:.2f} | {sum(agg.values()) / n:.2f} | {top} |")

@@ -291,7 +291,7 @@ __device__ __forceinline__ int xcd_tile(int bid, int nb) {
 // is lane-linear per wave instruction (16 rows x 64 B); the swizzle is applied on the
 // global source address.
 template <typename T, int BM, int BN, int STAGES, int EPI, bool CONV, int FM = 0>
-__global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : 2) : (BM == 256 ? (BN == 256 ? 1 : 2) : (STAGES == 2 ? (CONV || EPI == 3 ? 4 : 5) : 2))) void gemm_nt_kernel(const T* __restrict__ A, int64_t lda,
+__global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 3 : 2)) : (BM == 256 ? (BN == 256 ? 1 : 2) : (STAGES == 2 ? (CONV || EPI == 3 ? 4 : 5) : 2))) void gemm_nt_kernel(const T* __restrict__ A, int64_t lda,
                                                          const T* __restrict__ B, int64_t ldb,
                                                          T* C, int64_t ldc, int64_t M, int N, int K,
                                                          int ntn, EpiArgs ep, const T* Cin,
@@ -1353,7 +1353,12 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
       return;
     }
   }
-  if (N % 128 == 0) {
+  // MPIT_F32_BN64=1: fp32 GEMMs on 128x64 tiles (3 blocks per CU instead of 2) — A/B knob
+  static const bool f32_bn64 = [] {
+    const char* e = std::getenv("MPIT_F32_BN64");
+    return e && std::string(e) == "1";
+  }();
+  if (N % 128 == 0 && !(F32 && f32_bn64)) {
     if (stages == 4) MPIT_NT_LAUNCH(128, 128, 4);
     else if (stages == 3) MPIT_NT_LAUNCH(128, 128, 3);
     else MPIT_NT_LAUNCH(128, 128, 2);

@@ -76,3 +76,25 @@ def test_overlap_equals_non_overlapped_on_gpu_three_ranks():
     for prec in ("fp32", "bf16"):
         same, diff = res[0][prec]
         assert same, (prec, diff)
+
+
+def test_shard_pusher_weight_decay_for_gradientless_params():
+    """A parameter without a gradient this step still pushes its weight-decay term
+    b*aux (asyncsgd/optim-downpour.lua:24 adds l2wd*w to the whole dfdx)."""
+    torch.manual_seed(0)
+    model = get_model("cnn7", num_classes=10)
+    flat = FlatParams(model)
+    pc = _FakeClient(flat.numel, 2)
+    pc.tx[:] = 0.0
+    flat.steal_grads()
+    pusher = ShardPusher(flat, pc)
+    aux = torch.randn(flat.numel)
+    pusher.arm(-0.1, aux, 0.25)
+    frozen = flat.params[0]
+    frozen.requires_grad_(False)  # no gradient this step
+    x, y = torch.randn(2, 3, 28, 28), torch.randint(0, 10, (2,))
+    torch.nn.functional.nll_loss(model(x), y).backward()
+    pusher.finish()
+    off, n = flat.offsets[0], frozen.numel()
+    torch.testing.assert_close(pc.tx[off:off + n], 0.25 * aux[off:off + n])
+    frozen.requires_grad_(True)

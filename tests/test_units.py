@@ -268,3 +268,45 @@ def test_info_errors_keyvals():
     assert "TRUNCATE" in misc.Error_string(misc.ERR_TRUNCATE)
     k = misc.Comm_create_keyval()
     assert misc.Comm_free_keyval(k) == misc.KEYVAL_INVALID
+
+
+def test_bf16_wire_initialises_server_with_exact_fp32(world):
+    """EASGD with a bf16 elastic-difference wire: the first client's fp32 weights reach the
+    server shard bit for bit (the init push travels through the fp32 rx window,
+    BiCNN/pserver.lua:272-278), not rounded through the bf16 push window."""
+    reset_groups()
+    torch.manual_seed(7)
+    w = torch.randn(333) * 1.2345  # not representable in bf16
+    conf = dict(rank=0, sranks=[0], cranks=[0], plong=333, opt=ServerOpt("sum"), ps_id=21,
+                grad_dtype=torch.bfloat16)
+    srv = PServer(conf)
+    srv.start(block=False)
+    pc = PClient(conf)
+    pc.start(torch.zeros(333), torch.zeros(333, dtype=torch.bfloat16), init=w)
+    pc.wait()
+    srv.native.sync()
+    assert torch.equal(srv.p.view(torch.int32), w.view(torch.int32))
+    pc.stop()
+    srv.wait_done()
+
+
+def test_eamsgd_lr0_still_applies_elastic_step(world):
+    """lr == 0: no local gradient step, but a sync step still pulls w toward the center by
+    sug = mva*(w - center) (asyncsgd/optim-eamsgd.lua:69-70)."""
+    torch.manual_seed(8)
+    w = torch.randn(200)
+    center = torch.randn(200)
+    srv, pc = _single_ps(200, init=torch.zeros(200))
+    pc.async_send_param(center)
+    pc.wait()
+    calls = []
+    cfg = dict(lr=0.0, mva=0.3, su=1, mom=0.0, pclient=pc)
+    w0 = w.clone()
+    mp.optim.eamsgd(lambda x: calls.append(1) or (torch.tensor(0.0), torch.zeros_like(x)), w, cfg, {})
+    pc.wait()
+    sug = 0.3 * (w0 - center)
+    torch.testing.assert_close(w, w0 - sug)
+    torch.testing.assert_close(srv.p, center + sug)
+    assert not calls  # no forward/backward at lr 0
+    pc.stop()
+    srv.wait_done()

@@ -501,6 +501,9 @@ class Comm:
     def Issend(self, buf, dest: int, tag: int = 0, count=None, datatype=None) -> Request:
         return self._isend(buf, dest, tag, self._ctx, True, count, datatype)
 
+    # MPI's buffered / ready modes: the engine never needs the user's attached buffer (eager
+    # messages are copied into the shm ring, large ones wait for the receiver) and a ready
+    # send is a correct standard send, so both are the standard mode
     Ibsend = Isend
     Irsend = Isend
 
@@ -520,15 +523,17 @@ class Comm:
              count=None, datatype=None) -> Status:
         return self.Irecv(buf, source, tag, count, datatype).Wait(status)
 
-    def Sendrecv(self, sendbuf, dest, sendtag, recvbuf, source=ANY_SOURCE, recvtag=ANY_TAG, status=None) -> Status:
-        rr = self.Irecv(recvbuf, source, recvtag)
-        sr = self.Isend(sendbuf, dest, sendtag)
+    def Sendrecv(self, sendbuf, dest, sendtag, recvbuf, source=ANY_SOURCE, recvtag=ANY_TAG, status=None,
+                 sendcount=None, sendtype=None, recvcount=None, recvtype=None) -> Status:
+        rr = self.Irecv(recvbuf, source, recvtag, recvcount, recvtype)
+        sr = self.Isend(sendbuf, dest, sendtag, sendcount, sendtype)
         sr.Wait()
         return rr.Wait(status)
 
-    def Sendrecv_replace(self, buf, dest, sendtag, source=ANY_SOURCE, recvtag=ANY_TAG, status=None) -> Status:
+    def Sendrecv_replace(self, buf, dest, sendtag, source=ANY_SOURCE, recvtag=ANY_TAG, status=None,
+                         count=None, datatype=None) -> Status:
         tmp = buf.clone()
-        return self.Sendrecv(tmp, dest, sendtag, buf, source, recvtag, status)
+        return self.Sendrecv(tmp, dest, sendtag, buf, source, recvtag, status, count, datatype, count, datatype)
 
     def Iprobe(self, source: int = ANY_SOURCE, tag: int = ANY_TAG, status: Optional[Status] = None) -> bool:
         src = self._to_world(source) if source >= 0 else source
@@ -547,25 +552,25 @@ class Comm:
         return st
 
     # persistent requests
-    def Send_init(self, buf, dest, tag=0) -> Request:
+    def Send_init(self, buf, dest, tag=0, count=None, datatype=None) -> Request:
         r = Request(self)
         r._status = Status()
-        r.persistent = lambda: self.Isend(buf, dest, tag)
+        r.persistent = lambda: self.Isend(buf, dest, tag, count, datatype)
         return r
 
     Bsend_init = Send_init
     Rsend_init = Send_init
 
-    def Ssend_init(self, buf, dest, tag=0) -> Request:
+    def Ssend_init(self, buf, dest, tag=0, count=None, datatype=None) -> Request:
         r = Request(self)
         r._status = Status()
-        r.persistent = lambda: self.Issend(buf, dest, tag)
+        r.persistent = lambda: self.Issend(buf, dest, tag, count, datatype)
         return r
 
-    def Recv_init(self, buf, source=ANY_SOURCE, tag=ANY_TAG) -> Request:
+    def Recv_init(self, buf, source=ANY_SOURCE, tag=ANY_TAG, count=None, datatype=None) -> Request:
         r = Request(self)
         r._status = Status()
-        r.persistent = lambda: self.Irecv(buf, source, tag)
+        r.persistent = lambda: self.Irecv(buf, source, tag, count, datatype)
         return r
 
     # object convenience (mpiT.serialize / deserialize, init.lua:111-132)

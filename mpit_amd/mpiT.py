@@ -136,6 +136,7 @@ def Send(buf, count, datatype, dest, tag, comm):
     return SUCCESS
 
 
+# buffered / ready sends are standard sends on this engine (see Comm.Ibsend)
 Bsend = Rsend = Send
 
 
@@ -152,7 +153,7 @@ def Isend(buf, count, datatype, dest, tag, comm):
     return comm.Isend(buf, dest, tag, count=count, datatype=_buf(buf, count, datatype)[2])
 
 
-Ibsend = Irsend = Isend
+Ibsend = Irsend = Isend  # see Bsend
 
 
 def Issend(buf, count, datatype, dest, tag, comm):
@@ -164,26 +165,32 @@ def Irecv(buf, count, datatype, source, tag, comm):
 
 
 def Sendrecv(sendbuf, sendcount, sendtype, dest, sendtag, recvbuf, recvcount, recvtype, source, recvtag, comm, status=None):
-    return comm.Sendrecv(sendbuf, dest, sendtag, recvbuf, source, recvtag, status)
+    _, sc, st = _buf(sendbuf, sendcount, sendtype)
+    _, rc, rt = _buf(recvbuf, recvcount, recvtype)
+    return comm.Sendrecv(sendbuf, dest, sendtag, recvbuf, source, recvtag, status, sc, st, rc, rt)
 
 
 def Sendrecv_replace(buf, count, datatype, dest, sendtag, source, recvtag, comm, status=None):
-    return comm.Sendrecv_replace(buf, dest, sendtag, source, recvtag, status)
+    _, c, dt = _buf(buf, count, datatype)
+    return comm.Sendrecv_replace(buf, dest, sendtag, source, recvtag, status, c, dt)
 
 
 def Send_init(buf, count, datatype, dest, tag, comm):
-    return comm.Send_init(buf, dest, tag)
+    _, c, dt = _buf(buf, count, datatype)
+    return comm.Send_init(buf, dest, tag, c, dt)
 
 
 Bsend_init = Rsend_init = Send_init
 
 
 def Ssend_init(buf, count, datatype, dest, tag, comm):
-    return comm.Ssend_init(buf, dest, tag)
+    _, c, dt = _buf(buf, count, datatype)
+    return comm.Ssend_init(buf, dest, tag, c, dt)
 
 
 def Recv_init(buf, count, datatype, source, tag, comm):
-    return comm.Recv_init(buf, source, tag)
+    _, c, dt = _buf(buf, count, datatype)
+    return comm.Recv_init(buf, source, tag, c, dt)
 
 
 def Start(request):

@@ -112,6 +112,29 @@ for _ in range(3):
     mp.Waitall([ps, pr])
 ok("sendrecv_persistent")
 
+# ---- the mpiT facade honours count and datatype on Sendrecv / Sendrecv_replace / persistent
+# requests: 3 of 8 floats, and a strided vector type (every other element)
+f_out = torch.arange(8, dtype=torch.float32) + 100 * r
+f_in = torch.full((8,), -1.0)
+mpiT.Sendrecv(f_out, 3, mpiT.FLOAT, (r + 1) % n, 31, f_in, 3, mpiT.FLOAT, (r - 1) % n, 31, W)
+src = (r - 1) % n
+assert f_in[:3].tolist() == [100.0 * src + i for i in range(3)] and f_in[3:].eq(-1).all(), f_in
+vec = dt.Type_vector(4, 1, 2, dt.FLOAT)
+vec.Commit()
+rep = torch.arange(8, dtype=torch.float32) + 100 * r
+mpiT.Sendrecv_replace(rep, 1, vec, (r + 1) % n, 32, (r - 1) % n, 32, W)
+want = torch.arange(8, dtype=torch.float32) + 100 * r
+want[0::2] = torch.arange(0, 8, 2, dtype=torch.float32) + 100 * src
+assert torch.equal(rep, want), rep
+p_in = torch.full((8,), -1.0)
+pr = mpiT.Recv_init(p_in, 2, mpiT.FLOAT, (r - 1) % n, 33, W)
+ps = mpiT.Send_init(f_out, 2, mpiT.FLOAT, (r + 1) % n, 33, W)
+pr.Start()
+ps.Start()
+mp.Waitall([ps, pr])
+assert p_in[:2].tolist() == [100.0 * src, 100.0 * src + 1] and p_in[2:].eq(-1).all(), p_in
+ok("facade_count_datatype")
+
 # ---- X2/X3: Allreduce, Iallreduce (Test before Wait false-or-true, after Wait true)
 a = torch.full((1 << 16,), float(r + 1), device=dev)
 W.Allreduce(a, a, mp.SUM)

@@ -7,7 +7,7 @@ import pytest
 from mp_util import ROOT, run_ranks
 
 CHECKS = ["ring_send_recv", "large_message", "probe_any_source", "message_ordering", "cancel_recv", "ssend",
-          "sendrecv_persistent", "allreduce_iallreduce", "reductions", "collectives", "groups_comms", "topologies",
+          "sendrecv_persistent", "facade_count_datatype", "allreduce_iallreduce", "reductions", "collectives", "groups_comms", "topologies",
           "datatypes", "windows", "mpi_io", "intercomm", "mpiT_api", "objects"]
 
 

@@ -126,3 +126,28 @@ def test_goot_mlaunch_roles(tmp_path):
     out = _launch(4, "goot.py", ["--optimizer", "eamsgd", "--subset", "--max-steps", "3", "--batch", "32",
                                  "--save", str(tmp_path / "g")], str(tmp_path))
     assert "[goot] epoch" in out and "[goot] rank" in out
+
+
+def test_load_files_reference_format(tmp_path):
+    """BiCNN/prepareData.lua's text formats: embedding `word<TAB>v1 .. vD`, train
+    `labels<TAB>x<TAB>question<TAB>answer`, valid/test `labels<TAB>question<TAB>pool`,
+    label2answer `label<TAB>answer`; sentences padded with convWidth SENTBEGIN in front and
+    convWidth-1 SENTEND behind, out-of-vocabulary words get new ids."""
+    from mpit_amd.apps.qa_data import SENTBEGIN, SENTEND, load_files
+
+    (tmp_path / "emb.txt").write_text("what\t0.1 0.2 0.3\nis\t0.4 0.5 0.6\n")
+    (tmp_path / "l2a.txt").write_text("0\tit is red\n1\tit is blue\n2\tnone\n")
+    (tmp_path / "train.txt").write_text("0\tx\twhat is red\tit is red\n1 2\tx\twhat is blue\tit is blue\n")
+    (tmp_path / "valid.txt").write_text("0\twhat is it\t0 1 2\n")
+    (tmp_path / "test1.txt").write_text("1\twhat\t1 2\n")
+    d = load_files(str(tmp_path / "emb.txt"), str(tmp_path / "train.txt"), str(tmp_path / "l2a.txt"),
+                   str(tmp_path / "valid.txt"), tests=[str(tmp_path / "test1.txt")], emb_dim=3, conv_width=2)
+    what, is_ = d.word2idx["what"], d.word2idx["is"]
+    assert d.embedding_matrix()[what].tolist() == pytest.approx([0.1, 0.2, 0.3])
+    labels, q, a = d.train[1]
+    assert labels == [1, 2]
+    assert q[:2] == [SENTBEGIN, SENTBEGIN] and q[-1:] == [SENTEND] and q[2:4] == [what, is_]
+    assert a == d.answers[1]
+    assert d.valid[0][0] == [0] and d.valid[0][2] == [0, 1, 2]
+    assert len(d.tests) == 1 and d.tests[0][0][2] == [1, 2]
+    assert len(d.word2idx) == d.embedding_matrix().shape[0]

@@ -416,39 +416,24 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
       // fragment in registers
 #pragma unroll
       for (int kk = 0; kk < BK / 16; ++kk) {
-        // all fragment reads first; B split; then row by row: split A_i, its 6*TN MFMAs —
-        // the split of row i+1 has no dependence on row i's MFMAs, so the scheduler can
-        // issue it under them
-        float4 xa[TM][2], xb[TN][2];
+        bf16x8 ah[TM], am[TM], al[TM], bh[TN], bm[TN], bl[TN];
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           const int r = wm * WM + i * 32 + fr;
-          xa[i][0] = *reinterpret_cast<const float4*>(As + r * BK + swzk<BKB>(r, 4 * kk + 2 * fh) * 4);
-          xa[i][1] = *reinterpret_cast<const float4*>(As + r * BK + swzk<BKB>(r, 4 * kk + 2 * fh + 1) * 4);
+          const float4 x0 = *reinterpret_cast<const float4*>(As + r * BK + swzk<BKB>(r, 4 * kk + 2 * fh) * 4);
+          const float4 x1 = *reinterpret_cast<const float4*>(As + r * BK + swzk<BKB>(r, 4 * kk + 2 * fh + 1) * 4);
+          const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+          split3(v, ah[i], am[i], al[i]);
         }
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int r = wn * WN + j * 32 + fr;
-          xb[j][0] = *reinterpret_cast<const float4*>(Bs + r * BK + swzk<BKB>(r, 4 * kk + 2 * fh) * 4);
-          xb[j][1] = *reinterpret_cast<const float4*>(Bs + r * BK + swzk<BKB>(r, 4 * kk + 2 * fh + 1) * 4);
-        }
-        bf16x8 bh[TN], bm[TN], bl[TN];
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const float v[8] = {xb[j][0].x, xb[j][0].y, xb[j][0].z, xb[j][0].w,
-                              xb[j][1].x, xb[j][1].y, xb[j][1].z, xb[j][1].w};
+          const float4 x0 = *reinterpret_cast<const float4*>(Bs + r * BK + swzk<BKB>(r, 4 * kk + 2 * fh) * 4);
+          const float4 x1 = *reinterpret_cast<const float4*>(Bs + r * BK + swzk<BKB>(r, 4 * kk + 2 * fh + 1) * 4);
+          const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
           split3(v, bh[j], bm[j], bl[j]);
         }
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          bf16x8 ah[1], am[1], al[1];
-          const float v[8] = {xa[i][0].x, xa[i][0].y, xa[i][0].z, xa[i][0].w,
-                              xa[i][1].x, xa[i][1].y, xa[i][1].z, xa[i][1].w};
-          split3(v, ah[0], am[0], al[0]);
-          f32x16(&hrow)[1][TN] = *reinterpret_cast<f32x16(*)[1][TN]>(&acc[i]);
-          f32x16(&lrow)[1][TN] = *reinterpret_cast<f32x16(*)[1][TN]>(&tacc[i]);
-          mfma_x3<1, TN>(hrow, lrow, ah, am, al, bh, bm, bl, true);
-        }
+        mfma_x3<TM, TN>(acc, tacc, ah, am, al, bh, bm, bl, true);
       }
       continue;
     } else if constexpr (F32) {

@@ -17,7 +17,8 @@ over ranks.
 
 Precision: the headline is **fp32** — the reference trains fp32 Float/CudaTensors
 (asyncsgd/glaunch.lua:11, BiCNN/plaunch.lua:200) — with fp32 weights, activations and
-gradients on the hand-written v_mfma_f32_32x32x2_f32 kernels. bf16 autocast (fp32 master
+gradients on the hand-written gfx950 kernels (every GEMM-shaped op as exact bf16x6 split
+products on the bf16 MFMA, ops/conv.py). bf16 autocast (fp32 master
 weights) is reported as the secondary field ``secondary.bf16_autocast`` of the same job.
 
 Also reported, outside the timed region (``--no-secondary`` skips them):

@@ -5,9 +5,11 @@ Two compute dtypes, chosen per call from the input and the autocast state (:func
 * bf16 (bf16 autocast / bf16 tensors): ``v_mfma_f32_32x32x16_bf16``, fp32 accumulate, bf16
   activations; the fp32 master weights are cast once per step (:class:`WeightCastPlan`);
 * fp32 (fp32 tensors, no autocast — the reference's training precision,
-  asyncsgd/glaunch.lua:11, BiCNN/plaunch.lua:200): ``v_mfma_f32_32x32x2_f32``, exact fp32
-  products and accumulation, fp32 activations; the forward reads the fp32 master weight
-  itself, the backward-data its fp32 (tap-flipped) transpose.
+  asyncsgd/glaunch.lua:11, BiCNN/plaunch.lua:200): fp32 operands split in registers into
+  three bf16 planes and multiplied as six ``v_mfma_f32_32x32x16_bf16`` partial products
+  (exact to fp32 accuracy, ``tests/test_fp32_path.py``; ``MPIT_F32_MFMA=native`` selects the
+  fp32-input ``v_mfma_f32_32x32x2_f32`` instead), fp32 activations; the forward reads the
+  fp32 master weight itself, the backward-data its fp32 (tap-flipped) transpose.
 
 A stride-1 1x1 convolution over a channels_last activation is a GEMM over its [N*H*W, C]
 row-major view. Measured on MI355X (benchmarks/conv_vs_gemm.py, ResNet-50 at batch 256)

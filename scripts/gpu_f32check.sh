@@ -1,9 +1,9 @@
 #!/bin/bash
-# fp32 gemm_nt with the row-interleaved split/MFMA order: numerics, probes, bench x2.
+# fp32 gemm_nt change check: numerics, probes, bench x2 (TAG names the output dir).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-D=gpurun_out/rowint
+D=gpurun_out/${TAG:-f32check}
 mkdir -p $D
 timeout -k 10 300 python -u -m pytest tests/test_fp32_path.py -m gpu -q --timeout 120 --timeout-method thread > $D/pytest.log 2>&1; rc=$?
 tail -1 $D/pytest.log; [ $rc -ge 124 ] && exit $rc

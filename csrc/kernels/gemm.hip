@@ -792,11 +792,65 @@ __device__ __forceinline__ int tswz(int row, int ch) {
   else return ch ^ (((row >> 1) & 1) << 2);
 }
 
+// In-kernel split reduction (replaces split_reduce_kernel launches): every split writes its
+// partial tile write-through, takes a ticket for its (tile, group of kReduceGroup splits);
+// the block whose ticket comes last sums the group's partials in split order, and when
+// there is more than one group the last group-reducer of the tile sums the group sums in
+// group order into out (out = beta*out + sum) — the same additions in the same order as
+// the two split_reduce levels, so the result is bitwise the one of the separate launches.
+// Hand-off as in bn_tiles_finalize_kernel (bn_act.hip): sc1 stores, s_waitcnt, barrier,
+// one agent-scope ticket add per workgroup; the consumer: agent acquire, then plain loads.
+constexpr int kReduceGroup = 32;
+constexpr int kTnTicketSlots = 16;
+constexpr int kTnMaxTickets = 8192;
+__device__ uint32_t g_tn_tickets[kTnTicketSlots * kTnMaxTickets];
+
+struct TnRed {
+  float* out;      // final [N][K] (null: separate split_reduce launches)
+  float* mid;      // [groups][N][K] group sums (groups > 1)
+  uint32_t* tick;  // this launch's ticket set: [tiles][groups + 1]
+  float beta;
+  int ns, groups;
+};
+
+__device__ __forceinline__ void st_wt(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// sum rows n0..n0+TBN, cols k0..k0+TBK of nsrc [N][K] slices starting at src (slice stride
+// N*K) in slice order; 256 threads, float4 per element group
+template <int TBN, int TBK>
+__device__ __forceinline__ void tn_tile_sum(const float* src, int nsrc, int64_t slice, int N, int K, int n0, int k0,
+                                            float* dst, bool final_store, float beta, bool wt) {
+  constexpr int C4 = TBK / 4;
+  for (int e = threadIdx.x; e < TBN * C4; e += 256) {
+    const int n = n0 + e / C4, k = k0 + (e % C4) * 4;
+    const int64_t o = int64_t(n) * K + k;
+    float4 a = *reinterpret_cast<const float4*>(src + o);
+    for (int q = 1; q < nsrc; ++q) {
+      const float4 b = *reinterpret_cast<const float4*>(src + int64_t(q) * slice + o);
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    if (final_store) {
+      if (beta != 0.f) {
+        const float4 c = *reinterpret_cast<const float4*>(dst + o);
+        a.x += beta * c.x; a.y += beta * c.y; a.z += beta * c.z; a.w += beta * c.w;
+      }
+      *reinterpret_cast<float4*>(dst + o) = a;
+    } else if (wt) {
+      st_wt(dst + o, a.x); st_wt(dst + o + 1, a.y); st_wt(dst + o + 2, a.z); st_wt(dst + o + 3, a.w);
+    } else {
+      *reinterpret_cast<float4*>(dst + o) = a;
+    }
+  }
+}
+
 template <typename T, int TBN, int TBK, int STAGES, bool CONV, int FM = 0>
 __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y, int64_t ldy,
                                                          const T* __restrict__ X, int64_t ldx,
                                                          float* __restrict__ part, int64_t M, int N, int K,
-                                                         int64_t rows_per_split, int ntk, int ntiles, ConvGeo geo) {
+                                                         int64_t rows_per_split, int ntk, int ntiles, ConvGeo geo,
+                                                         TnRed red) {
   constexpr int WN = TBN / 2, WK = TBK / 2;
   constexpr int TM = WN / 32, TN = WK / 32;
   constexpr int EPC = epc<T>();
@@ -1037,6 +1091,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y
   }
   // D[n][k]: column k = lane&31, row n = (v&3) + 8*(v>>2) + 4*(lane>>5)
   float* out = part + int64_t(split) * N * K;
+  const bool fused = red.tick != nullptr;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1045,13 +1100,43 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y
       for (int v = 0; v < 16; ++v) {
         const int n = n0 + wn * WN + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fh;
         const int k = k0 + wk * WK + j * 32 + fr;
-        out[int64_t(n) * K + k] = acc[i][j][v];
+        if (fused) st_wt(out + int64_t(n) * K + k, acc[i][j][v]);
+        else out[int64_t(n) * K + k] = acc[i][j][v];
       }
+  if (!fused) return;
+  __shared__ uint32_t prev;
+  const int64_t slice = int64_t(N) * K;
+  const int grp = split / kReduceGroup, g0 = grp * kReduceGroup, gn = min(red.ns, g0 + kReduceGroup) - g0;
+  uint32_t* tk = red.tick + int64_t(tile) * (red.groups + 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) prev = atomicAdd(&tk[grp], 1u);
+  __syncthreads();
+  if (prev != uint32_t(gn - 1)) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(&tk[grp], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (red.groups == 1) {  // one level: the group sum is the result
+    tn_tile_sum<TBN, TBK>(part + int64_t(g0) * slice, gn, slice, N, K, n0, k0, red.out, true, red.beta, false);
+    return;
+  }
+  tn_tile_sum<TBN, TBK>(part + int64_t(g0) * slice, gn, slice, N, K, n0, k0, red.mid + int64_t(grp) * slice, false,
+                        0.f, true);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) prev = atomicAdd(&tk[red.groups], 1u);
+  __syncthreads();
+  if (prev != uint32_t(red.groups - 1)) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(&tk[red.groups], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  tn_tile_sum<TBN, TBK>(red.mid, red.groups, slice, N, K, n0, k0, red.out, true, red.beta, false);
 }
 
 // Split reduction, one level: block (x, y) sums splits [y*G, y*G+G) of its float4
 // lanes into out2[y] (or, when gridDim.y == 1, into out with out = beta*out + sum).
-constexpr int kReduceGroup = 32;
 __global__ __launch_bounds__(256) void split_reduce_kernel(const float4* __restrict__ part, int nsplit, int64_t n4,
                                                            float4* __restrict__ out, float beta) {
   const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -1472,6 +1557,27 @@ static void launch_tn_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
   const auto* x = reinterpret_cast<const T*>(X);
   const ConvGeo g = geo ? *geo : ConvGeo{};
   const dim3 grid(unsigned(int64_t(ntiles) * ns));
+  // MPIT_TN_FUSED=1: the split reduction runs inside the GEMM (last block per tile / group).
+  // Bitwise equal to the split_reduce launches but slower on ResNet-50's wgrads (the tail sum
+  // of a tile is left to one block: profiles/tn_fused_reduction_ab_r02.md), so opt-in.
+  static const bool fused_env = [] {
+    const char* e = std::getenv("MPIT_TN_FUSED");
+    return e && std::string(e) == "1";
+  }();
+  TnRed red{};
+  const int ngr = ns > kReduceGroup ? int(tn_groups(ns)) : 1;
+  const bool fused = !direct && fused_env && int64_t(ntiles) * (ngr + 1) <= kTnMaxTickets;
+  if (fused) {
+    static std::atomic<uint32_t> launches{0};
+    uint32_t* base = nullptr;
+    hip_check(hipGetSymbolAddress(reinterpret_cast<void**>(&base), HIP_SYMBOL(g_tn_tickets)), "tn ticket symbol");
+    red.tick = base + size_t(launches.fetch_add(1) % kTnTicketSlots) * kTnMaxTickets;
+    red.out = reinterpret_cast<float*>(out);
+    red.mid = part + int64_t(ns) * N * K;
+    red.beta = beta;
+    red.ns = ns;
+    red.groups = ngr;
+  }
   // MPIT_GEMM_TN_STAGES: ring depth (A/B measurements; bf16 4 by default). fp32 stages
   // twice the bytes per row and computes 16x longer per staged step: 2 stages.
   static const int tn_stages = [] {
@@ -1484,16 +1590,16 @@ static void launch_tn_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
     const size_t shm = size_t(ST) * kRows * (tbn + tbk) * sizeof(T);                                             \
     if (geo && F32 && f32_mode() == 1)                                                                           \
       hipLaunchKernelGGL((gemm_tn_kernel<T, A, B, ST, true, F32 ? 1 : 0>), grid, dim3(256), shm, s, y, ldy, x,     \
-                         ldx, part, M, N, K, rps, ntk, ntiles, g);                                                 \
+                         ldx, part, M, N, K, rps, ntk, ntiles, g, red);                                            \
     else if (F32 && f32_mode() == 1)                                                                               \
       hipLaunchKernelGGL((gemm_tn_kernel<T, A, B, ST, false, F32 ? 1 : 0>), grid, dim3(256), shm, s, y, ldy, x,    \
-                         ldx, part, M, N, K, rps, ntk, ntiles, g);                                                 \
+                         ldx, part, M, N, K, rps, ntk, ntiles, g, red);                                            \
     else if (geo)                                                                                                  \
       hipLaunchKernelGGL((gemm_tn_kernel<T, A, B, ST, true>), grid, dim3(256), shm, s, y, ldy, x, ldx, part, M, N, \
-                         K, rps, ntk, ntiles, g);                                                                  \
+                         K, rps, ntk, ntiles, g, red);                                                             \
     else                                                                                                           \
       hipLaunchKernelGGL((gemm_tn_kernel<T, A, B, ST, false>), grid, dim3(256), shm, s, y, ldy, x, ldx, part, M,   \
-                         N, K, rps, ntk, ntiles, g);                                                               \
+                         N, K, rps, ntk, ntiles, g, red);                                                          \
   } while (0)
 #define MPIT_TN_LAUNCH(A, B)               \
   do {                                     \
@@ -1507,7 +1613,7 @@ static void launch_tn_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
 #undef MPIT_TN_LAUNCH
 #undef MPIT_TN_LAUNCH1
   hip_check(hipGetLastError(), "gemm_tn launch");
-  if (!direct) {
+  if (!direct && !fused) {
     const int64_t n4 = int64_t(N) * K / 4;
     const unsigned gx = unsigned((n4 + 255) / 256);
     const int64_t groups = tn_groups(ns);

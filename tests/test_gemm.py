@@ -1,10 +1,14 @@
 """MFMA GEMM kernels (csrc/kernels/gemm.hip) and the 1x1-conv op built on them, against
 plain PyTorch fp32 references of the same math."""
+import os
+
 import pytest
 import torch
 import torch.nn.functional as F
 
 from mpit_amd.ops import conv as C
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def test_convnhwc_cpu_fallback_matches_conv2d():
@@ -217,3 +221,24 @@ def test_gemm_nt_tile_stats_large_mean(M):
     cd = c.double()
     torch.testing.assert_close(mean, cd.mean(0), rtol=1e-7, atol=1e-4)
     torch.testing.assert_close(var, cd.var(0, unbiased=False), rtol=1e-4, atol=1e-5)
+
+
+@gpu
+def test_tn_fused_split_reduction_bitwise(tmp_path):
+    """The in-kernel split reduction (MPIT_TN_FUSED=1) adds the partials in the order of
+    the split_reduce launches: identical bits, for gemm_tn (one and two reduction levels,
+    beta 0 and 1) and conv_wgrad, bf16 and fp32 operands."""
+    import subprocess
+    import sys
+
+    res = {}
+    for fused in ("0", "1"):
+        path = str(tmp_path / f"tn{fused}.pt")
+        env = dict(os.environ, MPIT_TN_FUSED=fused)
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "mp", "tn_fused_check.py"), path],
+                           env=env, capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-3000:]
+        res[fused] = torch.load(path, weights_only=True)
+    assert res["0"].keys() == res["1"].keys()
+    for k in res["0"]:
+        assert torch.equal(res["0"][k].view(torch.int32), res["1"][k].view(torch.int32)), k

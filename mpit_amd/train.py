@@ -14,6 +14,8 @@ Optimizers: ``downpour`` (async SGD), ``eamsgd`` / ``easgd`` (elastic averaging)
 """
 from __future__ import annotations
 
+import os
+
 import time
 from dataclasses import dataclass, field
 from typing import Optional
@@ -104,6 +106,14 @@ class Trainer:
             # time-slice the card (4 ranks: 8136 -> 1809 img/s)
             WgradStream.enable(self.on_gpu and (not st.shared_devices or WgradStream.forced())
                                and cfg.extra.get("wgrad_stream", True))
+        # The step's critical path (forward, input gradients, BN, pushes) runs on a
+        # high-priority stream; the backward-weight GEMMs of the side stream (lowest priority)
+        # then only take the CUs the critical path leaves free, instead of delaying its small
+        # kernels (BN finalize, apply) behind big split-K GEMMs. MPIT_HP_STREAM=0: off.
+        self.hp_stream = None
+        if self.on_gpu and os.environ.get("MPIT_HP_STREAM", "1") != "0" and not st.shared_devices:
+            lo, hi = torch.cuda.Stream.priority_range()
+            self.hp_stream = torch.cuda.Stream(self.device, priority=min(lo, hi))
         if self.push_steal:
             # push each shard during the backward as soon as its gradients are complete
             if cfg.extra.get("overlap_push", True):
@@ -207,7 +217,14 @@ class Trainer:
     def step(self):
         """One training step of this worker; returns the loss tensor (not synced)."""
         with _trace.range("step"):
-            return self._step()
+            if self.hp_stream is None:
+                return self._step()
+            cur = torch.cuda.current_stream(self.device)
+            self.hp_stream.wait_stream(cur)
+            with torch.cuda.stream(self.hp_stream):
+                fx = self._step()
+            cur.wait_stream(self.hp_stream)
+            return fx
 
     def _step(self):
         c = self.cfg

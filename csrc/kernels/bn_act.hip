@@ -22,6 +22,7 @@
 #include <atomic>
 #include <cmath>
 #include <stdexcept>
+#include <cstdlib>
 #include <string>
 
 #include "ew.h"
@@ -214,7 +215,12 @@ __device__ __forceinline__ void fin_fwd_channel(int c, double a, double b, int C
 //        shifted sums bn_finalize_fwd_kernel expects (shift = row 0 of x), fp64 inside;
 //   plain (backward reductions): tile sums are added.
 constexpr int kTileRows = 128;
-constexpr int kTileLanes = 16;    // row lanes per channel (64 channels x 16 = 1024 threads)
+// row lanes per channel of bn_tiles_finalize_kernel: 4 (64 channels x 4 = 256 threads) by
+// default — in the backward the finalize shares the GPU with the side stream's weight-gradient
+// GEMMs, and a 1024-thread block must wait for a whole CU's worth of free slots
+// (profiles/bn_finalize_lanes_ab_r02.md); MPIT_BN_FIN_LANES=16 restores the wide block
+constexpr int kFinLanesWide = 16;
+constexpr int kFinLanesNarrow = 4;
 constexpr int kTicketSlots = 64;  // rotating ticket sets (one per launch in flight)
 constexpr int kMaxChBlocks = 32;  // C <= 2048
 
@@ -239,7 +245,7 @@ struct FinArgs {
   float* coef;
 };
 
-template <typename T, bool CHAN>
+template <typename T, bool CHAN, int kTileLanes>
 __global__ __launch_bounds__(64 * kTileLanes) void bn_tiles_finalize_kernel(const float* __restrict__ part, int nt,
                                                                             int C, int64_t M, const T* __restrict__ x,
                                                                             int rows_per_group, float* lvl,
@@ -352,8 +358,16 @@ void launch_tiles_finalize(hipStream_t s, const float* part, int64_t nt, int C, 
   uint32_t* tick = base + size_t(launches.fetch_add(1) % kTicketSlots) * kMaxChBlocks;
   int rpg;
   const int g = tile_groups(nt, &rpg);
-  hipLaunchKernelGGL((bn_tiles_finalize_kernel<T, CHAN>), dim3(nchb, g), dim3(64 * kTileLanes), 0, s, part, int(nt),
-                     C, M, x, rpg, lvl, tick, fa);
+  static const bool wide = [] {
+    const char* e = std::getenv("MPIT_BN_FIN_LANES");
+    return e && std::atoi(e) == 16;
+  }();
+  if (wide)
+    hipLaunchKernelGGL((bn_tiles_finalize_kernel<T, CHAN, kFinLanesWide>), dim3(nchb, g), dim3(64 * kFinLanesWide), 0,
+                       s, part, int(nt), C, M, x, rpg, lvl, tick, fa);
+  else
+    hipLaunchKernelGGL((bn_tiles_finalize_kernel<T, CHAN, kFinLanesNarrow>), dim3(nchb, g), dim3(64 * kFinLanesNarrow),
+                       0, s, part, int(nt), C, M, x, rpg, lvl, tick, fa);
 }
 
 // ---------------------------------------------------------------- forward: apply

@@ -1,7 +1,9 @@
 """Library reference point for the MFMA GEMMs: torch.matmul (hipBLASLt) bf16 on GEMM shapes
 of the ResNet-50 convolutions (implicit-GEMM M x N x K), against gemm_probe.py's numbers.
 
-    python benchmarks/mm_probe.py M N K [M N K ...]
+    python benchmarks/mm_probe.py [--f32] M N K [M N K ...]
+
+--f32: fp32 operands (hipBLASLt's fp32 path), the library point for the fp32 (bf16x6) GEMMs.
 """
 import json
 import sys
@@ -10,11 +12,14 @@ import torch
 
 
 def main():
-    a = list(map(int, sys.argv[1:]))
+    args = sys.argv[1:]
+    f32 = "--f32" in args
+    dt = torch.float32 if f32 else torch.bfloat16
+    a = [int(v) for v in args if v != "--f32"]
     for i in range(0, len(a), 3):
         M, N, K = a[i:i + 3]
-        x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
-        w = torch.randn(K, N, device="cuda").to(torch.bfloat16)
+        x = torch.randn(M, K, device="cuda").to(dt)
+        w = torch.randn(K, N, device="cuda").to(dt)
         for _ in range(5):
             y = x @ w
         torch.cuda.synchronize()
@@ -26,7 +31,7 @@ def main():
         e.record()
         torch.cuda.synchronize()
         ms = s.elapsed_time(e) / it
-        print(json.dumps({"mm": [M, N, K], "ms": round(ms, 4), "tflops": round(2.0 * M * N * K / ms / 1e9, 1)}),
+        print(json.dumps({"mm": [M, N, K], "dtype": "fp32" if f32 else "bf16", "ms": round(ms, 4), "tflops": round(2.0 * M * N * K / ms / 1e9, 1)}),
               flush=True)
 
 

@@ -126,6 +126,8 @@ PYBIND11_MODULE(_mpit, m) {
       py::arg("red_mean2") = 0, py::arg("f32") = false);
   m.def("gemm_tn_supported", &gemm_tn_supported);
   m.def("gemm_tn_ws_floats", &gemm_tn_ws_floats);
+  m.def("device_cu_count", &device_cu_count);
+  m.def("stream_create_cu_masked", &stream_create_cu_masked);
   m.def(
       "gemm_tn",
       [](int dev, uintptr_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X, int64_t ldx,

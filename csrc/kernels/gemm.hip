@@ -39,6 +39,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <array>
 #include <vector>
@@ -1263,6 +1264,20 @@ int cu_count(int dev) {
 
 }  // namespace
 
+int device_cu_count(int dev) { return cu_count(dev); }
+
+// A stream whose dispatches only use the CUs set in `mask` (bit i of word i / 32 = CU i).
+// The backward-weight side stream runs on such a stream so a few CUs stay free for the
+// critical path's small kernels (BN finalize / apply) instead of queueing behind
+// side-stream GEMM blocks that hold every CU's registers (ops/conv.py WgradStream).
+uintptr_t stream_create_cu_masked(int dev, const std::vector<uint32_t>& mask) {
+  if (mask.empty()) throw std::invalid_argument("stream_create_cu_masked: empty mask");
+  hip_check(hipSetDevice(dev), "hipSetDevice");
+  hipStream_t s = nullptr;
+  hip_check(hipExtStreamCreateWithCUMask(&s, uint32_t(mask.size()), mask.data()), "hipExtStreamCreateWithCUMask");
+  return reinterpret_cast<uintptr_t>(s);
+}
+
 bool gemm_nt_supported(int64_t M, int N, int K, bool f32) {
   return M > 0 && N > 0 && K > 0 && N % 64 == 0 && K % (f32 ? 16 : kBK) == 0;
 }
@@ -1311,6 +1326,16 @@ static int f32_mode() {
   return m;
 }
 
+// MPIT_GEMM_LOG=1: one stderr line per GEMM launch (kind, M, N, K, conv, epilogue / splits),
+// in issue order — scripts/gemm_calls.py joins it with a kernel trace for per-call TFLOP/s
+static bool gemm_log() {
+  static const bool on = [] {
+    const char* e = std::getenv("MPIT_GEMM_LOG");
+    return e && std::string(e) == "1";
+  }();
+  return on;
+}
+
 template <typename T>
 static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B,
                         int64_t ldb, uintptr_t C, int64_t ldc, uintptr_t cin, uintptr_t cmask, const ConvGeo* geo,
@@ -1336,6 +1361,9 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
     }
   }
   hip_check(hipSetDevice(dev), "hipSetDevice");
+  if (gemm_log())
+    std::fprintf(stderr, "MPIT_GEMM nt %lld %d %d conv=%d epi=%d f32=%d\n", (long long)M, N, K, geo ? 1 : 0, epi,
+                 F32 ? 1 : 0);
   const auto* a = reinterpret_cast<const T*>(A);
   const auto* b = reinterpret_cast<const T*>(B);
   auto* c = reinterpret_cast<T*>(C);
@@ -1547,6 +1575,9 @@ static void launch_tn_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
   int64_t rps;
   int tbn, tbk;
   const int ns = tn_plan(dev, M, N, K, &rps, &tbn, &tbk, geo ? geo->C : 0);
+  if (gemm_log())
+    std::fprintf(stderr, "MPIT_GEMM tn %lld %d %d conv=%d splits=%d f32=%d\n", (long long)M, N, K, geo ? 1 : 0, ns,
+                 F32 ? 1 : 0);
   const int ntk = K / tbk;
   const int ntiles = (N / tbn) * ntk;
   const bool direct = ns == 1 && beta == 0.f;

@@ -124,6 +124,9 @@ void gemm_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64
 // out[N,K] (fp32) = beta*out + Y[M,N]^T . X[M,K]  (split over M; ws: gemm_tn_ws_floats)
 bool gemm_tn_supported(int64_t M, int N, int K);
 int64_t gemm_tn_ws_floats(int dev, int64_t M, int N, int K);
+// compute units of device `dev`; a stream restricted to the CUs of `mask` (gemm.hip)
+int device_cu_count(int dev);
+uintptr_t stream_create_cu_masked(int dev, const std::vector<uint32_t>& mask);
 void gemm_tn(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X, int64_t ldx,
              uintptr_t out, uintptr_t ws, float beta, bool f32 = false);
 // fp32 w[R][T][Cc] -> bf16 wb[R][T][Cc] (optional) and bf16 tap-flipped transpose

@@ -95,8 +95,31 @@ class WgradStream:
             return None
         st = cls._side.get(dev.index)
         if st is None:
-            st = cls._side[dev.index] = torch.cuda.Stream(dev)
+            st = cls._side[dev.index] = cls._make_side(dev)
         return st
+
+    @staticmethod
+    def cu_mask(ncu: int, reserve: int) -> list:
+        """CU mask (32-bit words, bit i = CU i) of the side stream: every CU except
+        ``reserve`` kept for the critical path, picked on the diagonal of (i % 8, i // 8) so
+        they spread evenly whether consecutive CU ids walk the XCDs or fill one XCD first."""
+        period = max(1, ncu // max(1, reserve))
+        words = [0] * ((ncu + 31) // 32)
+        for i in range(ncu):
+            if ((i % 8) + (i // 8)) % period != 0:
+                words[i // 32] |= 1 << (i % 32)
+        return words
+
+    @classmethod
+    def _make_side(cls, dev: torch.device):
+        # MPIT_SIDE_CU_RESERVE=R: the side stream may not use R of the device's CUs, so the
+        # critical path's small kernels always find a free CU (default 0 = all CUs)
+        reserve = int(os.environ.get("MPIT_SIDE_CU_RESERVE", "0"))
+        if reserve <= 0:
+            return torch.cuda.Stream(dev)
+        m = native()
+        handle = m.stream_create_cu_masked(dev.index, cls.cu_mask(m.device_cu_count(dev.index), reserve))
+        return torch.cuda.ExternalStream(handle, device=dev)
 
     @classmethod
     def join(cls):

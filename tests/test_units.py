@@ -310,3 +310,17 @@ def test_eamsgd_lr0_still_applies_elastic_step(world):
     assert not calls  # no forward/backward at lr 0
     pc.stop()
     srv.wait_done()
+
+
+def test_side_stream_cu_mask_spread():
+    """MPIT_SIDE_CU_RESERVE keeps R CUs out of the side stream's mask, spread evenly over
+    both candidate CU-id layouts (id % 8 and consecutive runs of 32)."""
+    from mpit_amd.ops.conv import WgradStream
+
+    for reserve in (32, 64):
+        words = WgradStream.cu_mask(256, reserve)
+        assert len(words) == 8
+        off = [i for i in range(256) if not (words[i // 32] >> (i % 32)) & 1]
+        assert len(off) == reserve
+        assert all(sum(1 for i in off if i % 8 == x) == reserve // 8 for x in range(8))
+        assert all(sum(1 for i in off if i // 32 == b) == reserve // 8 for b in range(8))

@@ -67,6 +67,10 @@ class WgradStream:
     enabled = False
     _side = {}
     _pending = set()
+    # MPIT_WGRAD_AFTER=1: the side stream starts a convolution's weight gradient after its
+    # input-gradient GEMM (so it overlaps the memory-bound BN backward that follows instead
+    # of sharing the CUs with that compute-bound GEMM); default: before it
+    after = os.environ.get("MPIT_WGRAD_AFTER", "0") == "1"
 
     @classmethod
     def enable(cls, on: bool = True):
@@ -337,7 +341,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         m = native()
         dev, s = x.device.index, _stream(x)
         dx = dw = None
-        side = WgradStream.begin(x.device) if ctx.needs_input_grad[1] else None
+        side = WgradStream.begin(x.device) if ctx.needs_input_grad[1] and not WgradStream.after else None
         extra, emask = ctx.slot.take() if ctx.slot is not None else (None, None)
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x, memory_format=torch.channels_last)
@@ -356,6 +360,8 @@ class _Conv1x1Fn(torch.autograd.Function):
             if part is not None:
                 ctx.link.publish(part, nt, dx, part2)
         if ctx.needs_input_grad[1]:
+            if WgradStream.after:
+                side = WgradStream.begin(x.device)
             dw = torch.empty(ctx.wshape, dtype=torch.float32, device=x.device)
             nws = m.gemm_tn_ws_floats(dev, M, co, ci)
             ws = torch.empty(nws, dtype=torch.float32, device=x.device) if nws else None
@@ -447,7 +453,7 @@ def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None):
     m = native()
     dev, st = x.device.index, _stream(x)
     dx = dw = None
-    side = WgradStream.begin(x.device) if ctx.needs_input_grad[1] else None
+    side = WgradStream.begin(x.device) if ctx.needs_input_grad[1] and not WgradStream.after else None
     if ctx.needs_input_grad[0]:
         if stride == 1 and wt is not None:
             # backward-data = forward conv of dz with the flipped, transposed weight
@@ -477,6 +483,8 @@ def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None):
             dx = torch.ops.aten.convolution_backward(dz, x, wv, None, [stride, stride], [pad, pad], [1, 1], False,
                                                      [0, 0], 1, [True, False, False])[0]
     if ctx.needs_input_grad[1]:
+        if WgradStream.after:
+            side = WgradStream.begin(x.device)
         dw = torch.empty((co, c, r, s), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
         nws = m.conv_wgrad_ws_floats(dev, nb, h, w, c, co, r, s, stride, pad)
         ws = torch.empty(nws, dtype=torch.float32, device=x.device) if nws else None

@@ -17,6 +17,10 @@ post-accumulate-grad hook counts finished parameters per bucket and launches the
 non-blocking all-reduce (RCCL on its own stream) as soon as it is complete. ``finish()``
 waits for the outstanding buckets; the 1/N averaging is fused into the optimizer kernel
 (``gscale``).
+
+``wire="bf16"``: each bucket is cast into a bf16 mirror of the flat gradient and reduced in
+bf16 (half the bytes on every xGMI link), then cast back into the fp32 gradient at
+``finish()``; the sum of the N gradients is rounded to bf16 once per ring step.
 """
 from __future__ import annotations
 
@@ -30,9 +34,13 @@ from ..utils.flat import FlatParams
 
 class BucketedAllreduce:
     def __init__(self, model: torch.nn.Module, flat: FlatParams, bucket_mb: float = 25.0, comm: Optional[Comm] = None,
-                 first_bucket_mb: float = 4.0):
+                 first_bucket_mb: float = 4.0, wire: str = "fp32"):
+        if wire not in ("fp32", "bf16"):
+            raise ValueError(f"BucketedAllreduce: wire must be fp32 or bf16, not {wire!r}")
         self.comm = comm or COMM_WORLD()
         self.flat = flat
+        self.wire = wire
+        self.wbuf = torch.empty(flat.numel, dtype=torch.bfloat16, device=flat.grad.device) if wire == "bf16" else None
         es = flat.grad.element_size()
         cap = int(bucket_mb * (1 << 20)) // es
         first = min(cap, int(first_bucket_mb * (1 << 20)) // es) if first_bucket_mb > 0 else cap
@@ -75,6 +83,10 @@ class BucketedAllreduce:
     def _launch(self, b):
         lo, hi = self.buckets[b]
         seg = self.flat.grad[lo:hi]
+        if self.wbuf is not None:
+            seg16 = self.wbuf[lo:hi]
+            seg16.copy_(seg)  # cast on the compute stream, ordered before the collective
+            seg = seg16
         self.reqs[b] = self.comm.Iallreduce(seg, seg, SUM)
 
     def finish(self):
@@ -82,8 +94,11 @@ class BucketedAllreduce:
         for b in range(len(self.buckets)):
             if self.reqs[b] is None:
                 self._launch(b)
-        for r in self.reqs:
+        for b, r in enumerate(self.reqs):
             r.Wait()
+            if self.wbuf is not None:
+                lo, hi = self.buckets[b]
+                self.flat.grad[lo:hi].copy_(self.wbuf[lo:hi])
         self.reqs = [None] * len(self.buckets)
         self.pending = list(self.sizes)
 

@@ -51,7 +51,7 @@ class TrainConfig:
     channels_last: bool = True
     datapath: int = 2  # 0 fused remote kernel, 1 serial SDMA, 2 per-client link streams
     staleness: int = -1  # bounded staleness (SSP) for the PS; -1 = fully asynchronous
-    wire_dtype: str = "fp32"  # "bf16": EASGD elastic differences cross xGMI in bf16
+    wire_dtype: str = "fp32"  # "bf16": EASGD elastic differences / all-reduce buckets cross xGMI in bf16
     server_rule: Optional[ServerOpt] = None
     seed: int = 1234
     bucket_mb: float = 25.0  # allreduce bucket size (parallel/ddp.py sizing note)
@@ -86,7 +86,7 @@ class Trainer:
         if cfg.optimizer == "allreduce":
             from .parallel.ddp import BucketedAllreduce
 
-            self.ddp = BucketedAllreduce(self.model, self.flat, bucket_mb=cfg.bucket_mb)
+            self.ddp = BucketedAllreduce(self.model, self.flat, bucket_mb=cfg.bucket_mb, wire=cfg.wire_dtype)
         else:
             self._start_ps()
         # Downpour su=1 on the GPU: let autograd hand over its gradient tensors and gather

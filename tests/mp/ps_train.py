@@ -17,7 +17,8 @@ dp = int(os.environ.get("T_DATAPATH", "0"))
 mp.Init()
 nc = 10 if model in ("lenet", "cnn7") else 1000
 tr = Trainer(TrainConfig(model=model, batch=batch, num_classes=nc, optimizer=opt, topology=topo, lr=0.05,
-                         mva=0.45, su=int(os.environ.get("T_SU", "1")), datapath=dp, servers=1))
+                         mva=0.45, su=int(os.environ.get("T_SU", "1")), datapath=dp, servers=1,
+                         wire_dtype=os.environ.get("T_WIRE", "fp32")))
 secs, loss = timed_steps(tr, steps, 2)
 # every push has been acked before the barrier inside timed_steps: one more pull gives
 # every worker the final server state — compare a checksum across ranks

@@ -45,10 +45,11 @@ def test_downpour_colocated_gpu_two_ranks_one_device(dp):
     assert max(cs) - min(cs) < 1e-6 * max(1.0, abs(cs[0])), cs
 
 
-def test_sync_allreduce_dp_cpu():
-    r = _result(run_ranks("ps_train.py", 3, {"MPIT_CPU_ONLY": "1", "T_OPT": "allreduce"}))
+@pytest.mark.parametrize("wire", ["fp32", "bf16"])
+def test_sync_allreduce_dp_cpu(wire):
+    r = _result(run_ranks("ps_train.py", 3, {"MPIT_CPU_ONLY": "1", "T_OPT": "allreduce", "T_WIRE": wire}))
     cs = eval(re.search(r"checksums=(\[.*?\])", r).group(1))
-    # synchronous DP keeps every replica bit-identical
+    # synchronous DP keeps every replica bit-identical (bf16 wire too: all ranks cast back the same sums)
     assert max(cs) == min(cs), cs
 
 

@@ -1532,11 +1532,23 @@ bool gemm_tn_supported(int64_t M, int N, int K) { return M > 0 && N % 64 == 0 &&
 // split-K plan: number of splits over M and rows per split, sized so the grid holds
 // about as many blocks as can be resident (bf16 4-stage / fp32 2-stage ring: 64 KiB of
 // LDS per 128x128 tile)
+// MPIT_TN_OCC=1: one gemm_tn block per CU (its LDS request padded to kTnCapShm), so a CU
+// running a backward-weight block of the side stream always has room for one block of the
+// critical path's GEMMs (64 KiB) next to it; the split plan then targets one block per CU.
+constexpr size_t kTnCapShm = 92 * 1024;
+static bool tn_cap1() {
+  static const bool on = [] {
+    const char* e = std::getenv("MPIT_TN_OCC");
+    return e && std::string(e) == "1";
+  }();
+  return on;
+}
+
 static int tn_plan(int dev, int64_t M, int N, int K, int64_t* rows_per_split, int* tbn, int* tbk, int cin = 0) {
   *tbn = N % 128 == 0 ? 128 : 64;
   *tbk = (cin ? cin : K) % 128 == 0 ? 128 : 64;  // conv: a column tile never straddles two taps
   const int64_t ntiles = int64_t(N / *tbn) * (K / *tbk);
-  const int per_cu = 2 * (128 / *tbn) * (128 / *tbk);
+  const int per_cu = tn_cap1() ? 1 : 2 * (128 / *tbn) * (128 / *tbk);
   const int64_t target = int64_t(per_cu) * cu_count(dev);
   // floor: one more block than there are slots would run as a whole second round
   int64_t ns = std::max<int64_t>(1, target / ntiles);
@@ -1616,9 +1628,25 @@ static void launch_tn_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
     return e && std::atoi(e) <= 2 ? 2 : 4;
   }();
   const int stages = F32 ? 2 : tn_stages;
+#define MPIT_TN_OPT_IN(A, B, ST, CV, FMV)                                                                          \
+  do {                                                                                                             \
+    static const bool opted = (hip_check(hipFuncSetAttribute(reinterpret_cast<const void*>(                       \
+                                                             &gemm_tn_kernel<T, A, B, ST, CV, FMV>),              \
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize, int(shm)),    \
+                                     "hipFuncSetAttribute"),                                                       \
+                               true);                                                                              \
+    (void)opted;                                                                                                   \
+  } while (0)
 #define MPIT_TN_LAUNCH1(A, B, ST)                                                                                  \
   do {                                                                                                             \
-    const size_t shm = size_t(ST) * kRows * (tbn + tbk) * sizeof(T);                                             \
+    size_t shm = size_t(ST) * kRows * (tbn + tbk) * sizeof(T);                                                   \
+    if (tn_cap1()) {                                                                                               \
+      shm = std::max(shm, kTnCapShm);                                                                              \
+      if (geo && F32 && f32_mode() == 1) MPIT_TN_OPT_IN(A, B, ST, true, F32 ? 1 : 0);                              \
+      else if (F32 && f32_mode() == 1) MPIT_TN_OPT_IN(A, B, ST, false, F32 ? 1 : 0);                               \
+      else if (geo) MPIT_TN_OPT_IN(A, B, ST, true, 0);                                                             \
+      else MPIT_TN_OPT_IN(A, B, ST, false, 0);                                                                     \
+    }                                                                                                              \
     if (geo && F32 && f32_mode() == 1)                                                                           \
       hipLaunchKernelGGL((gemm_tn_kernel<T, A, B, ST, true, F32 ? 1 : 0>), grid, dim3(256), shm, s, y, ldy, x,     \
                          ldx, part, M, N, K, rps, ntk, ntiles, g, red);                                            \
@@ -1643,6 +1671,7 @@ static void launch_tn_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
   else MPIT_TN_LAUNCH(64, 64);
 #undef MPIT_TN_LAUNCH
 #undef MPIT_TN_LAUNCH1
+#undef MPIT_TN_OPT_IN
   hip_check(hipGetLastError(), "gemm_tn launch");
   if (!direct && !fused) {
     const int64_t n4 = int64_t(N) * K / 4;

@@ -1,5 +1,6 @@
 #include "engine.h"
 
+#include <sys/prctl.h>
 #include <unistd.h>
 #include <xmmintrin.h>
 
@@ -8,6 +9,7 @@
 
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
@@ -705,6 +707,15 @@ void Engine::check_peers() {
 
 void Engine::progress_loop() {
   if (device_ >= 0) hipSetDevice(device_);
+  // 1 us timer slack: the idle back-off sleeps 20 us, and with the default 50 us slack each
+  // wake-up (gated push -> server apply -> completion -> reply) can overshoot to ~70 us,
+  // time the GPU idles at every step boundary of a parameter-server step
+  // (MPIT_TIMER_SLACK_NS overrides; 0 keeps the default)
+  {
+    const char* e = std::getenv("MPIT_TIMER_SLACK_NS");
+    const long ns = e ? std::atol(e) : 1000L;
+    if (ns > 0) prctl(PR_SET_TIMERSLACK, static_cast<unsigned long>(ns), 0, 0, 0);
+  }
   int idle = 0;
   uint64_t last_act = 0;
   auto last_check = std::chrono::steady_clock::now();

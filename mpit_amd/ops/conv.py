@@ -689,16 +689,19 @@ class WeightCastPlan:
             host = torch.empty(self.njobs * m.cast_job_bytes(), dtype=torch.uint8)
             self.nblocks = m.cast_jobs_build(host.data_ptr(), specs)
             self.table = host.to(self.mods[0][0].weight.device)
+        # bind once per build (nn.Module.__setattr__ per conv per step costs ~0.1 ms of host
+        # time at the start of every forward, while the GPU idles); run() only flips valid
+        for mod, _, pair in self.mods:
+            mod._mpit_wcast = (self, pair)
 
     def run(self):
-        if any(mod.weight.data_ptr() != ptr for mod, ptr, _ in self.mods):
+        # (parameters dict lookups: Module.__getattr__ per conv per step is measurable host time)
+        if any(mod._parameters["weight"].data_ptr() != ptr for mod, ptr, _ in self.mods):
             self._build()  # parameters moved (FlatParams.rebind)
         if self.table is not None:
             dev = self.table.device
             native().cast_jobs_run(dev.index, torch.cuda.current_stream(dev).cuda_stream, self.table.data_ptr(),
                                    self.njobs, self.nblocks)
-        for mod, _, pair in self.mods:
-            mod._mpit_wcast = (self, pair)
         self.valid = True
 
     def invalidate(self):

@@ -67,6 +67,10 @@ class Trainer:
         self.rank, self.world = st.rank, st.world
         self.device = st.device if st.device is not None else torch.device("cpu")
         self.on_gpu = self.device.type == "cuda"
+        if self.on_gpu and os.environ.get("MPIT_BLAS") == "rocblas":
+            # the classifier's GEMMs (the only library GEMMs left) on rocBLAS instead of
+            # hipBLASLt (A/B knob: host-side cost per call, GPU bubble around the fc layer)
+            torch.backends.cuda.preferred_blas_library("cublas")
         # identical initial weights on every rank (per-rank seeds for data only)
         torch.manual_seed(cfg.seed)
         model = get_model(cfg.model, num_classes=cfg.num_classes)

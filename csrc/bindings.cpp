@@ -87,12 +87,14 @@ PYBIND11_MODULE(_mpit, m) {
       "bn_act_bwd",
       [](int dev, uintptr_t s, bool bf16, uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t dx, uintptr_t dres,
          int64_t M, int C, uintptr_t gamma, uintptr_t mean, uintptr_t rstd, uintptr_t dgamma, uintptr_t dbeta,
-         uintptr_t ws, bool relu, uintptr_t part, int64_t npart) {
-        bn_act_bwd(dev, S(s), bf16, dy, mask, x, dx, dres, M, C, gamma, mean, rstd, dgamma, dbeta, ws, relu, part, npart);
+         uintptr_t ws, bool relu, uintptr_t part, int64_t npart, uintptr_t coef) {
+        bn_act_bwd(dev, S(s), bf16, dy, mask, x, dx, dres, M, C, gamma, mean, rstd, dgamma, dbeta, ws, relu, part, npart,
+                   coef);
       },
       py::arg("dev"), py::arg("stream"), py::arg("bf16"), py::arg("dy"), py::arg("mask"), py::arg("x"), py::arg("dx"),
       py::arg("dres"), py::arg("M"), py::arg("C"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
-      py::arg("dgamma"), py::arg("dbeta"), py::arg("ws"), py::arg("relu"), py::arg("part") = 0, py::arg("npart") = 0);
+      py::arg("dgamma"), py::arg("dbeta"), py::arg("ws"), py::arg("relu"), py::arg("part") = 0, py::arg("npart") = 0,
+      py::arg("coef") = 0);
   m.def(
       "bn_pair_apply",
       [](int dev, uintptr_t s, uintptr_t x1, uintptr_t coef1, uintptr_t x2, uintptr_t coef2, uintptr_t y, int64_t M,
@@ -115,15 +117,20 @@ PYBIND11_MODULE(_mpit, m) {
       [](int dev, uintptr_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B, int64_t ldb, uintptr_t C,
          int64_t ldc, uintptr_t stats, uintptr_t cin, uintptr_t cmask, uintptr_t red_part, uintptr_t red_x,
          uintptr_t red_mask, uintptr_t red_mean, int64_t red_row0, uintptr_t red_part2, uintptr_t red_x2,
-         uintptr_t red_mean2, bool f32) {
-        const BnRed r{red_part, red_x, red_mask, red_mean, red_row0, red_part2, red_x2, red_mean2};
+         uintptr_t red_mean2, bool f32, uintptr_t fold_coef, uintptr_t fold_gamma, uintptr_t fold_rstd,
+         uintptr_t fold_dgamma, uintptr_t fold_dbeta, uintptr_t fold_lvl) {
+        BnRed r{red_part, red_x, red_mask, red_mean, red_row0, red_part2, red_x2, red_mean2};
+        r.fcoef = fold_coef; r.fgamma = fold_gamma; r.frstd = fold_rstd;
+        r.fdgamma = fold_dgamma; r.fdbeta = fold_dbeta; r.flvl = fold_lvl;
         gemm_nt(dev, S(s), M, N, K, A, lda, B, ldb, C, ldc, stats, cin, cmask, &r, f32);
       },
       py::arg("dev"), py::arg("stream"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("A"), py::arg("lda"),
       py::arg("B"), py::arg("ldb"), py::arg("C"), py::arg("ldc"), py::arg("stats") = 0, py::arg("cin") = 0,
       py::arg("cmask") = 0, py::arg("red_part") = 0, py::arg("red_x") = 0, py::arg("red_mask") = 0,
       py::arg("red_mean") = 0, py::arg("red_row0") = 0, py::arg("red_part2") = 0, py::arg("red_x2") = 0,
-      py::arg("red_mean2") = 0, py::arg("f32") = false);
+      py::arg("red_mean2") = 0, py::arg("f32") = false, py::arg("fold_coef") = 0, py::arg("fold_gamma") = 0,
+      py::arg("fold_rstd") = 0, py::arg("fold_dgamma") = 0, py::arg("fold_dbeta") = 0, py::arg("fold_lvl") = 0);
+  m.def("gemm_nt_fold_lvl_floats", &gemm_nt_fold_lvl_floats);
   m.def("gemm_tn_supported", &gemm_tn_supported);
   m.def("gemm_tn_ws_floats", &gemm_tn_ws_floats);
   m.def("device_cu_count", &device_cu_count);
@@ -166,15 +173,20 @@ PYBIND11_MODULE(_mpit, m) {
       [](int dev, uintptr_t s, int Nb, int H, int W, int C, int Co, int R, int S_, int stride, int pad, uintptr_t x,
          uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t cin, uintptr_t bias, bool relu, uintptr_t red_part,
          uintptr_t red_x, uintptr_t red_mask, uintptr_t red_mean, int64_t red_row0, uintptr_t red_part2,
-         uintptr_t red_x2, uintptr_t red_mean2, bool f32) {
-        const BnRed r{red_part, red_x, red_mask, red_mean, red_row0, red_part2, red_x2, red_mean2};
+         uintptr_t red_x2, uintptr_t red_mean2, bool f32, uintptr_t fold_coef, uintptr_t fold_gamma,
+         uintptr_t fold_rstd, uintptr_t fold_dgamma, uintptr_t fold_dbeta, uintptr_t fold_lvl) {
+        BnRed r{red_part, red_x, red_mask, red_mean, red_row0, red_part2, red_x2, red_mean2};
+        r.fcoef = fold_coef; r.fgamma = fold_gamma; r.frstd = fold_rstd;
+        r.fdgamma = fold_dgamma; r.fdbeta = fold_dbeta; r.flvl = fold_lvl;
         conv_fwd(dev, S(s), Nb, H, W, C, Co, R, S_, stride, pad, x, w, y, stats, cin, bias, relu, &r, f32);
       },
       py::arg("dev"), py::arg("stream"), py::arg("Nb"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("Co"),
       py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("x"), py::arg("w"), py::arg("y"),
       py::arg("stats") = 0, py::arg("cin") = 0, py::arg("bias") = 0, py::arg("relu") = false, py::arg("red_part") = 0,
       py::arg("red_x") = 0, py::arg("red_mask") = 0, py::arg("red_mean") = 0, py::arg("red_row0") = 0,
-      py::arg("red_part2") = 0, py::arg("red_x2") = 0, py::arg("red_mean2") = 0, py::arg("f32") = false);
+      py::arg("red_part2") = 0, py::arg("red_x2") = 0, py::arg("red_mean2") = 0, py::arg("f32") = false,
+      py::arg("fold_coef") = 0, py::arg("fold_gamma") = 0, py::arg("fold_rstd") = 0, py::arg("fold_dgamma") = 0,
+      py::arg("fold_dbeta") = 0, py::arg("fold_lvl") = 0);
   m.def("conv_dgrad_strided_wfloats", &conv_dgrad_strided_wfloats);
   m.def(
       "conv_dgrad_strided_weights",

@@ -699,7 +699,7 @@ void fwd_impl(int dev, hipStream_t s, const T* x, const T* res, T* y, int64_t M,
 template <typename T>
 void bwd_impl(hipStream_t s, const T* dy, const uint8_t* mask, const T* x, T* dx, T* dres, int64_t M, int C,
               const float* gamma, const float* mean, const float* rstd, float* dgamma, float* dbeta, float* ws,
-              bool relu, const float* gpart, int64_t npart) {
+              bool relu, const float* gpart, int64_t npart, const float* coef_in) {
   constexpr int V = Vec<T>::N;
   check_shape(M, C, V, reinterpret_cast<uintptr_t>(x));
   if (relu && !mask) throw std::invalid_argument("bn_act backward: ReLU needs the forward mask");
@@ -708,17 +708,19 @@ void bwd_impl(hipStream_t s, const T* dy, const uint8_t* mask, const T* x, T* dx
   const int R = blk / G;
   int64_t rpb;
   const int nb = stat_blocks(M, R, &rpb);
-  float* coef = ws;  // [3][C]
+  const float* coef = coef_in ? coef_in : ws;  // [3][C]
   float* part = ws + 3 * C;
   const size_t shm = size_t(R) * 2 * C * sizeof(float);
-  if (gpart) {  // reductions already produced by the GEMM that wrote dy (gemm.hip EPI_BNRED)
+  if (coef_in) {
+    // coefficients, dgamma and dbeta already written by the GEMM that produced dy
+  } else if (gpart) {  // reductions already produced by the GEMM that wrote dy (gemm.hip EPI_BNRED)
     FinArgs fa{};
     fa.gamma = gamma;
     fa.mean = mean;
     fa.rstd = rstd;
     fa.dgamma = dgamma;
     fa.dbeta = dbeta;
-    fa.coef = coef;
+    fa.coef = ws;
     launch_tiles_finalize<T, false>(s, gpart, npart, C, M, x, part, fa);
   } else {
     if (relu)
@@ -728,7 +730,7 @@ void bwd_impl(hipStream_t s, const T* dy, const uint8_t* mask, const T* x, T* dx
       hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false>), dim3(nb), dim3(blk), shm, s, dy, mask, x, mean, M, C, rpb,
                          part);
     hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinK), 0, s, part, nb,
-                       C, M, gamma, mean, rstd, dgamma, dbeta, coef);
+                       C, M, gamma, mean, rstd, dgamma, dbeta, ws);
   }
   const int64_t nvec = M * G;
   const dim3 g(apply_grid(nvec, blk)), b(blk);
@@ -786,18 +788,19 @@ void bn_act_apply(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res,
 
 void bn_act_bwd(int dev, hipStream_t s, bool bf16, uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t dx,
                 uintptr_t dres, int64_t M, int C, uintptr_t gamma, uintptr_t mean, uintptr_t rstd, uintptr_t dgamma,
-                uintptr_t dbeta, uintptr_t ws, bool relu, uintptr_t part, int64_t npart) {
+                uintptr_t dbeta, uintptr_t ws, bool relu, uintptr_t part, int64_t npart, uintptr_t coef) {
   hip_check(hipSetDevice(dev), "hipSetDevice");
   auto F = [](uintptr_t p) { return reinterpret_cast<float*>(p); };
   const auto* mk = reinterpret_cast<const uint8_t*>(mask);
+  if (coef && !dx) throw std::invalid_argument("bn_act backward: given coefficients need dx");
   if (bf16)
     bwd_impl<uint16_t>(s, reinterpret_cast<const uint16_t*>(dy), mk, reinterpret_cast<const uint16_t*>(x),
                        reinterpret_cast<uint16_t*>(dx), reinterpret_cast<uint16_t*>(dres), M, C, F(gamma), F(mean),
-                       F(rstd), F(dgamma), F(dbeta), F(ws), relu, F(part), npart);
+                       F(rstd), F(dgamma), F(dbeta), F(ws), relu, F(part), npart, F(coef));
   else
     bwd_impl<float>(s, reinterpret_cast<const float*>(dy), mk, reinterpret_cast<const float*>(x),
                     reinterpret_cast<float*>(dx), reinterpret_cast<float*>(dres), M, C, F(gamma), F(mean), F(rstd),
-                    F(dgamma), F(dbeta), F(ws), relu, F(part), npart);
+                    F(dgamma), F(dbeta), F(ws), relu, F(part), npart, F(coef));
 }
 
 template <typename T>

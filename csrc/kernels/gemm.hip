@@ -39,6 +39,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <array>
@@ -204,7 +205,22 @@ struct EpiArgs {
   float* part2;                // EPI_BNRED2: the second BN of a bn_pair (same gradient and mask)
   const void* x2;
   const float* mean2;
+  // EPI_BNRED fold (fcoef != null): the BN backward's finalize runs in this GEMM's last
+  // blocks (see the end of gemm_nt_kernel's epilogue) instead of a separate launch
+  const float* fgamma;         // BN weight [N] or null (1)
+  const float* frstd;          // BN 1/std [N]
+  float* fdgamma;              // outputs [N] (or null)
+  float* fdbeta;
+  float* fcoef;                // [3][N] the BN backward's apply coefficients
+  float* flvl;                 // [groups][2][N] group sums
+  uint32_t* ftick;             // this launch's tickets [ntn][groups + 1]
+  int fgroup;                  // M-tiles per group
 };
+
+// write-through (sc1) store: visible to a reader on any XCD without an L2 write-back
+__device__ __forceinline__ void st_wt(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // source line for padding taps: LDS DMA of zeros (any chunk of a 256-B row, either type)
 __device__ __attribute__((aligned(256))) uint16_t g_zero_line[256] = {};
@@ -264,6 +280,95 @@ __device__ __forceinline__ void wait_vmcnt() {
 __device__ __forceinline__ int xcd_tile(int bid, int nb) {
   const int x = bid % 8, q = nb / 8, r = nb % 8;
   return x * q + min(x, r) + bid / 8;
+}
+
+// BN backward finalize folded into the EPI_BNRED GEMM (replaces the separate
+// bn_tiles_finalize launch, which in the backward waits for CU slots behind the side
+// stream's weight-gradient GEMMs): tickets per (column tile, group of fgroup M-tiles) —
+// the group's last block sums the group's partial rows (fp64, row order) into flvl; the
+// last group-folder of the column tile sums the groups in group order and writes dgamma,
+// dbeta and the apply coefficients (bn_act.hip fin_bwd_channel's math). Deterministic; the
+// hand-off is bn_tiles_finalize_kernel's: write-through stores, s_waitcnt, barrier, one
+// agent-scope ticket add per workgroup, agent acquire in the consumer.
+constexpr int kFoldSlots = 16;
+constexpr int kFoldMax = 8192;
+constexpr int kFoldMaxGroups = 128;
+__device__ uint32_t g_fold_tickets[kFoldSlots * kFoldMax];
+
+template <int BN, int HALVES>
+__device__ __forceinline__ void bnred_fold(const EpiArgs& ep, void* smem, int64_t M, int N, int mt, int nt, int n0) {
+  constexpr int NT = 256, L = NT / BN;  // lanes per column
+  const int t = threadIdx.x, cl = t % BN, kl = t / BN;
+  const int64_t mtn = (M + HALVES * 128 - 1) / (HALVES * 128);
+  const int fg = ep.fgroup;
+  const int ngr = int((mtn + fg - 1) / fg);
+  const int grp = mt / fg;
+  const int gsz = int(min<int64_t>(fg, mtn - int64_t(grp) * fg));
+  uint32_t* tk = ep.ftick + size_t(nt) * size_t(ngr + 1);
+  uint32_t* flag = reinterpret_cast<uint32_t*>(smem);
+  double* sd = reinterpret_cast<double*>(smem) + 2;  // [2][L][BN]
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every partial store of this block issued and retired; LDS reads done
+  if (t == 0) flag[0] = atomicAdd(&tk[grp], 1u);
+  __syncthreads();
+  if (flag[0] != uint32_t(gsz - 1)) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int64_t nparts = (M + 127) / 128;
+  const int64_t r0 = int64_t(grp) * fg * HALVES, r1 = min(nparts, r0 + int64_t(gsz) * HALVES);
+  double a = 0, b = 0;
+  for (int64_t r = r0 + kl; r < r1; r += L) {
+    a += double(ep.part[(r * 2) * N + n0 + cl]);
+    b += double(ep.part[(r * 2 + 1) * N + n0 + cl]);
+  }
+  sd[kl * BN + cl] = a;
+  sd[(L + kl) * BN + cl] = b;
+  __syncthreads();
+  if (kl == 0) {
+#pragma unroll
+    for (int k = 1; k < L; ++k) {
+      a += sd[k * BN + cl];
+      b += sd[(L + k) * BN + cl];
+    }
+    st_wt(ep.flvl + (int64_t(grp) * 2) * N + n0 + cl, float(a));
+    st_wt(ep.flvl + (int64_t(grp) * 2 + 1) * N + n0 + cl, float(b));
+  }
+  if (t == 0) __hip_atomic_store(&tk[grp], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) flag[0] = atomicAdd(&tk[ngr], 1u);
+  __syncthreads();
+  if (flag[0] != uint32_t(ngr - 1)) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  a = b = 0;
+  for (int g = kl; g < ngr; g += L) {
+    a += double(ep.flvl[(int64_t(g) * 2) * N + n0 + cl]);
+    b += double(ep.flvl[(int64_t(g) * 2 + 1) * N + n0 + cl]);
+  }
+  sd[kl * BN + cl] = a;
+  sd[(L + kl) * BN + cl] = b;
+  __syncthreads();
+  if (t == 0) __hip_atomic_store(&tk[ngr], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (kl != 0) return;
+  a = b = 0;
+#pragma unroll
+  for (int k = 0; k < L; ++k) {  // lane order, as the finalize kernel's LDS combine
+    a += sd[k * BN + cl];
+    b += sd[(L + k) * BN + cl];
+  }
+  const int c = n0 + cl;
+  const float rs = ep.frstd[c];
+  if (ep.fdgamma) ep.fdgamma[c] = float(b) * rs;
+  if (ep.fdbeta) ep.fdbeta[c] = float(a);
+  const float A = (ep.fgamma ? ep.fgamma[c] : 1.f) * rs;
+  const float mdz = float(a / double(M)), mdx = float(b / double(M));
+  const float Cc = -A * rs * rs * mdx;
+  ep.fcoef[c] = A;
+  ep.fcoef[N + c] = Cc;
+  ep.fcoef[2 * N + c] = -A * mdz - Cc * ep.mean[c];
 }
 
 // ------------------------------------------------------------------------------ NT GEMM
@@ -761,8 +866,13 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
           b += red[(k * 3 + 1) * BN + n];
           if constexpr (DUAL) c3 += red[(k * 3 + 2) * BN + n];
         }
-        prow[n] = a;
-        prow[N + n] = b;
+        if (EPI == EPI_BNRED && ep.fcoef != nullptr) {  // read by the folding block (any XCD)
+          st_wt(prow + n, a);
+          st_wt(prow + N + n, b);
+        } else {
+          prow[n] = a;
+          prow[N + n] = b;
+        }
         if constexpr (DUAL) {
           float* prow2 = ep.part2 + (ep.row0 + tile) * 2 * int64_t(N) + n0;
           prow2[n] = a;
@@ -770,6 +880,9 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
         }
       }
     }
+  }
+  if constexpr (EPI == EPI_BNRED) {
+    if (ep.fcoef != nullptr) bnred_fold<BN, HALVES>(ep, smem, M, N, mt, nt, n0);
   }
 }
 
@@ -813,10 +926,6 @@ struct TnRed {
   float beta;
   int ns, groups;
 };
-
-__device__ __forceinline__ void st_wt(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // sum rows n0..n0+TBN, cols k0..k0+TBK of nsrc [N][K] slices starting at src (slice stride
 // N*K) in slice order; 256 threads, float4 per element group
@@ -1286,6 +1395,8 @@ int64_t gemm_nt_stats_floats(int64_t M, int N) { return gemm_nt_tiles(M) * 2 * i
 
 int64_t gemm_nt_tiles(int64_t M) { return (M + 127) / 128; }
 
+int64_t gemm_nt_fold_lvl_floats(int N) { return int64_t(kFoldMaxGroups) * 2 * N; }
+
 // Block tile of gemm_nt: 0 = 128 x (128 | 64), 1 = 256 x 128, 2 = 256 x 256;
 // MPIT_GEMM_TILE=128|256x128|256 selects one (A/B runs, large plain GEMMs). fp32 runs the
 // 128-row tiles only (its MFMA is 16x slower per FLOP: LDS-bound tile shapes do not matter).
@@ -1336,11 +1447,26 @@ static bool gemm_log() {
   return on;
 }
 
+// group size (M-tiles) and ticket set of a folded BN finalize: <= kFoldMaxGroups groups of
+// >= 16 M-tiles; a rotating set of ticket counters per launch (reset to zero by their last
+// user, so a set is free once its launch retired)
+static void fold_plan(EpiArgs& ep, int64_t mtn, int ntn) {
+  const int64_t fg = std::max<int64_t>(16, (mtn + kFoldMaxGroups - 1) / kFoldMaxGroups);
+  const int64_t ngr = (mtn + fg - 1) / fg;
+  if (int64_t(ntn) * (ngr + 1) > kFoldMax) throw std::invalid_argument("gemm_nt: BN fold ticket table too small");
+  static std::atomic<uint32_t> launches{0};
+  uint32_t* base = nullptr;
+  hip_check(hipGetSymbolAddress(reinterpret_cast<void**>(&base), HIP_SYMBOL(g_fold_tickets)), "fold ticket symbol");
+  ep.ftick = base + size_t(launches.fetch_add(1) % kFoldSlots) * kFoldMax;
+  ep.fgroup = int(fg);
+}
+
 template <typename T>
 static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B,
                         int64_t ldb, uintptr_t C, int64_t ldc, uintptr_t cin, uintptr_t cmask, const ConvGeo* geo,
-                        const EpiArgs& ep, int epi, uintptr_t bias, bool relu) {
+                        const EpiArgs& ep_in, int epi, uintptr_t bias, bool relu) {
   constexpr bool F32 = sizeof(T) == 4;
+  EpiArgs ep = ep_in;  // the fold's group size and ticket set are filled in per launch
   constexpr int EPC = epc<T>();
   if (!gemm_nt_supported(M, N, K, F32))
     throw std::invalid_argument(std::string("gemm_nt: need N % 64 == 0 and K % ") + (F32 ? "16" : "32") +
@@ -1354,6 +1480,8 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
   if (epi != EPI_NONE) {
     if (!ep.part) throw std::invalid_argument("gemm_nt: reduction epilogue needs a partials buffer");
     if (epi == EPI_BNRED2 && geo) throw std::invalid_argument("gemm_nt: paired BN reduction is for 1x1 GEMMs");
+    if (ep.fcoef && (epi != EPI_BNRED || ep.row0 != 0 || !ep.frstd || !ep.flvl))
+      throw std::invalid_argument("gemm_nt: the BN finalize fold needs a single-launch EPI_BNRED with rstd and lvl");
     if (epi == EPI_BNRED || epi == EPI_BNRED2) {
       if (!ep.x || !ep.mean || ldc != N) throw std::invalid_argument("gemm_nt: BN reduction needs x, mean, ldc == N");
       check_ptr(reinterpret_cast<uintptr_t>(ep.x), "BN x");
@@ -1441,6 +1569,7 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
     const int ntn = N / BN;                                                                                    \
     const int64_t nb = mtn * ntn;                                                                              \
     if (nb > INT32_MAX) throw std::invalid_argument("gemm_nt: too many tiles");                               \
+    if (ep.fcoef) fold_plan(ep, mtn, ntn);                                                                     \
     /* LDS: the k-tile ring, reused by the epilogue's output tile and reduction table */                      \
     const size_t shm = std::max({size_t(ST) * (BM + BN) * size_t(nt_bkb(BM, BN, fm)),                          \
                                  size_t(BM) * BN * sizeof(T), size_t(256) * 8 * 3 * sizeof(float)});          \
@@ -1509,6 +1638,14 @@ static EpiArgs epi_args(uintptr_t stats, const BnRed* r, int* mode) {
     ep.mean = reinterpret_cast<const float*>(r->mean);
     ep.row0 = r->row0;
     *mode = EPI_BNRED;
+    if (r->fcoef) {
+      ep.fcoef = reinterpret_cast<float*>(r->fcoef);
+      ep.fgamma = reinterpret_cast<const float*>(r->fgamma);
+      ep.frstd = reinterpret_cast<const float*>(r->frstd);
+      ep.fdgamma = reinterpret_cast<float*>(r->fdgamma);
+      ep.fdbeta = reinterpret_cast<float*>(r->fdbeta);
+      ep.flvl = reinterpret_cast<float*>(r->flvl);
+    }
     if (r->part2) {
       if (!r->x2 || !r->mean2) throw std::invalid_argument("gemm_nt: second BN reduction needs x2 and mean2");
       ep.part2 = reinterpret_cast<float*>(r->part2);
@@ -1943,6 +2080,7 @@ void conv_dgrad_strided(int dev, hipStream_t s, int Nb, int H, int W, int C, int
     // contribute nothing)
     int mode;
     EpiArgs ep = epi_args(0, red, &mode);
+    ep.fcoef = nullptr;  // several launches write the partials: no folded finalize
     ep.row0 += row0;
     row0 += gemm_nt_tiles(M);
     launch_nt(dev, s, M, C, K, dy, Co, wcls + uintptr_t(c.base) * (f32 ? 4 : 2), K, dx, C, 0, 0, &g, ep, mode, f32);

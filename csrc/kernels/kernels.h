@@ -84,7 +84,10 @@ void bn_act_apply(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res,
 // produced by the GEMM that wrote dy (EPI_BNRED) — the reduction pass is skipped.
 void bn_act_bwd(int dev, hipStream_t s, bool bf16, uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t dx,
                 uintptr_t dres, int64_t M, int C, uintptr_t gamma, uintptr_t mean, uintptr_t rstd, uintptr_t dgamma,
-                uintptr_t dbeta, uintptr_t ws, bool relu, uintptr_t part = 0, int64_t npart = 0);
+                uintptr_t dbeta, uintptr_t ws, bool relu, uintptr_t part = 0, int64_t npart = 0,
+                uintptr_t coef = 0);
+// coef (optional): the apply coefficients [3][C] already computed (the finalize folded into
+// the GEMM that wrote dy, BnRed::fcoef; dgamma / dbeta written there too): apply pass only.
 
 // bn_act_fwd with y == 0 / bn_act_bwd with dx == 0 only compute the coefficients into
 // ws[0, 2C) (scale, shift) / ws[0, 3C) (A, C, B) and the running stats / dgamma, dbeta.
@@ -114,7 +117,11 @@ struct BnRed {
   uintptr_t part = 0, x = 0, mask = 0, mean = 0;
   int64_t row0 = 0;
   uintptr_t part2 = 0, x2 = 0, mean2 = 0;
+  // fold the BN backward's finalize into the GEMM (single EPI_BNRED launch): coefficients
+  // [3][N], dgamma / dbeta [N], from gamma (or 0) and rstd; lvl: gemm_nt_fold_lvl_floats(N)
+  uintptr_t fcoef = 0, fgamma = 0, frstd = 0, fdgamma = 0, fdbeta = 0, flvl = 0;
 };
+int64_t gemm_nt_fold_lvl_floats(int N);
 bool gemm_nt_supported(int64_t M, int N, int K, bool f32 = false);
 int64_t gemm_nt_tiles(int64_t M);
 int64_t gemm_nt_stats_floats(int64_t M, int N);

@@ -38,7 +38,7 @@ def _cl(x: torch.Tensor) -> torch.Tensor:
 
 
 # how often each fused hand-over fired (tests assert the fused path ran)
-COUNTERS = {"fwd_tile_stats": 0, "bwd_linked": 0}
+COUNTERS = {"fwd_tile_stats": 0, "bwd_linked": 0, "bwd_folded": 0}
 
 
 class BNLink:
@@ -51,11 +51,14 @@ class BNLink:
     if it receives exactly that tensor, unmodified — when autograd summed gradients from
     several consumers it falls back to its own reduction pass."""
 
-    __slots__ = ("x", "mask", "mean", "part", "npart", "dy_ptr", "dy_ver", "x2", "mean2", "part2")
+    __slots__ = ("x", "mask", "mean", "part", "npart", "dy_ptr", "dy_ver", "x2", "mean2", "part2", "w", "rstd",
+                 "fold")
 
     def __init__(self):
         self.x = self.mask = self.mean = self.part = None
         self.x2 = self.mean2 = self.part2 = None  # the shortcut BN of a bn_pair
+        self.w = self.rstd = None  # BN weight (fp32) and 1/std: the consumer may fold the finalize
+        self.fold = None  # (coef [3C], dgamma, dbeta) written by the consumer's GEMM
         self.npart = 0
         self.dy_ptr = self.dy_ver = None
 
@@ -65,18 +68,27 @@ class BNLink:
         return (self.x is not None and self.mean is not None and x.dtype == self.x.dtype
                 and self.x.shape == x.shape)
 
-    def publish(self, part: torch.Tensor, npart: int, dy: torch.Tensor, part2: torch.Tensor = None):
-        self.part, self.npart, self.part2 = part, int(npart), part2
+    def publish(self, part: torch.Tensor, npart: int, dy: torch.Tensor, part2: torch.Tensor = None, fold=None):
+        self.part, self.npart, self.part2, self.fold = part, int(npart), part2, fold
         self.dy_ptr, self.dy_ver = dy.data_ptr(), dy._version
 
     def take(self, dy: torch.Tensor, pair: bool = False):
+        """(part, npart[, part2]) for a matching gradient, else empty; a folded finalize's
+        buffers are left in ``self.fold`` for :meth:`take_fold`."""
         part, npart, part2 = self.part, self.npart, self.part2
         ok = part is not None and dy.data_ptr() == self.dy_ptr and dy._version == self.dy_ver
         ok = ok and (part2 is not None or not pair)
         self.part = self.x = self.mask = self.mean = self.x2 = self.mean2 = self.part2 = None
+        self.w = self.rstd = None
+        if not ok:
+            self.fold = None
         if pair:
             return (part, npart, part2) if ok else (None, 0, None)
         return (part, npart) if ok else (None, 0)
+
+    def take_fold(self):
+        fold, self.fold = self.fold, None
+        return fold
 
 
 def tile_stats_of(x: torch.Tensor):
@@ -122,6 +134,7 @@ class _BNActFn(torch.autograd.Function):
         ctx.link = link
         if link is not None:
             link.x, link.mask, link.mean = x, mask, mean
+            link.w, link.rstd = w, rstd
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.res_slot = res_slot
@@ -145,16 +158,25 @@ class _BNActFn(torch.autograd.Function):
         dgamma = torch.empty(C, dtype=torch.float32, device=x.device) if ctx.has_w else None
         dbeta = torch.empty(C, dtype=torch.float32, device=x.device) if ctx.has_b else None
         ws = torch.empty(m.bn_workspace_floats(C), dtype=torch.float32, device=x.device)
-        # reductions folded into the consumer convolution's backward-data GEMM (BNLink)
+        # reductions folded into the consumer convolution's backward-data GEMM (BNLink); with
+        # a folded finalize the GEMM also left the coefficients, dgamma and dbeta
         part, npart = ctx.link.take(dy) if ctx.link is not None else (None, 0)
+        fold = ctx.link.take_fold() if part is not None else None
+        coef = 0
         if part is not None:
             COUNTERS["bwd_linked"] += 1
+        if fold is not None:
+            COUNTERS["bwd_folded"] += 1
+            coef = fold[0].data_ptr()
+            dgamma = fold[1] if ctx.has_w else None
+            dbeta = fold[2] if ctx.has_b else None
+            part, npart = None, 0
         m.bn_act_bwd(dev, stream, x.dtype == torch.bfloat16, dy.data_ptr(),
                      mask.data_ptr() if mask is not None else 0, x.data_ptr(), dx.data_ptr(),
                      dres.data_ptr() if dres is not None else 0, M, C, w.data_ptr() if w is not None else 0,
                      mean.data_ptr(), rstd.data_ptr(), dgamma.data_ptr() if dgamma is not None else 0,
                      dbeta.data_ptr() if dbeta is not None else 0, ws.data_ptr(), bool(ctx.relu),
-                     part=part.data_ptr() if part is not None else 0, npart=npart)
+                     part=part.data_ptr() if part is not None else 0, npart=npart, coef=coef)
         if ctx.res_slot is not None:  # the shortcut's gradient is added by the block's first conv
             if park:
                 if not ctx.res_slot.put(dy, mask):

@@ -214,18 +214,32 @@ def cast_transpose(w: torch.Tensor, dtype=torch.bfloat16):
     return wb, wt
 
 
-def _red_args(link, c: int, ntiles: int, device):
-    """(kernel keyword arguments, partials, second partials or None) of a BN backward
-    reduction folded into a backward-data GEMM (see ops/bn.py BNLink; a bn_pair link also
-    reduces for its shortcut BN)."""
+# MPIT_BN_FOLD=0: the BN backward's finalize as its own launch instead of in the GEMM
+_BN_FOLD = os.environ.get("MPIT_BN_FOLD", "1") != "0"
+
+
+def _red_args(link, c: int, ntiles: int, device, fold: bool = False):
+    """(kernel keyword arguments, partials, second partials or None, fold buffers or None)
+    of a BN backward reduction folded into a backward-data GEMM (see ops/bn.py BNLink; a
+    bn_pair link also reduces for its shortcut BN). ``fold`` (single-launch GEMMs, single
+    BN): the GEMM's last blocks also run the BN backward's finalize and write its apply
+    coefficients, dgamma and dbeta — the separate finalize launch (which in the backward
+    waits for CU slots behind the side stream's GEMMs) disappears."""
     part = torch.empty(ntiles * 2 * c, dtype=torch.float32, device=device)
     kw = dict(red_part=part.data_ptr(), red_x=link.x.data_ptr(),
               red_mask=link.mask.data_ptr() if link.mask is not None else 0, red_mean=link.mean.data_ptr())
-    part2 = None
+    part2 = fb = None
     if link.x2 is not None:
         part2 = torch.empty(ntiles * 2 * c, dtype=torch.float32, device=device)
         kw.update(red_part2=part2.data_ptr(), red_x2=link.x2.data_ptr(), red_mean2=link.mean2.data_ptr())
-    return kw, part, part2
+    elif fold and _BN_FOLD and link.rstd is not None:
+        buf = torch.empty(5 * c + native().gemm_nt_fold_lvl_floats(c), dtype=torch.float32, device=device)
+        coef, dgamma, dbeta, lvl = buf[: 3 * c], buf[3 * c: 4 * c], buf[4 * c: 5 * c], buf[5 * c:]
+        kw.update(fold_coef=coef.data_ptr(), fold_gamma=link.w.data_ptr() if link.w is not None else 0,
+                  fold_rstd=link.rstd.data_ptr(), fold_dgamma=dgamma.data_ptr(), fold_dbeta=dbeta.data_ptr(),
+                  fold_lvl=lvl.data_ptr())
+        fb = (coef, dgamma, dbeta)
+    return kw, part, part2, fb
 
 
 def _link_of(x: torch.Tensor, dt, pair_ok: bool = True):
@@ -348,7 +362,7 @@ class _Conv1x1Fn(torch.autograd.Function):
             kw, part, part2 = {}, None, None
             if ctx.link is not None:  # the producing BN's backward reduction, in the epilogue
                 nt = m.gemm_nt_tiles(M)
-                kw, part, part2 = _red_args(ctx.link, ci, nt, x.device)
+                kw, part, part2, fb = _red_args(ctx.link, ci, nt, x.device, fold=True)
             if extra is not None:  # gradient parked by the block (GradSlot): added in the epilogue
                 extra = _to(extra, dt)
                 if extra.shape != x.shape:
@@ -358,7 +372,7 @@ class _Conv1x1Fn(torch.autograd.Function):
             else:
                 m.gemm_nt(dev, s, M, ci, co, dy.data_ptr(), co, wt.data_ptr(), co, dx.data_ptr(), ci, 0, f32=f32, **kw)
             if part is not None:
-                ctx.link.publish(part, nt, dx, part2)
+                ctx.link.publish(part, nt, dx, part2, fb)
         if ctx.needs_input_grad[1]:
             if WgradStream.after:
                 side = WgradStream.begin(x.device)
@@ -461,11 +475,11 @@ def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None):
             kw, part, nt = {}, None, 0
             if link is not None:
                 nt = m.gemm_nt_tiles(nb * h * w)
-                kw, part, _ = _red_args(link, c, nt, x.device)
+                kw, part, _, fb = _red_args(link, c, nt, x.device, fold=True)
             m.conv_fwd(dev, st, nb, ho, wo, co, c, r, s, 1, r - 1 - pad, dz.data_ptr(), wt.data_ptr(),
                        dx.data_ptr(), f32=f32, **kw)
             if part is not None:
-                link.publish(part, nt, dx)
+                link.publish(part, nt, dx, None, fb)
         elif wt is not None:
             # strided: stride^2 parity classes, each a stride-1 implicit GEMM over dz whose
             # epilogue writes its pixels of dx (wt = the packed class weights)
@@ -473,7 +487,7 @@ def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None):
             kw, part, nt = {}, None, 0
             if link is not None:
                 nt = m.conv_dgrad_strided_tiles(nb, h, w, c, co, r, s, stride, pad)
-                kw, part, _ = _red_args(link, c, nt, x.device)
+                kw, part, _, _ = _red_args(link, c, nt, x.device)
             m.conv_dgrad_strided(dev, st, nb, h, w, c, co, r, s, stride, pad, dz.data_ptr(), wt.data_ptr(),
                                  dx.data_ptr(), f32=f32, **kw)
             if part is not None:

@@ -115,6 +115,9 @@ def test_chained_blocks_fold_bn_passes(stride):
     # bn1, bn2 of both blocks + bn3 of block 1 (block 2's bn3 output is the loss input); with
     # a downsample shortcut block 1's bn3 and shortcut BN are one pair, both linked
     assert fired["bwd_linked"] == (6 if down is not None else 5), fired
+    # the finalize runs inside the producing GEMM for single-launch backward-data GEMMs of a
+    # single BN (not the strided parity classes, not a bn_pair)
+    assert fired["bwd_folded"] == (3 if down is not None else 5), fired
     grads1 = {n: p.grad.detach().clone() for n, p in net.named_parameters()}
     net.zero_grad(set_to_none=True)
 
@@ -172,3 +175,49 @@ def test_weight_cast_plan_matches_per_call_casts():
         plan.invalidate()
         y2 = net(x)
     assert torch.equal(y1, y2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_folded_bn_finalize_matches_separate_launch(dtype):
+    """BN backward finalize inside the backward-data GEMM (ops/conv.py _red_args fold) vs the
+    separate bn_tiles_finalize launch: same gradients up to summation order, on a tall layer
+    (12544 rows: several fold groups) and the downsample / 3x3 / 1x1 mix of two blocks."""
+    from mpit_amd.ops import bn as bnmod
+    from mpit_amd.ops import conv as convmod
+
+    torch.manual_seed(11)
+    b1 = Bottleneck(256, 64)
+    b2 = Bottleneck(256, 64)
+    net = torch.nn.Sequential(b1, b2).cuda().to(memory_format=torch.channels_last)
+    for m in net.modules():
+        if isinstance(m, BatchNormAct2d):
+            m.weight.data.uniform_(0.5, 1.5)
+            m.bias.data.uniform_(-0.2, 0.2)
+    x = torch.randn(16, 256, 28, 28, device="cuda").contiguous(memory_format=torch.channels_last)
+    g = torch.randn(16, 256, 28, 28, device="cuda").contiguous(memory_format=torch.channels_last)
+
+    def run(fold):
+        saved = convmod._BN_FOLD
+        convmod._BN_FOLD = fold
+        try:
+            c0 = bnmod.COUNTERS["bwd_folded"]
+            xi = x.clone().to(dtype).requires_grad_(True)
+            with torch.autocast("cuda", dtype=torch.bfloat16, enabled=dtype == torch.bfloat16):
+                y = net(xi)
+            y.backward(g.to(y.dtype))
+            torch.cuda.synchronize()
+            grads = {n: p.grad.detach().float().clone() for n, p in net.named_parameters()}
+            grads["x"] = xi.grad.detach().float().clone()
+            net.zero_grad(set_to_none=True)
+            return grads, bnmod.COUNTERS["bwd_folded"] - c0
+        finally:
+            convmod._BN_FOLD = saved
+
+    g_sep, n_sep = run(False)
+    g_fold, n_fold = run(True)
+    assert n_sep == 0 and n_fold == 5, (n_sep, n_fold)
+    tol = 2e-5 if dtype == torch.float32 else 2e-2
+    for n in g_sep:
+        assert torch.isfinite(g_fold[n]).all(), n
+        assert _rel(g_fold[n], g_sep[n]) < tol, (n, _rel(g_fold[n], g_sep[n]))

@@ -16,6 +16,7 @@ run n8_downpour 400 $TR --nproc-per-node 8 bench.py --gpus 8 --batch 32 --steps 
 run n4_downpour 300 $TR --nproc-per-node 4 bench.py --gpus 4 --batch 64 --steps 5 --warmup 2
 run n3_dedicated 300 $TR --nproc-per-node 3 bench.py --gpus 3 --batch 64 --steps 5 --warmup 2 --topology dedicated --servers 1
 run n2_eamsgd 300 $TR --nproc-per-node 2 bench.py --gpus 2 --batch 64 --steps 5 --warmup 2 --optimizer eamsgd --su 2 --wire bf16
+run n2_allreduce_bf16wire 300 $TR --nproc-per-node 2 bench.py --gpus 2 --batch 64 --steps 5 --warmup 2 --optimizer allreduce --wire bf16
 run n1_allreduce 300 python -u bench.py --optimizer allreduce --steps 10 --warmup 3
 run n1_alexnet_ssp 300 python -u bench.py --model alexnet --batch 256 --staleness 2 --steps 10 --warmup 3
 run n1_vgg16_easgd_bf16 300 python -u bench.py --model vgg16 --batch 64 --optimizer eamsgd --su 2 --steps 10 --warmup 3 --dtype bf16

@@ -290,3 +290,23 @@ def test_resnet50_fp32_step_runs_native():
     assert torch.isfinite(loss)
     for m in convs:
         assert m.weight.grad is not None and torch.isfinite(m.weight.grad).all()
+
+
+@pytest.mark.gpu
+def test_fp32_training_tracks_fp64_like_stock_pytorch():
+    """ResNet-50 on the fp32 mpit kernels: forward loss and first-step gradients as close to
+    an fp64 CPU reference as the same network in stock PyTorch fp32 (benchmarks/loss_parity.py)."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "benchmarks"))
+    import loss_parity
+
+    r = loss_parity.run(batch=8, size=64, steps=2, lr=0.02, classes=10)
+    print(r["step0_grad_rel_err"], r["step0_grad_worst_tensor_rel_err"], r["loss_fp64_cpu"], r["loss_mpit_fp32"])
+    assert all(l == l for l in r["loss_mpit_fp32"]), r["loss_mpit_fp32"]
+    # the forward loss at the shared starting point and the first gradients are the
+    # precision measures (later steps amplify any fp32 rounding chaotically)
+    assert abs(r["loss_mpit_fp32"][0] - r["loss_fp64_cpu"][0]) <= 1e-5 * abs(r["loss_fp64_cpu"][0])
+    ours, stock = r["step0_grad_rel_err"]["mpit_fp32"], r["step0_grad_rel_err"]["stock_fp32"]
+    assert ours <= 4 * stock + 1e-6, (ours, stock)

@@ -1686,7 +1686,18 @@ static int tn_plan(int dev, int64_t M, int N, int K, int64_t* rows_per_split, in
   *tbk = (cin ? cin : K) % 128 == 0 ? 128 : 64;  // conv: a column tile never straddles two taps
   const int64_t ntiles = int64_t(N / *tbn) * (K / *tbk);
   const int per_cu = tn_cap1() ? 1 : 2 * (128 / *tbn) * (128 / *tbk);
-  const int64_t target = int64_t(per_cu) * cu_count(dev);
+  // MPIT_TN_SPLIT_MUL=k: k times the splits (shorter blocks that free their CU sooner for
+  // the critical path's kernels, at k times the partial-sum traffic) — A/B knob
+  // (MPIT_TN_SPLIT_DIV=k: 1/k of them — longer blocks, less partial-sum traffic)
+  static const int split_mul = [] {
+    const char* e = std::getenv("MPIT_TN_SPLIT_MUL");
+    return e ? std::max(1, std::min(8, std::atoi(e))) : 1;
+  }();
+  static const int split_div = [] {
+    const char* e = std::getenv("MPIT_TN_SPLIT_DIV");
+    return e ? std::max(1, std::min(8, std::atoi(e))) : 1;
+  }();
+  const int64_t target = std::max<int64_t>(1, int64_t(per_cu) * cu_count(dev) * split_mul / split_div);
   // floor: one more block than there are slots would run as a whole second round
   int64_t ns = std::max<int64_t>(1, target / ntiles);
   const int64_t min_rows = 8 * kRows;  // keep >= 8 staged steps per block

@@ -192,7 +192,8 @@ class Trainer:
         if not getattr(self, "steal", False):
             self.flat.zero_grad()
         if self.wcast is not None:  # the weights as they are now, for this forward/backward only
-            self.wcast.run()
+            with _trace.range("wcast"):
+                self.wcast.run()
         try:
             with _trace.range("fwd"):
                 if self.on_gpu and self.cfg.amp:

@@ -4,6 +4,7 @@
 #include <unistd.h>
 #include <xmmintrin.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <csignal>
 
@@ -719,6 +720,9 @@ void Engine::progress_loop() {
   int idle = 0;
   uint64_t last_act = 0;
   auto last_check = std::chrono::steady_clock::now();
+  // idle iterations spent yielding before the 20 us sleeps (MPIT_PROGRESS_YIELDS, default 4096)
+  int yields = 4096;
+  if (const char* e = std::getenv("MPIT_PROGRESS_YIELDS")) yields = std::max(256, std::atoi(e));
   while (running_.load(std::memory_order_relaxed)) {
     const auto now = std::chrono::steady_clock::now();
     if (now - last_check > std::chrono::milliseconds(500)) {
@@ -737,7 +741,7 @@ void Engine::progress_loop() {
       last_act = act;
     } else if (++idle < 256) {
       _mm_pause();
-    } else if (idle < 4096) {
+    } else if (idle < yields) {
       std::this_thread::yield();
     } else {
       std::this_thread::sleep_for(std::chrono::microseconds(20));

@@ -15,6 +15,8 @@ import time
 
 import torch
 
+from ..utils import trace as _trace
+
 from .. import ops
 
 
@@ -70,7 +72,8 @@ def downpour(opfunc, w, config, state=None):
     if pusher is not None and pc is not None and su == 1:
         # shards pushed (with their pulls) from inside the backward as they complete
         # (parallel/overlap.py); what is left here is the last shards' round trip
-        pusher.arm(-lr * gscale, w if l2wd else None, -lr * l2wd)
+        with _trace.range("push_arm"):
+            pusher.arm(-lr * gscale, w if l2wd else None, -lr * l2wd)
         try:
             fx, _ = opfunc(w)
         except BaseException:

@@ -15,6 +15,7 @@ Optimizers: ``downpour`` (async SGD), ``eamsgd`` / ``easgd`` (elastic averaging)
 from __future__ import annotations
 
 import os
+import sys
 
 import time
 from dataclasses import dataclass, field
@@ -225,7 +226,8 @@ class Trainer:
             if self.hp_stream is None:
                 return self._step()
             cur = torch.cuda.current_stream(self.device)
-            self.hp_stream.wait_stream(cur)
+            with _trace.range("hp_wait"):
+                self.hp_stream.wait_stream(cur)
             with torch.cuda.stream(self.hp_stream):
                 fx = self._step()
             cur.wait_stream(self.hp_stream)
@@ -383,6 +385,26 @@ class Trainer:
         return float(out.item())
 
 
+def gc_settle():
+    """After setup / warmup: collect once, then move every surviving object (model, optimizer
+    and PS state, CUDA caches) to Python's permanent generation (``gc.freeze``) so the
+    cyclic collector's periodic full passes no longer walk them in the middle of a step —
+    a host stall of a few hundred us that the GPU sees as idle time at the step boundary.
+    MPIT_GC_FREEZE=0 leaves the collector alone."""
+    if os.environ.get("MPIT_GC_FREEZE", "1") != "0":
+        import gc
+
+        gc.collect()
+        gc.freeze()
+    if os.environ.get("MPIT_THREAD_DUMP") == "1":  # diagnostics: Python threads at the timed region
+        import threading
+
+        print("mpit threads:", [(t.name, t.daemon) for t in threading.enumerate()], file=sys.stderr, flush=True)
+    sw = os.environ.get("MPIT_SWITCH_US")
+    if sw:  # A/B knob: the interpreter's GIL switch interval (default 5000 us)
+        sys.setswitchinterval(float(sw) * 1e-6)
+
+
 def timed_steps(tr: Trainer, steps: int, warmup: int):
     """Warm up, then time exactly `steps` steps bracketed by barrier + device sync on both
     sides. Returns (max seconds over ranks, last loss)."""
@@ -392,6 +414,7 @@ def timed_steps(tr: Trainer, steps: int, warmup: int):
             loss = tr.step()
     tr.sync()
     tr.barrier()
+    gc_settle()
     t0 = time.perf_counter()
     if tr.is_worker:
         for _ in range(steps):

@@ -1,7 +1,12 @@
 #include "ps.h"
 #include "trace.h"
 
+#include <xmmintrin.h>
+
+#include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <stdexcept>
@@ -516,7 +521,25 @@ void PSClient::on_reply(const Msg&) {
   pending_.notify_all();
 }
 
+// The worker waits here every step while the GPU finishes its backward (tens of ms).
+// MPIT_WAIT_SPIN_US > 0 polls (pause) for up to that long before the futex sleep, keeping
+// the core awake for the step start that follows (device clients only). Measured within
+// noise of sleeping at once (profiles/step_start_host_r02.md): default 0.
 void PSClient::wait() {
+  static const int64_t spin_us = [] {
+    const char* e = std::getenv("MPIT_WAIT_SPIN_US");
+    return e ? std::max<int64_t>(0, std::atoll(e)) : int64_t(0);
+  }();
+  if (spin_us > 0 && eng_.device() >= 0) {  // GPU workers only (CPU ranks share few cores)
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 0;; ++i) {
+      if (pending_.load(std::memory_order_acquire) <= 0) return;
+      _mm_pause();
+      if ((i & 1023) == 0 &&
+          std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us))
+        break;
+    }
+  }
   for (;;) {
     const int64_t v = pending_.load(std::memory_order_acquire);
     if (v <= 0) return;

@@ -732,6 +732,37 @@ class WeightCastPlan:
 
 # ------------------------------------------------------------------ the 7x7 stem
 
+class _StemPackBuf:
+    """The zero-padded NHWC4 stem input, kept across steps: the zero border and the fourth
+    channel are written once, each step copies only the image into the interior (one copy
+    kernel instead of a full-size fill + copy, and no per-step allocation of the buffer).
+    A buffer still saved for a pending backward (``busy``) is never reused: the next
+    forward then takes a fresh one. MPIT_STEM_PACK_REUSE=0: pad anew every call."""
+
+    enabled = os.environ.get("MPIT_STEM_PACK_REUSE", "1") != "0"
+    bufs = {}
+
+    @classmethod
+    def get(cls, x: torch.Tensor, pad: int, hp: int, wp: int, dt):
+        v = _to(x, dt).permute(0, 2, 3, 1)  # NHWC view of the channels_last tensor
+        n, h, w, c = v.shape
+        if not cls.enabled:
+            return F.pad(v, (0, 4 - c, pad, wp - w - pad, pad, hp - h - pad)), None
+        key = (x.device, dt, n, h, w, c, pad, hp, wp)
+        ent = cls.bufs.get(key)
+        if ent is None or ent[1]:
+            # [buffer, busy, stream of the last backward that read it if not this one's, its event]
+            ent = [torch.zeros((n, hp, wp, 4), dtype=dt, device=x.device), False, None]
+            cls.bufs[key] = ent
+        if ent[2] is not None:  # that backward ran on another stream: order the copy after it
+            torch.cuda.current_stream(x.device).wait_event(ent[2])
+            ent[2] = None
+        ent[1] = True  # busy until the backward that reads it has been issued
+        ent[0][:, pad:pad + h, pad:pad + w, :c].copy_(v)
+        ent.append(_stream(x))  # the stream of this forward (popped by the backward)
+        return ent[0], ent
+
+
 def _stem_pack_input(x: torch.Tensor, pad: int, hp: int, wp: int, dt=torch.bfloat16) -> torch.Tensor:
     """[N, 3, H, W] -> zero-padded NHWC4 [N, hp, wp, 4] in ``dt`` (one pad kernel)."""
     v = _to(x, dt).permute(0, 2, 3, 1)  # NHWC view of the channels_last tensor
@@ -761,7 +792,7 @@ class _StemConvFn(torch.autograd.Function):
         f32 = dt == torch.float32
         ho, wo = (h + 2 * pad - r) // stride + 1, (w + 2 * pad - s) // stride + 1
         hp, wp = max(h + 2 * pad, (ho - 1) * stride + 8), max(w + 2 * pad, (wo - 1) * stride + 8)
-        xp = _stem_pack_input(x, pad, hp, wp, dt)
+        xp, ent = _StemPackBuf.get(x, pad, hp, wp, dt)
         wb = _stem_pack_weight(weight, dt)
         y = torch.empty((nb, co, ho, wo), dtype=dt, device=x.device, memory_format=torch.channels_last)
         st = None
@@ -772,6 +803,10 @@ class _StemConvFn(torch.autograd.Function):
                                wb.data_ptr(), y.data_ptr(), st.data_ptr() if st is not None else 0, f32=f32)
         ctx.save_for_backward(xp)
         ctx.geo = (nb, hp, wp, co, ho, wo, stride, tuple(weight.shape))
+        ctx.pack = ent
+        if ent is not None and not ctx.needs_input_grad[1]:
+            ent[1] = False  # no backward will read it
+            del ent[3:]
         return y
 
     @staticmethod
@@ -789,6 +824,16 @@ class _StemConvFn(torch.autograd.Function):
             ws = torch.empty(nws, dtype=torch.float32, device=xp.device) if nws else None
             m.conv_stem_wgrad(dev, _stream(xp), nb, hp, wp, co, ho, wo, stride, dy.data_ptr(), xp.data_ptr(),
                               dwp.data_ptr(), ws.data_ptr() if ws is not None else 0, f32=dt == torch.float32)
+        if ctx.pack is not None:
+            # the wgrad reading the buffer is queued; a forward on the same stream is ordered
+            # after it, one on another stream waits on an event
+            ent = ctx.pack
+            fwd_stream = ent.pop() if len(ent) > 3 else None
+            if fwd_stream is not None and fwd_stream != _stream(xp):
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(xp.device))
+                ent[2] = ev
+            ent[1] = False
             _, c, r, s = wshape
             dw = dwp[:, :r, :s, :c].permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
         return None, dw, None, None, None, None

@@ -40,3 +40,50 @@ def test_stem_emits_bn_stats():
     yf = y.double().permute(0, 2, 3, 1).reshape(-1, 64)
     assert torch.allclose(sums[0], yf.sum(0), atol=1e-1, rtol=1e-3)
     assert torch.allclose(sums[1], (yf * yf).sum(0), atol=1e-1, rtol=1e-3)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_stem_pack_buffer_reuse(dt):
+    """The padded stem input buffer kept across steps (_StemPackBuf) gives the same outputs
+    and weight gradients as padding anew, across steps with new images, with two forwards
+    before their backwards (the busy buffer is not reused) and with the backward on
+    another stream."""
+    from mpit_amd.ops import conv as C
+
+    torch.manual_seed(3)
+    conv = C.StemConv(3, 64, 7, 2, 3).cuda().to(memory_format=torch.channels_last)
+    xs = [torch.randn(4, 3, 64, 64, device="cuda").to(dt).contiguous(memory_format=torch.channels_last)
+          for _ in range(4)]
+
+    def steps(reuse):
+        C._StemPackBuf.enabled = reuse
+        C._StemPackBuf.bufs.clear()
+        out = []
+        try:
+            for x in xs[:2]:  # one forward + backward per step
+                conv.weight.grad = None
+                y = conv(x)
+                y.float().square().sum().backward()
+                out += [y.detach().float().clone(), conv.weight.grad.clone()]
+            conv.weight.grad = None  # two forwards, then both backwards
+            ya, yb = conv(xs[2]), conv(xs[3])
+            (ya.float().square().sum() + yb.float().sum()).backward()
+            out += [ya.detach().float().clone(), yb.detach().float().clone(), conv.weight.grad.clone()]
+            conv.weight.grad = None  # backward on a side stream, then a forward on the main one
+            y = conv(xs[0])
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                y.float().square().sum().backward()
+            torch.cuda.current_stream().wait_stream(side)
+            y2 = conv(xs[1])
+            out += [conv.weight.grad.clone(), y2.detach().float().clone()]
+            torch.cuda.synchronize()
+            return out
+        finally:
+            C._StemPackBuf.enabled = True
+            C._StemPackBuf.bufs.clear()
+
+    a, b = steps(False), steps(True)
+    for i, (u, v) in enumerate(zip(a, b)):
+        assert torch.equal(u, v), i

@@ -824,6 +824,8 @@ class _StemConvFn(torch.autograd.Function):
             ws = torch.empty(nws, dtype=torch.float32, device=xp.device) if nws else None
             m.conv_stem_wgrad(dev, _stream(xp), nb, hp, wp, co, ho, wo, stride, dy.data_ptr(), xp.data_ptr(),
                               dwp.data_ptr(), ws.data_ptr() if ws is not None else 0, f32=dt == torch.float32)
+            _, c, r, s = wshape
+            dw = dwp[:, :r, :s, :c].permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
         if ctx.pack is not None:
             # the wgrad reading the buffer is queued; a forward on the same stream is ordered
             # after it, one on another stream waits on an event
@@ -834,8 +836,6 @@ class _StemConvFn(torch.autograd.Function):
                 ev.record(torch.cuda.current_stream(xp.device))
                 ent[2] = ev
             ent[1] = False
-            _, c, r, s = wshape
-            dw = dwp[:, :r, :s, :c].permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
         return None, dw, None, None, None, None
 
 

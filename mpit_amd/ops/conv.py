@@ -770,10 +770,23 @@ def _stem_pack_input(x: torch.Tensor, pad: int, hp: int, wp: int, dt=torch.bfloa
     return F.pad(v, (0, 4 - c, pad, wp - w - pad, pad, hp - h - pad))
 
 
+_STEM_WBUF = {}
+
+
 def _stem_pack_weight(weight: torch.Tensor, dt=torch.bfloat16) -> torch.Tensor:
-    """[Co, C<=4, R<=8, S<=8] -> [Co, 8, 8, 4] in ``dt``, zero-extended."""
+    """[Co, C<=4, R<=8, S<=8] -> [Co, 8, 8, 4] in ``dt``, zero-extended. With
+    ``_StemPackBuf.enabled`` the zero-extended buffer is kept per (device, stream, shape):
+    it is only read by this step's forward GEMM, queued on the same stream before the next
+    step's refill, so only the weight itself is copied in each step."""
     co, c, r, s = weight.shape
-    wp = torch.zeros((co, 8, 8, 4), dtype=dt, device=weight.device)
+    wp = None
+    if _StemPackBuf.enabled and weight.is_cuda:
+        key = (weight.device, dt, co, c, r, s, _stream(weight))
+        wp = _STEM_WBUF.get(key)
+        if wp is None:
+            wp = _STEM_WBUF[key] = torch.zeros((co, 8, 8, 4), dtype=dt, device=weight.device)
+    if wp is None:
+        wp = torch.zeros((co, 8, 8, 4), dtype=dt, device=weight.device)
     wp[:, :r, :s, :c] = weight.permute(0, 2, 3, 1)
     return wp
 

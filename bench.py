@@ -63,8 +63,41 @@ def _make(a, mp_train, amp: bool, topology: str, servers: int, ps_id: int):
     cfg = mp_train.TrainConfig(model=a.model, batch=a.batch, optimizer=a.optimizer, topology=topology,
                                servers=servers, su=a.su, lr=lr, mva=mva, mom=0.0, amp=amp,
                                channels_last=not a.no_channels_last, datapath=a.datapath, staleness=a.staleness,
-                               wire_dtype=a.wire, extra={"ps_id": ps_id})
+                               wire_dtype=a.wire, extra={"ps_id": ps_id, "shards_per_server": a.emulate_shards})
     return mp_train.Trainer(cfg)
+
+
+def _devices(W, tr) -> list:
+    """[(rank, device index, PCI bus id)] of every rank: the record itself shows which GPUs ran."""
+    import torch
+
+    mine = (W.Get_rank(), None, None)
+    if tr.on_gpu:
+        p = torch.cuda.get_device_properties(tr.device)
+        mine = (W.Get_rank(), tr.device.index, f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}")
+    return [list(x) for x in W.allgather_obj(mine)]
+
+
+def _rccl_probe(W, tr, st) -> dict:
+    """A live check, not a predicate: one dist.all_reduce over every rank on the NCCL (RCCL)
+    process group, and what came back."""
+    import torch
+    import torch.distributed as dist
+
+    out = {"backend": None, "ranks": None, "ok": False}
+    if not (tr.on_gpu and dist.is_initialized()) or st.shared_devices:
+        out["reason"] = "ranks share a GPU (RCCL needs one GPU per rank)" if st.shared_devices else "no GPU group"
+        return out
+    try:
+        x = torch.ones(1, device=tr.device)
+        dist.all_reduce(x)
+        torch.cuda.synchronize(tr.device)
+        seen = W.allgather_obj(float(x.item()))
+        out.update(backend=dist.get_backend(), ranks=dist.get_world_size(), ok=all(v == st.world for v in seen),
+                   sums=seen)
+    except Exception as e:  # reported, never fatal to the headline
+        out["error"] = f"{type(e).__name__}: {e}"
+    return out
 
 
 def main(argv=None) -> int:
@@ -89,6 +122,10 @@ def main(argv=None) -> int:
     ap.add_argument("--no-amp", action="store_true", help="alias of --dtype fp32 (kept for old scripts)")
     ap.add_argument("--no-secondary", action="store_true", help="headline only")
     ap.add_argument("--no-channels-last", action="store_true")
+    ap.add_argument("--emulate-shards", type=int, default=1,
+                    help="K > 1: split the (single) server's shard into K shards, each pushed from inside the "
+                         "backward and served through the remote-client pipeline (link stream, inbox / outbox) — "
+                         "one GPU carrying the per-worker shard traffic of an N=K job (diagnostic, not the headline)")
     ap.add_argument("--miopen-find", action="store_true",
                     help="exhaustive MIOpen algorithm search for what still runs on MIOpen (the fc layer)")
     a = ap.parse_args(argv)
@@ -101,6 +138,8 @@ def main(argv=None) -> int:
               file=sys.stderr)
         return 2
 
+    if a.emulate_shards > 1:
+        os.environ["MPIT_PS_FORCE_PIPE"] = "1"  # the local client takes the remote-client pipeline
     import torch
 
     torch.backends.cudnn.benchmark = a.miopen_find
@@ -135,9 +174,8 @@ def main(argv=None) -> int:
     check = tr.verify_ps() if (tr.pc is not None or tr.ps_server is not None) else None
     tr.stop()
     st = mp.runtime.state()
-    rccl = None
-    if world > 1 and tr.on_gpu:
-        rccl = bool(W._use_rccl(torch.zeros(1, device=tr.device)))
+    devices = _devices(W, tr)
+    rccl = _rccl_probe(W, tr, st) if world > 1 else None
     if not a.no_secondary and world > 1 and a.optimizer != "allreduce":
         from mpit_amd.instruments import allreduce_time, ps_pingpong
 
@@ -174,8 +212,9 @@ def main(argv=None) -> int:
             "config": {"model": a.model, "global_batch": a.batch * nworkers, "seq_len": None, "image_size": shape[-1],
                        "parallelism": par, "optimizer": a.optimizer, "su": a.su, "per_gpu_batch": a.batch,
                        "master_weights": "fp32", "loss_last": lossv},
-            "world": st.world, "shared_devices": st.shared_devices, "rccl": rccl,
+            "world": st.world, "shared_devices": st.shared_devices, "devices": devices, "rccl": rccl,
             "ps_check": check,
+            **({"emulate_shards": a.emulate_shards} if a.emulate_shards > 1 else {}),
             "secondary": secondary,
             "secondary_s": round(time.perf_counter() - t_sec, 2),
         }

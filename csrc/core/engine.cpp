@@ -1,8 +1,13 @@
 #include "engine.h"
 
+#include <linux/futex.h>
 #include <sys/prctl.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 #include <xmmintrin.h>
+
+#include <climits>
+#include <ctime>
 
 #include <algorithm>
 #include <cerrno>
@@ -20,7 +25,32 @@ namespace {
 void hipc(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("mpit engine HIP error in ") + what + ": " + hipGetErrorString(e));
 }
+
+double env_seconds(const char* name, double dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::max(0.0, std::atof(e)) : dflt;
+}
 }  // namespace
+
+void futex_wake_all(void* addr, bool shared) {
+  ::syscall(SYS_futex, addr, shared ? FUTEX_WAKE : FUTEX_WAKE_PRIVATE, INT_MAX, nullptr, nullptr, 0);
+}
+
+void futex_wait(void* addr, uint32_t expect, int64_t timeout_us, bool shared) {
+  timespec ts{};
+  timespec* tp = nullptr;
+  if (timeout_us >= 0) {
+    ts.tv_sec = time_t(timeout_us / 1000000);
+    ts.tv_nsec = long(timeout_us % 1000000) * 1000L;
+    tp = &ts;
+  }
+  ::syscall(SYS_futex, addr, shared ? FUTEX_WAIT : FUTEX_WAIT_PRIVATE, expect, tp, nullptr, 0);
+}
+
+double Engine::wait_timeout_s() {
+  static const double t = env_seconds("MPIT_WAIT_TIMEOUT_S", 600.0);
+  return t;
+}
 
 Engine::Engine(const std::string& shm_name, int world, int rank, bool create, int device, int64_t bulk_bytes)
     : world_(world), rank_(rank), device_(device) {
@@ -67,6 +97,11 @@ void Engine::shutdown() {
       copies_.clear();
     }
     {
+      std::lock_guard<std::mutex> g(ev_mu_);
+      for (auto e : ev_pool_) hipEventDestroy(e);
+      ev_pool_.clear();
+    }
+    {
       std::lock_guard<std::mutex> g(ipc_mu_);
       for (auto& kv : ipc_cache_) hipIpcCloseMemHandle(kv.second.ptr);
       ipc_cache_.clear();
@@ -86,8 +121,8 @@ std::shared_ptr<Req> Engine::get_req(int64_t id) {
 }
 
 void Engine::finish_req(const std::shared_ptr<Req>& r, int state) {
-  r->state.store(state, std::memory_order_release);
-  r->state.notify_all();
+  r->state.store(state, std::memory_order_seq_cst);
+  futex_wake_all(&r->state, false);
 }
 
 bool Engine::match(const Msg& h, const Req& r) const {
@@ -100,8 +135,9 @@ bool Engine::push_msg_locked(int dst, const Msg& m) {
   const uint64_t tail = ring->tail.load(std::memory_order_acquire);
   if (head - tail >= uint64_t(kRingSlots)) return false;
   ring->slots[head % kRingSlots] = m;
-  ring->head.store(head + 1, std::memory_order_release);
+  ring->head.store(head + 1, std::memory_order_seq_cst);
   msgs_sent_.fetch_add(1, std::memory_order_relaxed);
+  this->ring(dst);
   return true;
 }
 
@@ -118,7 +154,8 @@ int64_t Engine::bulk_write_locked(int dst, const uint8_t* p, int64_t n) {
   const int64_t first = std::min(m, cap - off);
   std::memcpy(data + off, p, size_t(first));
   if (m > first) std::memcpy(data, p + first, size_t(m - first));
-  b->wpos.store(w + uint64_t(m), std::memory_order_release);
+  b->wpos.store(w + uint64_t(m), std::memory_order_seq_cst);
+  ring(dst);
   return m;
 }
 
@@ -135,7 +172,8 @@ int64_t Engine::bulk_read(int src, uint8_t* p, int64_t n) {
   const int64_t first = std::min(m, cap - off);
   std::memcpy(p, data + off, size_t(first));
   if (m > first) std::memcpy(p + first, data, size_t(m - first));
-  b->rpos.store(r + uint64_t(m), std::memory_order_release);
+  b->rpos.store(r + uint64_t(m), std::memory_order_seq_cst);
+  ring(src);  // the sender may be waiting for space
   return m;
 }
 
@@ -225,7 +263,7 @@ int64_t Engine::isend(const void* buf, int64_t nbytes, bool dev, int dst, int ta
   std::lock_guard<std::mutex> g(mu_);
   reqs_[r->id] = r;
   sendq_[dst].push_back(r);
-  activity_.fetch_add(1);
+  kick();
   return r->id;
 }
 
@@ -256,7 +294,7 @@ int64_t Engine::irecv(void* buf, int64_t cap, bool dev, int src, int tag, int ct
     return r->id;
   }
   posted_.push_back(r);
-  activity_.fetch_add(1);
+  kick();
   return r->id;
 }
 
@@ -275,10 +313,22 @@ bool Engine::test(int64_t id, Status* st, bool keep) {
 
 void Engine::wait(int64_t id, Status* st) {
   auto r = get_req(id);
-  for (;;) {
-    int s = r->state.load(std::memory_order_acquire);
-    if (s != RS_PENDING) break;
-    r->state.wait(RS_PENDING, std::memory_order_acquire);
+  const double tmo = wait_timeout_s();
+  const auto t0 = std::chrono::steady_clock::now();
+  while (r->state.load(std::memory_order_seq_cst) == RS_PENDING) {
+    int64_t left_us = -1;
+    if (tmo > 0) {
+      const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (el >= tmo)
+        throw std::runtime_error("mpit: Wait timed out after " + std::to_string(int(tmo)) + " s (" +
+                                 (r->is_send ? "send to rank " + std::to_string(r->dst)
+                                             : "receive from rank " + std::to_string(r->src)) +
+                                 ", tag " + std::to_string(r->tag) + "; MPIT_WAIT_TIMEOUT_S)");
+      left_us = int64_t((tmo - el) * 1e6) + 1;
+    }
+    // bounded slices: the abort flag of a failed peer is checked by the progress thread,
+    // which _exits the process, so the slice only bounds the deadline check
+    futex_wait(&r->state, RS_PENDING, left_us < 0 ? 1000000 : std::min<int64_t>(left_us, 1000000), false);
   }
   test(id, st, false);
 }
@@ -336,9 +386,19 @@ bool Engine::iprobe(int src, int tag, int ctx, Status* st) {
 
 void Engine::probe(int src, int tag, int ctx, Status* st) {
   int spins = 0;
+  const double tmo = wait_timeout_s();
+  const auto t0 = std::chrono::steady_clock::now();
   while (!iprobe(src, tag, ctx, st)) {
-    if (++spins < 1000) _mm_pause();
-    else std::this_thread::sleep_for(std::chrono::microseconds(10));
+    if (++spins < 1000) {
+      _mm_pause();
+    } else {
+      std::this_thread::sleep_for(std::chrono::microseconds(10));
+      if (tmo > 0 && (spins & 1023) == 0 &&
+          std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > tmo)
+        throw std::runtime_error("mpit: Probe timed out after " + std::to_string(int(tmo)) +
+                                 " s (source " + std::to_string(src) + ", tag " + std::to_string(tag) +
+                                 "; MPIT_WAIT_TIMEOUT_S)");
+    }
   }
 }
 
@@ -360,8 +420,7 @@ void Engine::deliver_locked(Incoming& in) {
       hipc(hipSetDevice(device_), "hipSetDevice");
       auto keep = std::make_shared<std::vector<uint8_t>>(std::move(in.data));
       hipc(hipMemcpyAsync(r->rbuf, keep->data(), size_t(n), hipMemcpyHostToDevice, stream_), "hipMemcpyAsync(H2D)");
-      hipEvent_t ev;
-      hipc(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+      hipEvent_t ev = get_event();
       hipc(hipEventRecord(ev, stream_), "hipEventRecord");
       r->st.source = h.src;
       r->st.tag = h.tag;
@@ -417,8 +476,7 @@ void Engine::start_dev_pull_locked(Incoming& in) {
     remote = static_cast<const uint8_t*>(open_ipc(h.src, hd, false)) + h.aux0;
   }
   if (n > 0) hipc(hipMemcpyAsync(r->rbuf, remote, size_t(n), hipMemcpyDefault, stream_), "hipMemcpyAsync(pull)");
-  hipEvent_t ev;
-  hipc(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+  hipEvent_t ev = get_event();
   hipc(hipEventRecord(ev, stream_), "hipEventRecord");
   bytes_recv_.fetch_add(n, std::memory_order_relaxed);
   PendingCopy pc{ev, r, h.src, h.aux1, nullptr};
@@ -586,9 +644,34 @@ bool Engine::progress_sends_locked() {
 // --------------------------------------------------------------------------- device copies
 
 void Engine::track_copy(hipEvent_t ev, std::function<void()> then) {
-  std::lock_guard<std::mutex> g(copy_mu_);
-  copies_.push_back(PendingCopy{ev, nullptr, -1, 0, std::move(then)});
+  {
+    std::lock_guard<std::mutex> g(copy_mu_);
+    copies_.push_back(PendingCopy{ev, nullptr, -1, 0, std::move(then)});
+  }
+  kick();
 }
+
+hipEvent_t Engine::get_event() {
+  {
+    std::lock_guard<std::mutex> g(ev_mu_);
+    if (!ev_pool_.empty()) {
+      hipEvent_t e = ev_pool_.back();
+      ev_pool_.pop_back();
+      return e;
+    }
+  }
+  hipEvent_t e;
+  hipc(hipSetDevice(device_), "hipSetDevice");
+  hipc(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+  return e;
+}
+
+void Engine::put_event(hipEvent_t e) {
+  std::lock_guard<std::mutex> g(ev_mu_);
+  ev_pool_.push_back(e);
+}
+
+void Engine::record_event(hipEvent_t e, hipStream_t s) { hipc(hipEventRecord(e, s), "hipEventRecord"); }
 
 bool Engine::progress_copies() {
   std::vector<PendingCopy> done;
@@ -602,7 +685,7 @@ bool Engine::progress_copies() {
         ++i;
         continue;
       }
-      if (e != hipSuccess) std::fprintf(stderr, "[mpit rank %d] async copy failed: %s\n", rank_, hipGetErrorString(e));
+      if (e != hipSuccess) fatal(std::string("async device copy failed: ") + hipGetErrorString(e));
       done.push_back(copies_[i]);
       copies_[i] = copies_.back();
       copies_.pop_back();
@@ -610,7 +693,7 @@ bool Engine::progress_copies() {
   }
   if (done.empty()) return false;
   for (auto& c : done) {
-    hipEventDestroy(c.ev);
+    put_event(c.ev);
     if (c.ipc_owner >= 0) release_ipc(c.ipc_owner, c.ipc_key);
     if (c.req) {
       std::lock_guard<std::mutex> g(mu_);
@@ -630,13 +713,22 @@ bool Engine::progress_copies() {
 
 // --------------------------------------------------------------------------- progress
 
+void Engine::check_abort() {
+  Header* h = seg_->hdr();
+  if (!h->abort_flag.load(std::memory_order_acquire)) return;
+  const int code = h->abort_code ? h->abort_code : 1;
+  if (h->abort_rank >= 0 && h->abort_rank != rank_)
+    std::fprintf(stderr, "[mpit rank %d] job aborted by rank %d (code %d): %.*s\n", rank_, h->abort_rank, code,
+                 kAbortMsg, h->abort_msg);
+  else if (h->abort_rank < 0)
+    std::fprintf(stderr, "[mpit rank %d] job aborted by a peer (code %d)\n", rank_, code);
+  std::fflush(stderr);
+  ::_exit(code);
+}
+
 bool Engine::progress_once() {
   bool did = false;
-  if (seg_->hdr()->abort_flag.load(std::memory_order_relaxed)) {
-    std::fprintf(stderr, "[mpit rank %d] job aborted by a peer (code %d)\n", rank_, seg_->hdr()->abort_code);
-    std::fflush(stderr);
-    ::_exit(seg_->hdr()->abort_code ? seg_->hdr()->abort_code : 1);
-  }
+  check_abort();
   {
     std::lock_guard<std::mutex> g(mu_);
     did |= progress_recvs_locked();
@@ -656,7 +748,10 @@ bool Engine::progress_once() {
     try {
       h(m);
     } catch (const std::exception& e) {
-      std::fprintf(stderr, "[mpit rank %d] active-message handler %d failed: %s\n", rank_, m.tag, e.what());
+      // a PS server that cannot apply / serve a shard would leave every client waiting
+      // forever: the whole job fails now, with the reason (init.lua:168-171)
+      fatal("active-message handler " + std::to_string(m.tag) + " (from rank " + std::to_string(m.src) +
+            ") failed: " + e.what());
     }
     did = true;
   }
@@ -670,7 +765,7 @@ bool Engine::progress_once() {
     try {
       did |= h();
     } catch (const std::exception& e) {
-      std::fprintf(stderr, "[mpit rank %d] progress hook failed: %s\n", rank_, e.what());
+      fatal(std::string("progress hook failed: ") + e.what());
     }
   }
   return did;
@@ -699,11 +794,62 @@ void Engine::check_peers() {
     if (dead) {
       std::fprintf(stderr, "[mpit rank %d] peer rank %d (pid %d) died; aborting the job\n", rank_, r, ri.pid);
       std::fflush(stderr);
-      h->abort_code = 70;
-      h->abort_flag.store(1, std::memory_order_release);
+      publish_abort("rank " + std::to_string(r) + " (pid " + std::to_string(ri.pid) + ") died", 70);
       ::_exit(70);
     }
   }
+}
+
+void Engine::ring(int r) {
+  RankInfo& ri = seg_->hdr()->ranks[r];
+  // seq_cst pairs with park(): either the sleeper sees the producer's data on its final
+  // re-check, or the producer sees `sleeping` and wakes it
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  if (ri.sleeping.load(std::memory_order_seq_cst)) {
+    ri.doorbell.fetch_add(1, std::memory_order_seq_cst);
+    futex_wake_all(&ri.doorbell, true);
+  }
+}
+
+void Engine::kick() {
+  activity_.fetch_add(1, std::memory_order_seq_cst);
+  ring(rank_);
+}
+
+bool Engine::idle_deep_ok() {
+  // parking on the doorbell is safe only when every pending event is one a producer
+  // rings for: nothing of ours waits on a GPU event, a full ring / bulk stream or a
+  // half-read payload, and no AM is queued
+  if (gpu_pending_.load(std::memory_order_acquire) > 0) return false;
+  {
+    std::lock_guard<std::mutex> g(copy_mu_);
+    if (!copies_.empty()) return false;
+  }
+  {
+    std::lock_guard<std::mutex> g(am_mu_);
+    if (!pending_am_.empty()) return false;
+  }
+  std::lock_guard<std::mutex> g(mu_);
+  for (int d = 0; d < world_; ++d)
+    if (!sendq_[d].empty() || !ctrlq_[d].empty() || streaming_[d]) return false;
+  return true;
+}
+
+void Engine::park(int64_t timeout_us) {
+  RankInfo& ri = seg_->hdr()->ranks[rank_];
+  const uint32_t v = ri.doorbell.load(std::memory_order_seq_cst);
+  ri.sleeping.store(1, std::memory_order_seq_cst);
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  // final re-check after announcing: incoming headers / bulk bytes, local requests
+  bool work = seg_->hdr()->abort_flag.load(std::memory_order_seq_cst) != 0 || !running_.load();
+  for (int s = 0; s < world_ && !work; ++s) {
+    Ring* rg = seg_->ring(s, rank_);
+    BulkHdr* b = seg_->bulk(s, rank_);
+    work = rg->head.load(std::memory_order_seq_cst) != rg->tail.load(std::memory_order_relaxed) ||
+           b->wpos.load(std::memory_order_seq_cst) != b->rpos.load(std::memory_order_relaxed);
+  }
+  if (!work) futex_wait(&ri.doorbell, v, timeout_us, true);
+  ri.sleeping.store(0, std::memory_order_relaxed);
 }
 
 void Engine::progress_loop() {
@@ -717,12 +863,18 @@ void Engine::progress_loop() {
     const long ns = e ? std::atol(e) : 1000L;
     if (ns > 0) prctl(PR_SET_TIMERSLACK, static_cast<unsigned long>(ns), 0, 0, 0);
   }
+  // Idle back-off: 256 pauses, then MPIT_PROGRESS_YIELDS yields (default 64), then either
+  // a 20 us sleep (something only polling can see completes: a GPU event, a full ring) or
+  // a park on this rank's futex doorbell until a producer rings it (<= 50 ms, so the peer
+  // check still runs). Round 2 spun up to 4096 yields per idle period: with 8+ ranks on a
+  // CPU quota the spinning threads themselves ate the quota (throttling) — parked threads
+  // cost nothing.
   int idle = 0;
   uint64_t last_act = 0;
   auto last_check = std::chrono::steady_clock::now();
-  // idle iterations spent yielding before the 20 us sleeps (MPIT_PROGRESS_YIELDS, default 4096)
-  int yields = 4096;
-  if (const char* e = std::getenv("MPIT_PROGRESS_YIELDS")) yields = std::max(256, std::atoi(e));
+  int yields = 64;
+  if (const char* e = std::getenv("MPIT_PROGRESS_YIELDS")) yields = std::max(0, std::atoi(e));
+  const bool deep = std::getenv("MPIT_PROGRESS_PARK") == nullptr || std::atoi(std::getenv("MPIT_PROGRESS_PARK")) != 0;
   while (running_.load(std::memory_order_relaxed)) {
     const auto now = std::chrono::steady_clock::now();
     if (now - last_check > std::chrono::milliseconds(500)) {
@@ -733,7 +885,7 @@ void Engine::progress_loop() {
     try {
       did = progress_once();
     } catch (const std::exception& e) {
-      std::fprintf(stderr, "[mpit rank %d] progress error: %s\n", rank_, e.what());
+      fatal(std::string("progress error: ") + e.what());
     }
     const uint64_t act = activity_.load(std::memory_order_relaxed);
     if (did || act != last_act) {
@@ -741,8 +893,10 @@ void Engine::progress_loop() {
       last_act = act;
     } else if (++idle < 256) {
       _mm_pause();
-    } else if (idle < yields) {
+    } else if (idle < 256 + yields) {
       std::this_thread::yield();
+    } else if (deep && idle_deep_ok()) {
+      park(50000);
     } else {
       std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
@@ -762,7 +916,7 @@ void Engine::register_am(int id, AmHandler h) {
       ++it;
     }
   }
-  activity_.fetch_add(1);
+  kick();
 }
 
 void Engine::send_am(int dst, int id, const void* payload, int64_t n, int64_t aux0, int64_t aux1, int64_t aux2) {
@@ -776,9 +930,11 @@ void Engine::send_am(int dst, int id, const void* payload, int64_t n, int64_t au
   m.aux1 = aux1;
   m.aux2 = aux2;
   if (n > 0) std::memcpy(m.data, payload, size_t(n));
-  std::lock_guard<std::mutex> g(mu_);
-  ctrlq_[dst].push_back(m);
-  activity_.fetch_add(1);
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    ctrlq_[dst].push_back(m);
+  }
+  kick();
 }
 
 int Engine::add_hook(std::function<bool()> h) {
@@ -803,11 +959,22 @@ void Engine::barrier() {
     h->bar_gen.fetch_add(1, std::memory_order_acq_rel);
   } else {
     int spins = 0;
+    const double tmo = wait_timeout_s();
+    const auto t0 = std::chrono::steady_clock::now();
     while (h->bar_gen.load(std::memory_order_acquire) == gen) {
-      if (h->abort_flag.load(std::memory_order_relaxed)) ::_exit(h->abort_code ? h->abort_code : 1);
-      if (++spins < 2000) _mm_pause();
-      else if (spins < 20000) std::this_thread::yield();
-      else std::this_thread::sleep_for(std::chrono::microseconds(20));
+      check_abort();
+      if (++spins < 2000) {
+        _mm_pause();
+      } else if (spins < 2256) {
+        std::this_thread::yield();
+      } else {
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+        if (tmo > 0 && (spins & 255) == 0 &&
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > tmo)
+          fatal("barrier timed out after " + std::to_string(int(tmo)) + " s (" +
+                std::to_string(h->bar_count.load()) + " of " + std::to_string(world_) +
+                " ranks arrived; MPIT_WAIT_TIMEOUT_S)");
+      }
     }
   }
 }
@@ -831,12 +998,33 @@ std::vector<std::string> Engine::allgather_small(const std::string& blob) {
   return out;
 }
 
+void Engine::publish_abort(const std::string& why, int code) {
+  // the reason goes in before the flag (release), so a peer that sees the flag reads a
+  // complete message; if another rank failed first its reason is kept
+  Header* h = seg_->hdr();
+  if (h->abort_flag.load(std::memory_order_acquire) == 0) {
+    h->abort_code = code;
+    h->abort_rank = rank_;
+    std::snprintf(h->abort_msg, kAbortMsg, "%s", why.c_str());
+    h->abort_flag.store(1, std::memory_order_seq_cst);
+  }
+  for (int r = 0; r < world_; ++r) ring(r);
+}
+
 void Engine::abort(int code) {
-  seg_->hdr()->abort_code = code;
-  seg_->hdr()->abort_flag.store(1, std::memory_order_release);
+  char why[64];
+  std::snprintf(why, sizeof(why), "MPI_Abort(%d)", code);
+  publish_abort(why, code ? code : 1);
   std::fprintf(stderr, "[mpit rank %d] Abort(%d)\n", rank_, code);
   std::fflush(stderr);
   ::_exit(code ? code : 1);
+}
+
+void Engine::fatal(const std::string& why, int code) {
+  publish_abort(why, code);
+  std::fprintf(stderr, "[mpit rank %d] fatal: %s\n", rank_, why.c_str());
+  std::fflush(stderr);
+  ::_exit(code);
 }
 
 }  // namespace mpit

@@ -37,6 +37,11 @@ namespace mpit {
 constexpr int kAnySource = -1;
 constexpr int kAnyTag = -1;
 
+// Raw futex on a 32-bit word. shared: the word lives in the cross-process segment.
+// futex_wait returns when woken, when *addr != expect, or after timeout_us (< 0: none).
+void futex_wake_all(void* addr, bool shared);
+void futex_wait(void* addr, uint32_t expect, int64_t timeout_us, bool shared);
+
 struct Status {
   int source = -1;
   int tag = -1;
@@ -132,9 +137,32 @@ class Engine {
   void remove_hook(int id);
   // track an async device copy; `then` runs on the progress thread when it is done
   void track_copy(hipEvent_t ev, std::function<void()> then);
+  // pooled completion events (no hipEventCreate / Destroy per message): events handed to
+  // track_copy return to the pool when their copy is done
+  hipEvent_t get_event();
+  void put_event(hipEvent_t e);
+  static void record_event(hipEvent_t e, hipStream_t s);
 
   void abort(int code);
+  // A fatal error of this rank's runtime (a failed active-message handler, a failed HIP
+  // call on the progress thread): publish the reason in the segment, raise the job-wide
+  // abort flag, wake every rank and exit. Every other rank then prints the reason and
+  // exits with the same code — the reference's co_ping assert(false), init.lua:168-171.
+  [[noreturn]] void fatal(const std::string& why, int code = 71);
   void shutdown();
+
+  // wake rank r's progress thread if it is parked on its doorbell
+  void ring(int r);
+  // new local work for this rank's progress thread (a posted request, a gated send)
+  void kick();
+  // outstanding GPU-side completions polled by hooks (PS gates): while > 0 the progress
+  // thread polls every ~20 us instead of parking on its doorbell
+  void gpu_pending_add(int64_t d) {
+    gpu_pending_.fetch_add(d, std::memory_order_acq_rel);
+    if (d > 0) kick();
+  }
+  // deadlines (seconds, 0 = none): MPIT_WAIT_TIMEOUT_S for Wait/Probe/Barrier
+  static double wait_timeout_s();
 
   hipStream_t comm_stream() const { return stream_; }
   // IPC helpers (also used by windows)
@@ -159,6 +187,10 @@ class Engine {
   bool progress_sends_locked();
   bool progress_recvs_locked();
   bool progress_copies();
+  void check_abort();
+  void publish_abort(const std::string& why, int code);
+  bool idle_deep_ok();
+  void park(int64_t timeout_us);
   bool push_msg_locked(int dst, const Msg& m);
   int64_t bulk_write_locked(int dst, const uint8_t* p, int64_t n);
   int64_t bulk_read(int src, uint8_t* p, int64_t n);
@@ -190,6 +222,8 @@ class Engine {
 
   std::mutex copy_mu_;
   std::vector<PendingCopy> copies_;
+  std::mutex ev_mu_;
+  std::vector<hipEvent_t> ev_pool_;
 
   std::mutex am_mu_;
   std::unordered_map<int, AmHandler> am_;
@@ -211,6 +245,7 @@ class Engine {
 
   std::atomic<int64_t> bytes_sent_{0}, bytes_recv_{0}, msgs_sent_{0};
   std::atomic<uint64_t> activity_{0};
+  std::atomic<int64_t> gpu_pending_{0};
   uint64_t bar_local_gen_ = 0;
 };
 

@@ -42,13 +42,23 @@ PSServer::PSServer(Engine& eng, int ps_id, Window& rx, Window& tx, std::vector<i
       datapath_(datapath),
       staleness_(staleness),
       grad_bf16_(grad_bf16),
-      init_rank_(init_rank) {
+      init_rank_(init_rank),
+      init_left_(shard_len) {
   for (auto s : state) st_.push_back(reinterpret_cast<void*>(s));
   static const int need[] = {0, 3, 2, 2, 1, 2};
   if (rule_.kind < 0 || rule_.kind > 5) throw std::invalid_argument("mpit: unknown server rule");
   if (int(st_.size()) < need[rule_.kind]) throw std::invalid_argument("mpit: missing server optimizer state buffers");
   if (device_ && eng_.device() < 0) throw std::invalid_argument("mpit: device server on a rank without a device");
   if (device_ && datapath_ == 1 && !inbox_) throw std::invalid_argument("mpit: datapath 1 needs an inbox buffer");
+  if (const char* e = std::getenv("MPIT_PS_FORCE_PIPE")) force_pipe_ = std::atoi(e) != 0;
+  if (const char* e = std::getenv("MPIT_PS_FAULT")) {
+    const std::string f(e);
+    const std::string kind = f.substr(0, f.find(':'));
+    fault_kind_ = kind == "grad" ? 1 : kind == "pull" ? 2 : kind == "param" ? 3 : kind == "drop" ? 4 : 0;
+    if (f.find(':') != std::string::npos) fault_at_ = std::max(1, std::atoi(f.c_str() + f.find(':') + 1));
+    if (const char* r = std::getenv("MPIT_PS_FAULT_RANK"))
+      if (std::atoi(r) != eng_.rank()) fault_kind_ = 0;
+  }
   clock_.assign(clients_.size(), 0);
   if (device_) {
     hipp(hipSetDevice(eng_.device()), "hipSetDevice");
@@ -57,12 +67,15 @@ PSServer::PSServer(Engine& eng, int ps_id, Window& rx, Window& tx, std::vector<i
     hipp(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi), "server stream");
     if (datapath_ == 2) {
       const size_t nc = clients_.size();
-      cstream_.resize(nc);
+      size_t nl = nc;
+      if (const char* e = std::getenv("MPIT_PS_LINK_STREAMS"))
+        if (std::atoi(e) > 0) nl = std::min(nc, size_t(std::atoi(e)));
+      cstream_.resize(std::max<size_t>(nl, 1));
+      for (auto& cs : cstream_) hipp(hipStreamCreateWithPriority(&cs, hipStreamNonBlocking, hi), "link stream");
       ev_in_.resize(nc);
       ev_up_.resize(nc);
       ev_out_.resize(nc);
       for (size_t i = 0; i < nc; ++i) {
-        hipp(hipStreamCreateWithPriority(&cstream_[i], hipStreamNonBlocking, hi), "link stream");
         hipp(hipEventCreateWithFlags(&ev_in_[i], hipEventDisableTiming), "event");
         hipp(hipEventCreateWithFlags(&ev_up_[i], hipEventDisableTiming), "event");
         hipp(hipEventCreateWithFlags(&ev_out_[i], hipEventDisableTiming), "event");
@@ -89,9 +102,8 @@ PSServer::~PSServer() {
 }
 
 void PSServer::finish_on(hipStream_t s, std::function<void()> then) {
-  hipEvent_t ev;
-  hipp(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
-  hipp(hipEventRecord(ev, s), "hipEventRecord");
+  hipEvent_t ev = eng_.get_event();
+  Engine::record_event(ev, s);
   eng_.track_copy(ev, std::move(then));
 }
 
@@ -112,6 +124,24 @@ int PSServer::client_index(int world_rank) const {
   return -1;
 }
 
+Sub PSServer::sub_of(const Msg& m) const {
+  if (m.aux2 <= 0) return Sub{0, len_};
+  const Sub sb{m.aux1 - off_, m.aux2};
+  if (sb.o < 0 || sb.o + sb.n > len_)
+    throw std::out_of_range("mpit: PS message names elements [" + std::to_string(m.aux1) + ", " +
+                            std::to_string(m.aux1 + m.aux2) + ") outside this server's shard");
+  return sb;
+}
+
+bool PSServer::maybe_fault(int kind) {
+  // drop (4): the Nth and every later gradient push is silently ignored (a stuck server)
+  if (fault_kind_ == 4 && kind == 1) return fault_seen_.fetch_add(1) + 1 >= fault_at_;
+  if (fault_kind_ == kind && fault_seen_.fetch_add(1) + 1 == fault_at_)
+    throw std::runtime_error("PS server " + std::to_string(ps_id_) + " on rank " + std::to_string(eng_.rank()) +
+                             ": injected fault (MPIT_PS_FAULT)");
+  return false;
+}
+
 void PSServer::on_msg(const Msg& m) {
   const int tag = (m.tag - 4096) % 16;
   // asyncsgd/pserver.lua:152-158: the shard is initialised from the first client's
@@ -122,33 +152,37 @@ void PSServer::on_msg(const Msg& m) {
   }
   switch (tag) {
     case kTagInit:
-      if (m.aux0 != off_ || m.aux1 != len_)
-        std::fprintf(stderr, "[mpit ps %d] client %d shard (%lld,%lld) != server shard (%lld,%lld)\n", ps_id_, m.src,
-                     (long long)m.aux0, (long long)m.aux1, (long long)off_, (long long)len_);
+      // a client's shard entry must lie inside this server's shard
+      if (m.aux0 < off_ || m.aux0 + m.aux1 > off_ + len_)
+        std::fprintf(stderr, "[mpit ps %d] client %d shard (%lld,%lld) outside server shard (%lld,%lld)\n", ps_id_,
+                     m.src, (long long)m.aux0, (long long)m.aux1, (long long)off_, (long long)len_);
       break;
-    case kTagParam:
-      do_param(m.src, (m.aux0 & kPsFromRx) != 0);
-      if (init_rank_ >= 0 && m.src == init_rank_) {
+    case kTagParam: {
+      const Sub sb = sub_of(m);
+      do_param(m.src, (m.aux0 & kPsFromRx) != 0, sb);
+      if (init_rank_ >= 0 && m.src == init_rank_ && (init_left_ -= sb.n) <= 0) {
         init_rank_ = -1;
         std::vector<Msg> later;
         later.swap(backlog_);
         for (auto& x : later) on_msg(x);
       }
       break;
-    case kTagGrad: do_grad(m.src, (m.aux0 & kPsWithPull) != 0); break;
+    }
+    case kTagGrad: do_grad(m.src, (m.aux0 & kPsWithPull) != 0, sub_of(m)); break;
     case kTagHeader: {
+      const Sub sb = sub_of(m);
       const int ci = client_index(m.src);
       if (staleness_ >= 0 && ci >= 0) {
         int64_t mn = clock_[0];
         for (auto c : clock_) mn = std::min(mn, c);
         if (clock_[size_t(ci)] - mn > staleness_) {
           std::lock_guard<std::mutex> g(mu_);
-          deferred_.push_back(m.src);
+          deferred_.push_back({m.src, sb});
           ++stats_.deferred;
           break;
         }
       }
-      do_pull(m.src);
+      do_pull(m.src, sb);
       break;
     }
     case kTagStop: {
@@ -171,73 +205,74 @@ void PSServer::finish(std::function<void()> then) {
     then();
     return;
   }
-  hipEvent_t ev;
-  hipp(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
-  hipp(hipEventRecord(ev, stream_), "hipEventRecord");
-  eng_.track_copy(ev, std::move(then));
+  finish_on(stream_, std::move(then));
 }
 
 void PSServer::reply(int c, int tag) { eng_.send_am(c, ps_am_id(ps_id_, tag), nullptr, 0); }
 
-void PSServer::apply_rule(const void* g, void* out) {
+void PSServer::apply_rule(const void* g, void* out, Sub sb) {
   const int dev = device_ ? eng_.device() : -1;
   const uint32_t bf = grad_bf16_ ? 2u : 0u;
   const int v = out ? kOut : 0;
   auto P = [](const void* x) { return reinterpret_cast<uintptr_t>(x); };
-  std::vector<uintptr_t> ptrs{P(p_), P(g)};
-  for (size_t k = 0; k < st_.size(); ++k) {
-    static const int need[] = {0, 3, 2, 2, 1, 2};
-    if (int(k) < need[rule_.kind]) ptrs.push_back(P(st_[k]));
-  }
+  auto F = [&](void* x) { return P(static_cast<uint8_t*>(x) + sb.o * 4); };  // fp32 state at the piece
+  std::vector<uintptr_t> ptrs{F(p_), P(g)};
+  static const int need[] = {0, 3, 2, 2, 1, 2};
+  for (size_t k = 0; k < st_.size(); ++k)
+    if (int(k) < need[rule_.kind]) ptrs.push_back(F(st_[k]));
   if (out) ptrs.push_back(P(out));
   ServerRule r = rule_;  // progress thread only; lr may be changed concurrently (set_lr)
   r.lr = lr_.load(std::memory_order_relaxed);
+  // the rule's step counter advances once per client push: on its first piece
+  const bool first = sb.o == 0;
   switch (r.kind) {
     case 0:
-      ew_update(kApply, v, dev, stream_, len_, ptrs, bf, {r.a});
+      ew_update(kApply, v, dev, stream_, sb.n, ptrs, bf, {r.a});
       break;
     case 1:
-      ew_update(kRMSProp, v | kAdd, dev, stream_, len_, ptrs, bf, {r.decay, r.lr, r.mom, r.eps});
+      ew_update(kRMSProp, v | kAdd, dev, stream_, sb.n, ptrs, bf, {r.decay, r.lr, r.mom, r.eps});
       break;
     case 2: {  // BiCNN/pserver.lua:147-154: bias correction on floor(t/stepDiv)+1
-      ++t_;
+      if (first) ++t_;
       const double k = double(t_.load() / std::max<int64_t>(1, r.step_div) + 1);
       const double lr_t = r.lr * std::sqrt(1.0 - std::pow(double(r.b2), k)) / (1.0 - std::pow(double(r.b1), k));
-      ew_update(kAdam, v, dev, stream_, len_, ptrs, bf, {r.b1, r.b2, r.eps, float(lr_t)});
+      ew_update(kAdam, v, dev, stream_, sb.n, ptrs, bf, {r.b1, r.b2, r.eps, float(lr_t)});
       break;
     }
     case 3: {  // BiCNN/pserver.lua:163-170
-      ++t_;
+      if (first) ++t_;
       const double lr_t = r.lr / (1.0 - std::pow(double(r.b1), double(t_.load())));
-      ew_update(kAdamax, v, dev, stream_, len_, ptrs, bf, {r.b1, r.b2, r.eps, float(lr_t)});
+      ew_update(kAdamax, v, dev, stream_, sb.n, ptrs, bf, {r.b1, r.b2, r.eps, float(lr_t)});
       break;
     }
-    case 4: {  // BiCNN/pserver.lua:177-182
-      const float clr = float(r.lr / (1.0 + double(t_.load()) * r.lrd));
-      ++t_;
-      ew_update(kAdagrad, v, dev, stream_, len_, ptrs, bf, {r.eps, clr});
+    case 4: {  // BiCNN/pserver.lua:177-182 (clr on the count before this push)
+      const int64_t t = first ? t_.fetch_add(1) : t_.load() - 1;
+      const float clr = float(r.lr / (1.0 + double(t) * r.lrd));
+      ew_update(kAdagrad, v, dev, stream_, sb.n, ptrs, bf, {r.eps, clr});
       break;
     }
     case 5:  // BiCNN/pserver.lua:189-193
-      ++t_;
-      ew_update(kAdadelta, v, dev, stream_, len_, ptrs, bf, {r.rho, r.eps, r.lr});
+      if (first) ++t_;
+      ew_update(kAdadelta, v, dev, stream_, sb.n, ptrs, bf, {r.rho, r.eps, r.lr});
       break;
   }
-  version_.fetch_add(1);
+  if (sb.o + sb.n == len_) version_.fetch_add(1);
 }
 
-void PSServer::do_param(int c, bool from_rx) {
+void PSServer::do_param(int c, bool from_rx, Sub sb) {
   TraceRange tr("ps_server_param");
+  maybe_fault(3);
   const int m = member_of(c);
   const Window& w = from_rx ? rx_ : tx_;  // rx is always fp32
   const bool bf = grad_bf16_ && !from_rx;
   const int64_t es = bf ? 2 : 4;
-  const uint8_t* src = reinterpret_cast<const uint8_t*>(w.remote_ptr(m)) + off_ * es;
+  const uint8_t* src = reinterpret_cast<const uint8_t*>(w.remote_ptr(m)) + (off_ + sb.o) * es;
   if (!device_ && w.remote_device(m)) throw std::runtime_error("mpit: host server cannot read a device window");
   if (device_) hipp(hipSetDevice(eng_.device()), "hipSetDevice");
   // p (fp32) = pushed shard (fp32 | bf16): one copy / cast kernel, or a host loop
-  ew_update(kCopy, 0, device_ ? eng_.device() : -1, stream_, len_,
-            {reinterpret_cast<uintptr_t>(p_), reinterpret_cast<uintptr_t>(src)}, bf ? 2u : 0u, {1.f});
+  ew_update(kCopy, 0, device_ ? eng_.device() : -1, stream_, sb.n,
+            {reinterpret_cast<uintptr_t>(static_cast<uint8_t*>(p_) + sb.o * 4), reinterpret_cast<uintptr_t>(src)},
+            bf ? 2u : 0u, {1.f});
   {
     std::lock_guard<std::mutex> g(mu_);
     ++stats_.param_pushes;
@@ -245,37 +280,40 @@ void PSServer::do_param(int c, bool from_rx) {
   finish([this, c] { reply(c, kTagParamTail); });
 }
 
-void PSServer::copy_out(int c) {
+void PSServer::copy_out(int c, Sub sb) {
   const int m = member_of(c);
-  uint8_t* dst = reinterpret_cast<uint8_t*>(rx_.remote_ptr(m)) + off_ * 4;
+  uint8_t* dst = reinterpret_cast<uint8_t*>(rx_.remote_ptr(m)) + (off_ + sb.o) * 4;
+  const uint8_t* src = static_cast<const uint8_t*>(p_) + sb.o * 4;
   if (device_) {
     hipp(hipSetDevice(eng_.device()), "hipSetDevice");
     if (datapath_ != 1)
-      ew_update(kCopy, 0, eng_.device(), stream_, len_, {reinterpret_cast<uintptr_t>(dst), reinterpret_cast<uintptr_t>(p_)},
+      ew_update(kCopy, 0, eng_.device(), stream_, sb.n, {reinterpret_cast<uintptr_t>(dst), reinterpret_cast<uintptr_t>(src)},
                 0u, {1.f});
     else
-      hipp(hipMemcpyAsync(dst, p_, size_t(len_) * 4, hipMemcpyDefault, stream_), "param pull copy");
+      hipp(hipMemcpyAsync(dst, src, size_t(sb.n) * 4, hipMemcpyDefault, stream_), "param pull copy");
   } else {
     if (rx_.remote_device(m)) throw std::runtime_error("mpit: host server cannot write a device rx window");
-    std::memcpy(dst, p_, size_t(len_) * 4);
+    std::memcpy(dst, src, size_t(sb.n) * 4);
   }
 }
 
-void PSServer::do_pull(int c) {
+void PSServer::do_pull(int c, Sub sb) {
   TraceRange tr("ps_server_pull");
+  maybe_fault(2);
   const int ci = client_index(c);
   if (pipelined(ci, c)) {
-    // snapshot the shard in update order on stream_, push it over the client's link
+    // snapshot the piece in update order on stream_, push it over the client's link
     hipp(hipSetDevice(eng_.device()), "hipSetDevice");
-    hipStream_t cs = cstream_[size_t(ci)];
-    uint8_t* out = stage_ + size_t(ci) * size_t(len_) * 8 + size_t(len_) * 4;
-    uint8_t* dst = reinterpret_cast<uint8_t*>(rx_.remote_ptr(member_of(c))) + off_ * 4;
+    hipStream_t cs = link(ci);
+    uint8_t* out = stage_ + size_t(ci) * size_t(len_) * 8 + size_t(len_) * 4 + size_t(sb.o) * 4;
+    uint8_t* dst = reinterpret_cast<uint8_t*>(rx_.remote_ptr(member_of(c))) + (off_ + sb.o) * 4;
+    const uint8_t* src = static_cast<const uint8_t*>(p_) + sb.o * 4;
     hipp(hipStreamWaitEvent(stream_, ev_out_[size_t(ci)], 0), "wait outbox free");
-    ew_update(kCopy, 0, eng_.device(), stream_, len_, {reinterpret_cast<uintptr_t>(out), reinterpret_cast<uintptr_t>(p_)},
+    ew_update(kCopy, 0, eng_.device(), stream_, sb.n, {reinterpret_cast<uintptr_t>(out), reinterpret_cast<uintptr_t>(src)},
               0u, {1.f});
     hipp(hipEventRecord(ev_up_[size_t(ci)], stream_), "record snapshot");
     hipp(hipStreamWaitEvent(cs, ev_up_[size_t(ci)], 0), "link waits snapshot");
-    hipp(hipMemcpyAsync(dst, out, size_t(len_) * 4, hipMemcpyDefault, cs), "param push (link)");
+    hipp(hipMemcpyAsync(dst, out, size_t(sb.n) * 4, hipMemcpyDefault, cs), "param push (link)");
     hipp(hipEventRecord(ev_out_[size_t(ci)], cs), "record outbox sent");
     {
       std::lock_guard<std::mutex> g(mu_);
@@ -284,7 +322,7 @@ void PSServer::do_pull(int c) {
     finish_on(cs, [this, c] { reply(c, kTagSendParam); });
     return;
   }
-  copy_out(c);
+  copy_out(c, sb);
   {
     std::lock_guard<std::mutex> g(mu_);
     ++stats_.pulls;
@@ -292,15 +330,17 @@ void PSServer::do_pull(int c) {
   finish([this, c] { reply(c, kTagSendParam); });
 }
 
-void PSServer::do_grad(int c, bool pull) {
+void PSServer::do_grad(int c, bool pull, Sub sb) {
   TraceRange tr(pull ? "ps_server_update+pull" : "ps_server_update");
+  if (maybe_fault(1)) return;
   const int m = member_of(c);
   const int64_t es = grad_bf16_ ? 2 : 4;
-  const void* g = reinterpret_cast<const uint8_t*>(tx_.remote_ptr(m)) + off_ * es;
+  const void* g = reinterpret_cast<const uint8_t*>(tx_.remote_ptr(m)) + (off_ + sb.o) * es;
   const int ci = client_index(c);
   bool defer_pull = false;
   if (ci >= 0) {
-    ++clock_[size_t(ci)];
+    // one push per client per step: counted on the piece that ends the shard
+    if (sb.o + sb.n == len_) ++clock_[size_t(ci)];
     if (pull && staleness_ >= 0) {
       int64_t mn = clock_[0];
       for (auto x : clock_) mn = std::min(mn, x);
@@ -309,24 +349,24 @@ void PSServer::do_grad(int c, bool pull) {
   }
   if (!device_ && tx_.remote_device(m)) throw std::runtime_error("mpit: host server cannot read a device tx window");
   if (pipelined(ci, c)) {
-    // link stream: pull the gradient shard into this client's inbox; stream_: fused update
+    // link stream: pull the gradient piece into this client's inbox; stream_: fused update
     // (+ snapshot into the outbox when a pull is due); link stream: push the snapshot
     hipp(hipSetDevice(eng_.device()), "hipSetDevice");
     const size_t k = size_t(ci);
-    hipStream_t cs = cstream_[k];
-    uint8_t* in = stage_ + k * size_t(len_) * 8;
-    uint8_t* out = in + size_t(len_) * 4;
+    hipStream_t cs = link(ci);
+    uint8_t* in = stage_ + k * size_t(len_) * 8 + size_t(sb.o * es);
+    uint8_t* out = stage_ + k * size_t(len_) * 8 + size_t(len_) * 4 + size_t(sb.o) * 4;
     const bool push_back = pull && !defer_pull;
-    hipp(hipMemcpyAsync(in, g, size_t(len_ * es), hipMemcpyDefault, cs), "grad pull (link)");
+    hipp(hipMemcpyAsync(in, g, size_t(sb.n * es), hipMemcpyDefault, cs), "grad pull (link)");
     hipp(hipEventRecord(ev_in_[k], cs), "record inbox full");
     hipp(hipStreamWaitEvent(stream_, ev_in_[k], 0), "update waits inbox");
     if (push_back) hipp(hipStreamWaitEvent(stream_, ev_out_[k], 0), "update waits outbox free");
-    apply_rule(in, push_back ? out : nullptr);
+    apply_rule(in, push_back ? out : nullptr, sb);
     hipp(hipEventRecord(ev_up_[k], stream_), "record update");
     hipp(hipStreamWaitEvent(cs, ev_up_[k], 0), "link waits update");  // inbox reusable after this
     if (push_back) {
-      uint8_t* dst = reinterpret_cast<uint8_t*>(rx_.remote_ptr(m)) + off_ * 4;
-      hipp(hipMemcpyAsync(dst, out, size_t(len_) * 4, hipMemcpyDefault, cs), "param push (link)");
+      uint8_t* dst = reinterpret_cast<uint8_t*>(rx_.remote_ptr(m)) + (off_ + sb.o) * 4;
+      hipp(hipMemcpyAsync(dst, out, size_t(sb.n) * 4, hipMemcpyDefault, cs), "param push (link)");
       hipp(hipEventRecord(ev_out_[k], cs), "record outbox sent");
     }
     {
@@ -334,7 +374,7 @@ void PSServer::do_grad(int c, bool pull) {
       ++stats_.grads;
       if (push_back) ++stats_.pulls;
       if (defer_pull) {
-        deferred_.push_back(c);
+        deferred_.push_back({c, sb});
         ++stats_.deferred;
       }
     }
@@ -347,22 +387,23 @@ void PSServer::do_grad(int c, bool pull) {
   }
   void* fused_out = nullptr;
   if (pull && !defer_pull && (datapath_ != 1 || !device_))
-    fused_out = reinterpret_cast<uint8_t*>(rx_.remote_ptr(m)) + off_ * 4;
+    fused_out = reinterpret_cast<uint8_t*>(rx_.remote_ptr(m)) + (off_ + sb.o) * 4;
   if (device_) {
     hipp(hipSetDevice(eng_.device()), "hipSetDevice");
     if (datapath_ == 1) {
-      hipp(hipMemcpyAsync(inbox_, g, size_t(len_ * es), hipMemcpyDefault, stream_), "grad inbox copy");
-      g = inbox_;
+      void* ib = static_cast<uint8_t*>(inbox_) + sb.o * es;
+      hipp(hipMemcpyAsync(ib, g, size_t(sb.n * es), hipMemcpyDefault, stream_), "grad inbox copy");
+      g = ib;
     }
   }
-  apply_rule(g, fused_out);
-  if (pull && !defer_pull && !fused_out) copy_out(c);
+  apply_rule(g, fused_out, sb);
+  if (pull && !defer_pull && !fused_out) copy_out(c, sb);
   {
     std::lock_guard<std::mutex> lk(mu_);
     ++stats_.grads;
     if (pull && !defer_pull) ++stats_.pulls;
     if (defer_pull) {
-      deferred_.push_back(c);
+      deferred_.push_back({c, sb});
       ++stats_.deferred;
     }
   }
@@ -375,21 +416,21 @@ void PSServer::do_grad(int c, bool pull) {
 
 void PSServer::release_deferred() {
   if (staleness_ < 0) return;
-  std::deque<int> ready;
+  std::deque<std::pair<int, Sub>> ready;
   {
     std::lock_guard<std::mutex> g(mu_);
     if (deferred_.empty()) return;
     int64_t mn = clock_.empty() ? 0 : clock_[0];
     for (auto x : clock_) mn = std::min(mn, x);
-    std::deque<int> keep;
-    for (int c : deferred_) {
-      const int ci = client_index(c);
-      if (ci < 0 || clock_[size_t(ci)] - mn <= staleness_) ready.push_back(c);
-      else keep.push_back(c);
+    std::deque<std::pair<int, Sub>> keep;
+    for (auto& d : deferred_) {
+      const int ci = client_index(d.first);
+      if (ci < 0 || clock_[size_t(ci)] - mn <= staleness_) ready.push_back(d);
+      else keep.push_back(d);
     }
     deferred_.swap(keep);
   }
-  for (int c : ready) do_pull(c);
+  for (auto& d : ready) do_pull(d.first, d.second);
 }
 
 void PSServer::wait_done() {
@@ -431,8 +472,8 @@ PSClient::PSClient(Engine& eng, int ps_id, std::vector<int> servers, std::vector
     throw std::invalid_argument("mpit: PSClient shard table mismatch");
   auto gq = std::make_shared<GateQueue>();
   gq_ = gq;
-  int dev = eng_.device();
-  hook_ = eng_.add_hook([gq, dev]() {
+  Engine* e = &eng_;
+  hook_ = eng_.add_hook([gq, e]() {
     bool did = false;
     for (;;) {
       GateQueue::Gate g;
@@ -441,12 +482,19 @@ PSClient::PSClient(Engine& eng, int ps_id, std::vector<int> servers, std::vector
         if (gq->q.empty()) break;
         g = gq->q.front();
         if (g.ev) {
-          hipSetDevice(dev);
-          if (hipEventQuery(g.ev) == hipErrorNotReady) break;
+          hipSetDevice(e->device());
+          const hipError_t st = hipEventQuery(g.ev);
+          if (st == hipErrorNotReady) break;
+          if (st != hipSuccess)
+            throw std::runtime_error(std::string("PS client gate: GPU work before a push failed: ") +
+                                     hipGetErrorString(st));
         }
         gq->q.pop_front();
       }
-      if (g.ev) hipEventDestroy(g.ev);
+      if (g.ev) {
+        e->put_event(g.ev);
+        e->gpu_pending_add(-1);
+      }
       g.send();
       did = true;
     }
@@ -471,79 +519,114 @@ void PSClient::gate(hipStream_t s, std::function<void()> send) {
   // client always gates its AM on the work queued so far on s
   if (eng_.device() >= 0) {
     hipp(hipSetDevice(eng_.device()), "hipSetDevice");
-    hipp(hipEventCreateWithFlags(&g.ev, hipEventDisableTiming), "hipEventCreate");
-    hipp(hipEventRecord(g.ev, s), "hipEventRecord");
+    g.ev = eng_.get_event();
+    Engine::record_event(g.ev, s);
   }
-  std::lock_guard<std::mutex> l(gq_->mu);
-  gq_->q.push_back(g);
+  {
+    std::lock_guard<std::mutex> l(gq_->mu);
+    gq_->q.push_back(g);
+  }
+  if (g.ev) eng_.gpu_pending_add(1);
+  else eng_.kick();
+}
+
+// the message of shard entry k: whole-shard entries carry no piece (aux2 = 0)
+void PSClient::send_entry(int k, int tag, int64_t flags) {
+  const bool whole = std::count(servers_.begin(), servers_.end(), servers_[size_t(k)]) == 1;
+  eng_.send_am(servers_[size_t(k)], ps_am_id(ps_id_, tag), nullptr, 0, flags, whole ? 0 : offs_[size_t(k)],
+               whole ? 0 : lens_[size_t(k)]);
 }
 
 void PSClient::send_grad(hipStream_t s, bool with_pull) {
   const int64_t n = int64_t(servers_.size());
   pending_.fetch_add(with_pull ? 2 * n : n);
-  gate(s, [this, with_pull] {
-    for (int srv : servers_) eng_.send_am(srv, ps_am_id(ps_id_, kTagGrad), nullptr, 0, with_pull ? kPsWithPull : 0);
+  gate(s, [this, with_pull, n] {
+    for (int k = 0; k < int(n); ++k) send_entry(k, kTagGrad, with_pull ? kPsWithPull : 0);
   });
 }
 
 void PSClient::send_grad_to(hipStream_t s, int k, bool with_pull) {
   if (k < 0 || k >= int(servers_.size())) throw std::out_of_range("PSClient::send_grad_to: bad shard");
   pending_.fetch_add(with_pull ? 2 : 1);
-  const int srv = servers_[k];
-  gate(s, [this, srv, with_pull] {
-    eng_.send_am(srv, ps_am_id(ps_id_, kTagGrad), nullptr, 0, with_pull ? kPsWithPull : 0);
-  });
+  gate(s, [this, k, with_pull] { send_entry(k, kTagGrad, with_pull ? kPsWithPull : 0); });
 }
 
 void PSClient::recv_param(hipStream_t s) {
-  pending_.fetch_add(int64_t(servers_.size()));
+  const int n = int(servers_.size());
+  pending_.fetch_add(n);
   // ordered behind any gated push of this client
-  gate(s, [this] {
-    for (int srv : servers_) eng_.send_am(srv, ps_am_id(ps_id_, kTagHeader), nullptr, 0);
+  gate(s, [this, n] {
+    for (int k = 0; k < n; ++k) send_entry(k, kTagHeader, 0);
   });
 }
 
 void PSClient::send_param(hipStream_t s, bool from_rx) {
-  pending_.fetch_add(int64_t(servers_.size()));
-  gate(s, [this, from_rx] {
-    for (int srv : servers_) eng_.send_am(srv, ps_am_id(ps_id_, kTagParam), nullptr, 0, from_rx ? kPsFromRx : 0);
+  const int n = int(servers_.size());
+  pending_.fetch_add(n);
+  gate(s, [this, from_rx, n] {
+    for (int k = 0; k < n; ++k) send_entry(k, kTagParam, from_rx ? kPsFromRx : 0);
   });
 }
 
 void PSClient::stop() {
   wait();
-  for (int srv : servers_) eng_.send_am(srv, ps_am_id(ps_id_, kTagStop), nullptr, 0);
+  std::vector<int> done;
+  for (int srv : servers_) {  // one stop per server, however many entries it has
+    if (std::find(done.begin(), done.end(), srv) != done.end()) continue;
+    done.push_back(srv);
+    eng_.send_am(srv, ps_am_id(ps_id_, kTagStop), nullptr, 0);
+  }
 }
 
 void PSClient::on_reply(const Msg&) {
   replies_.fetch_add(1);
-  pending_.fetch_sub(1);
-  pending_.notify_all();
+  pending_.fetch_sub(1, std::memory_order_seq_cst);
+  reply_seq_.fetch_add(1, std::memory_order_seq_cst);
+  futex_wake_all(&reply_seq_, false);
 }
 
 // The worker waits here every step while the GPU finishes its backward (tens of ms).
 // MPIT_WAIT_SPIN_US > 0 polls (pause) for up to that long before the futex sleep, keeping
 // the core awake for the step start that follows (device clients only). Measured within
 // noise of sleeping at once (profiles/step_start_host_r02.md): default 0.
+// MPIT_PS_TIMEOUT_S (default 300, 0 = never): a reply missing that long means a server is
+// gone or stuck — raise with what is missing instead of hanging the job (a server that
+// fails raises the job-wide abort itself, Engine::fatal; this covers the silent cases).
 void PSClient::wait() {
   static const int64_t spin_us = [] {
     const char* e = std::getenv("MPIT_WAIT_SPIN_US");
     return e ? std::max<int64_t>(0, std::atoll(e)) : int64_t(0);
   }();
+  static const double timeout_s = [] {
+    const char* e = std::getenv("MPIT_PS_TIMEOUT_S");
+    return e ? std::max(0.0, std::atof(e)) : 300.0;
+  }();
+  const auto t0 = std::chrono::steady_clock::now();
   if (spin_us > 0 && eng_.device() >= 0) {  // GPU workers only (CPU ranks share few cores)
-    const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t i = 0;; ++i) {
       if (pending_.load(std::memory_order_acquire) <= 0) return;
       _mm_pause();
-      if ((i & 1023) == 0 &&
-          std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us))
-        break;
+      if ((i & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us)) break;
     }
   }
   for (;;) {
-    const int64_t v = pending_.load(std::memory_order_acquire);
+    const uint32_t seq = reply_seq_.load(std::memory_order_seq_cst);
+    const int64_t v = pending_.load(std::memory_order_seq_cst);
     if (v <= 0) return;
-    pending_.wait(v, std::memory_order_acquire);
+    int64_t slice_us = 1000000;
+    if (timeout_s > 0) {
+      const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (el >= timeout_s) {
+        std::string srv;
+        for (size_t k = 0; k < servers_.size(); ++k) srv += (k ? "," : "") + std::to_string(servers_[k]);
+        throw std::runtime_error("mpit: PS client " + std::to_string(eng_.rank()) + " waited " +
+                                 std::to_string(int(timeout_s)) + " s for " + std::to_string(v) +
+                                 " server replies (servers " + srv + ", ps " + std::to_string(ps_id_) +
+                                 "); a server is gone or stuck (MPIT_PS_TIMEOUT_S)");
+      }
+      slice_us = std::min<int64_t>(slice_us, int64_t((timeout_s - el) * 1e6) + 1);
+    }
+    futex_wait(&reply_seq_, seq, slice_us, false);
   }
 }
 

@@ -73,6 +73,14 @@ struct ServerStats {
   int64_t grads = 0, pulls = 0, param_pushes = 0, deferred = 0;
 };
 
+// A contiguous piece of a server's shard named by a message: [o, o + n) relative to the
+// shard start. A client normally addresses whole shards; a client that splits one server's
+// shard into several entries (bench.py --emulate-shards: K shards on one GPU) sends the
+// absolute offset / length of its entry in aux1 / aux2 (tags 2, 4, 5).
+struct Sub {
+  int64_t o = 0, n = 0;
+};
+
 class PSServer {
  public:
   // members: world ranks of the window members, in window member order; clients: the
@@ -98,11 +106,13 @@ class PSServer {
 
  private:
   void on_msg(const Msg& m);
-  void do_param(int c, bool from_rx = false);
-  void do_grad(int c, bool pull);
-  void do_pull(int c);
-  void apply_rule(const void* g, void* out);
-  void copy_out(int c);
+  Sub sub_of(const Msg& m) const;
+  bool maybe_fault(int kind);
+  void do_param(int c, bool from_rx, Sub sb);
+  void do_grad(int c, bool pull, Sub sb);
+  void do_pull(int c, Sub sb);
+  void apply_rule(const void* g, void* out, Sub sb);
+  void copy_out(int c, Sub sb);
   void reply(int c, int tag);
   void finish(std::function<void()> then);
   void release_deferred();
@@ -129,19 +139,32 @@ class PSServer {
   // gradient pulls and parameter pushes of different clients run concurrently over
   // their own xGMI links (SDMA copies) and only the local fused update is serialised on
   // stream_. stage_ = [clients][inbox | outbox] of shard_len fp32 each.
+  // MPIT_PS_LINK_STREAMS=k caps the link streams (client i uses stream i % k); default one
+  // per client. The link streams carry only SDMA copies and event waits.
   std::vector<hipStream_t> cstream_;
+  hipStream_t link(int ci) const { return cstream_[size_t(ci) % cstream_.size()]; }
   std::vector<hipEvent_t> ev_in_, ev_up_, ev_out_;
   uint8_t* stage_ = nullptr;
   void finish_on(hipStream_t s, std::function<void()> then);
-  // the worker on this very GPU is served by the fused local kernel (no copies at all)
-  bool pipelined(int ci, int c) const { return device_ && datapath_ == 2 && ci >= 0 && c != eng_.rank(); }
+  // the worker on this very GPU is served by the fused local kernel (no copies at all),
+  // unless MPIT_PS_FORCE_PIPE=1 (the K-shard emulation: every push takes the link path)
+  bool force_pipe_ = false;
+  bool pipelined(int ci, int c) const {
+    return device_ && datapath_ == 2 && ci >= 0 && (c != eng_.rank() || force_pipe_);
+  }
+  // fault injection (tests of the fail-fast path): MPIT_PS_FAULT=grad|pull|param[:N] throws
+  // in the Nth such request, drop[:N] silently ignores gradient pushes from the Nth on;
+  // MPIT_PS_FAULT_RANK=r limits it to the server on rank r
+  int fault_kind_ = 0, fault_at_ = 1;
+  std::atomic<int> fault_seen_{0};
   std::atomic<int> stopped_{0};
   std::atomic<int64_t> version_{0};
   int init_rank_;                 // client whose parameter push initialises the shard (-1: ready)
+  int64_t init_left_;             // elements of the shard that push has still to cover
   std::vector<Msg> backlog_;      // grads / pulls that arrived before that push
   std::atomic<int64_t> t_{0};  // rule step counter (adam / adamax / adagrad / adadelta)
   std::vector<int64_t> clock_;  // pushes received per client (SSP)
-  std::deque<int> deferred_;     // clients whose pull waits for stragglers
+  std::deque<std::pair<int, Sub>> deferred_;  // pulls (client, piece) waiting for stragglers
   mutable std::mutex mu_;
   std::condition_variable cv_;
   ServerStats stats_;
@@ -149,6 +172,8 @@ class PSServer {
 
 class PSClient {
  public:
+  // one entry per shard: (server rank, absolute offset, length). A server normally appears
+  // once; several entries of one server split its shard (emulation of K shards).
   PSClient(Engine& eng, int ps_id, std::vector<int> servers, std::vector<int64_t> offs, std::vector<int64_t> lens);
   ~PSClient();
   void start();            // register reply handlers, send shard info (tag 1)
@@ -160,7 +185,9 @@ class PSClient {
                                    // gated on s when rx is still being read there
   void send_param(hipStream_t s, bool from_rx = false);
   void stop();
-  void wait();             // until every outstanding reply arrived (GIL released)
+  // until every outstanding reply arrived (GIL released); raises after MPIT_PS_TIMEOUT_S
+  // (default 300 s, 0 = never) with the number of replies still missing
+  void wait();
   bool test() const { return pending_.load() == 0; }
   int64_t pending() const { return pending_.load(); }
   int64_t replies() const { return replies_.load(); }
@@ -168,6 +195,7 @@ class PSClient {
  private:
   struct GateQueue;
   void gate(hipStream_t s, std::function<void()> send);
+  void send_entry(int k, int tag, int64_t flags);
   void on_reply(const Msg& m);
   Engine& eng_;
   std::shared_ptr<GateQueue> gq_;
@@ -177,6 +205,7 @@ class PSClient {
   std::vector<int64_t> offs_, lens_;
   std::atomic<int64_t> pending_{0};
   std::atomic<int64_t> replies_{0};
+  std::atomic<uint32_t> reply_seq_{0};  // futex word bumped by every reply
 };
 
 }  // namespace mpit

@@ -67,6 +67,11 @@ Segment::Segment(const std::string& name, int world, int rank, bool create, int6
     new (&hdr_->abort_flag) std::atomic<int32_t>(0);
     new (&hdr_->bar_count) std::atomic<uint64_t>(0);
     new (&hdr_->bar_gen) std::atomic<uint64_t>(0);
+    hdr_->abort_rank = -1;
+    for (int r = 0; r < kMaxRanks; ++r) {
+      new (&hdr_->ranks[r].doorbell) std::atomic<uint32_t>(0);
+      new (&hdr_->ranks[r].sleeping) std::atomic<int32_t>(0);
+    }
     for (int s = 0; s < world; ++s)
       for (int d = 0; d < world; ++d) {
         new (&ring(s, d)->head) std::atomic<uint64_t>(0);

@@ -69,7 +69,14 @@ struct alignas(64) RankInfo {
   int32_t device;
   int32_t pad;
   char host[48];
+  // An idle progress thread parks on `doorbell` (a futex word shared across processes)
+  // after announcing itself in `sleeping`; whoever hands it work (a ring message, bulk
+  // bytes, a freed ring slot, a local request) bumps the word and wakes it (engine.cpp).
+  alignas(64) std::atomic<uint32_t> doorbell;
+  std::atomic<int32_t> sleeping;
 };
+
+constexpr int kAbortMsg = 256;
 
 struct alignas(64) Header {
   uint64_t magic;
@@ -80,7 +87,8 @@ struct alignas(64) Header {
   std::atomic<int32_t> nattached;
   std::atomic<int32_t> abort_flag;
   int32_t abort_code;
-  int32_t pad;
+  int32_t abort_rank;  // the rank that raised the fatal error (abort_msg is its reason)
+  char abort_msg[kAbortMsg];
   alignas(64) std::atomic<uint64_t> bar_count;
   alignas(64) std::atomic<uint64_t> bar_gen;
   alignas(64) RankInfo ranks[kMaxRanks];

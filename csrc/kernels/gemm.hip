@@ -43,6 +43,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <array>
+#include <map>
+#include <mutex>
 #include <vector>
 #include <stdexcept>
 #include <string>
@@ -290,7 +292,9 @@ __device__ __forceinline__ int xcd_tile(int bid, int nb) {
 // dbeta and the apply coefficients (bn_act.hip fin_bwd_channel's math). Deterministic; the
 // hand-off is bn_tiles_finalize_kernel's: write-through stores, s_waitcnt, barrier, one
 // agent-scope ticket add per workgroup, agent acquire in the consumer.
-constexpr int kFoldSlots = 16;
+constexpr int kFoldSlots = 32;  // kFoldStreams groups of kFoldPerStream ticket sets
+constexpr int kFoldPerStream = 4;
+constexpr int kFoldStreams = kFoldSlots / kFoldPerStream;
 constexpr int kFoldMax = 8192;
 constexpr int kFoldMaxGroups = 128;
 __device__ uint32_t g_fold_tickets[kFoldSlots * kFoldMax];
@@ -1448,16 +1452,37 @@ static bool gemm_log() {
 }
 
 // group size (M-tiles) and ticket set of a folded BN finalize: <= kFoldMaxGroups groups of
-// >= 16 M-tiles; a rotating set of ticket counters per launch (reset to zero by their last
-// user, so a set is free once its launch retired)
-static void fold_plan(EpiArgs& ep, int64_t mtn, int ntn) {
+// >= 16 M-tiles. Ticket counters are reset to zero by their last user, so a set is free
+// once its launch retired — guaranteed only for launches of the SAME stream (stream
+// order). Each (device, stream) therefore owns its own group of kFoldPerStream sets and
+// rotates within it; two folded GEMMs in flight on different streams never share a set.
+static void fold_plan(EpiArgs& ep, int dev, hipStream_t s, int64_t mtn, int ntn) {
   const int64_t fg = std::max<int64_t>(16, (mtn + kFoldMaxGroups - 1) / kFoldMaxGroups);
   const int64_t ngr = (mtn + fg - 1) / fg;
   if (int64_t(ntn) * (ngr + 1) > kFoldMax) throw std::invalid_argument("gemm_nt: BN fold ticket table too small");
-  static std::atomic<uint32_t> launches{0};
+  struct Group {
+    int index;
+    uint32_t next;
+  };
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, Group> groups;
+  static std::map<int, int> used;  // groups handed out per device
+  uint32_t slot;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = groups.find({dev, s});
+    if (it == groups.end()) {
+      int& u = used[dev];
+      if (u >= kFoldStreams)
+        throw std::runtime_error("gemm_nt: the BN finalize fold was used from more than " +
+                                 std::to_string(kFoldStreams) + " streams of one device (MPIT_BN_FOLD=0 disables it)");
+      it = groups.emplace(std::make_pair(dev, s), Group{u++, 0}).first;
+    }
+    slot = uint32_t(it->second.index * kFoldPerStream) + (it->second.next++ % kFoldPerStream);
+  }
   uint32_t* base = nullptr;
   hip_check(hipGetSymbolAddress(reinterpret_cast<void**>(&base), HIP_SYMBOL(g_fold_tickets)), "fold ticket symbol");
-  ep.ftick = base + size_t(launches.fetch_add(1) % kFoldSlots) * kFoldMax;
+  ep.ftick = base + size_t(slot) * kFoldMax;
   ep.fgroup = int(fg);
 }
 
@@ -1569,7 +1594,7 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
     const int ntn = N / BN;                                                                                    \
     const int64_t nb = mtn * ntn;                                                                              \
     if (nb > INT32_MAX) throw std::invalid_argument("gemm_nt: too many tiles");                               \
-    if (ep.fcoef) fold_plan(ep, mtn, ntn);                                                                     \
+    if (ep.fcoef) fold_plan(ep, dev, s, mtn, ntn);                                                                 \
     /* LDS: the k-tile ring, reused by the epilogue's output tile and reduction table */                      \
     const size_t shm = std::max({size_t(ST) * (BM + BN) * size_t(nt_bkb(BM, BN, fm)),                          \
                                  size_t(BM) * BN * sizeof(T), size_t(256) * 8 * 3 * sizeof(float)});          \

@@ -761,11 +761,15 @@ class Comm:
         m = buf.numel()
         bounds = [m * k // n for k in range(n + 1)]
         chunk = [buf[bounds[k]: bounds[k + 1]] for k in range(n)]
-        tmp = torch.empty(max(bounds[k + 1] - bounds[k] for k in range(n)), dtype=buf.dtype, device=buf.device)
+        # two receive buffers: step s's op kernel (queued on the compute stream) may still
+        # read tmp[s % 2] while step s + 1's receive lands — the engine pulls on its own
+        # stream. Step s + 2 reuses it only after step s + 1's send synchronised the stream.
+        cap = max(bounds[k + 1] - bounds[k] for k in range(n))
+        tmps = [torch.empty(cap, dtype=buf.dtype, device=buf.device) for _ in range(2)]
         right, left = (r + 1) % n, (r - 1) % n
         for s in range(n - 1):  # reduce-scatter: rank r ends owning chunk (r + 1) % n
             si, ri = (r - s) % n, (r - s - 1) % n
-            t = tmp[: chunk[ri].numel()]
+            t = tmps[s % 2][: chunk[ri].numel()]
             rq = self._crecv(t, left, 10)
             sq = self._csend(chunk[si], right, 10)
             rq.Wait()

@@ -737,10 +737,32 @@ class _StemPackBuf:
     channel are written once, each step copies only the image into the interior (one copy
     kernel instead of a full-size fill + copy, and no per-step allocation of the buffer).
     A buffer still saved for a pending backward (``busy``) is never reused: the next
-    forward then takes a fresh one. MPIT_STEM_PACK_REUSE=0: pad anew every call."""
+    forward then takes a fresh one. Every use (the forward's copy + GEMM, the backward's
+    weight-gradient GEMM) records the entry's event on its stream; a later use on another
+    stream waits on it first, so a refill never overtakes a pending reader whatever the
+    streams. MPIT_STEM_PACK_REUSE=0: pad anew every call."""
 
     enabled = os.environ.get("MPIT_STEM_PACK_REUSE", "1") != "0"
     bufs = {}
+
+    class Entry:
+        __slots__ = ("buf", "busy", "event", "stream")
+
+        def __init__(self, buf):
+            self.buf, self.busy, self.event, self.stream = buf, False, None, None
+
+        def order_after_last_use(self, dev):
+            cur = torch.cuda.current_stream(dev)
+            if self.event is not None and self.stream != cur.cuda_stream:
+                cur.wait_event(self.event)
+
+        def used(self, dev):
+            """Record the last use (queued on the current stream)."""
+            cur = torch.cuda.current_stream(dev)
+            if self.event is None:
+                self.event = torch.cuda.Event()
+            self.event.record(cur)
+            self.stream = cur.cuda_stream
 
     @classmethod
     def get(cls, x: torch.Tensor, pad: int, hp: int, wp: int, dt):
@@ -750,17 +772,13 @@ class _StemPackBuf:
             return F.pad(v, (0, 4 - c, pad, wp - w - pad, pad, hp - h - pad)), None
         key = (x.device, dt, n, h, w, c, pad, hp, wp)
         ent = cls.bufs.get(key)
-        if ent is None or ent[1]:
-            # [buffer, busy, stream of the last backward that read it if not this one's, its event]
-            ent = [torch.zeros((n, hp, wp, 4), dtype=dt, device=x.device), False, None]
+        if ent is None or ent.busy:
+            ent = cls.Entry(torch.zeros((n, hp, wp, 4), dtype=dt, device=x.device))
             cls.bufs[key] = ent
-        if ent[2] is not None:  # that backward ran on another stream: order the copy after it
-            torch.cuda.current_stream(x.device).wait_event(ent[2])
-            ent[2] = None
-        ent[1] = True  # busy until the backward that reads it has been issued
-        ent[0][:, pad:pad + h, pad:pad + w, :c].copy_(v)
-        ent.append(_stream(x))  # the stream of this forward (popped by the backward)
-        return ent[0], ent
+        ent.order_after_last_use(x.device)
+        ent.busy = True  # until the backward that reads it has been issued
+        ent.buf[:, pad:pad + h, pad:pad + w, :c].copy_(v)
+        return ent.buf, ent
 
 
 def _stem_pack_input(x: torch.Tensor, pad: int, hp: int, wp: int, dt=torch.bfloat16) -> torch.Tensor:
@@ -787,7 +805,8 @@ def _stem_pack_weight(weight: torch.Tensor, dt=torch.bfloat16) -> torch.Tensor:
             wp = _STEM_WBUF[key] = torch.zeros((co, 8, 8, 4), dtype=dt, device=weight.device)
     if wp is None:
         wp = torch.zeros((co, 8, 8, 4), dtype=dt, device=weight.device)
-    wp[:, :r, :s, :c] = weight.permute(0, 2, 3, 1)
+    with torch.no_grad():  # a cached buffer must not carry an autograd edge to the weight
+        wp[:, :r, :s, :c] = weight.permute(0, 2, 3, 1)
     return wp
 
 
@@ -817,9 +836,10 @@ class _StemConvFn(torch.autograd.Function):
         ctx.save_for_backward(xp)
         ctx.geo = (nb, hp, wp, co, ho, wo, stride, tuple(weight.shape))
         ctx.pack = ent
-        if ent is not None and not ctx.needs_input_grad[1]:
-            ent[1] = False  # no backward will read it
-            del ent[3:]
+        if ent is not None:
+            ent.used(x.device)
+            if not ctx.needs_input_grad[1]:
+                ent.busy = False  # no backward will read it
         return y
 
     @staticmethod
@@ -840,15 +860,9 @@ class _StemConvFn(torch.autograd.Function):
             _, c, r, s = wshape
             dw = dwp[:, :r, :s, :c].permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
         if ctx.pack is not None:
-            # the wgrad reading the buffer is queued; a forward on the same stream is ordered
-            # after it, one on another stream waits on an event
-            ent = ctx.pack
-            fwd_stream = ent.pop() if len(ent) > 3 else None
-            if fwd_stream is not None and fwd_stream != _stream(xp):
-                ev = torch.cuda.Event()
-                ev.record(torch.cuda.current_stream(xp.device))
-                ent[2] = ev
-            ent[1] = False
+            # the wgrad reading the buffer is queued: the next refill is ordered after it
+            ctx.pack.used(xp.device)
+            ctx.pack.busy = False
         return None, dw, None, None, None, None
 
 

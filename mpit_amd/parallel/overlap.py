@@ -39,7 +39,7 @@ _PUSH_ON_SIDE = os.environ.get("MPIT_PUSH_ON_SIDE", "0") == "1"
 class ShardPusher:
     def __init__(self, flat, pclient):
         self.flat, self.pc = flat, pclient
-        ranges = [pclient.sinfo[s] for s in pclient.sranks]  # (offset, length) per shard
+        ranges = [(o, n) for (_, o, n) in pclient.entries]  # (offset, length) per pushed shard
         self.nshards = len(ranges)
         self.params = list(flat.params)
         self.spans = []  # shards each parameter overlaps

@@ -282,12 +282,23 @@ class PClient:
         self.ps_id = int(_conf_get(conf, "ps_id", 0))
         self.grad_dtype = _conf_get(conf, "grad_dtype", torch.float32)
         self.state = state or {}
-        self.sinfo = {s: r for s, r in zip(self.sranks, shard_ranges(self.plong, len(self.sranks)))}
+        # K > 1 splits every server's shard into K entries, each pushed / pulled as its own
+        # shard (bench.py --emulate-shards: the N=K shard traffic of one worker on one GPU)
+        self.shards_per_server = max(1, int(_conf_get(conf, "shards_per_server", 1)))
+        self._set_layout()
         self.native = None
         self.rx = self.tx = None
         self._user_p = self._user_g = None
         self._pull_pending = False
         self.on = False
+
+    def _set_layout(self):
+        self.sinfo = {s: r for s, r in zip(self.sranks, shard_ranges(self.plong, len(self.sranks)))}
+        self.entries = []  # (server rank, offset, length) per pushed / pulled shard
+        for s in self.sranks:
+            off, n = self.sinfo[s]
+            for o, m in shard_ranges(n, self.shards_per_server) if n >= self.shards_per_server else [(0, n)]:
+                self.entries.append((s, off + o, m))
 
     def _stream(self) -> int:
         if self.rx is not None and self.rx.is_cuda:
@@ -301,7 +312,7 @@ class PClient:
         if p.numel() != self.plong:
             if self.plong == 0:
                 self.plong = p.numel()
-                self.sinfo = {s: r for s, r in zip(self.sranks, shard_ranges(self.plong, len(self.sranks)))}
+                self._set_layout()
             else:
                 raise ValueError(f"param size {p.numel()} != plong {self.plong}")
         if g is None:
@@ -316,9 +327,8 @@ class PClient:
             _pending_servers.pop(self.ps_id)._launch(grp)
         self.rx, self.tx = grp.rx_t, grp.tx_t
         self._user_p, self._user_g = self.rx, self.tx
-        offs = [self.sinfo[s][0] for s in self.sranks]
-        lens = [self.sinfo[s][1] for s in self.sranks]
-        self.native = native().PSClient(_rt.engine(), self.ps_id, self.sranks, offs, lens)
+        self.native = native().PSClient(_rt.engine(), self.ps_id, [e[0] for e in self.entries],
+                                        [e[1] for e in self.entries], [e[2] for e in self.entries])
         self.native.start()
         self.on = True
         # the first client initialises every shard with its parameters
@@ -342,8 +352,9 @@ class PClient:
             self._pull_pending = True
 
     def async_send_grad_shard(self, k: int, pull: bool = False):
-        """Push shard ``k`` (index into ``sranks``) of the gradient buffer only, gated on
-        the work queued so far on the current stream (see parallel/overlap.py)."""
+        """Push shard ``k`` (index into ``entries``; one per server unless
+        ``shards_per_server`` > 1) of the gradient buffer only, gated on the work queued so
+        far on the current stream (see parallel/overlap.py)."""
         _trace.mark(f"ps_push_shard{k}")
         self.native.send_grad_to(self._stream(), int(k), bool(pull))
         if pull:

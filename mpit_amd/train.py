@@ -167,7 +167,8 @@ class Trainer:
         # pushed by Downpour stay fp32 (they are summed into the fp32 master shard)
         wire = torch.bfloat16 if (c.wire_dtype == "bf16" and c.optimizer in ("eamsgd", "easgd")) else torch.float32
         conf = dict(rank=self.rank, sranks=self.sranks, cranks=self.cranks, plong=self.plong, opt=rule,
-                    datapath=c.datapath, staleness=c.staleness, grad_dtype=wire, ps_id=int(c.extra.get("ps_id", 0)))
+                    datapath=c.datapath, staleness=c.staleness, grad_dtype=wire, ps_id=int(c.extra.get("ps_id", 0)),
+                    shards_per_server=int(c.extra.get("shards_per_server", 1)))
         if self.is_server:
             self.ps_server = PServer(conf)
             self.ps_server.start(block=False)
@@ -255,13 +256,15 @@ class Trainer:
     # ------------------------------------------------------------------ checkpoint / resume
     def save_checkpoint(self, directory: str) -> str:
         """Collective: every rank writes its part of the job's state at a quiescent point
-        (after a barrier every push of every worker has been applied and acked): workers
+        (every worker first retires its in-flight push — EAMSGD leaves one outstanding —
+        so after the barrier every push of every worker has been applied and acked): workers
         their flat parameters, model buffers, local optimizer state and RNG states;
         server ranks their shard, server optimizer state and rule counters
         (utils/checkpoint.py). The reference saves only worker models / the tester's
         parameters (asyncsgd/goot.lua:246-254, BiCNN/bicnn.lua:590-594)."""
         from .utils import checkpoint
 
+        self.retire_pushes()
         self.sync()
         self.barrier()
         for m in self.model.modules():
@@ -330,6 +333,7 @@ class Trainer:
         from .parallel.ps import shard_ranges
 
         W = COMM_WORLD()
+        self.retire_pushes()
         self.sync()
         self.barrier()
         if self.pc is not None:
@@ -360,6 +364,12 @@ class Trainer:
         return {"ok": not bad and len(srv) == len(self.sranks), "shards": len(self.sranks),
                 "workers": sum(v["worker"] is not None for v in allv), "mismatches": bad[:8]}
 
+    def retire_pushes(self):
+        """Wait until every push / pull this worker issued has been acknowledged (EAMSGD
+        deliberately leaves its last elastic push in flight, asyncsgd/optim-eamsgd.lua:65-67)."""
+        if self.pc is not None:
+            self.pc.wait()
+
     def run_server(self):
         """Block a dedicated server rank until all workers sent stop."""
         if self.ps_server is not None and not self.is_worker:
@@ -385,17 +395,21 @@ class Trainer:
         return float(out.item())
 
 
-def gc_settle():
+def gc_settle() -> bool:
     """After setup / warmup: collect once, then move every surviving object (model, optimizer
     and PS state, CUDA caches) to Python's permanent generation (``gc.freeze``) so the
     cyclic collector's periodic full passes no longer walk them in the middle of a step —
     a host stall of a few hundred us that the GPU sees as idle time at the step boundary.
+    Returns True when it froze; the caller unfreezes after its timed region (frozen
+    objects are never collected, and trainers hold reference cycles).
     MPIT_GC_FREEZE=0 leaves the collector alone."""
+    frozen = False
     if os.environ.get("MPIT_GC_FREEZE", "1") != "0":
         import gc
 
         gc.collect()
         gc.freeze()
+        frozen = True
     if os.environ.get("MPIT_THREAD_DUMP") == "1":  # diagnostics: Python threads at the timed region
         import threading
 
@@ -403,6 +417,7 @@ def gc_settle():
     sw = os.environ.get("MPIT_SWITCH_US")
     if sw:  # A/B knob: the interpreter's GIL switch interval (default 5000 us)
         sys.setswitchinterval(float(sw) * 1e-6)
+    return frozen
 
 
 def timed_steps(tr: Trainer, steps: int, warmup: int):
@@ -414,7 +429,7 @@ def timed_steps(tr: Trainer, steps: int, warmup: int):
             loss = tr.step()
     tr.sync()
     tr.barrier()
-    gc_settle()
+    frozen = gc_settle()
     t0 = time.perf_counter()
     if tr.is_worker:
         for _ in range(steps):
@@ -422,4 +437,8 @@ def timed_steps(tr: Trainer, steps: int, warmup: int):
     tr.sync()
     tr.barrier()
     dt = time.perf_counter() - t0
+    if frozen:
+        import gc
+
+        gc.unfreeze()
     return tr.max_over_ranks(dt), loss

@@ -16,9 +16,15 @@ steps = int(os.environ.get("T_STEPS", "6"))
 dp = int(os.environ.get("T_DATAPATH", "0"))
 mp.Init()
 nc = 10 if model in ("lenet", "cnn7") else 1000
+rule = None
+if os.environ.get("T_RULE"):
+    from mpit_amd.parallel.ps import ServerOpt
+
+    rule = ServerOpt(os.environ["T_RULE"], lr=1e-3, step_div=2)
 tr = Trainer(TrainConfig(model=model, batch=batch, num_classes=nc, optimizer=opt, topology=topo, lr=0.05,
                          mva=0.45, su=int(os.environ.get("T_SU", "1")), datapath=dp, servers=1,
-                         wire_dtype=os.environ.get("T_WIRE", "fp32")))
+                         wire_dtype=os.environ.get("T_WIRE", "fp32"), server_rule=rule,
+                         extra={"shards_per_server": int(os.environ.get("T_SPS", "1"))}))
 secs, loss = timed_steps(tr, steps, 2)
 # every push has been acked before the barrier inside timed_steps: one more pull gives
 # every worker the final server state — compare a checksum across ranks
@@ -26,6 +32,7 @@ if tr.pc is not None and opt == "downpour":
     tr.pc.async_recv_param()
     tr.pc.wait()
 cs = torch.tensor([float(tr.flat.flat.double().sum())], dtype=torch.float64)
+bits = int(tr.flat.flat.view(torch.int32).to(torch.int64).sum())
 allcs = torch.zeros(mp.get_size(), dtype=torch.float64)
 mp.COMM_WORLD().Allgather(cs, allcs)
 ls = torch.tensor([float(loss) if loss is not None else float("nan")], dtype=torch.float64)
@@ -35,5 +42,5 @@ stats = tr.ps_server.stats() if tr.ps_server is not None else {}
 tr.stop()
 if mp.get_rank() == 0:
     print(f"RESULT opt={opt} topo={topo} secs={secs:.4f} loss={float(loss) if loss is not None else -1:.4f} "
-          f"checksums={allcs.tolist()} losses={all_loss.tolist()} stats={stats}", flush=True)
+          f"checksums={allcs.tolist()} losses={all_loss.tolist()} stats={stats} bits={bits}", flush=True)
 mp.Finalize()

@@ -32,3 +32,10 @@ def test_resume_bitwise_colocated_cpu():
 def test_resume_bitwise_gpu_two_ranks_one_device():
     res = _res(run_ranks("ckpt_resume.py", 2, {"T_OPT": "downpour", "T_TOPO": "dedicated"}))
     assert res[0]["server_equal"] and res[1]["worker_equal"], res
+
+
+def test_eamsgd_in_flight_push_retired_three_ranks_cpu():
+    """verify_ps / save_checkpoint retire EAMSGD's outstanding push first."""
+    res = _res(run_ranks("eamsgd_verify.py", 3, {"MPIT_CPU_ONLY": "1"}))
+    for r in res:
+        assert all(r["oks"]) and r["final"], res

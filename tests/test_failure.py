@@ -19,3 +19,47 @@ def test_peer_crash_aborts_the_job():
     assert procs[1].returncode == 9
     assert procs[0].returncode == 70, outs[0]
     assert "peer rank 1" in outs[0] and "should not get here" not in outs[0]
+
+
+def _run_fault(env_extra, n=3, timeout=90):
+    import time
+
+    port = free_port()
+    procs = []
+    t0 = time.time()
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), MPIT_CPU_ONLY="1", PYTHONPATH=ROOT, **env_extra)
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp", "ps_fault.py")], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    outs = []
+    for p in procs:
+        try:
+            outs.append(p.communicate(timeout=timeout)[0])
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise AssertionError("a rank hung after a server fault")
+    return [p.returncode for p in procs], outs, time.time() - t0
+
+
+def test_server_fault_aborts_every_rank():
+    """A failing server handler (injected HIP-style error in the update) ends the whole
+    job: the failing rank exits 71 with the reason, every other rank exits 71 printing
+    the same reason, nobody prints past the training loop."""
+    rcs, outs, dt = _run_fault({"MPIT_PS_FAULT": "grad:3", "MPIT_PS_FAULT_RANK": "1"})
+    assert all(rc == 71 for rc in rcs), (rcs, outs)
+    assert "fatal: active-message handler" in outs[1] and "injected fault" in outs[1], outs[1]
+    for r in (0, 2):
+        assert "job aborted by rank 1 (code 71)" in outs[r] and "injected fault" in outs[r], outs[r]
+    assert not any("should not get here" in o for o in outs)
+
+
+def test_stuck_server_times_out():
+    """A server that silently stops answering (drops pushes) trips the clients' PS wait
+    deadline: the waiting rank raises with what is missing, the job ends non-zero."""
+    rcs, outs, dt = _run_fault({"MPIT_PS_FAULT": "drop:4", "MPIT_PS_FAULT_RANK": "0", "MPIT_PS_TIMEOUT_S": "3"})
+    assert all(rc != 0 for rc in rcs), (rcs, outs)
+    assert any("MPIT_PS_TIMEOUT_S" in o for o in outs), outs
+    assert not any("should not get here" in o for o in outs)
+    assert dt < 60, dt

@@ -18,6 +18,7 @@ class _FakeClient:
     def __init__(self, plong, nserv):
         self.sranks = list(range(nserv))
         self.sinfo = {s: r for s, r in zip(self.sranks, shard_ranges(plong, nserv))}
+        self.entries = [(s, *self.sinfo[s]) for s in self.sranks]
         self.tx = torch.full((plong,), float("nan"))
         self.pushed = []
 

@@ -64,3 +64,21 @@ def test_baseline_config1_lenet_easgd_dedicated_cpu():
     stats = eval(re.search(r"stats=(\{.*\})", r).group(1))
     assert stats, r  # rank 0 is the dedicated server
     assert stats["grads"] + stats.get("params", 0) >= 1, stats
+
+
+@pytest.mark.parametrize("rule", ["", "adam"])
+def test_split_shard_entries_bitwise_cpu(rule):
+    """A shard pushed / pulled as K pieces (bench.py --emulate-shards) gives the same
+    parameters, bit for bit, as the whole shard: the pieces apply the same rule to disjoint
+    ranges, and a server-side Adam advances its step counter once per push."""
+    bits = []
+    for k in (1, 3):
+        r = _result(run_ranks("ps_train.py", 1, {"MPIT_CPU_ONLY": "1", "T_SPS": str(k), "T_RULE": rule}))
+        bits.append(int(re.search(r"bits=(-?\d+)", r).group(1)))
+    assert bits[0] == bits[1], bits
+
+
+def test_split_shard_entries_two_ranks_cpu():
+    r = _result(run_ranks("ps_train.py", 2, {"MPIT_CPU_ONLY": "1", "T_SPS": "4"}))
+    cs = eval(re.search(r"checksums=(\[.*?\])", r).group(1))
+    assert max(cs) - min(cs) < 1e-6 * max(1.0, abs(cs[0])), cs

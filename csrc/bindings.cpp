@@ -60,6 +60,11 @@ PYBIND11_MODULE(_mpit, m) {
     dot(dev, S(stream), reinterpret_cast<const void*>(x), reinterpret_cast<const void*>(y), bf16, n,
         reinterpret_cast<float*>(out), reinterpret_cast<float*>(ws));
   });
+  m.def("clamp_scan", [](int dev, uintptr_t stream, uintptr_t G, uintptr_t g, uintptr_t p, int64_t P, int64_t ldg,
+                         int n, float l1, float l2, float c) {
+    clamp_scan(dev, S(stream), reinterpret_cast<float*>(G), reinterpret_cast<const float*>(g),
+               reinterpret_cast<const float*>(p), P, ldg, n, l1, l2, c);
+  });
   m.def("multi_copy", [](int dev, uintptr_t stream, uintptr_t table, int64_t nchunks, float scale) {
     multi_copy(dev, S(stream), reinterpret_cast<const CopyChunk*>(table), nchunks, scale);
   });

@@ -46,6 +46,12 @@ void norms(int dev, hipStream_t s, const void* x, bool bf16, int64_t n, float* o
 // out[0] = Σ x*y (fp32 accumulate), deterministic
 void dot(int dev, hipStream_t s, const void* x, const void* y, bool bf16, int64_t n, float* out, float* ws);
 
+// G[j] = clamp(G[j] + g[k][j] + l1*sign(p[j]) + l2*p[j], -c, c) for k = 0..n-1 in order
+// (c <= 0: no clamp): the reference's per-example regularise + clamp of the accumulated
+// gradient (BiCNN/bicnn.lua:398-409). g: n rows of stride ldg floats. fp32, dev < 0 = host.
+void clamp_scan(int dev, hipStream_t s, float* G, const float* g, const float* p, int64_t P, int64_t ldg, int n,
+                float l1, float l2, float c);
+
 // ---- multi-tensor pack / unpack with cast (multi_copy.hip) ------------------------
 struct CopyChunk {
   uint64_t src;    // byte address of the first element

@@ -6,7 +6,9 @@
 // result is bitwise reproducible — cdna_hip_programming.md Guideline 12).
 #include "kernels.h"
 #include "ew.h"
+#include <algorithm>
 #include <cmath>
+#include <stdexcept>
 
 namespace mpit {
 namespace {
@@ -129,7 +131,67 @@ int nblocks(int64_t n) {
 
 bool aligned(const void* p, bool bf) { return reinterpret_cast<uintptr_t>(p) % (bf ? 8 : 16) == 0; }
 
+// Clamped running sum over examples (K11 per example, BiCNN/bicnn.lua:398-409): every
+// violating example adds its gradient and the regulariser to the accumulated gradient,
+// which is then clamped — G = clamp(G + g_k + l1*sign(p) + l2*p, -c, c) for k = 0..n-1.
+// Sequential in k, independent in the element: one thread owns 4 consecutive elements
+// (float4 loads of every row g_k, coalesced across the wave), G stays in registers.
+__device__ __forceinline__ float clampc(float v, float c) { return c > 0.f ? fminf(fmaxf(v, -c), c) : v; }
+
+__global__ __launch_bounds__(kRB) void clamp_scan_kernel(float* __restrict__ G, const float* __restrict__ g,
+                                                          const float* __restrict__ p, int64_t P, int64_t ldg, int n,
+                                                          float l1, float l2, float c) {
+  const int64_t i4 = int64_t(blockIdx.x) * kRB + threadIdx.x;
+  const int64_t base = i4 * 4;
+  if (base >= P) return;
+  if (base + 4 <= P) {
+    float4 acc = *reinterpret_cast<const float4*>(G + base);
+    const float4 pv = *reinterpret_cast<const float4*>(p + base);
+    const float r[4] = {l1 * ((pv.x > 0.f) - (pv.x < 0.f)) + l2 * pv.x, l1 * ((pv.y > 0.f) - (pv.y < 0.f)) + l2 * pv.y,
+                        l1 * ((pv.z > 0.f) - (pv.z < 0.f)) + l2 * pv.z, l1 * ((pv.w > 0.f) - (pv.w < 0.f)) + l2 * pv.w};
+    for (int k = 0; k < n; ++k) {
+      const float4 v = *reinterpret_cast<const float4*>(g + int64_t(k) * ldg + base);
+      acc.x = clampc(acc.x + v.x + r[0], c);
+      acc.y = clampc(acc.y + v.y + r[1], c);
+      acc.z = clampc(acc.z + v.z + r[2], c);
+      acc.w = clampc(acc.w + v.w + r[3], c);
+    }
+    *reinterpret_cast<float4*>(G + base) = acc;
+  } else {
+    for (int64_t j = base; j < P; ++j) {
+      float a = G[j];
+      const float r = l1 * ((p[j] > 0.f) - (p[j] < 0.f)) + l2 * p[j];
+      for (int k = 0; k < n; ++k) a = clampc(a + g[int64_t(k) * ldg + j] + r, c);
+      G[j] = a;
+    }
+  }
+}
+
 }  // namespace
+
+void clamp_scan(int dev, hipStream_t s, float* G, const float* g, const float* p, int64_t P, int64_t ldg, int n,
+                float l1, float l2, float c) {
+  if (n <= 0 || P <= 0) return;
+  if (dev < 0) {
+    for (int64_t j = 0; j < P; ++j) {
+      float a = G[j];
+      const float r = l1 * float((p[j] > 0.f) - (p[j] < 0.f)) + l2 * p[j];
+      for (int k = 0; k < n; ++k) {
+        a = a + g[int64_t(k) * ldg + j] + r;
+        if (c > 0.f) a = std::min(std::max(a, -c), c);
+      }
+      G[j] = a;
+    }
+    return;
+  }
+  if (!aligned(G, false) || !aligned(g, false) || !aligned(p, false) || ldg % 4)
+    throw std::invalid_argument("mpit.clamp_scan: fp32 operands must be 16-B aligned, ldg % 4 == 0");
+  hip_check(hipSetDevice(dev), "hipSetDevice");
+  const int64_t threads = (P + 3) / 4;
+  hipLaunchKernelGGL(clamp_scan_kernel, dim3(unsigned((threads + kRB - 1) / kRB)), dim3(kRB), 0, s, G, g, p, P, ldg, n,
+                     l1, l2, c);
+  hip_check(hipGetLastError(), "clamp_scan launch");
+}
 
 void norms(int dev, hipStream_t s, const void* x, bool bf16, int64_t n, float* out, float* ws) {
   if (dev < 0) {

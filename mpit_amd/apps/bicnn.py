@@ -45,7 +45,7 @@ import mpit_amd as mp
 from mpit_amd import ops
 from mpit_amd.apps.qa_data import load_binary, load_files, pad_batch, save_binary, synthetic_qa
 from mpit_amd.launch import master_freq
-from mpit_amd.models.bicnn import (BiCNN, draw_negatives, first_violations, gesd, margin_ranking_loss,
+from mpit_amd.models.bicnn import (BiCNN, draw_negatives, first_violations, gesd, margin_ranking_loss, parity_grad_,
                                    parity_loss)
 from mpit_amd.optim import ALL as OPTIMS
 from mpit_amd.parallel.ps import PClient, PServer, ServerOpt
@@ -94,6 +94,9 @@ def build_args(argv=None):
     f("L1reg", type=float, default=0.0)
     f("L2reg", type=float, default=1e-4)
     f("gradClip", type=float, default=0.5)
+    # parity (default): regularise + clamp the accumulated gradient after every violating
+    # example, as the reference does (bicnn.lua:398-409); batch: once per mini-batch
+    f("clipMode", default="parity", choices=["parity", "batch"])
     f("weightDecay", type=float, default=1e-6)
     # optimisation (plaunch.lua:11-38)
     f("optimization", default="downpour")
@@ -380,6 +383,10 @@ def train(a, rank, model, flat, plong, data, dev, pc, log, ev, cranks):
                             return torch.zeros((), device=dev), flat.grad  # every example skipped
                         idx = torch.tensor(sel, device=dev)
                         an1 = pad_batch([data.answers[chosen[i]] for i in sel]).to(dev)
+                        if a.clipMode == "parity" and (a.L1reg or a.L2reg or a.gradClip > 0):
+                            loss = parity_grad_(model, flat, q[idx], ap_[idx], an1, a.margin, a.L1reg, a.L2reg,
+                                                a.gradClip)
+                            return loss.detach(), flat.grad
                         loss = parity_loss(model, q[idx], ap_[idx], an1, a.margin)
                     loss.backward()
                     if a.L1reg or a.L2reg or a.gradClip:

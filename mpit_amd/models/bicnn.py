@@ -169,6 +169,55 @@ def parity_loss(model: "BiCNN", q, a_pos, a_neg, margin: float):
     return F.relu(margin - sp + sn[:, 0]).sum()
 
 
+def per_example_grads(model: "BiCNN", flat, q, a_pos, a_neg, margin: float) -> torch.Tensor:
+    """[n, flat.numel] fp32: row k = the gradient of example k's margin loss alone, laid out
+    like the flat parameter vector (``flat``: utils/flat.py FlatParams of ``model``). One
+    batched backward (torch.func.vmap over per-example grads) instead of the reference's
+    one backward per example."""
+    from torch.func import functional_call, grad, vmap
+
+    names = [n for n, _ in model.named_parameters()]
+    params = {n: p.detach() for n, p in model.named_parameters()}
+
+    def one(pr, qi, api, ani):
+        sp, sn = functional_call(model, pr, (qi[None], api[None], ani[None, None]))
+        return F.relu(margin - sp + sn[:, 0]).sum()
+
+    gd = vmap(grad(one), in_dims=(None, 0, 0, 0))(params, q, a_pos, a_neg)
+    n = q.shape[0]
+    out = torch.zeros((n, flat.numel), dtype=torch.float32, device=q.device)
+    for name, p, off in zip(names, flat.params, flat.offsets):
+        g = gd[name]
+        if flat.channels_last and p.dim() == 4:
+            g = g.permute(0, 1, 3, 4, 2)  # [n, o, h, w, i]: the flat buffer's NHWC order
+        out[:, off: off + p.numel()] = g.reshape(n, -1)
+    return out
+
+
+def parity_grad_(model: "BiCNN", flat, q, a_pos, a_neg, margin: float, l1: float, l2: float, clip: float,
+                 chunk: int = 16) -> torch.Tensor:
+    """The reference's per-example gradient rule for the violating examples (in order):
+    ``G += g_k; G += l1*sign(p) + l2*p; G = clamp(G, -clip, clip)`` after EVERY example
+    (BiCNN/bicnn.lua:376-409; ``clip <= 0`` = no clamp). Writes G into ``flat.grad`` and
+    returns the summed loss ``Σ_k (err_k + l1*|p|_1 + l2*|p|^2/2)`` (``f`` of the feval).
+    Per-example gradients come ``chunk`` examples at a time (:func:`per_example_grads`);
+    the regularise + clamp chain runs as ONE fused pass per chunk (ops.clamp_scan_)."""
+    from .. import ops
+
+    G = flat.grad
+    G.zero_()
+    n = q.shape[0]
+    for s in range(0, n, chunk):
+        g = per_example_grads(model, flat, q[s:s + chunk], a_pos[s:s + chunk], a_neg[s:s + chunk], margin)
+        ops.clamp_scan_(G, g, flat.flat[: flat.numel], l1, l2, clip)
+    with torch.no_grad():
+        loss = parity_loss(model, q, a_pos, a_neg, margin)
+        if l1 or l2:
+            nm = ops.norms(flat.flat[: flat.numel])
+            loss = loss + n * (l1 * nm[0] + 0.5 * l2 * nm[1])
+    return loss
+
+
 @register("bicnn")
 def bicnn(num_classes=None, **kw):
     return BiCNN(**kw)

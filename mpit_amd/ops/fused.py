@@ -169,6 +169,28 @@ def regclip_(g, p, gscale=1.0, l1=0.0, l2=0.0, clip=0.0):
     return g
 
 
+def clamp_scan_(G: torch.Tensor, g: torch.Tensor, p: torch.Tensor, l1: float = 0.0, l2: float = 0.0,
+                clip: float = 0.0) -> torch.Tensor:
+    """K11 per example (BiCNN/bicnn.lua:398-409): for each row ``g[k]`` in order,
+    ``G = clamp(G + g[k] + l1*sign(p) + l2*p, -clip, clip)`` (``clip <= 0``: no clamp) — the
+    reference regularises and clamps the ACCUMULATED gradient after every violating example.
+    G, p: [P] fp32; g: [n, ldg >= P] fp32 rows. One pass over g (HIP on the GPU)."""
+    if G.dtype != torch.float32 or g.dtype != torch.float32 or p.dtype != torch.float32:
+        raise TypeError("clamp_scan_ takes fp32 tensors")
+    if g.dim() != 2 or g.stride(1) != 1 or not G.is_contiguous() or not p.is_contiguous():
+        raise ValueError("clamp_scan_: G, p contiguous [P]; g [n, ldg] with unit column stride")
+    P = G.numel()
+    if p.numel() != P or g.shape[1] < P or g.device != G.device or p.device != G.device:
+        raise ValueError("clamp_scan_: shape / device mismatch")
+    if g.shape[0] == 0:
+        return G
+    dev = G.device.index if G.is_cuda else -1
+    stream = torch.cuda.current_stream(G.device).cuda_stream if G.is_cuda else 0
+    native().clamp_scan(dev, stream, G.data_ptr(), g.data_ptr(), p.data_ptr(), P, g.stride(0), g.shape[0],
+                        float(l1), float(l2), float(clip))
+    return G
+
+
 def scale_(x, a):
     """K14: ``x *= a`` (asyncsgd/goot.lua:213)."""
     _launch(_R().SCALE, 0, [x], [a], bf_ok=(0,))

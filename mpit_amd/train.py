@@ -72,6 +72,26 @@ class Trainer:
             # the classifier's GEMMs (the only library GEMMs left) on rocBLAS instead of
             # hipBLASLt (A/B knob: host-side cost per call, GPU bubble around the fc layer)
             torch.backends.cuda.preferred_blas_library("cublas")
+        # The step's critical path (forward, input gradients, BN, pushes) runs on a
+        # high-priority stream; the backward-weight GEMMs of the side stream (lowest priority)
+        # then only take the CUs the critical path leaves free, instead of delaying its small
+        # kernels (BN finalize, apply) behind big split-K GEMMs. MPIT_HP_STREAM=0: off.
+        self.hp_stream = None
+        if self.on_gpu and os.environ.get("MPIT_HP_STREAM", "1") != "0" and not st.shared_devices:
+            lo, hi = torch.cuda.Stream.priority_range()
+            self.hp_stream = torch.cuda.Stream(self.device, priority=min(lo, hi))
+        # MPIT_HP_INIT=1: build everything (model, flat buffers, PS, hooks) on the stream the
+        # steps run on (AccumulateGrad stream diagnostic, benchmarks/diag_accgrad.py)
+        if self.hp_stream is not None and os.environ.get("MPIT_HP_INIT", "0") == "1":
+            cur = torch.cuda.current_stream(self.device)
+            self.hp_stream.wait_stream(cur)
+            with torch.cuda.stream(self.hp_stream):
+                self._build(cfg, st)
+            cur.wait_stream(self.hp_stream)
+        else:
+            self._build(cfg, st)
+
+    def _build(self, cfg, st):
         # identical initial weights on every rank (per-rank seeds for data only)
         torch.manual_seed(cfg.seed)
         model = get_model(cfg.model, num_classes=cfg.num_classes)
@@ -111,14 +131,6 @@ class Trainer:
             # time-slice the card (4 ranks: 8136 -> 1809 img/s)
             WgradStream.enable(self.on_gpu and (not st.shared_devices or WgradStream.forced())
                                and cfg.extra.get("wgrad_stream", True))
-        # The step's critical path (forward, input gradients, BN, pushes) runs on a
-        # high-priority stream; the backward-weight GEMMs of the side stream (lowest priority)
-        # then only take the CUs the critical path leaves free, instead of delaying its small
-        # kernels (BN finalize, apply) behind big split-K GEMMs. MPIT_HP_STREAM=0: off.
-        self.hp_stream = None
-        if self.on_gpu and os.environ.get("MPIT_HP_STREAM", "1") != "0" and not st.shared_devices:
-            lo, hi = torch.cuda.Stream.priority_range()
-            self.hp_stream = torch.cuda.Stream(self.device, priority=min(lo, hi))
         if self.push_steal:
             # push each shard during the backward as soon as its gradients are complete
             if cfg.extra.get("overlap_push", True):

@@ -151,3 +151,79 @@ def test_load_files_reference_format(tmp_path):
     assert d.valid[0][0] == [0] and d.valid[0][2] == [0, 1, 2]
     assert len(d.tests) == 1 and d.tests[0][0][2] == [1, 2]
     assert len(d.word2idx) == d.embedding_matrix().shape[0]
+
+
+def _seq_parity_grad(model, flat, q, ap, an, margin, l1, l2, clip):
+    """The reference's feval loop, literally (BiCNN/bicnn.lua:376-409): per violating
+    example one backward into the running gradient, then the regulariser, then the clamp."""
+    import torch.nn.functional as F
+
+    params = list(model.parameters())
+    G = torch.zeros(flat.numel)
+    p = flat.flat[: flat.numel].detach()
+    for k in range(q.shape[0]):
+        sp, sn = model(q[k:k + 1], ap[k:k + 1], an[k:k + 1, None])
+        gs = torch.autograd.grad(F.relu(margin - sp + sn[:, 0]).sum(), params)
+        for g, off in zip(gs, flat.offsets):
+            G[off: off + g.numel()] += g.reshape(-1)
+        G += l1 * torch.sign(p) + l2 * p
+        G.clamp_(-clip, clip)
+    return G
+
+
+@pytest.mark.parametrize("l1,l2,clip", [(0.0, 1e-4, 0.5), (1e-3, 1e-4, 0.02), (0.0, 0.0, 0.005)])
+def test_bicnn_parity_clamp_matches_sequential_loop(l1, l2, clip):
+    """-clipMode parity: the accumulated gradient is regularised and clamped after every
+    violating example (once per batch gave +0.2 where the reference gives -0.1)."""
+    from mpit_amd.models.bicnn import BiCNN, parity_grad_
+    from mpit_amd.utils.flat import FlatParams
+
+    torch.manual_seed(0)
+    model = BiCNN(vocab=60, emb_dim=8, hidden=12, filters=16, conv_width=2)
+    flat = FlatParams(model)
+    n, t = 7, 9
+    q = torch.randint(1, 60, (n, t))
+    ap = torch.randint(1, 60, (n, t))
+    an = torch.randint(1, 60, (n, t))
+    q[:, 7:] = 0  # padding
+    an[2, 5:] = 0
+    margin = 5.0  # every example violates
+    loss = parity_grad_(model, flat, q, ap, an, margin, l1, l2, clip, chunk=3)
+    ref = _seq_parity_grad(model, flat, q, ap, an, margin, l1, l2, clip)
+    got = flat.grad[: flat.numel]
+    assert torch.allclose(got, ref, atol=2e-6, rtol=1e-5), (got - ref).abs().max()
+    if clip < 0.1:
+        assert (ref.abs() >= clip * 0.999).any()  # the clamp was active
+    assert torch.isfinite(loss)
+
+
+def test_bicnn_parity_differs_from_batch_clamp():
+    """The example of VERDICT r02: +0.8 then -0.6 with clip 0.5 — parity gives -0.1."""
+    from mpit_amd import ops
+
+    G = torch.zeros(4)
+    g = torch.tensor([[0.8] * 4, [-0.6] * 4])
+    ops.clamp_scan_(G, g, torch.zeros(4), 0.0, 0.0, 0.5)
+    assert torch.allclose(G, torch.full((4,), -0.1))
+
+
+@pytest.mark.gpu
+def test_bicnn_parity_clamp_gpu_matches_cpu_loop():
+    """The parity rule on the GPU (vmap per-example grads + the HIP clamp_scan kernel)
+    against the literal sequential loop on the CPU (fp32)."""
+    import copy
+
+    from mpit_amd.models.bicnn import BiCNN, parity_grad_
+    from mpit_amd.utils.flat import FlatParams
+
+    torch.manual_seed(1)
+    base = BiCNN(vocab=80, emb_dim=16, hidden=24, filters=64, conv_width=2)
+    cpu_m, gpu_m = copy.deepcopy(base), copy.deepcopy(base).cuda()
+    fc, fg = FlatParams(cpu_m), FlatParams(gpu_m)
+    n, t = 10, 12
+    q, ap, an = (torch.randint(1, 80, (n, t)) for _ in range(3))
+    q[:, 9:] = 0
+    parity_grad_(gpu_m, fg, q.cuda(), ap.cuda(), an.cuda(), 5.0, 1e-3, 1e-4, 0.01, chunk=4)
+    ref = _seq_parity_grad(cpu_m, fc, q, ap, an, 5.0, 1e-3, 1e-4, 0.01)
+    got = fg.grad[: fg.numel].cpu()
+    assert torch.allclose(got, ref, atol=1e-5, rtol=1e-4), (got - ref).abs().max()

@@ -272,3 +272,24 @@ def test_pack_unpack(d):
     plan2.unpack(scale=2.0)
     for t, b in zip(ts, bts):
         close(b, t.to(torch.bfloat16), 1e-2)
+
+
+@pytest.mark.parametrize("d", DEVICES)
+@pytest.mark.parametrize("n", SIZES)
+def test_clamp_scan(d, n):
+    """K11 per example: G = clamp(G + g_k + l1 sign(p) + l2 p, -c, c) for k in order, vs a
+    plain PyTorch fp32 loop (HIP kernel on the GPU, host twin on the CPU)."""
+    dev = _dev(d)
+    rows, ldg = 5, n + (-n % 4) + 8
+    g = torch.zeros(rows, ldg)
+    for k in range(rows):
+        g[k, :n] = rnd(n + k, "cpu", -0.4, 0.4)[:n]
+    p = rnd(n + 11, "cpu")[:n].contiguous()
+    G0 = rnd(n + 13, "cpu", -0.3, 0.3)[:n].contiguous()
+    l1, l2, c = 1e-3, 1e-2, 0.25
+    ref = G0.clone()
+    for k in range(rows):
+        ref = (ref + g[k, :n] + l1 * torch.sign(p) + l2 * p).clamp(-c, c)
+    G = G0.to(dev)
+    ops.clamp_scan_(G, g.to(dev), p.to(dev), l1, l2, c)
+    close(G, ref)

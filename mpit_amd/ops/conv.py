@@ -681,7 +681,11 @@ class WeightCastPlan:
             if not w.is_cuda or w.dtype != torch.float32 or not w.is_contiguous(memory_format=torch.channels_last):
                 continue
             co, c, r, sw = w.shape
-            wb = _as_rsc(w) if f32 else torch.empty((co, r, sw, c), dtype=torch.bfloat16, device=w.device)
+            # a detached view: the plan outlives every step, and a view WITH autograd history
+            # would keep the weight's AccumulateGrad node (made at build time, on the stream
+            # current then) alive into every step — autograd then warns that the node's stream
+            # differs from the step's and inserts a cross-stream wait per weight
+            wb = _as_rsc(w.detach()) if f32 else torch.empty((co, r, sw, c), dtype=torch.bfloat16, device=w.device)
             if kind == 0:
                 wt = torch.empty((c, r, sw, co), dtype=self.dtype, device=w.device)
             elif kind == 1:

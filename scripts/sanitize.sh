@@ -1,7 +1,7 @@
 #!/bin/bash
 # Host sanitizer runs of the native runtime (csrc/core + the host side of csrc/kernels) on the
 # CPU: the multi-process API suite, parameter-server training (co-located, dedicated,
-# EASGD, SSP) under ASan and under TSan. Reports land in profiles/sanitizer_<kind>_r02.log.
+# EASGD, SSP) under ASan and under TSan. Reports land in profiles/sanitizer_<kind>_r03.log.
 #   bash scripts/sanitize.sh [address|thread ...]
 set -o pipefail
 cd "$(dirname "$0")/.." || exit 1
@@ -16,7 +16,7 @@ for k in $kinds; do
   export MPIT_CPU_ONLY=1 MPIT_NATIVE_SO=$so PYTHONPATH=$ROOT
   export ASAN_OPTIONS="detect_leaks=0:log_path=$logd/asan:abort_on_error=0"
   export TSAN_OPTIONS="suppressions=$ROOT/scripts/tsan.supp:log_path=$logd/tsan:halt_on_error=0:report_signal_unsafe=0:second_deadlock_stack=1"
-  out=$ROOT/profiles/sanitizer_${k}_r02.log
+  out=$ROOT/profiles/sanitizer_${k}_r03.log
   echo "# $k sanitizer run $(date -u +%FT%TZ), module $so" > $out
   run() {  # name nranks script [env...]
     local name=$1 n=$2 script=$3; shift 3
@@ -33,6 +33,7 @@ for k in $kinds; do
   run ps_eamsgd2 2 ps_train.py T_OPT=eamsgd
   run ps_su2 2 ps_train.py T_SU=2
   run ssp3 3 ssp_check.py
+  run ps_split2 2 ps_train.py T_SPS=3
   nrep=$(cat $logd/asan.* $logd/tsan.* 2>/dev/null | grep -cE "ERROR: AddressSanitizer|WARNING: ThreadSanitizer")
   echo "reports: $nrep" >> $out
   for f in $logd/asan.* $logd/tsan.*; do

@@ -19,7 +19,7 @@ if r == 0:
     s.start(block=True)
     st = s.stats()
     assert st["deferred"] >= 1, st
-    print("SSP_OK", st, flush=True)
+    print("RESULT SSP_OK", st, flush=True)
 else:
     pc = PClient(conf).start(torch.zeros(64), torch.ones(64))
     W_sub = None

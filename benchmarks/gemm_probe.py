@@ -35,7 +35,21 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
     args = sys.argv[1:]
     f32 = "--f32" in args
-    args = [a for a in args if a != "--f32"]
+    bsplit = "--bsplit" in args  # fp32: weight operand as three pre-split bf16 planes (FM 4)
+    args = [a for a in args if a not in ("--f32", "--bsplit")]
+
+    def planes(t):
+        t = t.float()
+        h = t.to(torch.bfloat16)
+        r = t - h.float()
+        m_ = r.to(torch.bfloat16)
+        return torch.stack([h, m_, (r - m_.float()).to(torch.bfloat16)]).contiguous()
+
+    def bp(t):  # (operand, bps) of a weight operand
+        if f32 and bsplit:
+            p = planes(t)
+            return p, p[0].numel()
+        return t, 0
     dt = torch.float32 if f32 else torch.bfloat16
     es = 4 if f32 else 2
     kind = args[0]
@@ -44,10 +58,10 @@ def main():
         it = int(args[4]) if len(args) > 4 else 50
         if kind == "nt":
             a = torch.randn(M, K, device="cuda").to(dt)
-            b = (torch.randn(N, K, device="cuda") * 0.05).to(dt)
+            b, bps = bp((torch.randn(N, K, device="cuda") * 0.05).to(dt))
             c = torch.empty(M, N, device="cuda", dtype=dt)
             ms = timeit(lambda: m.gemm_nt(0, st, M, N, K, a.data_ptr(), K, b.data_ptr(), K, c.data_ptr(), N, 0,
-                                          f32=f32), it)
+                                          f32=f32, bps=bps), it)
             by = es * (M * K + N * K + M * N)
         else:
             y = torch.randn(M, N, device="cuda").to(dt)
@@ -65,16 +79,16 @@ def main():
         pad = R // 2
         Ho, Wo = (H + 2 * pad - R) // S + 1, (W + 2 * pad - R) // S + 1
         x = torch.randn(Nb, H, W, C, device="cuda").to(dt)
-        w = (torch.randn(Co, R, R, C, device="cuda") * 0.05).to(dt)
+        w, wbps = bp((torch.randn(Co, R, R, C, device="cuda") * 0.05).to(dt))
         y = torch.randn(Nb, Ho, Wo, Co, device="cuda").to(dt)
         if kind == "conv":
             ms = timeit(lambda: m.conv_fwd(0, st, Nb, H, W, C, Co, R, R, S, pad, x.data_ptr(), w.data_ptr(),
-                                           y.data_ptr(), f32=f32), it)
+                                           y.data_ptr(), f32=f32, bps=wbps), it)
         elif kind == "dgrad":  # stride-1 backward-data = forward conv of dy with the transposed weight
-            wt = (torch.randn(C, R, R, Co, device="cuda") * 0.05).to(dt)
+            wt, tbps = bp((torch.randn(C, R, R, Co, device="cuda") * 0.05).to(dt))
             dx = torch.empty_like(x)
             ms = timeit(lambda: m.conv_fwd(0, st, Nb, Ho, Wo, Co, C, R, R, 1, R - 1 - pad, y.data_ptr(),
-                                           wt.data_ptr(), dx.data_ptr(), f32=f32), it)
+                                           wt.data_ptr(), dx.data_ptr(), f32=f32, bps=tbps), it)
         else:
             dw = torch.empty(Co, R, R, C, device="cuda")
             nws = m.conv_wgrad_ws_floats(0, Nb, H, W, C, Co, R, R, S, pad)
@@ -82,7 +96,7 @@ def main():
             ms = timeit(lambda: m.conv_wgrad(0, st, Nb, H, W, C, Co, R, R, S, pad, y.data_ptr(), x.data_ptr(),
                                              dw.data_ptr(), ws.data_ptr(), 0.0, f32=f32), it)
         fl = 2.0 * Nb * Ho * Wo * Co * R * R * C
-        by = es * (x.numel() + w.numel() + y.numel())
+        by = es * (x.numel() + (w[0].numel() if wbps else w.numel()) + y.numel())
     print(json.dumps({"args": sys.argv[1:], "ms": round(ms, 4), "tflops": round(fl / ms / 1e9, 1),
                       "hbm_tbs": round(by / ms / 1e9, 2)}), flush=True)
 

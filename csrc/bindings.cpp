@@ -123,18 +123,19 @@ PYBIND11_MODULE(_mpit, m) {
          int64_t ldc, uintptr_t stats, uintptr_t cin, uintptr_t cmask, uintptr_t red_part, uintptr_t red_x,
          uintptr_t red_mask, uintptr_t red_mean, int64_t red_row0, uintptr_t red_part2, uintptr_t red_x2,
          uintptr_t red_mean2, bool f32, uintptr_t fold_coef, uintptr_t fold_gamma, uintptr_t fold_rstd,
-         uintptr_t fold_dgamma, uintptr_t fold_dbeta, uintptr_t fold_lvl) {
+         uintptr_t fold_dgamma, uintptr_t fold_dbeta, uintptr_t fold_lvl, int64_t bps) {
         BnRed r{red_part, red_x, red_mask, red_mean, red_row0, red_part2, red_x2, red_mean2};
         r.fcoef = fold_coef; r.fgamma = fold_gamma; r.frstd = fold_rstd;
         r.fdgamma = fold_dgamma; r.fdbeta = fold_dbeta; r.flvl = fold_lvl;
-        gemm_nt(dev, S(s), M, N, K, A, lda, B, ldb, C, ldc, stats, cin, cmask, &r, f32);
+        gemm_nt(dev, S(s), M, N, K, A, lda, B, ldb, C, ldc, stats, cin, cmask, &r, f32, bps);
       },
       py::arg("dev"), py::arg("stream"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("A"), py::arg("lda"),
       py::arg("B"), py::arg("ldb"), py::arg("C"), py::arg("ldc"), py::arg("stats") = 0, py::arg("cin") = 0,
       py::arg("cmask") = 0, py::arg("red_part") = 0, py::arg("red_x") = 0, py::arg("red_mask") = 0,
       py::arg("red_mean") = 0, py::arg("red_row0") = 0, py::arg("red_part2") = 0, py::arg("red_x2") = 0,
       py::arg("red_mean2") = 0, py::arg("f32") = false, py::arg("fold_coef") = 0, py::arg("fold_gamma") = 0,
-      py::arg("fold_rstd") = 0, py::arg("fold_dgamma") = 0, py::arg("fold_dbeta") = 0, py::arg("fold_lvl") = 0);
+      py::arg("fold_rstd") = 0, py::arg("fold_dgamma") = 0, py::arg("fold_dbeta") = 0, py::arg("fold_lvl") = 0,
+      py::arg("bps") = 0);
   m.def("gemm_nt_fold_lvl_floats", &gemm_nt_fold_lvl_floats);
   m.def("gemm_tn_supported", &gemm_tn_supported);
   m.def("gemm_tn_ws_floats", &gemm_tn_ws_floats);
@@ -179,11 +180,11 @@ PYBIND11_MODULE(_mpit, m) {
          uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t cin, uintptr_t bias, bool relu, uintptr_t red_part,
          uintptr_t red_x, uintptr_t red_mask, uintptr_t red_mean, int64_t red_row0, uintptr_t red_part2,
          uintptr_t red_x2, uintptr_t red_mean2, bool f32, uintptr_t fold_coef, uintptr_t fold_gamma,
-         uintptr_t fold_rstd, uintptr_t fold_dgamma, uintptr_t fold_dbeta, uintptr_t fold_lvl) {
+         uintptr_t fold_rstd, uintptr_t fold_dgamma, uintptr_t fold_dbeta, uintptr_t fold_lvl, int64_t bps) {
         BnRed r{red_part, red_x, red_mask, red_mean, red_row0, red_part2, red_x2, red_mean2};
         r.fcoef = fold_coef; r.fgamma = fold_gamma; r.frstd = fold_rstd;
         r.fdgamma = fold_dgamma; r.fdbeta = fold_dbeta; r.flvl = fold_lvl;
-        conv_fwd(dev, S(s), Nb, H, W, C, Co, R, S_, stride, pad, x, w, y, stats, cin, bias, relu, &r, f32);
+        conv_fwd(dev, S(s), Nb, H, W, C, Co, R, S_, stride, pad, x, w, y, stats, cin, bias, relu, &r, f32, bps);
       },
       py::arg("dev"), py::arg("stream"), py::arg("Nb"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("Co"),
       py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("x"), py::arg("w"), py::arg("y"),
@@ -191,7 +192,7 @@ PYBIND11_MODULE(_mpit, m) {
       py::arg("red_x") = 0, py::arg("red_mask") = 0, py::arg("red_mean") = 0, py::arg("red_row0") = 0,
       py::arg("red_part2") = 0, py::arg("red_x2") = 0, py::arg("red_mean2") = 0, py::arg("f32") = false,
       py::arg("fold_coef") = 0, py::arg("fold_gamma") = 0, py::arg("fold_rstd") = 0, py::arg("fold_dgamma") = 0,
-      py::arg("fold_dbeta") = 0, py::arg("fold_lvl") = 0);
+      py::arg("fold_dbeta") = 0, py::arg("fold_lvl") = 0, py::arg("bps") = 0);
   m.def("conv_dgrad_strided_wfloats", &conv_dgrad_strided_wfloats);
   m.def(
       "conv_dgrad_strided_weights",
@@ -204,14 +205,15 @@ PYBIND11_MODULE(_mpit, m) {
       "conv_dgrad_strided",
       [](int dev, uintptr_t s, int Nb, int H, int W, int C, int Co, int R, int S_, int stride, int pad, uintptr_t dy,
          uintptr_t wcls, uintptr_t dx, uintptr_t red_part, uintptr_t red_x, uintptr_t red_mask, uintptr_t red_mean,
-         uintptr_t red_part2, uintptr_t red_x2, uintptr_t red_mean2, bool f32) {
+         uintptr_t red_part2, uintptr_t red_x2, uintptr_t red_mean2, bool f32, int64_t bps) {
         const BnRed r{red_part, red_x, red_mask, red_mean, 0, red_part2, red_x2, red_mean2};
-        conv_dgrad_strided(dev, S(s), Nb, H, W, C, Co, R, S_, stride, pad, dy, wcls, dx, &r, f32);
+        conv_dgrad_strided(dev, S(s), Nb, H, W, C, Co, R, S_, stride, pad, dy, wcls, dx, &r, f32, bps);
       },
       py::arg("dev"), py::arg("stream"), py::arg("Nb"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("Co"),
       py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("dy"), py::arg("wcls"), py::arg("dx"),
       py::arg("red_part") = 0, py::arg("red_x") = 0, py::arg("red_mask") = 0, py::arg("red_mean") = 0,
-      py::arg("red_part2") = 0, py::arg("red_x2") = 0, py::arg("red_mean2") = 0, py::arg("f32") = false);
+      py::arg("red_part2") = 0, py::arg("red_x2") = 0, py::arg("red_mean2") = 0, py::arg("f32") = false,
+      py::arg("bps") = 0);
   m.def("relu_bias_bwd_ws_floats", &relu_bias_bwd_ws_floats);
   m.def(
       "relu_bias_bwd",

@@ -243,7 +243,7 @@ __device__ __forceinline__ int swzk(int row, int chunk) {
 // fp32 bf16x6 with FM = 3 stages 32-deep k-tiles (128-B rows of 32 floats: two k16 MFMA steps
 // per barrier) instead of FM = 1's 16-deep ones.
 __host__ __device__ constexpr int nt_bkb(int BM, int BN, int FM = 0) {
-  return (BM == 256 && BN == 256) || FM == 3 ? 128 : 64;
+  return (BM == 256 && BN == 256) || FM == 3 || FM == 4 || FM >= 5 ? 128 : 64;
 }
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -406,19 +406,31 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
                                                          T* C, int64_t ldc, int64_t M, int N, int K,
                                                          int ntn, EpiArgs ep, const T* Cin,
                                                          const uint8_t* __restrict__ Cmask,
-                                                         const float* __restrict__ bias, int relu, ConvGeo geo) {
+                                                         const float* __restrict__ bias, int relu, ConvGeo geo,
+                                                         int64_t bps) {
   constexpr int NW = 4, NT = NW * 64;  // waves, threads
-  constexpr int WM = BM / 2, WN = BN / 2;
+  // wave grid over the tile: 2 x 2 (each wave 64 x 64 of a 128 x 128 tile), or for FM 9
+  // (pre-split B) 4 x 1: each wave owns 32 rows x all 128 columns, so every A row is split in
+  // registers by exactly one wave (the ready-made B planes are the shared operand)
+  constexpr int WGM = (sizeof(T) == 4 && FM == 9) ? 4 : 2, WGN = NW / WGM;
+  constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 32, TN = WN / 32;
   constexpr int EPC = epc<T>();                          // elements per 16-B chunk
   constexpr int BKB = nt_bkb(BM, BN, FM), BK = BKB / int(sizeof(T));
   constexpr int CPK = BKB / 16, RPI = 64 / CPK;          // 16-B chunks per row, rows per glds
   constexpr int IA = BM / RPI / NW, IB = BN / RPI / NW;  // glds instructions per wave per tile
-  constexpr int NI = IA + IB;
-  constexpr int TILE = (BM + BN) * BK;  // elements per stage
   constexpr bool F32 = sizeof(T) == 4;
+  // FM 4 (fp32, B pre-split): B arrives as three bf16 planes (h, m, l; plane stride bps
+  // elements, made once per step by the weight plan), staged as three 64-B-row images of
+  // 32 bf16 per row — the A operand alone is split in registers
+  constexpr bool BSPLIT = F32 && (FM == 4 || FM == 9);
+  constexpr int IBP = BSPLIT ? BN / 16 / NW : 0;  // glds per wave per B plane (16 rows x 64 B)
+  constexpr int NI = BSPLIT ? IA + 3 * IBP : IA + IB;
+  // elements (T) per stage: A rows, then B (fp32 rows, or 3 bf16 plane images = 1.5x the bytes)
+  constexpr int BTILE = BSPLIT ? 3 * BN * 32 / 2 : BN * BK;
+  constexpr int TILE = BM * BK + BTILE;
   static_assert(IA >= 1 && IB >= 1, "tile too small");
-  static_assert(!F32 || BKB == 64 || FM == 3, "fp32 tiles stage 64-B rows (FM 3: 128-B)");
+  static_assert(!F32 || BKB == 64 || FM == 3 || FM == 4 || FM >= 5, "fp32 tiles stage 64-B rows (FM 3: 128-B)");
   extern __shared__ __attribute__((aligned(16))) uint16_t smem_raw[];
   T* smem = reinterpret_cast<T*>(smem_raw);
   const T* zline = reinterpret_cast<const T*>(g_zero_line);
@@ -427,7 +439,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
   const int mt = tile / ntn, nt = tile % ntn;
   const int64_t m0 = int64_t(mt) * BM;
   const int n0 = nt * BN;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w >> 1, wn = w & 1;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, wm = w / WGN, wn = w % WGN;
 
   // source of this lane for each of the wave's glds instructions (k offset added per tile);
   // CONV: the output pixel of the row (first input pixel of its window) instead
@@ -457,6 +469,15 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
     const int row = (w * IB + i) * RPI + lane / CPK, c = swzk<BKB>(row, lane % CPK);
     pb[i] = B + int64_t(n0 + row) * ldb + c * EPC;
   }
+  const uint16_t* pbp[BSPLIT ? IBP : 1];
+  if constexpr (BSPLIT) {
+    const uint16_t* Bh = reinterpret_cast<const uint16_t*>(B);
+#pragma unroll
+    for (int i = 0; i < IBP; ++i) {
+      const int row = (w * IBP + i) * 16 + lane / 4, c = swz(row, lane % 4);
+      pbp[i] = Bh + int64_t(n0 + row) * ldb + c * 8;
+    }
+  }
   auto issue = [&](int kt, int buf) {
     T* As = smem + buf * TILE;
     T* Bs = As + BM * BK;
@@ -471,9 +492,18 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
         glds16(pa[i] + kt * BK, As + (w * IA + i) * RPI * BK);
       }
     }
+    if constexpr (BSPLIT) {
+      uint16_t* Bp = reinterpret_cast<uint16_t*>(Bs);
 #pragma unroll
-    for (int i = 0; i < IB; ++i)
-      glds16(pb[i] + kt * BK, Bs + (w * IB + i) * RPI * BK);
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int i = 0; i < IBP; ++i)
+          glds16(pbp[i] + p * bps + kt * 32, Bp + p * (BN * 32) + (w * IBP + i) * 16 * 32);
+    } else {
+#pragma unroll
+      for (int i = 0; i < IB; ++i)
+        glds16(pb[i] + kt * BK, Bs + (w * IB + i) * RPI * BK);
+    }
     if constexpr (CONV) {  // tiles are issued in k order: step to the next (tap, channel) slab
       kc += BK;
       if (kc == geo.C) {
@@ -520,7 +550,71 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
     if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
     const T* As = smem + (kt % STAGES) * TILE;
     const T* Bs = As + BM * BK;
-    if constexpr (F32 && (FM == 1 || FM == 3)) {
+    if constexpr (BSPLIT) {
+      // A: the lane's 8 floats of k16 step kk (chunks 4kk + 2fh, +1) split in registers;
+      // B: the same k (chunk 2kk + fh of a 64-B plane row) read ready-made from each plane
+      const uint16_t* Bp = reinterpret_cast<const uint16_t*>(Bs);
+#pragma unroll
+      for (int kk = 0; kk < BK / 16; ++kk) {
+        bf16x8 ah[TM], am[TM], al[TM], bh[TN], bm[TN], bl[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int r = wn * WN + j * 32 + fr;
+          const int o = r * 32 + swz(r, 2 * kk + fh) * 8;
+          bh[j] = *reinterpret_cast<const bf16x8*>(Bp + o);
+          bm[j] = *reinterpret_cast<const bf16x8*>(Bp + BN * 32 + o);
+          bl[j] = *reinterpret_cast<const bf16x8*>(Bp + 2 * BN * 32 + o);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int r = wm * WM + i * 32 + fr;
+          const float4 x0 = *reinterpret_cast<const float4*>(As + r * BK + swzk<BKB>(r, 4 * kk + 2 * fh) * 4);
+          const float4 x1 = *reinterpret_cast<const float4*>(As + r * BK + swzk<BKB>(r, 4 * kk + 2 * fh + 1) * 4);
+          const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+          split3(v, ah[i], am[i], al[i]);
+        }
+        mfma_x3<TM, TN>(acc, tacc, ah, am, al, bh, bm, bl, true);
+      }
+      continue;
+    } else if constexpr (F32 && FM >= 5 && FM <= 7) {
+      // TIMING ABLATION ONLY (MPIT_F32_ABLATE=nosplit): FM 3's loop with the operand split
+      // replaced by a reinterpretation of the raw fp32 bits (wrong numbers, zero VALU) — how
+      // fast the kernel would be if its operands arrived pre-split
+#pragma unroll
+      for (int kk = 0; kk < BK / 16; ++kk) {
+        bf16x8 ah[TM], am[TM], al[TM], bh[TN], bm[TN], bl[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int r = wm * WM + i * 32 + fr;
+          const float4 x0 = *reinterpret_cast<const float4*>(As + r * BK + swzk<BKB>(r, 4 * kk + 2 * fh) * 4);
+          const float4 x1 = *reinterpret_cast<const float4*>(As + r * BK + swzk<BKB>(r, 4 * kk + 2 * fh + 1) * 4);
+          if constexpr (FM == 6) {  // ablation 6: A split, B raw
+            const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+            split3(v, ah[i], am[i], al[i]);
+          } else {
+            ah[i] = __builtin_bit_cast(bf16x8, x0);
+            am[i] = __builtin_bit_cast(bf16x8, x1);
+            al[i] = ah[i];
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int r = wn * WN + j * 32 + fr;
+          const float4 x0 = *reinterpret_cast<const float4*>(Bs + r * BK + swzk<BKB>(r, 4 * kk + 2 * fh) * 4);
+          const float4 x1 = *reinterpret_cast<const float4*>(Bs + r * BK + swzk<BKB>(r, 4 * kk + 2 * fh + 1) * 4);
+          if constexpr (FM == 7) {  // ablation 7: A raw, B split
+            const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+            split3(v, bh[j], bm[j], bl[j]);
+          } else {
+            bh[j] = __builtin_bit_cast(bf16x8, x0);
+            bm[j] = __builtin_bit_cast(bf16x8, x1);
+            bl[j] = bh[j];
+          }
+        }
+        mfma_x3<TM, TN>(acc, tacc, ah, am, al, bh, bm, bl, true);
+      }
+      continue;
+    } else if constexpr (F32 && (FM == 1 || FM == 3)) {
       // bf16x6: the lane's 8 floats of a row in k16 step kk (chunks 4kk + 2fh, +1 of the row)
       // are exactly the k = 8fh + j operand of one v_mfma_f32_32x32x16_bf16; split each
       // fragment in registers
@@ -1317,6 +1411,61 @@ __device__ __forceinline__ void cast_tile(const float* __restrict__ w, int R, in
   }
 }
 
+// The bf16x6 operand split of one fp32 value: h = bf16(v), m = bf16(v - h), l = bf16(v - h - m)
+// (round to nearest; for normal numbers v == h + m + l exactly) — split3's arithmetic.
+__device__ __forceinline__ void split1(float v, uint16_t& h, uint16_t& m, uint16_t& l) {
+  h = f2bf(v);
+  const float r = v - bf2f(h);
+  m = f2bf(r);
+  l = f2bf(r - bf2f(m));
+}
+
+// cast_tile for the pre-split fp32 path: the same copy / transpose, written as three bf16
+// planes (h at p, m at p + plane, l at p + 2 * plane) for the FM 4 GEMMs. wb: planes or
+// null; wt: planes (pt > 0) or plain fp32 (pt == 0: the GEMM reading it splits in registers)
+__device__ __forceinline__ void cast_tile_planes(const float* __restrict__ w, int R, int Cc, int T,
+                                                 uint16_t* __restrict__ wb, int64_t pb, void* __restrict__ wt_,
+                                                 int64_t pt, const TapMap& map, int cx, int ry, int tap) {
+  __shared__ float tile[32][33];
+  const int c0 = cx * 32, r0 = ry * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int y = ty; y < 32; y += 8) {
+    const int r = r0 + y, c = c0 + tx;
+    if (r < R && c < Cc) {
+      const int64_t i = (int64_t(r) * T + tap) * Cc + c;
+      const float v = w[i];
+      if (wb) {
+        uint16_t h, m, l;
+        split1(v, h, m, l);
+        wb[i] = h;
+        wb[pb + i] = m;
+        wb[2 * pb + i] = l;
+      }
+      tile[y][tx] = v;
+    }
+  }
+  __syncthreads();
+  if (!wt_) return;
+  const int64_t base = map.base[tap];
+  const int tc = map.tc[tap], dt = map.dt[tap];
+  for (int y = ty; y < 32; y += 8) {
+    const int c = c0 + y, r = r0 + tx;
+    if (r < R && c < Cc) {
+      const int64_t o = base + (int64_t(c) * tc + dt) * R + r;
+      if (pt == 0) {
+        static_cast<float*>(wt_)[o] = tile[tx][y];
+        continue;
+      }
+      uint16_t* wt = static_cast<uint16_t*>(wt_);
+      uint16_t h, m, l;
+      split1(tile[tx][y], h, m, l);
+      wt[o] = h;
+      wt[pt + o] = m;
+      wt[2 * pt + o] = l;
+    }
+  }
+}
+
 template <typename O>
 __global__ __launch_bounds__(256) void cast_transpose_kernel(const float* __restrict__ w, int R, int Cc, int T,
                                                              O* __restrict__ wb, O* __restrict__ wt, TapMap map) {
@@ -1331,8 +1480,9 @@ struct CastJob {
   void* wb;
   void* wt;
   int R, Cc, T, tcx, tcy;  // tiles along Cc and R
-  int f32;                 // outputs are fp32 (no plain copy)
+  int f32;                 // outputs: 0 bf16, 1 fp32 (no plain copy), 2 pre-split bf16 planes
   int64_t block0;
+  int64_t pb, pt;          // plane strides (elements) of wb / wt when f32 == 2
   TapMap map;
 };
 
@@ -1352,7 +1502,10 @@ __global__ __launch_bounds__(256) void cast_batch_kernel(const CastJob* __restri
   const int64_t local = int64_t(blockIdx.x) - J.block0;
   const int per_tap = J.tcx * J.tcy;
   const int tap = int(local / per_tap), rem = int(local % per_tap);
-  if (J.f32)
+  if (J.f32 == 2)
+    cast_tile_planes(J.w, J.R, J.Cc, J.T, static_cast<uint16_t*>(J.wb), J.pb, J.wt, J.pt, J.map, rem % J.tcx,
+                     rem / J.tcx, tap);
+  else if (J.f32)
     cast_tile<float>(J.w, J.R, J.Cc, J.T, static_cast<float*>(J.wb), static_cast<float*>(J.wt), J.map, rem % J.tcx,
                      rem / J.tcx, tap);
   else
@@ -1489,7 +1642,7 @@ static void fold_plan(EpiArgs& ep, int dev, hipStream_t s, int64_t mtn, int ntn)
 template <typename T>
 static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B,
                         int64_t ldb, uintptr_t C, int64_t ldc, uintptr_t cin, uintptr_t cmask, const ConvGeo* geo,
-                        const EpiArgs& ep_in, int epi, uintptr_t bias, bool relu) {
+                        const EpiArgs& ep_in, int epi, uintptr_t bias, bool relu, int64_t bps) {
   constexpr bool F32 = sizeof(T) == 4;
   EpiArgs ep = ep_in;  // the fold's group size and ticket set are filled in per launch
   constexpr int EPC = epc<T>();
@@ -1535,9 +1688,29 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
     const char* e = std::getenv("MPIT_F32_BK");
     return e && std::atoi(e) == 16 ? 16 : 32;
   }();
-  const int fm = !F32 || f32_mode() != 1 ? 0
-                 : (f32_bk == 32 && K % 32 == 0 && (!geo || (geo->C % 32 == 0 && !geo->pitch)) ? 3 : 1);
-  const int nk = K / (fm == 3 ? 32 : nt_bk_of<T>());
+  static const int ablate = [] {
+    const char* e = std::getenv("MPIT_F32_ABLATE");
+    if (!e) return 0;
+    const std::string v(e);
+    return v == "nosplit" ? 5 : v == "splitA" ? 6 : v == "splitB" ? 7 : 0;
+  }();
+  int fm = !F32 || f32_mode() != 1 ? 0
+           : (f32_bk == 32 && K % 32 == 0 && (!geo || (geo->C % 32 == 0 && !geo->pitch)) ? 3 : 1);
+  if (fm == 3 && ablate) fm = ablate;
+  if (bps > 0) {  // B is three pre-split bf16 planes: only the FM 4 kernels read that
+    if (!F32 || fm != 3 || ablate || bps < int64_t(N) * ldb || ldb % 8)
+      throw std::invalid_argument("gemm_nt: pre-split B planes need the fp32 bf16x6 path with K % 32 == 0 "
+                                  "(and conv channels % 32 == 0), ldb % 8 == 0 and a plane stride >= N * ldb");
+    check_ptr(B + uintptr_t(bps) * 2, "B plane 1");
+    if (N % 128) throw std::invalid_argument("gemm_nt: pre-split B planes need N % 128 == 0");
+    // MPIT_F32_WAVES=2x2: the 2 x 2 wave grid (FM 4); default 4 x 1 (FM 9)
+    static const bool w22 = [] {
+      const char* e = std::getenv("MPIT_F32_WAVES");
+      return e && std::string(e) == "2x2";
+    }();
+    fm = w22 ? 4 : 9;
+  }
+  const int nk = K / (fm >= 3 ? 32 : nt_bk_of<T>());
   // MPIT_GEMM_STAGES caps the ring depth (A/B measurements). fp32: the 64 KB epilogue tile
   // of a 128x128 block holds a 4-deep 16-deep ring (or a 2-deep 32-deep one) for free.
   static const int max_stages = [] {
@@ -1548,7 +1721,7 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
     const char* e = std::getenv("MPIT_F32_STAGES");
     return e ? std::max(2, std::min(4, std::atoi(e))) : 0;
   }();
-  int cap = F32 && N % 128 == 0 ? (fm == 3 ? 2 : 4) : max_stages;
+  int cap = F32 && N % 128 == 0 ? (fm >= 3 ? 2 : 4) : max_stages;
   if (F32 && f32_stages) cap = f32_stages;
   const int stages = std::min(cap, nk >= 4 ? 4 : (nk == 3 ? 3 : 2));
   // (kernel templates are named at a non-template call site so their host stubs are emitted)
@@ -1564,22 +1737,50 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
 #define MPIT_NT_LAUNCH1(BM, BN, ST, EPI, CONV)                                                                       \
   do {                                                                                                             \
     if constexpr (F32) {                                                                                           \
+      if (fm >= 5 && fm <= 7) { /* timing ablations (MPIT_F32_ABLATE) */                                        \
+        if (fm == 5) {                                                                                             \
+          if (shm > 65536) MPIT_NT_OPT_IN(BM, BN, ST, EPI, CONV, 5);                                                \
+          hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, ST, EPI, CONV, 5>), dim3(unsigned(nb)), dim3(256), shm, s, \
+                             a, lda, b, ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g, bps);                          \
+        } else if (fm == 6) {                                                                                      \
+          if (shm > 65536) MPIT_NT_OPT_IN(BM, BN, ST, EPI, CONV, 6);                                                \
+          hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, ST, EPI, CONV, 6>), dim3(unsigned(nb)), dim3(256), shm, s, \
+                             a, lda, b, ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g, bps);                          \
+        } else {                                                                                                   \
+          if (shm > 65536) MPIT_NT_OPT_IN(BM, BN, ST, EPI, CONV, 7);                                                \
+          hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, ST, EPI, CONV, 7>), dim3(unsigned(nb)), dim3(256), shm, s, \
+                             a, lda, b, ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g, bps);                          \
+        }                                                                                                          \
+        break;                                                                                                     \
+      }                                                                                                            \
+      if (fm == 4) {                                                                                               \
+        if (shm > 65536) MPIT_NT_OPT_IN(BM, BN, ST, EPI, CONV, 4);                                                  \
+        hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, ST, EPI, CONV, 4>), dim3(unsigned(nb)), dim3(256), shm, s, a, \
+                           lda, b, ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g, bps);                          \
+        break;                                                                                                     \
+      }                                                                                                            \
+      if (fm == 9) {                                                                                               \
+        if (shm > 65536) MPIT_NT_OPT_IN(BM, BN, ST, EPI, CONV, 9);                                                  \
+        hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, ST, EPI, CONV, 9>), dim3(unsigned(nb)), dim3(256), shm, s, a, \
+                           lda, b, ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g, bps);                          \
+        break;                                                                                                     \
+      }                                                                                                            \
       if (fm == 3) {                                                                                               \
         if (shm > 65536) MPIT_NT_OPT_IN(BM, BN, ST, EPI, CONV, 3);                                                  \
         hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, ST, EPI, CONV, 3>), dim3(unsigned(nb)), dim3(256), shm, s, a, \
-                           lda, b, ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g);                               \
+                           lda, b, ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g, bps);                               \
         break;                                                                                                     \
       }                                                                                                            \
       if (fm == 1) {                                                                                               \
         if (shm > 65536) MPIT_NT_OPT_IN(BM, BN, ST, EPI, CONV, 1);                                                  \
         hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, ST, EPI, CONV, 1>), dim3(unsigned(nb)), dim3(256), shm, s, a, \
-                           lda, b, ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g);                               \
+                           lda, b, ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g, bps);                               \
         break;                                                                                                     \
       }                                                                                                            \
     }                                                                                                              \
     if (shm > 65536) MPIT_NT_OPT_IN(BM, BN, ST, EPI, CONV, 0);                                                      \
     hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, ST, EPI, CONV>), dim3(unsigned(nb)), dim3(256), shm, s, a, lda, b, \
-                       ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g);                                           \
+                       ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g, bps);                                           \
   } while (0)
 #define MPIT_NT_LAUNCH2(BM, BN, ST, CONV)                                                         \
   do {                                                                                              \
@@ -1596,12 +1797,13 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
     if (nb > INT32_MAX) throw std::invalid_argument("gemm_nt: too many tiles");                               \
     if (ep.fcoef) fold_plan(ep, dev, s, mtn, ntn);                                                                 \
     /* LDS: the k-tile ring, reused by the epilogue's output tile and reduction table */                      \
-    const size_t shm = std::max({size_t(ST) * (BM + BN) * size_t(nt_bkb(BM, BN, fm)),                          \
+    const size_t shm = std::max({size_t(ST) * (size_t(BM) * nt_bkb(BM, BN, fm) +                               \
+                                                (fm == 4 || fm == 9 ? size_t(BN) * 192 : size_t(BN) * nt_bkb(BM, BN, fm))), \
                                  size_t(BM) * BN * sizeof(T), size_t(256) * 8 * 3 * sizeof(float)});          \
     if (geo) MPIT_NT_LAUNCH2(BM, BN, ST, true);                                                           \
     else MPIT_NT_LAUNCH2(BM, BN, ST, false);                                                              \
   } while (0)
-  const int tcfg = nt_tile_config(N, K, geo != nullptr, geo ? geo->C : 0, F32);
+  const int tcfg = fm == 4 || fm == 9 ? 0 : nt_tile_config(N, K, geo != nullptr, geo ? geo->C : 0, F32);
   if constexpr (F32) {
     if (tcfg == 1) {
       MPIT_NT_LAUNCH(256, 128, 3);
@@ -1641,11 +1843,12 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
   hip_check(hipGetLastError(), "gemm_nt launch");
 }
 
+// bps > 0: B is three pre-split bf16 planes (h, m, l) of plane stride bps elements (fp32 only)
 static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B,
                       int64_t ldb, uintptr_t C, int64_t ldc, uintptr_t cin, uintptr_t cmask, const ConvGeo* geo,
-                      const EpiArgs& ep, int epi, bool f32, uintptr_t bias = 0, bool relu = false) {
-  if (f32) launch_nt_t<float>(dev, s, M, N, K, A, lda, B, ldb, C, ldc, cin, cmask, geo, ep, epi, bias, relu);
-  else launch_nt_t<uint16_t>(dev, s, M, N, K, A, lda, B, ldb, C, ldc, cin, cmask, geo, ep, epi, bias, relu);
+                      const EpiArgs& ep, int epi, bool f32, uintptr_t bias = 0, bool relu = false, int64_t bps = 0) {
+  if (f32) launch_nt_t<float>(dev, s, M, N, K, A, lda, B, ldb, C, ldc, cin, cmask, geo, ep, epi, bias, relu, bps);
+  else launch_nt_t<uint16_t>(dev, s, M, N, K, A, lda, B, ldb, C, ldc, cin, cmask, geo, ep, epi, bias, relu, bps);
 }
 
 // the reduction epilogue selected by the (stats, BN reduction) operands
@@ -1683,10 +1886,11 @@ static EpiArgs epi_args(uintptr_t stats, const BnRed* r, int* mode) {
 }
 
 void gemm_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B, int64_t ldb,
-             uintptr_t C, int64_t ldc, uintptr_t stats, uintptr_t cin, uintptr_t cmask, const BnRed* red, bool f32) {
+             uintptr_t C, int64_t ldc, uintptr_t stats, uintptr_t cin, uintptr_t cmask, const BnRed* red, bool f32,
+             int64_t bps) {
   int mode;
   const EpiArgs ep = epi_args(stats, red, &mode);
-  launch_nt(dev, s, M, N, K, A, lda, B, ldb, C, ldc, cin, cmask, nullptr, ep, mode, f32);
+  launch_nt(dev, s, M, N, K, A, lda, B, ldb, C, ldc, cin, cmask, nullptr, ep, mode, f32, 0, false, bps);
 }
 
 bool gemm_tn_supported(int64_t M, int N, int K) { return M > 0 && N % 64 == 0 && K % 64 == 0 && N > 0 && K > 0; }
@@ -1890,7 +2094,7 @@ bool conv_supported(int C, int Co) { return C % 32 == 0 && Co % 64 == 0; }
 
 void conv_fwd(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad,
               uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t cin, uintptr_t bias, bool relu,
-              const BnRed* red, bool f32) {
+              const BnRed* red, bool f32, int64_t bps) {
   if (!conv_supported(C, Co)) throw std::invalid_argument("conv_fwd: need C % 32 == 0 and Co % 64 == 0");
   if (int64_t(Nb) * H * W * C >= (int64_t(1) << 31)) throw std::invalid_argument("conv_fwd: input too large");
   int Ho, Wo;
@@ -1898,7 +2102,7 @@ void conv_fwd(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R
   const int64_t M = int64_t(Nb) * Ho * Wo;
   int mode;
   const EpiArgs ep = epi_args(stats, red, &mode);
-  launch_nt(dev, s, M, Co, R * S * C, x, C, w, int64_t(R) * S * C, y, Co, cin, 0, &g, ep, mode, f32, bias, relu);
+  launch_nt(dev, s, M, Co, R * S * C, x, C, w, int64_t(R) * S * C, y, Co, cin, 0, &g, ep, mode, f32, bias, relu, bps);
 }
 
 int64_t conv_wgrad_ws_floats(int dev, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad) {
@@ -2053,12 +2257,19 @@ int64_t cast_jobs_build(uintptr_t host_table, const std::vector<std::array<int64
   for (size_t k = 0; k < specs.size(); ++k) {
     const auto& q = specs[k];
     // q[0] = kind | f32 << 8 (fp32 outputs: transposes only, the plain copy is the master weight)
+    //        | 512: wb as three pre-split bf16 planes (else none: the forward reads the master)
+    //        | 1024: wt as three pre-split bf16 planes (else fp32)
     const int kind = int(q[0] & 0xff), Co = int(q[4]), C = int(q[5]), R = int(q[6]), S = int(q[7]);
     const int stride = int(q[8]), pad = int(q[9]);
     CastJob J{};
     J.w = reinterpret_cast<const float*>(q[1]);
-    J.f32 = int((q[0] >> 8) & 1);
-    J.wb = J.f32 ? nullptr : reinterpret_cast<void*>(q[2]);
+    const bool pl_b = (q[0] >> 9) & 1, pl_t = (q[0] >> 10) & 1;
+    J.f32 = pl_b || pl_t ? 2 : int((q[0] >> 8) & 1);
+    J.wb = (J.f32 == 1 || (J.f32 == 2 && !pl_b)) ? nullptr : reinterpret_cast<void*>(q[2]);
+    if (J.f32 == 2) {
+      J.pb = int64_t(Co) * R * S * C;
+      J.pt = !pl_t ? 0 : kind == 1 ? conv_dgrad_strided_wfloats(C, Co, R, S, stride, pad) : int64_t(C) * R * S * Co;
+    }
     J.wt = reinterpret_cast<void*>(q[3]);
     J.R = Co;
     J.Cc = C;
@@ -2093,7 +2304,7 @@ void cast_jobs_run(int dev, hipStream_t s, uintptr_t dev_table, int njobs, int64
 }
 
 void conv_dgrad_strided(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad,
-                        uintptr_t dy, uintptr_t wcls, uintptr_t dx, const BnRed* red, bool f32) {
+                        uintptr_t dy, uintptr_t wcls, uintptr_t dx, const BnRed* red, bool f32, int64_t bps) {
   if (C % 64 || Co % 32) throw std::invalid_argument("conv_dgrad_strided: need C % 64 == 0 and Co % 32 == 0");
   int Ho, Wo;
   conv_geo(H, W, C, R, S, stride, pad, &Ho, &Wo);
@@ -2119,7 +2330,9 @@ void conv_dgrad_strided(int dev, hipStream_t s, int Nb, int H, int W, int C, int
     ep.fcoef = nullptr;  // several launches write the partials: no folded finalize
     ep.row0 += row0;
     row0 += gemm_nt_tiles(M);
-    launch_nt(dev, s, M, C, K, dy, Co, wcls + uintptr_t(c.base) * (f32 ? 4 : 2), K, dx, C, 0, 0, &g, ep, mode, f32);
+    // bps > 0: wcls holds three bf16 planes of bps elements each (class offsets in elements)
+    launch_nt(dev, s, M, C, K, dy, Co, wcls + uintptr_t(c.base) * (f32 && !bps ? 4 : 2), K, dx, C, 0, 0, &g, ep, mode,
+              f32, 0, false, bps);
   }
 }
 

@@ -131,9 +131,11 @@ int64_t gemm_nt_fold_lvl_floats(int N);
 bool gemm_nt_supported(int64_t M, int N, int K, bool f32 = false);
 int64_t gemm_nt_tiles(int64_t M);
 int64_t gemm_nt_stats_floats(int64_t M, int N);
+// bps > 0 (fp32 only): B is three pre-split bf16 planes h, m, l (x = h + m + l exactly, see
+// cast_jobs kind flag 512) of bps elements each — the kernel splits only A in registers
 void gemm_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t A, int64_t lda, uintptr_t B, int64_t ldb,
              uintptr_t C, int64_t ldc, uintptr_t stats, uintptr_t cin, uintptr_t cmask = 0,
-             const BnRed* red = nullptr, bool f32 = false);
+             const BnRed* red = nullptr, bool f32 = false, int64_t bps = 0);
 // out[N,K] (fp32) = beta*out + Y[M,N]^T . X[M,K]  (split over M; ws: gemm_tn_ws_floats)
 bool gemm_tn_supported(int64_t M, int N, int K);
 int64_t gemm_tn_ws_floats(int dev, int64_t M, int N, int K);
@@ -162,7 +164,7 @@ bool conv_supported(int C, int Co);
 // bias (fp32 [Co], optional) and ReLU are applied in the epilogue.
 void conv_fwd(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad,
               uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t cin, uintptr_t bias = 0,
-              bool relu = false, const BnRed* red = nullptr, bool f32 = false);
+              bool relu = false, const BnRed* red = nullptr, bool f32 = false, int64_t bps = 0);
 // ReLU + bias backward: dz = dy * (y > 0) (bf16 [M, C]), db[c] = sum_m dz (fp32, optional,
 // deterministic); ws: relu_bias_bwd_ws_floats(C)
 // Backward-data of a strided conv (stride 2..4) as stride^2 parity-class implicit GEMMs
@@ -174,7 +176,8 @@ void conv_dgrad_strided_weights(int dev, hipStream_t s, uintptr_t w, int Co, int
 // partial rows a BN reduction over the strided backward-data writes (all classes)
 int64_t conv_dgrad_strided_tiles(int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad);
 void conv_dgrad_strided(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad,
-                        uintptr_t dy, uintptr_t wcls, uintptr_t dx, const BnRed* red = nullptr, bool f32 = false);
+                        uintptr_t dy, uintptr_t wcls, uintptr_t dx, const BnRed* red = nullptr, bool f32 = false,
+                        int64_t bps = 0);
 int64_t relu_bias_bwd_ws_floats(int C);
 void relu_bias_bwd(int dev, hipStream_t s, int64_t M, int C, uintptr_t dy, uintptr_t y, uintptr_t dz, uintptr_t db,
                    uintptr_t ws, bool f32 = false);

@@ -145,6 +145,23 @@ def mfma_dtype(x: torch.Tensor):
     return x.dtype if x.dtype in (torch.bfloat16, torch.float32) else None
 
 
+# MPIT_F32_BSPLIT=0: fp32 steps split the weight operand in the GEMM's registers like the
+# activation (round-2 kernels); default: the per-step weight plan writes it pre-split into
+# three bf16 planes and the GEMM splits only the activation (csrc/kernels/gemm.hip FM 4)
+_F32_BSPLIT = os.environ.get("MPIT_F32_BSPLIT", "1") != "0"
+
+
+def _bps(w: torch.Tensor, f32: bool) -> int:
+    """Plane stride of a pre-split weight operand ([3, ...] bf16 planes h, m, l) of an fp32
+    GEMM, else 0 (the operand is fp32 / the call is bf16)."""
+    return w[0].numel() if (f32 and w is not None and w.dtype == torch.bfloat16) else 0
+
+
+def _unsplit(w: torch.Tensor) -> torch.Tensor:
+    """fp32 weight back from its three bf16 planes (exact: w == h + m + l)."""
+    return (w[0].float() + w[1].float()) + w[2].float()
+
+
 def _to(x: torch.Tensor, dt) -> torch.Tensor:
     x = _cl(x)
     return x if x.dtype == dt else x.to(dt)
@@ -336,7 +353,7 @@ class _Conv1x1Fn(torch.autograd.Function):
             st, nt = _tile_stats(co, M, x.device)
             hold.append((st, nt))
         m.gemm_nt(x.device.index, _stream(x), M, co, ci, x.data_ptr(), ci, wb.data_ptr(), ci, y.data_ptr(), co,
-                  st.data_ptr() if st is not None else 0, f32=f32)
+                  st.data_ptr() if st is not None else 0, f32=f32, bps=_bps(wb, f32))
         ctx.save_for_backward(x, wt)
         ctx.wshape = weight.shape
         ctx.slot = slot
@@ -368,9 +385,11 @@ class _Conv1x1Fn(torch.autograd.Function):
                 if extra.shape != x.shape:
                     raise RuntimeError("GradSlot gradient does not match the convolution input")
                 m.gemm_nt(dev, s, M, ci, co, dy.data_ptr(), co, wt.data_ptr(), co, dx.data_ptr(), ci, 0,
-                          extra.data_ptr(), emask.data_ptr() if emask is not None else 0, f32=f32, **kw)
+                          extra.data_ptr(), emask.data_ptr() if emask is not None else 0, f32=f32, bps=_bps(wt, f32),
+                          **kw)
             else:
-                m.gemm_nt(dev, s, M, ci, co, dy.data_ptr(), co, wt.data_ptr(), co, dx.data_ptr(), ci, 0, f32=f32, **kw)
+                m.gemm_nt(dev, s, M, ci, co, dy.data_ptr(), co, wt.data_ptr(), co, dx.data_ptr(), ci, 0, f32=f32,
+                          bps=_bps(wt, f32), **kw)
             if part is not None:
                 ctx.link.publish(part, nt, dx, part2, fb)
         if ctx.needs_input_grad[1]:
@@ -461,9 +480,9 @@ def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None):
     """(dx, dw) of an NHWC implicit-GEMM conv from the gradient ``dz`` of its output; with a
     BNLink the backward-data GEMM also produces the producing BN's backward reduction."""
     nb, c, h, w = x.shape
-    co, r, s, _ = wb.shape
-    ho, wo = dz.shape[2], dz.shape[3]
     f32 = x.dtype == torch.float32
+    co, r, s, _ = wb.shape[-4:]  # (pre-split planes carry a leading dim of 3)
+    ho, wo = dz.shape[2], dz.shape[3]
     m = native()
     dev, st = x.device.index, _stream(x)
     dx = dw = None
@@ -477,7 +496,7 @@ def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None):
                 nt = m.gemm_nt_tiles(nb * h * w)
                 kw, part, _, fb = _red_args(link, c, nt, x.device, fold=True)
             m.conv_fwd(dev, st, nb, ho, wo, co, c, r, s, 1, r - 1 - pad, dz.data_ptr(), wt.data_ptr(),
-                       dx.data_ptr(), f32=f32, **kw)
+                       dx.data_ptr(), f32=f32, bps=_bps(wt, f32), **kw)
             if part is not None:
                 link.publish(part, nt, dx, None, fb)
         elif wt is not None:
@@ -489,11 +508,12 @@ def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None):
                 nt = m.conv_dgrad_strided_tiles(nb, h, w, c, co, r, s, stride, pad)
                 kw, part, _, _ = _red_args(link, c, nt, x.device)
             m.conv_dgrad_strided(dev, st, nb, h, w, c, co, r, s, stride, pad, dz.data_ptr(), wt.data_ptr(),
-                                 dx.data_ptr(), f32=f32, **kw)
+                                 dx.data_ptr(), f32=f32, bps=_bps(wt, f32), **kw)
             if part is not None:
                 link.publish(part, nt, dx)
         else:  # MIOpen's NHWC backward-data
-            wv = wb.permute(0, 3, 1, 2).to(x.dtype)  # [Co, C, R, S] view with channels_last strides
+            wf = _unsplit(wb) if _bps(wb, f32) else wb
+            wv = wf.permute(0, 3, 1, 2).to(x.dtype)  # [Co, C, R, S] view with channels_last strides
             dx = torch.ops.aten.convolution_backward(dz, x, wv, None, [stride, stride], [pad, pad], [1, 1], False,
                                                      [0, 0], 1, [True, False, False])[0]
     if ctx.needs_input_grad[1]:
@@ -559,7 +579,7 @@ class _ConvFn(torch.autograd.Function):
             hold.append((st, nt))
         native().conv_fwd(x.device.index, _stream(x), nb, h, w, c, co, r, s, stride, pad, x.data_ptr(), wb.data_ptr(),
                           y.data_ptr(), stats=st.data_ptr() if st is not None else 0,
-                          bias=b.data_ptr() if b is not None else 0, relu=bool(relu), f32=f32)
+                          bias=b.data_ptr() if b is not None else 0, relu=bool(relu), f32=f32, bps=_bps(wb, f32))
         ctx.save_for_backward(x, wb, wt, y if relu else None)
         ctx.geo = (stride, pad, bias is not None, bool(relu))
         ctx.link = link
@@ -667,6 +687,7 @@ class WeightCastPlan:
         specs, self.mods = [], []
         m = native()
         f32 = self.dtype == torch.float32
+        planes = f32 and _F32_BSPLIT
         for mod in self.model.modules():
             kind = None
             if isinstance(mod, Conv1x1) and mod.stride == (1, 1):
@@ -681,24 +702,36 @@ class WeightCastPlan:
             if not w.is_cuda or w.dtype != torch.float32 or not w.is_contiguous(memory_format=torch.channels_last):
                 continue
             co, c, r, sw = w.shape
+            # pre-split planes h, m, l (bf16, a leading dim of 3) for an fp32 step, per operand:
+            # only where the GEMM reading it runs 128-wide column tiles (N = co forward, c
+            # backward-data) — the 128x64 tiles of N = 64 keep 3 blocks per CU only with the
+            # smaller fp32 image, and split that operand in registers
+            pl_b = planes and co % 128 == 0
+            pl_t = planes and c % 128 == 0 and kind != 2
             # a detached view: the plan outlives every step, and a view WITH autograd history
             # would keep the weight's AccumulateGrad node (made at build time, on the stream
             # current then) alive into every step — autograd then warns that the node's stream
             # differs from the step's and inserts a cross-stream wait per weight
-            wb = _as_rsc(w.detach()) if f32 else torch.empty((co, r, sw, c), dtype=torch.bfloat16, device=w.device)
+            if f32 and not pl_b:
+                wb = _as_rsc(w.detach())
+            else:
+                wb = torch.empty(((3,) if pl_b else ()) + (co, r, sw, c), dtype=torch.bfloat16, device=w.device)
+            lt = (3,) if pl_t else ()
+            odt = torch.bfloat16 if pl_t else self.dtype
             if kind == 0:
-                wt = torch.empty((c, r, sw, co), dtype=self.dtype, device=w.device)
+                wt = torch.empty(lt + (c, r, sw, co), dtype=odt, device=w.device)
             elif kind == 1:
-                wt = torch.empty(m.conv_dgrad_strided_wfloats(c, co, r, sw, mod.stride[0], mod.padding[0]),
-                                 dtype=self.dtype, device=w.device)
+                wt = torch.empty(lt + (m.conv_dgrad_strided_wfloats(c, co, r, sw, mod.stride[0], mod.padding[0]),),
+                                 dtype=odt, device=w.device)
             else:
                 wt = None
             if isinstance(mod, Conv1x1):  # the 1x1 path takes 2-D [co, ci] / [ci, co] views
-                wb, wt = wb.reshape(co, c), wt.view(c, co)
-            if f32 and wt is None:
+                wb, wt = wb.reshape(((3,) if pl_b else ()) + (co, c)), wt.view(lt + (c, co))
+            if f32 and not (pl_b or pl_t) and wt is None:
                 self.mods.append((mod, w.data_ptr(), (wb, wt)))  # nothing to write
                 continue
-            specs.append([kind | (256 if f32 else 0), w.data_ptr(), 0 if f32 else wb.data_ptr(),
+            flags = kind | (256 if f32 else 0) | (512 if pl_b else 0) | (1024 if pl_t else 0)
+            specs.append([flags, w.data_ptr(), wb.data_ptr() if (pl_b or not f32) else 0,
                           wt.data_ptr() if wt is not None else 0, co, c, r, sw, mod.stride[0], mod.padding[0]])
             self.mods.append((mod, w.data_ptr(), (wb, wt)))
         self.njobs = len(specs)

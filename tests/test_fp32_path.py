@@ -249,7 +249,12 @@ def test_weight_cast_plan_fp32():
     down = torch.nn.Sequential(conv1x1(256, 512, 2), BatchNormAct2d(512, act=False))
     net = torch.nn.Sequential(Bottleneck(256, 128, 2, down), Bottleneck(512, 128)).cuda().to(
         memory_format=torch.channels_last)
-    plan = C.WeightCastPlan(net, torch.float32)
+    old = C._F32_BSPLIT
+    C._F32_BSPLIT = False  # the round-2 fp32 plan: forwards read the master, fp32 transposes
+    try:
+        plan = C.WeightCastPlan(net, torch.float32)
+    finally:
+        C._F32_BSPLIT = old
     plan.run()
     for mod, _, (wb, wt) in plan.mods:
         w = mod.weight
@@ -310,3 +315,70 @@ def test_fp32_training_tracks_fp64_like_stock_pytorch():
     assert abs(r["loss_mpit_fp32"][0] - r["loss_fp64_cpu"][0]) <= 1e-5 * abs(r["loss_fp64_cpu"][0])
     ours, stock = r["step0_grad_rel_err"]["mpit_fp32"], r["step0_grad_rel_err"]["stock_fp32"]
     assert ours <= 4 * stock + 1e-6, (ours, stock)
+
+
+def _bottleneck_net(seed=5):
+    from mpit_amd.models.resnet import Bottleneck, conv1x1
+    from mpit_amd.ops.bn import BatchNormAct2d
+
+    torch.manual_seed(seed)
+    down = torch.nn.Sequential(conv1x1(256, 512, 2), BatchNormAct2d(512, act=False))
+    return torch.nn.Sequential(Bottleneck(256, 128, 2, down), Bottleneck(512, 128)).cuda().to(
+        memory_format=torch.channels_last)
+
+
+@gpu
+def test_weight_cast_plan_fp32_planes_exact():
+    """The pre-split plan (default): every weight operand as three bf16 planes whose sum is
+    the fp32 master (forward) / its fp32 transpose (backward-data), exactly."""
+    net = _bottleneck_net()
+    assert C._F32_BSPLIT
+    plan = C.WeightCastPlan(net, torch.float32)
+    plan.run()
+    torch.cuda.synchronize()
+    for mod, _, (wb, wt) in plan.mods:
+        w = mod.weight.detach()
+        if wb.dtype == torch.bfloat16:
+            assert wb.shape[0] == 3 and w.shape[0] % 128 == 0
+            assert torch.equal(C._unsplit(wb).reshape(-1), C._as_rsc(w).reshape(-1))
+        else:
+            assert wb.data_ptr() == w.data_ptr()
+        if isinstance(mod, C.Conv1x1):
+            _, rt = C.cast_transpose(w, torch.float32)
+        elif mod.stride[0] > 1 and C.strided_dgrad_supported(w.shape[1], w.shape[0], mod.stride[0]):
+            _, rt = C.strided_dgrad_weights(w, mod.stride[0], mod.padding[0], torch.float32)
+        elif mod.stride[0] > 1:
+            rt = None
+        else:
+            _, rt = C.conv_weights(w, True, torch.float32)
+        assert (wt is None) == (rt is None)
+        if wt is not None:
+            got = C._unsplit(wt) if wt.dtype == torch.bfloat16 else wt
+            assert torch.equal(got.reshape(-1), rt.reshape(-1))
+
+
+@gpu
+def test_presplit_weights_bitwise_equal_register_split():
+    """GEMMs reading the pre-split weight planes (FM 4) give bit for bit what the in-register
+    split of the fp32 weights gives (FM 3): same planes, same MFMA sequence. Two bottleneck
+    blocks forward + backward (1x1, 3x3, strided dgrad classes, downsample)."""
+    def run(planes):
+        old = C._F32_BSPLIT
+        C._F32_BSPLIT = planes
+        try:
+            net = _bottleneck_net()
+            plan = C.WeightCastPlan(net, torch.float32)
+        finally:
+            C._F32_BSPLIT = old
+        torch.manual_seed(11)
+        x = _cl(torch.randn(4, 256, 14, 14, device="cuda")).requires_grad_(True)
+        plan.run()
+        y = net(x)
+        y.backward(torch.randn_like(y))
+        plan.invalidate()
+        torch.cuda.synchronize()
+        return [y.detach(), x.grad] + [p.grad for p in net.parameters()]
+
+    a, b = run(True), run(False)
+    for u, v in zip(a, b):
+        assert torch.equal(u.view(torch.int32), v.view(torch.int32))

@@ -635,8 +635,9 @@ class ConvAct2d(nn.Conv2d):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.fused(x):
+            dt = mfma_dtype(x)
             return _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0], self.bias, self.act, None, None,
-                                 None, mfma_dtype(x))
+                                 WeightCastPlan.cached(self, dt), dt)
         y = super().forward(x)
         return F.relu(y) if self.act else y
 
@@ -692,9 +693,11 @@ class WeightCastPlan:
             kind = None
             if isinstance(mod, Conv1x1) and mod.stride == (1, 1):
                 kind = 0
-            elif isinstance(mod, ConvNHWC):
+            elif isinstance(mod, (ConvNHWC, ConvAct2d)):
                 st = mod.stride[0]
                 co, c = mod.weight.shape[0], mod.weight.shape[1]
+                if c % 64 or co % 64:  # never on the MFMA path (conv_supported): no plan entry
+                    continue
                 kind = 0 if st == 1 else (1 if strided_dgrad_supported(c, co, st) else 2)
             if kind is None:
                 continue

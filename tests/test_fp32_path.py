@@ -382,3 +382,35 @@ def test_presplit_weights_bitwise_equal_register_split():
     a, b = run(True), run(False)
     for u, v in zip(a, b):
         assert torch.equal(u.view(torch.int32), v.view(torch.int32))
+
+
+@gpu
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_convact_weight_plan_bitwise(dt):
+    """VGG / AlexNet conv(+bias)+ReLU layers take their per-step weight operands from the
+    model's WeightCastPlan (bf16 casts, or fp32 pre-split planes): bit for bit the result of
+    casting / splitting per call."""
+    torch.manual_seed(2)
+    net = torch.nn.Sequential(C.ConvAct2d(64, 128, 3, padding=1), C.ConvAct2d(128, 128, 3, padding=1),
+                              C.ConvAct2d(128, 256, 3, stride=2, padding=1)).cuda().to(
+        memory_format=torch.channels_last)
+    x0 = _cl(torch.randn(4, 64, 20, 20, device="cuda"))
+
+    def run(plan):
+        net.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_(True)
+        if plan is not None:
+            plan.run()
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=dt == torch.bfloat16):
+            y = net(x)
+        y.float().sum().backward()
+        if plan is not None:
+            plan.invalidate()
+        torch.cuda.synchronize()
+        return [y.detach().float(), x.grad] + [p.grad.clone() for p in net.parameters()]
+
+    plan = C.WeightCastPlan(net, dt)
+    assert plan.njobs == 3
+    a, b = run(plan), run(None)
+    for u, v in zip(a, b):
+        assert torch.equal(u, v)

@@ -54,3 +54,22 @@ for nm in [float(a) for a in sys.argv[1:]] or [25.6, 3.2]:
         print(json.dumps({"n": n, "op": name, "us": round(ms * 1e3, 2), "tb_s": round(n * bpe / ms / 1e9, 2),
                           "unroll": os.environ.get("MPIT_EW_UNROLL", "auto"),
                           "grid": os.environ.get("MPIT_EW_GRID", "auto")}), flush=True)
+
+# K shard pieces due at once (a server at N = K with 3.2 M-element pieces): one apply_ per
+# piece vs ONE multi-segment launch (ops.apply_multi_), same bytes
+if os.environ.get("EW_MULTI", "1") != "0":
+    for k, nm in ((8, 3.2), (8, 0.8), (16, 0.8)):
+        n = int(nm * 1e6) // 64 * 64
+        ps = [torch.randn(n, device="cuda") for _ in range(k)]
+        gs = [torch.randn(n, device="cuda") for _ in range(k)]
+        ws = [torch.empty(n, device="cuda") for _ in range(k)]
+
+        def one_by_one():
+            for p, g, w in zip(ps, gs, ws):
+                ops.apply_(p, g, 0.5, out=w)
+
+        for name, fn in (("apply x%d launches 16B/elem" % k, one_by_one),
+                         ("apply_multi %d segments 16B/elem" % k, lambda: ops.apply_multi_(ps, gs, 0.5, outs=ws))):
+            ms = timeit(fn, per_graph=10)
+            print(json.dumps({"n": k * n, "pieces": k, "op": name, "us": round(ms * 1e3, 2),
+                              "tb_s": round(k * n * 16 / ms / 1e9, 2)}), flush=True)

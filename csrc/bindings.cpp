@@ -51,6 +51,14 @@ PYBIND11_MODULE(_mpit, m) {
          std::vector<float> sc) { ew_update(rule, variant, dev, S(stream), n, ptrs, bf, sc); },
       py::arg("rule"), py::arg("variant"), py::arg("dev"), py::arg("stream"), py::arg("n"), py::arg("ptrs"),
       py::arg("bf"), py::arg("scalars"));
+  m.def(
+      "ew_update_multi",
+      [](int rule, int variant, int dev, uintptr_t stream, std::vector<int64_t> ns,
+         std::vector<std::vector<uintptr_t>> ptrs, uint32_t bf, std::vector<float> sc) {
+        ew_update_multi(rule, variant, dev, S(stream), ns, ptrs, bf, sc);
+      },
+      py::arg("rule"), py::arg("variant"), py::arg("dev"), py::arg("stream"), py::arg("ns"), py::arg("ptrs"),
+      py::arg("bf"), py::arg("scalars"));
   m.def("norms", [](int dev, uintptr_t stream, uintptr_t x, bool bf16, int64_t n, uintptr_t out, uintptr_t ws) {
     norms(dev, S(stream), reinterpret_cast<const void*>(x), bf16, n, reinterpret_cast<float*>(out),
           reinterpret_cast<float*>(ws));
@@ -379,7 +387,8 @@ PYBIND11_MODULE(_mpit, m) {
       .def("stats", [](PSServer& s) {
         auto st = s.stats();
         return py::dict(py::arg("grads") = st.grads, py::arg("pulls") = st.pulls,
-                        py::arg("param_pushes") = st.param_pushes, py::arg("deferred") = st.deferred);
+                        py::arg("param_pushes") = st.param_pushes, py::arg("deferred") = st.deferred,
+                        py::arg("batches") = st.batches);
       });
 
   py::class_<PSClient>(m, "PSClient")

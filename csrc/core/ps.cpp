@@ -51,6 +51,7 @@ PSServer::PSServer(Engine& eng, int ps_id, Window& rx, Window& tx, std::vector<i
   if (device_ && eng_.device() < 0) throw std::invalid_argument("mpit: device server on a rank without a device");
   if (device_ && datapath_ == 1 && !inbox_) throw std::invalid_argument("mpit: datapath 1 needs an inbox buffer");
   if (const char* e = std::getenv("MPIT_PS_FORCE_PIPE")) force_pipe_ = std::atoi(e) != 0;
+  if (const char* e = std::getenv("MPIT_PS_BATCH")) batch_ = std::atoi(e) != 0;
   if (const char* e = std::getenv("MPIT_PS_FAULT")) {
     const std::string f(e);
     const std::string kind = f.substr(0, f.find(':'));
@@ -87,6 +88,13 @@ PSServer::PSServer(Engine& eng, int ps_id, Window& rx, Window& tx, std::vector<i
 
 PSServer::~PSServer() {
   for (int t = 1; t <= 8; ++t) eng_.register_am(ps_am_id(ps_id_, t), [](const Msg&) {});
+  if (fg_) {
+    {
+      std::lock_guard<std::mutex> g(fg_->mu);  // waits for a flush in progress
+      fg_->s = nullptr;
+    }
+    eng_.remove_hook(hook_);
+  }
   if (stream_) {
     hipSetDevice(eng_.device());
     for (auto s : cstream_) {
@@ -108,8 +116,94 @@ void PSServer::finish_on(hipStream_t s, std::function<void()> then) {
 }
 
 void PSServer::start() {
+  if (batch_ && device_ && (rule_.kind == 0 || rule_.kind == 1)) {
+    fg_ = std::make_shared<FlushGate>();
+    fg_->s = this;
+    auto fg = fg_;
+    hook_ = eng_.add_hook([fg]() {
+      std::lock_guard<std::mutex> g(fg->mu);
+      return fg->s ? fg->s->flush_grads() : false;
+    });
+  }
   for (int t : {kTagInit, kTagGrad, kTagParam, kTagHeader, kTagStop})
     eng_.register_am(ps_am_id(ps_id_, t), [this](const Msg& m) { on_msg(m); });
+}
+
+bool PSServer::batchable(int c) const {
+  return fg_ && datapath_ != 1 && !pipelined(client_index(c), c);
+}
+
+void PSServer::queue_grad(int c, bool pull, Sub sb) {
+  if (maybe_fault(1)) return;
+  for (const auto& q : pend_)
+    if (q.sb.o < sb.o + sb.n && sb.o < q.sb.o + q.sb.n) {  // same elements: keep the order
+      flush_grads();
+      break;
+    }
+  if (pend_.size() >= 16) flush_grads();
+  const int ci = client_index(c);
+  bool defer_pull = false;
+  if (ci >= 0) {
+    if (sb.o + sb.n == len_) ++clock_[size_t(ci)];
+    if (pull && staleness_ >= 0) {
+      int64_t mn = clock_[0];
+      for (auto x : clock_) mn = std::min(mn, x);
+      defer_pull = clock_[size_t(ci)] - mn > staleness_;
+    }
+  }
+  pend_.push_back({c, pull, defer_pull, sb});
+}
+
+bool PSServer::flush_grads() {
+  if (pend_.empty()) return false;
+  TraceRange tr("ps_server_update_batch");
+  std::vector<PendingGrad> batch;
+  batch.swap(pend_);
+  hipp(hipSetDevice(eng_.device()), "hipSetDevice");
+  const int64_t es = grad_bf16_ ? 2 : 4;
+  // two launches at most: the pieces that also write the pulled parameters (fused out
+  // operand), and the ones that do not
+  for (int wo = 0; wo < 2; ++wo) {
+    std::vector<int64_t> ns;
+    std::vector<std::vector<uintptr_t>> ptrs;
+    for (const auto& q : batch) {
+      const bool out = q.pull && !q.defer;
+      if (out != (wo == 1)) continue;
+      const int m = member_of(q.c);
+      const void* g = reinterpret_cast<const uint8_t*>(tx_.remote_ptr(m)) + (off_ + q.sb.o) * es;
+      void* o = out ? reinterpret_cast<uint8_t*>(rx_.remote_ptr(m)) + (off_ + q.sb.o) * 4 : nullptr;
+      ns.push_back(q.sb.n);
+      ptrs.push_back(rule_ptrs(g, o, q.sb));
+    }
+    if (ns.empty()) continue;
+    const uint32_t bf = grad_bf16_ ? 2u : 0u;
+    const int v = wo ? kOut : 0;
+    ServerRule r = rule_;
+    r.lr = lr_.load(std::memory_order_relaxed);
+    if (r.kind == 0) ew_update_multi(kApply, v, eng_.device(), stream_, ns, ptrs, bf, {r.a});
+    else ew_update_multi(kRMSProp, v | kAdd, eng_.device(), stream_, ns, ptrs, bf, {r.decay, r.lr, r.mom, r.eps});
+  }
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    for (const auto& q : batch) {
+      if (q.sb.o + q.sb.n == len_) version_.fetch_add(1);
+      ++stats_.grads;
+      if (q.pull && !q.defer) ++stats_.pulls;
+      if (q.defer) {
+        deferred_.push_back({q.c, q.sb});
+        ++stats_.deferred;
+      }
+    }
+    ++stats_.batches;
+  }
+  finish([this, batch] {
+    for (const auto& q : batch) {
+      reply(q.c, kTagGradTail);
+      if (q.pull && !q.defer) reply(q.c, kTagSendParam);
+    }
+  });
+  release_deferred();
+  return true;
 }
 
 int PSServer::member_of(int world_rank) const {
@@ -150,6 +244,8 @@ void PSServer::on_msg(const Msg& m) {
     backlog_.push_back(m);
     return;
   }
+  const bool qgrad = tag == kTagGrad && batchable(m.src);
+  if (!qgrad) flush_grads();  // every other message sees the queued updates applied first
   switch (tag) {
     case kTagInit:
       // a client's shard entry must lie inside this server's shard
@@ -168,7 +264,10 @@ void PSServer::on_msg(const Msg& m) {
       }
       break;
     }
-    case kTagGrad: do_grad(m.src, (m.aux0 & kPsWithPull) != 0, sub_of(m)); break;
+    case kTagGrad:
+      if (qgrad) queue_grad(m.src, (m.aux0 & kPsWithPull) != 0, sub_of(m));
+      else do_grad(m.src, (m.aux0 & kPsWithPull) != 0, sub_of(m));
+      break;
     case kTagHeader: {
       const Sub sb = sub_of(m);
       const int ci = client_index(m.src);
@@ -210,10 +309,7 @@ void PSServer::finish(std::function<void()> then) {
 
 void PSServer::reply(int c, int tag) { eng_.send_am(c, ps_am_id(ps_id_, tag), nullptr, 0); }
 
-void PSServer::apply_rule(const void* g, void* out, Sub sb) {
-  const int dev = device_ ? eng_.device() : -1;
-  const uint32_t bf = grad_bf16_ ? 2u : 0u;
-  const int v = out ? kOut : 0;
+std::vector<uintptr_t> PSServer::rule_ptrs(const void* g, void* out, Sub sb) const {
   auto P = [](const void* x) { return reinterpret_cast<uintptr_t>(x); };
   auto F = [&](void* x) { return P(static_cast<uint8_t*>(x) + sb.o * 4); };  // fp32 state at the piece
   std::vector<uintptr_t> ptrs{F(p_), P(g)};
@@ -221,6 +317,14 @@ void PSServer::apply_rule(const void* g, void* out, Sub sb) {
   for (size_t k = 0; k < st_.size(); ++k)
     if (int(k) < need[rule_.kind]) ptrs.push_back(F(st_[k]));
   if (out) ptrs.push_back(P(out));
+  return ptrs;
+}
+
+void PSServer::apply_rule(const void* g, void* out, Sub sb) {
+  const int dev = device_ ? eng_.device() : -1;
+  const uint32_t bf = grad_bf16_ ? 2u : 0u;
+  const int v = out ? kOut : 0;
+  const std::vector<uintptr_t> ptrs = rule_ptrs(g, out, sb);
   ServerRule r = rule_;  // progress thread only; lr may be changed concurrently (set_lr)
   r.lr = lr_.load(std::memory_order_relaxed);
   // the rule's step counter advances once per client push: on its first piece

@@ -34,6 +34,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
+#include <memory>
 #include <mutex>
 #include <vector>
 
@@ -71,6 +72,7 @@ struct ServerRule {
 
 struct ServerStats {
   int64_t grads = 0, pulls = 0, param_pushes = 0, deferred = 0;
+  int64_t batches = 0;  // multi-piece update launches (see PSServer::flush_grads)
 };
 
 // A contiguous piece of a server's shard named by a message: [o, o + n) relative to the
@@ -112,6 +114,28 @@ class PSServer {
   void do_grad(int c, bool pull, Sub sb);
   void do_pull(int c, Sub sb);
   void apply_rule(const void* g, void* out, Sub sb);
+  std::vector<uintptr_t> rule_ptrs(const void* g, void* out, Sub sb) const;
+  // gradient pieces of the direct (non-link) path that arrive in one progress sweep are
+  // applied together: ONE multi-segment launch (ew_update_multi) instead of one per piece.
+  // Plain apply / RMSProp only (their scalars do not change per push); a piece overlapping
+  // a queued one, any other message and the end of the sweep (engine hook) flush the queue
+  // in arrival order. MPIT_PS_BATCH=0 disables.
+  struct PendingGrad {
+    int c;
+    bool pull, defer;
+    Sub sb;
+  };
+  bool batchable(int c) const;
+  void queue_grad(int c, bool pull, Sub sb);
+  bool flush_grads();
+  bool batch_ = true;
+  std::vector<PendingGrad> pend_;
+  struct FlushGate {
+    std::mutex mu;
+    PSServer* s = nullptr;
+  };
+  std::shared_ptr<FlushGate> fg_;
+  int hook_ = -1;
   void copy_out(int c, Sub sb);
   void reply(int c, int tag);
   void finish(std::function<void()> then);

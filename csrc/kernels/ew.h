@@ -217,9 +217,127 @@ inline void pick_shape(int64_t n4, int& unroll, int64_t& cap) {
   if (env_g > 0) cap = env_g;
 }
 
+// ---- multi-segment form: ONE launch over up to kMaxSegs independent operand sets ----
+// (a parameter server applying several due shard pieces at once: 8 pieces of 3.2 M
+// elements are launch- and tail-bound one by one, one wave of the whole chip together).
+// Segments must be disjoint; every segment's operands 16-B (fp32) / 8-B (bf16) aligned.
+constexpr int kMaxSegs = 16;
+template <int NA>
+struct SegArrays {
+  void* p[kMaxSegs][NA];
+  int64_t n[kMaxSegs];
+  int64_t t0[kMaxSegs + 1];  // first block (one tile of kBlock float4) of each segment
+  int nseg;
+};
+
+template <int NA, uint32_t RD, uint32_t WR, uint32_t BF, class F>
+__global__ __launch_bounds__(kBlock) void ew_multi_kernel(SegArrays<NA> sa, F f) {
+  const int64_t b = blockIdx.x;
+  int s = 0;
+  while (s + 1 < sa.nseg && b >= sa.t0[s + 1]) ++s;
+  const int64_t n = sa.n[s], n4 = n >> 2;
+  const int64_t i4 = (b - sa.t0[s]) * kBlock + threadIdx.x;
+  float x[NA][4];
+  if (i4 < n4) {
+#pragma unroll
+    for (int k = 0; k < NA; ++k)
+      if ((RD >> k) & 1) {
+        if ((BF >> k) & 1) load4<true>(sa.p[s][k], i4, x[k]);
+        else load4<false>(sa.p[s][k], i4, x[k]);
+      }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float e[NA];
+#pragma unroll
+      for (int k = 0; k < NA; ++k) e[k] = x[k][j];
+      f(e);
+#pragma unroll
+      for (int k = 0; k < NA; ++k) x[k][j] = e[k];
+    }
+#pragma unroll
+    for (int k = 0; k < NA; ++k)
+      if ((WR >> k) & 1) {
+        if ((BF >> k) & 1) store4<true>(sa.p[s][k], i4, x[k]);
+        else store4<false>(sa.p[s][k], i4, x[k]);
+      }
+  }
+  // the segment's n % 4 tail: its last block
+  if (b + 1 == sa.t0[s + 1]) {
+    const int64_t i = (n4 << 2) + threadIdx.x;
+    if (i < n) {
+      float e[NA];
+#pragma unroll
+      for (int k = 0; k < NA; ++k)
+        if ((RD >> k) & 1) e[k] = ((BF >> k) & 1) ? load1<true>(sa.p[s][k], i) : load1<false>(sa.p[s][k], i);
+      f(e);
+#pragma unroll
+      for (int k = 0; k < NA; ++k)
+        if ((WR >> k) & 1) {
+          if ((BF >> k) & 1) store1<true>(sa.p[s][k], i, e[k]);
+          else store1<false>(sa.p[s][k], i, e[k]);
+        }
+    }
+  }
+}
+
+// Segment list of the current ew_update_multi call on this thread (see updates.hip): the
+// rule dispatch below is shared, and run_ew takes the segments from here when set.
+struct MultiSegs {
+  std::vector<std::vector<uintptr_t>> ptrs;
+  std::vector<int64_t> ns;
+};
+inline thread_local const MultiSegs* t_multi = nullptr;
+
+template <int NA, uint32_t RD, uint32_t WR, uint32_t BF, class F>
+void run_ew(const Arrays<NA>& a, int64_t n, const F& f, int dev, hipStream_t stream);
+
+template <int NA, uint32_t RD, uint32_t WR, uint32_t BF, class F>
+void run_ew_multi(const MultiSegs& ms, const F& f, int dev, hipStream_t stream) {
+  const size_t ns = ms.ns.size();
+  auto seg = [&](size_t i) {
+    Arrays<NA> a;
+    for (int k = 0; k < NA; ++k) a.p[k] = reinterpret_cast<void*>(ms.ptrs[i][size_t(k)]);
+    return a;
+  };
+  bool ok = dev >= 0 && ns <= size_t(kMaxSegs);
+  for (size_t i = 0; ok && i < ns; ++i) {
+    if (ms.ptrs[i].size() != size_t(NA)) throw std::invalid_argument("mpit: wrong number of operands");
+    for (int k = 0; k < NA; ++k) {
+      if (!(((RD | WR) >> k) & 1)) continue;
+      const uintptr_t al = ((BF >> k) & 1) ? 8 : 16;
+      if (ms.ptrs[i][size_t(k)] % al) ok = false;
+    }
+  }
+  if (!ok) {  // host, too many segments or unaligned: one pass per segment
+    for (size_t i = 0; i < ns; ++i) run_ew<NA, RD, WR, BF, F>(seg(i), ms.ns[i], f, dev, stream);
+    return;
+  }
+  SegArrays<NA> sa{};
+  int64_t t = 0;
+  int m = 0;
+  for (size_t i = 0; i < ns; ++i) {
+    if (ms.ns[i] <= 0) continue;
+    for (int k = 0; k < NA; ++k) sa.p[m][k] = reinterpret_cast<void*>(ms.ptrs[i][size_t(k)]);
+    sa.n[m] = ms.ns[i];
+    sa.t0[m] = t;
+    t += std::max<int64_t>(1, ((ms.ns[i] >> 2) + kBlock - 1) / kBlock);
+    ++m;
+  }
+  if (m == 0) return;
+  sa.t0[m] = t;
+  sa.nseg = m;
+  hipLaunchKernelGGL((ew_multi_kernel<NA, RD, WR, BF, F>), dim3(unsigned(t)), dim3(kBlock), 0, stream, sa, f);
+  hip_check(hipGetLastError(), "ew multi launch");
+}
+
 // dev < 0: host; otherwise launch on `stream` (which belongs to the current device).
 template <int NA, uint32_t RD, uint32_t WR, uint32_t BF, class F>
 void run_ew(const Arrays<NA>& a, int64_t n, const F& f, int dev, hipStream_t stream) {
+  if (const MultiSegs* ms = t_multi) {  // ew_update_multi: the segment list replaces (a, n)
+    t_multi = nullptr;
+    run_ew_multi<NA, RD, WR, BF, F>(*ms, f, dev, stream);
+    return;
+  }
   if (n <= 0) return;
   if (dev < 0) {
     run_host<NA, RD, WR, BF>(a, n, f);

@@ -267,7 +267,7 @@ __device__ __forceinline__ s16x4 ds_tr16(const uint16_t* p) {
 // other instruction of the kernels using this helper reads m0.
 __device__ __forceinline__ void glds16_asm(const void* src, void* lds) {
   const uint32_t l = __builtin_amdgcn_readfirstlane(uint32_t(reinterpret_cast<uintptr_t>((lds_void*)lds)));
-  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(l), "v"(src) : "memory");
+  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(l), "v"(src) : "memory", "m0");
 }
 
 template <int N>
@@ -478,6 +478,15 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
       pbp[i] = Bh + int64_t(n0 + row) * ldb + c * 8;
     }
   }
+  // fp32 tiles issue their LDS DMA from inline asm: with the builtin, hipcc cannot tell
+  // that the next stage's DMA targets the other ring buffer and drains it (vmcnt(0)) before
+  // the first fragment read of the current stage, so the load of stage kt + 1 never
+  // overlaps the MFMAs of stage kt (seen in the gfx950 disassembly of the STAGES = 2 loop).
+  // The counted wait_vmcnt + barrier at the top of each iteration orders the ring.
+  auto glds = [](const void* src, void* lds) {
+    if constexpr (sizeof(T) == 4) glds16_asm(src, lds);
+    else glds16(src, lds);
+  };
   auto issue = [&](int kt, int buf) {
     T* As = smem + buf * TILE;
     T* Bs = As + BM * BK;
@@ -487,9 +496,9 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
         const int hi = hi0[i] + kr, wi = wi0[i] + ks;
         const bool ok = unsigned(hi) < unsigned(geo.H) && unsigned(wi) < unsigned(geo.W);
         const T* src = ok ? A + (((img[i] + hi) * geo.W + wi) * pitch + kc + ca[i]) : zline + ca[i];
-        glds16(src, As + (w * IA + i) * RPI * BK);
+        glds(src, As + (w * IA + i) * RPI * BK);
       } else {
-        glds16(pa[i] + kt * BK, As + (w * IA + i) * RPI * BK);
+        glds(pa[i] + kt * BK, As + (w * IA + i) * RPI * BK);
       }
     }
     if constexpr (BSPLIT) {
@@ -498,11 +507,11 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
       for (int p = 0; p < 3; ++p)
 #pragma unroll
         for (int i = 0; i < IBP; ++i)
-          glds16(pbp[i] + p * bps + kt * 32, Bp + p * (BN * 32) + (w * IBP + i) * 16 * 32);
+          glds(pbp[i] + p * bps + kt * 32, Bp + p * (BN * 32) + (w * IBP + i) * 16 * 32);
     } else {
 #pragma unroll
       for (int i = 0; i < IB; ++i)
-        glds16(pb[i] + kt * BK, Bs + (w * IB + i) * RPI * BK);
+        glds(pb[i] + kt * BK, Bs + (w * IB + i) * RPI * BK);
     }
     if constexpr (CONV) {  // tiles are issued in k order: step to the next (tap, channel) slab
       kc += BK;
@@ -1343,6 +1352,206 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y
   tn_tile_sum<TBN, TBK>(red.mid, red.groups, slice, N, K, n0, k0, red.out, true, red.beta, false);
 }
 
+// fp32 backward-weight GEMM with the operand split done ONCE per element (round 3):
+// dW[n][k] = sum_m Y[m][n] X[m][k] over a 128 x 128 tile, rows in steps of 16.
+// The fp32 rows of the next step are staged in registers (each thread: 8 consecutive rows x
+// 2 adjacent columns, float2 loads — a wave covers 512 contiguous bytes per row), split
+// into the three bf16 planes h, m, l (split3: x = h + m + l) and written k-contiguous into
+// an LDS image [plane][column][16 k] — the transposition the MFMA fragments need (8
+// consecutive rows of one column) happens in that write, so every fragment is one
+// ds_read_b128 per plane. gemm_tn_kernel's fp32 path instead splits each element twice (two
+// waves read it) and reads each fragment with 8 ds_read_b32. Two LDS images alternate: the
+// split of step s + 1 and the MFMAs of step s run between the same pair of barriers.
+// MEASURED SLOWER than gemm_tn_kernel (profiles/wgrad_split_once_r03.md), so opt-in:
+// MPIT_TN_F32S=1.
+// Same planes, same MFMA sequence per output tile (mfma_x3), same k order: bitwise equal
+// to gemm_tn_kernel's bf16x6 path. CONV: X is the implicit im2col of an NHWC image, one tap
+// per column tile (C % 128 == 0); each thread tracks the output pixel of its first row.
+constexpr int kTsR = 16;  // rows per step
+// bf16 offset of (column c, k-half kh) in one plane of the image: 16-B chunk ch = 2c + kh,
+// bits 0..2 XORed with bits 2..4. Conflict-free both ways (exhaustive check over the lane
+// groups of MI355X_MICROARCH's LDS table): a ds_write_b128 group of 8 consecutive lanes
+// (chunks 4l + d) hits 8 distinct 16-B slots of 128 B, and a ds_read_b128 group of 16
+// fragment lanes (chunks 2(c0 + fr) + kh) 16 distinct slots of 256 B.
+__device__ __forceinline__ int tsc(int c, int kh) {
+  const int ch = 2 * c + kh;
+  return (ch ^ ((ch >> 2) & 7)) * 8;
+}
+template <bool CONV>
+__global__ __launch_bounds__(256, 2) void gemm_tn_f32s_kernel(const float* __restrict__ Y, int64_t ldy,
+                                                              const float* __restrict__ X, int64_t ldx,
+                                                              float* __restrict__ part, int64_t M, int N, int K,
+                                                              int64_t rows_per_split, int ntk, int ntiles, ConvGeo geo) {
+  constexpr int TB = 128, TM = 2, TN = 2, WN = 64, WK = 64;
+  constexpr int IMG = 3 * 256 * kTsR;  // bf16 elements of one LDS image
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem_raw[];
+  const int id = xcd_tile(blockIdx.x, gridDim.x);
+  const int tile = id % ntiles, split = id / ntiles;
+  const int n0 = (tile / ntk) * TB, k0 = (tile % ntk) * TB;
+  const int64_t r0 = int64_t(split) * rows_per_split;
+  const int64_t r1 = min(M, r0 + rows_per_split);
+  const int nrows = int(max<int64_t>(0, r1 - r0));
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6, wn = w >> 1, wk = w & 1;
+  const int fr = lane & 31, fh = lane >> 5;
+  // staging role: waves 0, 1 stage Y, waves 2, 3 stage X; rows 8*(w & 1) .. +7 of a step;
+  // columns 2*lane, 2*lane + 1 of the tile
+  const bool isx = w >= 2;
+  const int rh = w & 1;
+  const int col = 2 * lane;
+  const float* src = isx ? (X + (CONV ? 0 : k0 + col)) : (Y + n0 + col);
+  const int64_t ld = isx ? ldx : ldy;
+  // CONV: this column tile's tap (xr, xs) and channel offset, and the output pixel of the
+  // thread's first row of the current step
+  int xr = 0, xs = 0, xc = 0, pn = 0, pho = 0, pwo = 0, dn = 0, dh = 0, dw = 0;
+  if constexpr (CONV) {
+    const int tap = k0 / geo.C;
+    xc = k0 - tap * geo.C + col;
+    xr = tap / geo.S;
+    xs = tap - xr * geo.S;
+    const int hw = geo.Ho * geo.Wo;
+    const int64_t m = r0 + 8 * rh;
+    pn = int(m / hw);
+    const int rem = int(m - int64_t(pn) * hw);
+    pho = rem / geo.Wo;
+    pwo = rem - pho * geo.Wo;
+    dn = kTsR / hw;
+    dh = (kTsR - dn * hw) / geo.Wo;
+    dw = kTsR - dn * hw - dh * geo.Wo;
+  }
+  const int64_t nsteps = (nrows + kTsR - 1) / kTsR;
+
+  // the thread's 8 rows of step st (zeros past the split's end / for padding taps)
+  auto load = [&](int64_t st, f32x2 (&rg)[8]) {
+    const int rb = int(st) * kTsR + 8 * rh;
+    if constexpr (CONV) {
+      if (isx) {
+        int n = pn, ho = pho, wo = pwo;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int hi = ho * geo.stride - geo.pad + xr, wi = wo * geo.stride - geo.padw + xs;
+          const bool ok = rb + e < nrows && unsigned(hi) < unsigned(geo.H) && unsigned(wi) < unsigned(geo.W);
+          rg[e] = ok ? *reinterpret_cast<const f32x2*>(src + ((int64_t(n) * geo.H + hi) * geo.W + wi) * geo.C + xc)
+                     : f32x2{0.f, 0.f};
+          if (++wo == geo.Wo) {
+            wo = 0;
+            if (++ho == geo.Ho) {
+              ho = 0;
+              ++n;
+            }
+          }
+        }
+        // next step's first row: + kTsR rows (at most one carry per digit)
+        pwo += dw;
+        const int cw = pwo >= geo.Wo;
+        pwo -= cw ? geo.Wo : 0;
+        pho += dh + cw;
+        const int ch = pho >= geo.Ho;
+        pho -= ch ? geo.Ho : 0;
+        pn += dn + ch;
+        return;
+      }
+    }
+    const float* p = src + (r0 + rb) * ld;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      rg[e] = rb + e < nrows ? *reinterpret_cast<const f32x2*>(p + int64_t(e) * ld) : f32x2{0.f, 0.f};
+  };
+  // split the staged rows and write both columns' planes (k-contiguous) into image `buf`
+  auto store = [&](const f32x2 (&rg)[8], int buf) {
+    uint16_t* img = smem_raw + buf * IMG;
+    const int cc = (isx ? 128 : 0) + col;  // image column of the first of the two
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = rg[e][j];
+      bf16x8 h, m, l;
+      split3(v, h, m, l);
+      const int o = tsc(cc + j, rh);
+      *reinterpret_cast<bf16x8*>(img + o) = h;
+      *reinterpret_cast<bf16x8*>(img + 256 * kTsR + o) = m;
+      *reinterpret_cast<bf16x8*>(img + 2 * 256 * kTsR + o) = l;
+    }
+  };
+  f32x16 acc[TM][TN], lacc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[i][j][v] = lacc[i][j][v] = 0.f;
+  // the 24 MFMAs of step st from image `buf`
+  auto mma = [&](int buf) {
+    const uint16_t* img = smem_raw + buf * IMG;
+    bf16x8 ah[TM], am[TM], al[TM], bh[TN], bm[TN], bl[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int o = tsc(wn * WN + i * 32 + fr, fh);
+      ah[i] = *reinterpret_cast<const bf16x8*>(img + o);
+      am[i] = *reinterpret_cast<const bf16x8*>(img + 256 * kTsR + o);
+      al[i] = *reinterpret_cast<const bf16x8*>(img + 2 * 256 * kTsR + o);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int o = tsc(128 + wk * WK + j * 32 + fr, fh);
+      bh[j] = *reinterpret_cast<const bf16x8*>(img + o);
+      bm[j] = *reinterpret_cast<const bf16x8*>(img + 256 * kTsR + o);
+      bl[j] = *reinterpret_cast<const bf16x8*>(img + 2 * 256 * kTsR + o);
+    }
+    mfma_x3<TM, TN>(acc, lacc, ah, am, al, bh, bm, bl, false);
+  };
+  auto sync = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  // three register sets: the rows of step s + 3 are requested while step s computes, so a
+  // load has two steps (two barriers) to arrive before its split; images alternate per step
+  f32x2 q0[8], q1[8], q2[8];
+  if (nsteps > 0) load(0, q0);
+  if (nsteps > 1) load(1, q1);
+  if (nsteps > 2) load(2, q2);
+  if (nsteps > 0) store(q0, 0);
+  sync();
+  auto phase = [&](int64_t s, f32x2 (&rl)[8], const f32x2 (&rs)[8], int ib) {
+    if (s + 3 < nsteps) load(s + 3, rl);
+    mma(ib);
+    if (s + 1 < nsteps) store(rs, ib ^ 1);
+    sync();
+  };
+  // unrolled by 6 so the register sets keep static names: step s uses set s % 3, image s % 2
+  for (int64_t st = 0; st < nsteps; st += 6) {
+    phase(st, q0, q1, 0);
+    if (st + 1 >= nsteps) break;
+    phase(st + 1, q1, q2, 1);
+    if (st + 2 >= nsteps) break;
+    phase(st + 2, q2, q0, 0);
+    if (st + 3 >= nsteps) break;
+    phase(st + 3, q0, q1, 1);
+    if (st + 4 >= nsteps) break;
+    phase(st + 4, q1, q2, 0);
+    if (st + 5 >= nsteps) break;
+    phase(st + 5, q2, q0, 1);
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] += lacc[i][j];
+  // D[n][k]: column k = lane&31, row n = (v&3) + 8*(v>>2) + 4*(lane>>5) (gemm_tn_kernel's map)
+  float* out = part + int64_t(split) * N * K;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int n = n0 + wn * WN + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * fh;
+        const int k = k0 + wk * WK + j * 32 + fr;
+        out[int64_t(n) * K + k] = acc[i][j][v];
+      }
+}
+
 // Split reduction, one level: block (x, y) sums splits [y*G, y*G+G) of its float4
 // lanes into out2[y] (or, when gridDim.y == 1, into out with out = beta*out + sum).
 __global__ __launch_bounds__(256) void split_reduce_kernel(const float4* __restrict__ part, int nsplit, int64_t n4,
@@ -1702,7 +1911,7 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
       throw std::invalid_argument("gemm_nt: pre-split B planes need the fp32 bf16x6 path with K % 32 == 0 "
                                   "(and conv channels % 32 == 0), ldb % 8 == 0 and a plane stride >= N * ldb");
     check_ptr(B + uintptr_t(bps) * 2, "B plane 1");
-    if (N % 128) throw std::invalid_argument("gemm_nt: pre-split B planes need N % 128 == 0");
+    if (N % 64) throw std::invalid_argument("gemm_nt: pre-split B planes need N % 64 == 0");
     // MPIT_F32_WAVES=2x2: the 2 x 2 wave grid (FM 4); default 4 x 1 (FM 9)
     static const bool w22 = [] {
       const char* e = std::getenv("MPIT_F32_WAVES");
@@ -2005,6 +2214,23 @@ static void launch_tn_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
     return e && std::atoi(e) <= 2 ? 2 : 4;
   }();
   const int stages = F32 ? 2 : tn_stages;
+  // fp32 128 x 128 tiles, MPIT_TN_F32S=1: the split-once kernel (experiment; bitwise equal,
+  // slower so far: profiles/wgrad_split_once_r03.md)
+  static const bool f32s = [] {
+    const char* e = std::getenv("MPIT_TN_F32S");
+    return e && std::string(e) == "1";
+  }();
+  if (F32 && f32_mode() == 1 && f32s && !fused && tbn == 128 && tbk == 128 && (!geo || (!geo->pitch && geo->C % 128 == 0))) {
+    const size_t shm = size_t(2) * 3 * 256 * kTsR * 2;
+    const auto* yf = reinterpret_cast<const float*>(Y);
+    const auto* xf = reinterpret_cast<const float*>(X);
+    if (geo)
+      hipLaunchKernelGGL(gemm_tn_f32s_kernel<true>, grid, dim3(256), shm, s, yf, ldy, xf, ldx, part, M, N, K, rps, ntk,
+                         ntiles, g);
+    else
+      hipLaunchKernelGGL(gemm_tn_f32s_kernel<false>, grid, dim3(256), shm, s, yf, ldy, xf, ldx, part, M, N, K, rps,
+                         ntk, ntiles, g);
+  } else {
 #define MPIT_TN_OPT_IN(A, B, ST, CV, FMV)                                                                          \
   do {                                                                                                             \
     static const bool opted = (hip_check(hipFuncSetAttribute(reinterpret_cast<const void*>(                       \
@@ -2046,6 +2272,7 @@ static void launch_tn_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
   else if (tbn == 128) MPIT_TN_LAUNCH(128, 64);
   else if (tbk == 128) MPIT_TN_LAUNCH(64, 128);
   else MPIT_TN_LAUNCH(64, 64);
+  }
 #undef MPIT_TN_LAUNCH
 #undef MPIT_TN_LAUNCH1
 #undef MPIT_TN_OPT_IN

@@ -36,6 +36,10 @@ enum Variant : int {
 // dev < 0 → host; else launch on `s` (device `dev`). bf = bitmask of bf16 operands.
 void ew_update(int rule, int variant, int dev, hipStream_t s, int64_t n, const std::vector<uintptr_t>& ptrs,
                uint32_t bf, const std::vector<float>& sc);
+// The same rule over several disjoint segments (ns[i] elements, operands ptrs[i]) in ONE
+// launch (ew.h ew_multi_kernel); host, unaligned or > 16 segments: one pass per segment.
+void ew_update_multi(int rule, int variant, int dev, hipStream_t s, const std::vector<int64_t>& ns,
+                     const std::vector<std::vector<uintptr_t>>& ptrs, uint32_t bf, const std::vector<float>& sc);
 
 // ---- reductions (reduce.hip) ------------------------------------------------------
 // out[0] = Σ|x|, out[1] = Σx², out[2] = max|x|  (deterministic two-pass; `ws` holds

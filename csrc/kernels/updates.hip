@@ -192,4 +192,20 @@ void ew_update(int rule, int variant, int dev, hipStream_t s, int64_t n, const s
   }
 }
 
+void ew_update_multi(int rule, int variant, int dev, hipStream_t s, const std::vector<int64_t>& ns,
+                     const std::vector<std::vector<uintptr_t>>& ptrs, uint32_t bf, const std::vector<float>& sc) {
+  if (ns.size() != ptrs.size()) throw std::invalid_argument("mpit: ew_update_multi: one operand list per segment");
+  if (ns.empty()) return;
+  if (ns.size() == 1) {
+    ew_update(rule, variant, dev, s, ns[0], ptrs[0], bf, sc);
+    return;
+  }
+  const MultiSegs ms{ptrs, ns};
+  struct Reset {
+    ~Reset() { t_multi = nullptr; }
+  } reset;
+  t_multi = &ms;  // consumed by the one run_ew the rule dispatch reaches
+  ew_update(rule, variant, dev, s, ns[0], ptrs[0], bf, sc);
+}
+
 }  // namespace mpit

@@ -149,6 +149,9 @@ def mfma_dtype(x: torch.Tensor):
 # activation (round-2 kernels); default: the per-step weight plan writes it pre-split into
 # three bf16 planes and the GEMM splits only the activation (csrc/kernels/gemm.hip FM 4)
 _F32_BSPLIT = os.environ.get("MPIT_F32_BSPLIT", "1") != "0"
+# column width from which a weight operand is pre-split (MPIT_F32_PLANES_N=64: also the
+# N = 64 GEMMs on 128x64 tiles, 2 blocks per CU instead of 3)
+_F32_PLANES_N = int(os.environ.get("MPIT_F32_PLANES_N", "128"))
 
 
 def _bps(w: torch.Tensor, f32: bool) -> int:
@@ -709,8 +712,8 @@ class WeightCastPlan:
             # only where the GEMM reading it runs 128-wide column tiles (N = co forward, c
             # backward-data) — the 128x64 tiles of N = 64 keep 3 blocks per CU only with the
             # smaller fp32 image, and split that operand in registers
-            pl_b = planes and co % 128 == 0
-            pl_t = planes and c % 128 == 0 and kind != 2
+            pl_b = planes and co % _F32_PLANES_N == 0
+            pl_t = planes and c % _F32_PLANES_N == 0 and kind != 2
             # a detached view: the plan outlives every step, and a view WITH autograd history
             # would keep the weight's AccumulateGrad node (made at build time, on the stream
             # current then) alive into every step — autograd then warns that the node's stream

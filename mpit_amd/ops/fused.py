@@ -73,6 +73,37 @@ def apply_(p, g, a: float = 1.0, out=None):
     return p
 
 
+def apply_multi_(ps: Sequence[torch.Tensor], gs: Sequence[torch.Tensor], a: float = 1.0, outs=None):
+    """K1 over several disjoint (p, g[, out]) segments in ONE launch (a server applying all
+    the shard pieces that are due; ``csrc/kernels/ew.h`` ew_multi_kernel). Same result as
+    one :func:`apply_` per segment, bit for bit."""
+    R = _R()
+    if len(ps) != len(gs) or (outs is not None and len(outs) != len(ps)):
+        raise ValueError("apply_multi_: one gradient (and out) per parameter segment")
+    if not ps:
+        return ps
+    segs, ns, bf = [], [], None
+    for i, (p, g) in enumerate(zip(ps, gs)):
+        ts = [p, g] + ([outs[i]] if outs is not None else [])
+        ref = _check(ts)
+        if ref.device != ps[0].device:
+            raise ValueError("apply_multi_: segments on different devices")
+        b = sum(1 << k for k, t in enumerate(ts) if t.dtype == torch.bfloat16)
+        if b & 1:
+            raise TypeError("operand 0 of this rule must be float32")
+        if bf is not None and b != bf:
+            raise TypeError("apply_multi_: every segment needs the same operand dtypes")
+        bf = b
+        segs.append([t.data_ptr() for t in ts])
+        ns.append(ref.numel())
+    if ps[0].is_cuda:
+        dev, stream = ps[0].device.index, torch.cuda.current_stream(ps[0].device).cuda_stream
+    else:
+        dev, stream = -1, 0
+    native().ew_update_multi(R.APPLY, R.OUT if outs is not None else 0, dev, stream, ns, segs, bf, [float(a)])
+    return ps
+
+
 def apply_sum_(p, grads: Sequence[torch.Tensor], a: float = 1.0, out=None):
     """K1 multi-inbox: ``p += a*Σ g_k`` in one pass (1..8 inboxes)."""
     R = _R()

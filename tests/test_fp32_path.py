@@ -339,7 +339,7 @@ def test_weight_cast_plan_fp32_planes_exact():
     for mod, _, (wb, wt) in plan.mods:
         w = mod.weight.detach()
         if wb.dtype == torch.bfloat16:
-            assert wb.shape[0] == 3 and w.shape[0] % 128 == 0
+            assert wb.shape[0] == 3 and w.shape[0] % C._F32_PLANES_N == 0
             assert torch.equal(C._unsplit(wb).reshape(-1), C._as_rsc(w).reshape(-1))
         else:
             assert wb.data_ptr() == w.data_ptr()
@@ -414,3 +414,43 @@ def test_convact_weight_plan_bitwise(dt):
     a, b = run(plan), run(None)
     for u, v in zip(a, b):
         assert torch.equal(u, v)
+
+
+_WGRAD_CHILD = r"""
+import sys, torch
+sys.path.insert(0, sys.argv[2])
+from mpit_amd.ops import conv as C
+torch.manual_seed(5)
+outs = []
+for M, N, K in [(5000, 256, 128), (12544, 512, 1024), (333, 128, 128)]:
+    y, x = torch.randn(M, N, device="cuda"), torch.randn(M, K, device="cuda")
+    outs.append(C.gemm_tn(y, x))
+    outs.append(C.gemm_tn(y, x, out=torch.ones(N, K, device="cuda"), beta=1.0))
+for n, ci, co, hw, k, s in [(4, 128, 128, 14, 3, 1), (2, 128, 256, 15, 3, 2), (4, 256, 128, 14, 1, 1)]:
+    mod = C.ConvNHWC(ci, co, k, stride=s, padding=k // 2).cuda().to(memory_format=torch.channels_last)
+    xx = torch.randn(n, ci, hw, hw, device="cuda").contiguous(memory_format=torch.channels_last)
+    mod(xx).backward(torch.randn_like(mod(xx)))
+    outs.append(mod.weight.grad)
+torch.cuda.synchronize()
+torch.save([o.cpu() for o in outs], sys.argv[1])
+"""
+
+
+@gpu
+def test_wgrad_split_once_bitwise_equal_per_tile_split(tmp_path):
+    """The split-once fp32 wgrad kernel (gemm_tn_f32s_kernel: each staged element split into
+    bf16 h/m/l once, planes kept in LDS) gives bit for bit gemm_tn_kernel's bf16x6 result
+    (MPIT_TN_F32S=0): same planes, same MFMA order. The knob is read once per process, so
+    each side runs in its own process."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = []
+    for knob in ("1", "0"):
+        f = str(tmp_path / f"w{knob}.pt")
+        subprocess.run([sys.executable, "-c", _WGRAD_CHILD, f, root], check=True, timeout=300,
+                       env=dict(os.environ, MPIT_TN_F32S=knob))
+        res.append(torch.load(f, weights_only=True))
+    for i, (u, v) in enumerate(zip(*res)):
+        assert torch.equal(u.view(torch.int32), v.view(torch.int32)), (i, _rel(u, v))

@@ -59,6 +59,38 @@ def test_apply_bf16_grad_and_out(d):
 
 
 @pytest.mark.parametrize("d", DEVICES)
+@pytest.mark.parametrize("out", [False, True])
+def test_apply_multi_segment_equals_per_segment(d, out):
+    """One multi-segment launch over disjoint pieces (sizes with n % 4 tails, a one-element
+    piece, bf16 gradients) == one apply_ per piece, bit for bit."""
+    d = _dev(d)
+    sizes = [100003, 1, 4096, 7, 33333, 1024]
+    base = rnd(sum(sizes), d)
+    gb = rnd(sum(sizes) + 5, d, dtype=torch.bfloat16)[:sum(sizes)]
+    offs = [sum(sizes[:i]) for i in range(len(sizes))]
+    # 16-B aligned piece starts (the multi kernel's vector path) and an unaligned set (fallback)
+    for align in (True, False):
+        o = [(x + 3) // 4 * 4 if align else x for x in offs]
+        p1 = torch.zeros(o[-1] + sizes[-1] + 8, device=d)
+        p2 = p1.clone()
+        segs1 = [p1[a:a + n] for a, n in zip(o, sizes)]
+        segs2 = [p2[a:a + n] for a, n in zip(o, sizes)]
+        for s1, s2, a, n in zip(segs1, segs2, offs, sizes):
+            s1.copy_(base[a:a + n])
+            s2.copy_(base[a:a + n])
+        gs = [gb[a:a + n].clone() for a, n in zip(offs, sizes)]
+        o1 = [torch.empty(n, device=d) for n in sizes] if out else None
+        o2 = [torch.empty(n, device=d) for n in sizes] if out else None
+        ops.apply_multi_(segs1, gs, -0.3, outs=o1)
+        for i, (s2, g) in enumerate(zip(segs2, gs)):
+            ops.apply_(s2, g, -0.3, out=o2[i] if out else None)
+        assert torch.equal(p1, p2)
+        if out:
+            for u, v in zip(o1, o2):
+                assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("d", DEVICES)
 @pytest.mark.parametrize("ng", [1, 2, 3, 8])
 def test_apply_sum(d, ng):
     d = _dev(d)

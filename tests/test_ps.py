@@ -82,3 +82,17 @@ def test_split_shard_entries_two_ranks_cpu():
     r = _result(run_ranks("ps_train.py", 2, {"MPIT_CPU_ONLY": "1", "T_SPS": "4"}))
     cs = eval(re.search(r"checksums=(\[.*?\])", r).group(1))
     assert max(cs) - min(cs) < 1e-6 * max(1.0, abs(cs[0])), cs
+
+
+@pytest.mark.gpu
+def test_batched_server_updates_bitwise_gpu():
+    """HBM server, one worker pushing its shard as 4 pieces: the pieces a progress sweep
+    finds queued are applied by ONE multi-segment launch (PSServer::flush_grads); the
+    parameters equal the one-launch-per-piece server's (MPIT_PS_BATCH=0) bit for bit."""
+    bits, batches = [], []
+    for b in ("1", "0"):
+        r = _result(run_ranks("ps_train.py", 1, {"T_MODEL": "cnn7", "T_SPS": "4", "MPIT_PS_BATCH": b}))
+        bits.append(int(re.search(r"bits=(-?\d+)", r).group(1)))
+        batches.append(eval(re.search(r"stats=(\{.*\})", r).group(1)).get("batches", 0))
+    assert bits[0] == bits[1], bits
+    assert batches[1] == 0 and batches[0] >= 1, batches

@@ -388,7 +388,7 @@ PYBIND11_MODULE(_mpit, m) {
         auto st = s.stats();
         return py::dict(py::arg("grads") = st.grads, py::arg("pulls") = st.pulls,
                         py::arg("param_pushes") = st.param_pushes, py::arg("deferred") = st.deferred,
-                        py::arg("batches") = st.batches);
+                        py::arg("batches") = st.batches, py::arg("multi") = st.multi);
       });
 
   py::class_<PSClient>(m, "PSClient")

@@ -195,6 +195,7 @@ bool PSServer::flush_grads() {
       }
     }
     ++stats_.batches;
+    if (batch.size() >= 2) ++stats_.multi;
   }
   finish([this, batch] {
     for (const auto& q : batch) {

@@ -72,7 +72,8 @@ struct ServerRule {
 
 struct ServerStats {
   int64_t grads = 0, pulls = 0, param_pushes = 0, deferred = 0;
-  int64_t batches = 0;  // multi-piece update launches (see PSServer::flush_grads)
+  int64_t batches = 0;  // queued-update flushes (see PSServer::flush_grads)
+  int64_t multi = 0;    // of them, flushes that applied >= 2 pieces in one launch
 };
 
 // A contiguous piece of a server's shard named by a message: [o, o + n) relative to the

@@ -412,7 +412,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
   // wave grid over the tile: 2 x 2 (each wave 64 x 64 of a 128 x 128 tile), or for FM 9
   // (pre-split B) 4 x 1: each wave owns 32 rows x all 128 columns, so every A row is split in
   // registers by exactly one wave (the ready-made B planes are the shared operand)
-  constexpr int WGM = (sizeof(T) == 4 && FM == 9) ? 4 : 2, WGN = NW / WGM;
+  constexpr int WGM = (sizeof(T) == 4 && (FM == 9 || FM == 10)) ? 4 : 2, WGN = NW / WGM;
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 32, TN = WN / 32;
   constexpr int EPC = epc<T>();                          // elements per 16-B chunk
@@ -423,7 +423,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
   // FM 4 (fp32, B pre-split): B arrives as three bf16 planes (h, m, l; plane stride bps
   // elements, made once per step by the weight plan), staged as three 64-B-row images of
   // 32 bf16 per row — the A operand alone is split in registers
-  constexpr bool BSPLIT = F32 && (FM == 4 || FM == 9);
+  constexpr bool BSPLIT = F32 && (FM == 4 || FM == 9 || FM == 10);
   constexpr int IBP = BSPLIT ? BN / 16 / NW : 0;  // glds per wave per B plane (16 rows x 64 B)
   constexpr int NI = BSPLIT ? IA + 3 * IBP : IA + IB;
   // elements (T) per stage: A rows, then B (fp32 rows, or 3 bf16 plane images = 1.5x the bytes)
@@ -559,7 +559,57 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
     if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1, (kt + STAGES - 1) % STAGES);
     const T* As = smem + (kt % STAGES) * TILE;
     const T* Bs = As + BM * BK;
-    if constexpr (BSPLIT) {
+    if constexpr (F32 && FM == 10) {
+      // FM 10 (experiment, MPIT_F32_NT=acc1): FM 9 with the six products accumulated in ONE
+      // register set (standard fp32 accumulation instead of the separate small-term sum) and
+      // the fragments of step kk + 1 read before the split + MFMAs of step kk (the 64
+      // registers of the second accumulator hold the prefetched fragments)
+      const uint16_t* Bp = reinterpret_cast<const uint16_t*>(Bs);
+      constexpr int KK = BK / 16;
+      bf16x8 ph[2][TN], pm[2][TN], pl[2][TN];
+      float4 pa[2][TM][2];
+      auto rd = [&](int kk, int sl) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int r = wn * WN + j * 32 + fr;
+          const int o = r * 32 + swz(r, 2 * kk + fh) * 8;
+          ph[sl][j] = *reinterpret_cast<const bf16x8*>(Bp + o);
+          pm[sl][j] = *reinterpret_cast<const bf16x8*>(Bp + BN * 32 + o);
+          pl[sl][j] = *reinterpret_cast<const bf16x8*>(Bp + 2 * BN * 32 + o);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int r = wm * WM + i * 32 + fr;
+          pa[sl][i][0] = *reinterpret_cast<const float4*>(As + r * BK + swzk<BKB>(r, 4 * kk + 2 * fh) * 4);
+          pa[sl][i][1] = *reinterpret_cast<const float4*>(As + r * BK + swzk<BKB>(r, 4 * kk + 2 * fh + 1) * 4);
+        }
+      };
+      rd(0, 0);
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        if (kk + 1 < KK) rd(kk + 1, (kk + 1) & 1);
+        const int sl = kk & 1;
+        bf16x8 ah[TM], am[TM], al[TM];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const float4 x0 = pa[sl][i][0], x1 = pa[sl][i][1];
+          const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+          split3(v, ah[i], am[i], al[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pm[sl][j], ah[i], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ph[sl][j], am[i], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pm[sl][j], am[i], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pl[sl][j], ah[i], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ph[sl][j], al[i], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ph[sl][j], ah[i], acc[i][j], 0, 0, 0);
+          }
+      }
+      continue;
+    } else if constexpr (BSPLIT) {
       // A: the lane's 8 floats of k16 step kk (chunks 4kk + 2fh, +1) split in registers;
       // B: the same k (chunk 2kk + fh of a 64-B plane row) read ready-made from each plane
       const uint16_t* Bp = reinterpret_cast<const uint16_t*>(Bs);
@@ -1912,12 +1962,17 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
                                   "(and conv channels % 32 == 0), ldb % 8 == 0 and a plane stride >= N * ldb");
     check_ptr(B + uintptr_t(bps) * 2, "B plane 1");
     if (N % 64) throw std::invalid_argument("gemm_nt: pre-split B planes need N % 64 == 0");
-    // MPIT_F32_WAVES=2x2: the 2 x 2 wave grid (FM 4); default 4 x 1 (FM 9)
+    // MPIT_F32_WAVES=2x2: the 2 x 2 wave grid (FM 4); default 4 x 1 (FM 9);
+    // MPIT_F32_NT=acc1: FM 10 (one accumulator, fragment prefetch; experiment)
     static const bool w22 = [] {
       const char* e = std::getenv("MPIT_F32_WAVES");
       return e && std::string(e) == "2x2";
     }();
-    fm = w22 ? 4 : 9;
+    static const bool acc1 = [] {
+      const char* e = std::getenv("MPIT_F32_NT");
+      return e && std::string(e) == "acc1";
+    }();
+    fm = w22 ? 4 : (acc1 ? 10 : 9);
   }
   const int nk = K / (fm >= 3 ? 32 : nt_bk_of<T>());
   // MPIT_GEMM_STAGES caps the ring depth (A/B measurements). fp32: the 64 KB epilogue tile
@@ -1974,6 +2029,12 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
                            lda, b, ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g, bps);                          \
         break;                                                                                                     \
       }                                                                                                            \
+      if (fm == 10) {                                                                                              \
+        if (shm > 65536) MPIT_NT_OPT_IN(BM, BN, ST, EPI, CONV, 10);                                                 \
+        hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, ST, EPI, CONV, 10>), dim3(unsigned(nb)), dim3(256), shm, s, a, \
+                           lda, b, ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g, bps);                          \
+        break;                                                                                                     \
+      }                                                                                                            \
       if (fm == 3) {                                                                                               \
         if (shm > 65536) MPIT_NT_OPT_IN(BM, BN, ST, EPI, CONV, 3);                                                  \
         hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, ST, EPI, CONV, 3>), dim3(unsigned(nb)), dim3(256), shm, s, a, \
@@ -2007,12 +2068,12 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
     if (ep.fcoef) fold_plan(ep, dev, s, mtn, ntn);                                                                 \
     /* LDS: the k-tile ring, reused by the epilogue's output tile and reduction table */                      \
     const size_t shm = std::max({size_t(ST) * (size_t(BM) * nt_bkb(BM, BN, fm) +                               \
-                                                (fm == 4 || fm == 9 ? size_t(BN) * 192 : size_t(BN) * nt_bkb(BM, BN, fm))), \
+                                                (fm == 4 || fm >= 9 ? size_t(BN) * 192 : size_t(BN) * nt_bkb(BM, BN, fm))), \
                                  size_t(BM) * BN * sizeof(T), size_t(256) * 8 * 3 * sizeof(float)});          \
     if (geo) MPIT_NT_LAUNCH2(BM, BN, ST, true);                                                           \
     else MPIT_NT_LAUNCH2(BM, BN, ST, false);                                                              \
   } while (0)
-  const int tcfg = fm == 4 || fm == 9 ? 0 : nt_tile_config(N, K, geo != nullptr, geo ? geo->C : 0, F32);
+  const int tcfg = fm == 4 || fm >= 9 ? 0 : nt_tile_config(N, K, geo != nullptr, geo ? geo->C : 0, F32);
   if constexpr (F32) {
     if (tcfg == 1) {
       MPIT_NT_LAUNCH(256, 128, 3);

@@ -70,7 +70,11 @@ def test_apply_multi_segment_equals_per_segment(d, out):
     offs = [sum(sizes[:i]) for i in range(len(sizes))]
     # 16-B aligned piece starts (the multi kernel's vector path) and an unaligned set (fallback)
     for align in (True, False):
-        o = [(x + 3) // 4 * 4 if align else x for x in offs]
+        o, at = [], 0
+        for n in sizes:  # aligned: each piece starts at the next multiple of 4 after the last
+            at = (at + 3) // 4 * 4 if align else at
+            o.append(at)
+            at += n
         p1 = torch.zeros(o[-1] + sizes[-1] + 8, device=d)
         p2 = p1.clone()
         segs1 = [p1[a:a + n] for a, n in zip(o, sizes)]

@@ -86,13 +86,12 @@ def test_split_shard_entries_two_ranks_cpu():
 
 @pytest.mark.gpu
 def test_batched_server_updates_bitwise_gpu():
-    """HBM server, one worker pushing its shard as 4 pieces: the pieces a progress sweep
-    finds queued are applied by ONE multi-segment launch (PSServer::flush_grads); the
+    """HBM server, its co-located client pushing 4 pieces per step: the pieces a progress
+    sweep finds queued are applied by ONE multi-segment launch (PSServer::flush_grads); the
     parameters equal the one-launch-per-piece server's (MPIT_PS_BATCH=0) bit for bit."""
-    bits, batches = [], []
+    res = []
     for b in ("1", "0"):
-        r = _result(run_ranks("ps_train.py", 1, {"T_MODEL": "cnn7", "T_SPS": "4", "MPIT_PS_BATCH": b}))
-        bits.append(int(re.search(r"bits=(-?\d+)", r).group(1)))
-        batches.append(eval(re.search(r"stats=(\{.*\})", r).group(1)).get("batches", 0))
-    assert bits[0] == bits[1], bits
-    assert batches[1] == 0 and batches[0] >= 1, batches
+        r = _result(run_ranks("ps_batch.py", 1, {"MPIT_PS_BATCH": b}))
+        res.append((int(re.search(r"bits=(-?\d+)", r).group(1)), eval(re.search(r"stats=(\{.*\})", r).group(1))))
+    assert res[0][0] == res[1][0], res
+    assert res[1][1].get("batches", 0) == 0 and res[0][1].get("batches", 0) >= 1, res

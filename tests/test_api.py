@@ -61,3 +61,13 @@ def test_api_suite_gpu_two_ranks_one_device():
     out = run_ranks("api_suite.py", 2, {"T_DEVICE": "cuda"}, timeout=300)
     for c in CHECKS:
         assert f"OK {c}" in out, (c, out[-3000:])
+
+
+@pytest.mark.gpu
+def test_api_suite_gpu_three_ranks_one_device():
+    """HBM tensors with n > 2 ranks sharing a GPU take the point-to-point ring
+    all-reduce (RCCL cannot put two ranks on one device); its chunk updates read the receive
+    buffer asynchronously, so the ring alternates two of them (comm.py _ring_allreduce)."""
+    out = run_ranks("api_suite.py", 3, {"T_DEVICE": "cuda"}, timeout=300)
+    for c in CHECKS:
+        assert f"OK {c}" in out, (c, out[-3000:])

@@ -103,6 +103,12 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = False, sanitize: s
     os.makedirs(os.path.dirname(target), exist_ok=True)
     hdr_mtime = max([os.path.getmtime(h) for h in _headers()] + [0.0])
     all_jobs = _jobs(sanitize, build_dir)
+    # a tree shipped without its object files (the GPU box: build/ does not travel) whose
+    # module is newer than every source and header is up to date as it is
+    if not force and os.path.exists(target) and not all(os.path.exists(o) for (_, o, _) in all_jobs):
+        newest_src = max([os.path.getmtime(s) for (s, _, _) in all_jobs] + [hdr_mtime])
+        if os.path.getmtime(target) >= newest_src:
+            return target
     todo = [(s, o, c) for (s, o, c) in all_jobs if force or _stale(s, o, hdr_mtime)]
 
     def run(job):

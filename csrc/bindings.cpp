@@ -86,42 +86,46 @@ PYBIND11_MODULE(_mpit, m) {
       "bn_act_fwd",
       [](int dev, uintptr_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C, uintptr_t gamma,
          uintptr_t beta, uintptr_t rmean, uintptr_t rvar, uintptr_t save_mean, uintptr_t save_rstd, uintptr_t ws,
-         float momentum, float eps, bool relu, uintptr_t mask, uintptr_t stats, int64_t nstat) {
+         float momentum, float eps, bool relu, uintptr_t mask, uintptr_t stats, int64_t nstat, uintptr_t amax) {
         bn_act_fwd(dev, S(s), bf16, x, res, y, M, C, gamma, beta, rmean, rvar, save_mean, save_rstd, ws, momentum, eps,
-                   relu, mask, stats, nstat);
+                   relu, mask, stats, nstat, amax);
       },
       py::arg("dev"), py::arg("stream"), py::arg("bf16"), py::arg("x"), py::arg("res"), py::arg("y"), py::arg("M"),
       py::arg("C"), py::arg("gamma"), py::arg("beta"), py::arg("rmean"), py::arg("rvar"), py::arg("save_mean"),
       py::arg("save_rstd"), py::arg("ws"), py::arg("momentum"), py::arg("eps"), py::arg("relu"), py::arg("mask"),
-      py::arg("stats") = 0, py::arg("nstat") = 0);
+      py::arg("stats") = 0, py::arg("nstat") = 0, py::arg("amax") = 0);
   m.def("bn_act_apply", [](int dev, uintptr_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C,
                            uintptr_t coef, bool relu) { bn_act_apply(dev, S(s), bf16, x, res, y, M, C, coef, relu); });
   m.def(
       "bn_act_bwd",
       [](int dev, uintptr_t s, bool bf16, uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t dx, uintptr_t dres,
          int64_t M, int C, uintptr_t gamma, uintptr_t mean, uintptr_t rstd, uintptr_t dgamma, uintptr_t dbeta,
-         uintptr_t ws, bool relu, uintptr_t part, int64_t npart, uintptr_t coef) {
+         uintptr_t ws, bool relu, uintptr_t part, int64_t npart, uintptr_t coef, uintptr_t amax) {
         bn_act_bwd(dev, S(s), bf16, dy, mask, x, dx, dres, M, C, gamma, mean, rstd, dgamma, dbeta, ws, relu, part, npart,
-                   coef);
+                   coef, amax);
       },
       py::arg("dev"), py::arg("stream"), py::arg("bf16"), py::arg("dy"), py::arg("mask"), py::arg("x"), py::arg("dx"),
       py::arg("dres"), py::arg("M"), py::arg("C"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
       py::arg("dgamma"), py::arg("dbeta"), py::arg("ws"), py::arg("relu"), py::arg("part") = 0, py::arg("npart") = 0,
-      py::arg("coef") = 0);
+      py::arg("coef") = 0, py::arg("amax") = 0);
   m.def(
       "bn_pair_apply",
       [](int dev, uintptr_t s, uintptr_t x1, uintptr_t coef1, uintptr_t x2, uintptr_t coef2, uintptr_t y, int64_t M,
-         int C, uintptr_t mask, bool f32) { bn_pair_apply(dev, S(s), x1, coef1, x2, coef2, y, M, C, mask, f32); },
+         int C, uintptr_t mask, bool f32, uintptr_t amax, uintptr_t scratch) {
+        bn_pair_apply(dev, S(s), x1, coef1, x2, coef2, y, M, C, mask, f32, amax, scratch);
+      },
       py::arg("dev"), py::arg("stream"), py::arg("x1"), py::arg("coef1"), py::arg("x2"), py::arg("coef2"), py::arg("y"),
-      py::arg("M"), py::arg("C"), py::arg("mask"), py::arg("f32") = false);
+      py::arg("M"), py::arg("C"), py::arg("mask"), py::arg("f32") = false, py::arg("amax") = 0, py::arg("scratch") = 0);
   m.def(
       "bn_pair_bwd_apply",
       [](int dev, uintptr_t s, uintptr_t dy, uintptr_t mask, uintptr_t x1, uintptr_t coef1, uintptr_t dx1, uintptr_t x2,
-         uintptr_t coef2, uintptr_t dx2, int64_t M, int C,
-         bool f32) { bn_pair_bwd_apply(dev, S(s), dy, mask, x1, coef1, dx1, x2, coef2, dx2, M, C, f32); },
+         uintptr_t coef2, uintptr_t dx2, int64_t M, int C, bool f32, uintptr_t amax1, uintptr_t amax2,
+         uintptr_t scratch) {
+        bn_pair_bwd_apply(dev, S(s), dy, mask, x1, coef1, dx1, x2, coef2, dx2, M, C, f32, amax1, amax2, scratch);
+      },
       py::arg("dev"), py::arg("stream"), py::arg("dy"), py::arg("mask"), py::arg("x1"), py::arg("coef1"),
       py::arg("dx1"), py::arg("x2"), py::arg("coef2"), py::arg("dx2"), py::arg("M"), py::arg("C"),
-      py::arg("f32") = false);
+      py::arg("f32") = false, py::arg("amax1") = 0, py::arg("amax2") = 0, py::arg("scratch") = 0);
   m.def("gemm_nt_supported", &gemm_nt_supported, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("f32") = false);
   m.def("gemm_nt_stats_floats", &gemm_nt_stats_floats);
   m.def("gemm_nt_tiles", &gemm_nt_tiles);
@@ -131,10 +135,12 @@ PYBIND11_MODULE(_mpit, m) {
          int64_t ldc, uintptr_t stats, uintptr_t cin, uintptr_t cmask, uintptr_t red_part, uintptr_t red_x,
          uintptr_t red_mask, uintptr_t red_mean, int64_t red_row0, uintptr_t red_part2, uintptr_t red_x2,
          uintptr_t red_mean2, bool f32, uintptr_t fold_coef, uintptr_t fold_gamma, uintptr_t fold_rstd,
-         uintptr_t fold_dgamma, uintptr_t fold_dbeta, uintptr_t fold_lvl, int64_t bps) {
+         uintptr_t fold_dgamma, uintptr_t fold_dbeta, uintptr_t fold_lvl, int64_t bps, uintptr_t amax_a,
+         uintptr_t amax_b) {
         BnRed r{red_part, red_x, red_mask, red_mean, red_row0, red_part2, red_x2, red_mean2};
         r.fcoef = fold_coef; r.fgamma = fold_gamma; r.frstd = fold_rstd;
         r.fdgamma = fold_dgamma; r.fdbeta = fold_dbeta; r.flvl = fold_lvl;
+        r.amax_a = amax_a; r.amax_b = amax_b;
         gemm_nt(dev, S(s), M, N, K, A, lda, B, ldb, C, ldc, stats, cin, cmask, &r, f32, bps);
       },
       py::arg("dev"), py::arg("stream"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("A"), py::arg("lda"),
@@ -143,7 +149,7 @@ PYBIND11_MODULE(_mpit, m) {
       py::arg("red_mean") = 0, py::arg("red_row0") = 0, py::arg("red_part2") = 0, py::arg("red_x2") = 0,
       py::arg("red_mean2") = 0, py::arg("f32") = false, py::arg("fold_coef") = 0, py::arg("fold_gamma") = 0,
       py::arg("fold_rstd") = 0, py::arg("fold_dgamma") = 0, py::arg("fold_dbeta") = 0, py::arg("fold_lvl") = 0,
-      py::arg("bps") = 0);
+      py::arg("bps") = 0, py::arg("amax_a") = 0, py::arg("amax_b") = 0);
   m.def("gemm_nt_fold_lvl_floats", &gemm_nt_fold_lvl_floats);
   m.def("gemm_tn_supported", &gemm_tn_supported);
   m.def("gemm_tn_ws_floats", &gemm_tn_ws_floats);
@@ -152,9 +158,12 @@ PYBIND11_MODULE(_mpit, m) {
   m.def(
       "gemm_tn",
       [](int dev, uintptr_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X, int64_t ldx,
-         uintptr_t out, uintptr_t ws, float beta, bool f32) { gemm_tn(dev, S(s), M, N, K, Y, ldy, X, ldx, out, ws, beta, f32); },
+         uintptr_t out, uintptr_t ws, float beta, bool f32, uintptr_t amax_y, uintptr_t amax_x) {
+        gemm_tn(dev, S(s), M, N, K, Y, ldy, X, ldx, out, ws, beta, f32, amax_y, amax_x);
+      },
       py::arg("dev"), py::arg("stream"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("Y"), py::arg("ldy"),
-      py::arg("X"), py::arg("ldx"), py::arg("out"), py::arg("ws"), py::arg("beta"), py::arg("f32") = false);
+      py::arg("X"), py::arg("ldx"), py::arg("out"), py::arg("ws"), py::arg("beta"), py::arg("f32") = false,
+      py::arg("amax_y") = 0, py::arg("amax_x") = 0);
   m.def(
       "cast_transpose",
       [](int dev, uintptr_t s, uintptr_t w, int R, int Cc, uintptr_t wb, uintptr_t wt, int taps, bool f32) {
@@ -163,7 +172,7 @@ PYBIND11_MODULE(_mpit, m) {
       py::arg("dev"), py::arg("stream"), py::arg("w"), py::arg("R"), py::arg("Cc"), py::arg("wb"), py::arg("wt"),
       py::arg("taps") = 1, py::arg("f32") = false);
   m.def("cast_job_bytes", &cast_job_bytes);
-  m.def("cast_jobs_build", [](uintptr_t table, std::vector<std::array<int64_t, 10>> specs) {
+  m.def("cast_jobs_build", [](uintptr_t table, std::vector<std::array<int64_t, 11>> specs) {
     return cast_jobs_build(table, specs);
   });
   m.def("cast_jobs_run", [](int dev, uintptr_t s, uintptr_t table, int njobs, int64_t nblocks) {
@@ -188,10 +197,12 @@ PYBIND11_MODULE(_mpit, m) {
          uintptr_t w, uintptr_t y, uintptr_t stats, uintptr_t cin, uintptr_t bias, bool relu, uintptr_t red_part,
          uintptr_t red_x, uintptr_t red_mask, uintptr_t red_mean, int64_t red_row0, uintptr_t red_part2,
          uintptr_t red_x2, uintptr_t red_mean2, bool f32, uintptr_t fold_coef, uintptr_t fold_gamma,
-         uintptr_t fold_rstd, uintptr_t fold_dgamma, uintptr_t fold_dbeta, uintptr_t fold_lvl, int64_t bps) {
+         uintptr_t fold_rstd, uintptr_t fold_dgamma, uintptr_t fold_dbeta, uintptr_t fold_lvl, int64_t bps,
+         uintptr_t amax_a, uintptr_t amax_b) {
         BnRed r{red_part, red_x, red_mask, red_mean, red_row0, red_part2, red_x2, red_mean2};
         r.fcoef = fold_coef; r.fgamma = fold_gamma; r.frstd = fold_rstd;
         r.fdgamma = fold_dgamma; r.fdbeta = fold_dbeta; r.flvl = fold_lvl;
+        r.amax_a = amax_a; r.amax_b = amax_b;
         conv_fwd(dev, S(s), Nb, H, W, C, Co, R, S_, stride, pad, x, w, y, stats, cin, bias, relu, &r, f32, bps);
       },
       py::arg("dev"), py::arg("stream"), py::arg("Nb"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("Co"),
@@ -200,7 +211,8 @@ PYBIND11_MODULE(_mpit, m) {
       py::arg("red_x") = 0, py::arg("red_mask") = 0, py::arg("red_mean") = 0, py::arg("red_row0") = 0,
       py::arg("red_part2") = 0, py::arg("red_x2") = 0, py::arg("red_mean2") = 0, py::arg("f32") = false,
       py::arg("fold_coef") = 0, py::arg("fold_gamma") = 0, py::arg("fold_rstd") = 0, py::arg("fold_dgamma") = 0,
-      py::arg("fold_dbeta") = 0, py::arg("fold_lvl") = 0, py::arg("bps") = 0);
+      py::arg("fold_dbeta") = 0, py::arg("fold_lvl") = 0, py::arg("bps") = 0, py::arg("amax_a") = 0,
+      py::arg("amax_b") = 0);
   m.def("conv_dgrad_strided_wfloats", &conv_dgrad_strided_wfloats);
   m.def(
       "conv_dgrad_strided_weights",
@@ -213,15 +225,17 @@ PYBIND11_MODULE(_mpit, m) {
       "conv_dgrad_strided",
       [](int dev, uintptr_t s, int Nb, int H, int W, int C, int Co, int R, int S_, int stride, int pad, uintptr_t dy,
          uintptr_t wcls, uintptr_t dx, uintptr_t red_part, uintptr_t red_x, uintptr_t red_mask, uintptr_t red_mean,
-         uintptr_t red_part2, uintptr_t red_x2, uintptr_t red_mean2, bool f32, int64_t bps) {
-        const BnRed r{red_part, red_x, red_mask, red_mean, 0, red_part2, red_x2, red_mean2};
+         uintptr_t red_part2, uintptr_t red_x2, uintptr_t red_mean2, bool f32, int64_t bps, uintptr_t amax_a,
+         uintptr_t amax_b) {
+        BnRed r{red_part, red_x, red_mask, red_mean, 0, red_part2, red_x2, red_mean2};
+        r.amax_a = amax_a; r.amax_b = amax_b;
         conv_dgrad_strided(dev, S(s), Nb, H, W, C, Co, R, S_, stride, pad, dy, wcls, dx, &r, f32, bps);
       },
       py::arg("dev"), py::arg("stream"), py::arg("Nb"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("Co"),
       py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("dy"), py::arg("wcls"), py::arg("dx"),
       py::arg("red_part") = 0, py::arg("red_x") = 0, py::arg("red_mask") = 0, py::arg("red_mean") = 0,
       py::arg("red_part2") = 0, py::arg("red_x2") = 0, py::arg("red_mean2") = 0, py::arg("f32") = false,
-      py::arg("bps") = 0);
+      py::arg("bps") = 0, py::arg("amax_a") = 0, py::arg("amax_b") = 0);
   m.def("relu_bias_bwd_ws_floats", &relu_bias_bwd_ws_floats);
   m.def(
       "relu_bias_bwd",
@@ -248,12 +262,12 @@ PYBIND11_MODULE(_mpit, m) {
   m.def(
       "conv_wgrad",
       [](int dev, uintptr_t s, int Nb, int H, int W, int C, int Co, int R, int S_, int stride, int pad, uintptr_t dy,
-         uintptr_t x, uintptr_t dw, uintptr_t ws, float beta, bool f32) {
-        conv_wgrad(dev, S(s), Nb, H, W, C, Co, R, S_, stride, pad, dy, x, dw, ws, beta, f32);
+         uintptr_t x, uintptr_t dw, uintptr_t ws, float beta, bool f32, uintptr_t amax_y, uintptr_t amax_x) {
+        conv_wgrad(dev, S(s), Nb, H, W, C, Co, R, S_, stride, pad, dy, x, dw, ws, beta, f32, amax_y, amax_x);
       },
       py::arg("dev"), py::arg("stream"), py::arg("Nb"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("Co"),
       py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("dy"), py::arg("x"), py::arg("dw"),
-      py::arg("ws"), py::arg("beta"), py::arg("f32") = false);
+      py::arg("ws"), py::arg("beta"), py::arg("f32") = false, py::arg("amax_y") = 0, py::arg("amax_x") = 0);
 
   py::class_<Engine>(m, "Engine")
       .def(py::init<const std::string&, int, int, bool, int, int64_t>(), py::arg("name"), py::arg("world"),

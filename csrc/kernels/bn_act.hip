@@ -76,6 +76,65 @@ struct Vec<float> {
 // block size: the largest multiple of G that is <= 256 (G = channel groups per row)
 inline int block_for(int G) { return G >= 256 ? G : (256 / G) * G; }
 
+// ---------------------------------------------------------------- output bound (fp16x3)
+// An apply kernel that produces the next convolution's fp32 GEMM operand also writes max|out|
+// over the whole tensor: the fp16x3 GEMMs (gemm.hip FM 11) derive the operand's power-of-two
+// scale from it. Each block writes its maximum (write-through) to scratch[blockIdx], takes a
+// ticket, and the launch's last block reduces scratch into *amax and resets the ticket — no
+// pre-zeroed output, no host round trip. Ticket sets rotate per launch over kAmaxSlots
+// (launches in flight at once: the BN kernels run on one stream; two per pair launch).
+constexpr int kAmaxSlots = 64;
+__device__ uint32_t g_amax_tickets[kAmaxSlots];
+
+struct AmaxOut {
+  float* amax;      // null: not wanted
+  float* scratch;   // >= gridDim.x floats
+  uint32_t* tick;
+};
+
+AmaxOut amax_out(uintptr_t amax, float* scratch) {
+  AmaxOut o{reinterpret_cast<float*>(amax), scratch, nullptr};
+  if (!amax) return o;
+  static std::atomic<uint32_t> launches{0};
+  uint32_t* base = nullptr;
+  hip_check(hipGetSymbolAddress(reinterpret_cast<void**>(&base), HIP_SYMBOL(g_amax_tickets)), "amax ticket symbol");
+  o.tick = base + launches.fetch_add(1) % kAmaxSlots;
+  return o;
+}
+
+__device__ __forceinline__ float block_max(float m, float* red /* >= 16 floats of LDS */) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  const int w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = m;
+  __syncthreads();
+  float b = red[0];
+  for (int k = 1; k < nw; ++k) b = fmaxf(b, red[k]);
+  return b;  // every thread
+}
+
+__device__ __forceinline__ void amax_finish(float m, const AmaxOut& o) {
+  __shared__ float red[16];
+  __shared__ uint32_t prev;
+  const float b = block_max(m, red);
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(&o.scratch[blockIdx.x], b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    prev = atomicAdd(o.tick, 1u);
+  }
+  __syncthreads();
+  if (prev != gridDim.x - 1) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  float r = 0.f;
+  for (int k = threadIdx.x; k < int(gridDim.x); k += blockDim.x) r = fmaxf(r, o.scratch[k]);
+  r = block_max(r, red);
+  if (threadIdx.x == 0) {
+    *o.amax = r;
+    __hip_atomic_store(o.tick, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // ---------------------------------------------------------------- forward: statistics
 template <typename T>
 __global__ __launch_bounds__(1024) void bn_stats_kernel(const T* __restrict__ x, int64_t M, int C,
@@ -376,7 +435,7 @@ void launch_tiles_finalize(hipStream_t s, const float* part, int64_t nt, int C, 
 template <typename T, bool RES, bool RELU, bool MASK>
 __global__ __launch_bounds__(1024) void bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res,
                                                         T* __restrict__ y, const float* __restrict__ coef, int64_t nvec,
-                                                        int C, uint8_t* __restrict__ mask) {
+                                                        int C, uint8_t* __restrict__ mask, AmaxOut am) {
   constexpr int V = Vec<T>::N;
   const int G = C / V;
   int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -388,6 +447,7 @@ __global__ __launch_bounds__(1024) void bn_apply_kernel(const T* __restrict__ x,
     sc[v] = coef[g * V + v];
     sh[v] = coef[C + g * V + v];
   }
+  float mx = 0.f;
   for (; i < nvec; i += stride) {
     float a[V], rr[V];
     Vec<T>::load(x + i * V, a);
@@ -399,6 +459,7 @@ __global__ __launch_bounds__(1024) void bn_apply_kernel(const T* __restrict__ x,
       if constexpr (RES) t += rr[v];
       if constexpr (RELU) t = fmaxf(t, 0.f);
       a[v] = t;
+      mx = fmaxf(mx, fabsf(t));
     }
     Vec<T>::store(y + i * V, a);
     if constexpr (MASK) {  // (rounding to bf16 never flips the sign of a normal number)
@@ -407,6 +468,7 @@ __global__ __launch_bounds__(1024) void bn_apply_kernel(const T* __restrict__ x,
       mask[i] = uint8_t(bits);
     }
   }
+  if (am.amax) amax_finish(mx, am);
 }
 
 // ---------------------------------------------------------------- backward: reduce
@@ -510,7 +572,7 @@ template <typename T, bool RELU, bool RESGRAD>
 __global__ __launch_bounds__(1024) void bn_bwd_apply_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ mask,
                                                             const T* __restrict__ x, const float* __restrict__ coef,
                                                             T* __restrict__ dx, T* __restrict__ dres, int64_t nvec,
-                                                            int C) {
+                                                            int C, AmaxOut am) {
   constexpr int V = Vec<T>::N;
   const int G = C / V;
   int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -523,6 +585,7 @@ __global__ __launch_bounds__(1024) void bn_bwd_apply_kernel(const T* __restrict_
     Cc[v] = coef[C + g * V + v];
     B[v] = coef[2 * C + g * V + v];
   }
+  float mx = 0.f;
   for (; i < nvec; i += stride) {
     float d[V], xx[V];
     Vec<T>::load(dy + i * V, d);
@@ -535,10 +598,12 @@ __global__ __launch_bounds__(1024) void bn_bwd_apply_kernel(const T* __restrict_
       if constexpr (RELU) dz = (mb >> v) & 1u ? dz : 0.f;
       d[v] = dz;
       xx[v] = fmaf(A[v], dz, fmaf(Cc[v], xx[v], B[v]));
+      mx = fmaxf(mx, fabsf(xx[v]));
     }
     Vec<T>::store(dx + i * V, xx);
     if constexpr (RESGRAD) Vec<T>::store(dres + i * V, d);
   }
+  if (am.amax) amax_finish(mx, am);
 }
 
 // ---------------------------------------------------------------- BN pair (ResNet downsample)
@@ -549,7 +614,7 @@ __global__ __launch_bounds__(1024) void bn_pair_apply_kernel(const T* __restrict
                                                              const T* __restrict__ x2,
                                                              T* __restrict__ y, const float* __restrict__ coef1,
                                                              const float* __restrict__ coef2, int64_t nvec, int C,
-                                                             uint8_t* __restrict__ mask) {
+                                                             uint8_t* __restrict__ mask, AmaxOut am) {
   constexpr int V = 8;
   const int G = C / V;
   int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -563,6 +628,7 @@ __global__ __launch_bounds__(1024) void bn_pair_apply_kernel(const T* __restrict
     a2[v] = coef2[g * V + v];
     b2[v] = coef2[C + g * V + v];
   }
+  float mx = 0.f;
   for (; i < nvec; i += stride) {
     float p[V], q[V];
     Vec<T>::load(x1 + i * V, p);
@@ -573,10 +639,12 @@ __global__ __launch_bounds__(1024) void bn_pair_apply_kernel(const T* __restrict
       const float t = fmaxf(fmaf(p[v], a1[v], b1[v]) + fmaf(q[v], a2[v], b2[v]), 0.f);
       p[v] = t;
       bits |= uint32_t(t > 0.f) << v;
+      mx = fmaxf(mx, t);
     }
     Vec<T>::store(y + i * V, p);
     mask[i] = uint8_t(bits);
   }
+  if (am.amax) amax_finish(mx, am);
 }
 
 // dz = dy * mask; dx1 = A1 dz + C1 x1 + B1, dx2 = A2 dz + C2 x2 + B2 (coef [3][C] each)
@@ -584,7 +652,7 @@ template <typename T>
 __global__ __launch_bounds__(1024) void bn_pair_bwd_apply_kernel(
     const T* __restrict__ dy, const uint8_t* __restrict__ mask, const T* __restrict__ x1,
     const float* __restrict__ coef1, T* __restrict__ dx1, const T* __restrict__ x2,
-    const float* __restrict__ coef2, T* __restrict__ dx2, int64_t nvec, int C) {
+    const float* __restrict__ coef2, T* __restrict__ dx2, int64_t nvec, int C, AmaxOut am1, AmaxOut am2) {
   constexpr int V = 8;
   const int G = C / V;
   int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -600,6 +668,7 @@ __global__ __launch_bounds__(1024) void bn_pair_bwd_apply_kernel(
     C2[v] = coef2[C + g * V + v];
     B2[v] = coef2[2 * C + g * V + v];
   }
+  float m1 = 0.f, m2 = 0.f;
   for (; i < nvec; i += stride) {
     float d[V], p[V], q[V];
     Vec<T>::load(dy + i * V, d);
@@ -611,10 +680,14 @@ __global__ __launch_bounds__(1024) void bn_pair_bwd_apply_kernel(
       const float dz = (mb >> v) & 1u ? d[v] : 0.f;
       p[v] = fmaf(A1[v], dz, fmaf(C1[v], p[v], B1[v]));
       q[v] = fmaf(A2[v], dz, fmaf(C2[v], q[v], B2[v]));
+      m1 = fmaxf(m1, fabsf(p[v]));
+      m2 = fmaxf(m2, fabsf(q[v]));
     }
     Vec<T>::store(dx1 + i * V, p);
     Vec<T>::store(dx2 + i * V, q);
   }
+  if (am1.amax) amax_finish(m1, am1);
+  if (am2.amax) amax_finish(m2, am2);
 }
 
 void check_shape(int64_t M, int C, int V, uintptr_t ptr) {
@@ -639,7 +712,7 @@ int apply_grid(int64_t nvec, int block) {
 
 template <typename T>
 void launch_apply(hipStream_t s, const T* x, const T* res, T* y, int64_t M, int C, const float* coef, bool relu,
-                  uint8_t* mask) {
+                  uint8_t* mask, AmaxOut am = {}) {
   constexpr int V = Vec<T>::N;
   const int G = C / V;
   const int blk = block_for(G);
@@ -647,22 +720,24 @@ void launch_apply(hipStream_t s, const T* x, const T* res, T* y, int64_t M, int 
   const int grid = apply_grid(nvec, blk);
   const dim3 g(grid), b(blk);
   if (relu && mask) {
-    if (res) hipLaunchKernelGGL((bn_apply_kernel<T, true, true, true>), g, b, 0, s, x, res, y, coef, nvec, C, mask);
-    else hipLaunchKernelGGL((bn_apply_kernel<T, false, true, true>), g, b, 0, s, x, res, y, coef, nvec, C, mask);
+    if (res) hipLaunchKernelGGL((bn_apply_kernel<T, true, true, true>), g, b, 0, s, x, res, y, coef, nvec, C, mask, am);
+    else hipLaunchKernelGGL((bn_apply_kernel<T, false, true, true>), g, b, 0, s, x, res, y, coef, nvec, C, mask, am);
   } else if (relu) {
-    if (res) hipLaunchKernelGGL((bn_apply_kernel<T, true, true, false>), g, b, 0, s, x, res, y, coef, nvec, C, mask);
-    else hipLaunchKernelGGL((bn_apply_kernel<T, false, true, false>), g, b, 0, s, x, res, y, coef, nvec, C, mask);
+    if (res) hipLaunchKernelGGL((bn_apply_kernel<T, true, true, false>), g, b, 0, s, x, res, y, coef, nvec, C, mask, am);
+    else hipLaunchKernelGGL((bn_apply_kernel<T, false, true, false>), g, b, 0, s, x, res, y, coef, nvec, C, mask, am);
   } else {
-    if (res) hipLaunchKernelGGL((bn_apply_kernel<T, true, false, false>), g, b, 0, s, x, res, y, coef, nvec, C, mask);
-    else hipLaunchKernelGGL((bn_apply_kernel<T, false, false, false>), g, b, 0, s, x, res, y, coef, nvec, C, mask);
+    if (res) hipLaunchKernelGGL((bn_apply_kernel<T, true, false, false>), g, b, 0, s, x, res, y, coef, nvec, C, mask, am);
+    else hipLaunchKernelGGL((bn_apply_kernel<T, false, false, false>), g, b, 0, s, x, res, y, coef, nvec, C, mask, am);
   }
 }
 
 template <typename T>
 void fwd_impl(int dev, hipStream_t s, const T* x, const T* res, T* y, int64_t M, int C, const float* gamma,
               const float* beta, float* rmean, float* rvar, float* save_mean, float* save_rstd, float* ws,
-              float momentum, float eps, bool relu, uint8_t* mask, const float* tstats, int64_t nstat) {
+              float momentum, float eps, bool relu, uint8_t* mask, const float* tstats, int64_t nstat,
+              uintptr_t amax) {
   constexpr int V = Vec<T>::N;
+  const AmaxOut am = amax_out(y ? amax : 0, ws + 2 * C);  // the finalize's level buffer is free by then
   check_shape(M, C, V, reinterpret_cast<uintptr_t>(x));
   const int G = C / V;
   const int blk = block_for(G);
@@ -680,7 +755,7 @@ void fwd_impl(int dev, hipStream_t s, const T* x, const T* res, T* y, int64_t M,
     fa.save_rstd = save_rstd;
     fa.coef = coef;
     launch_tiles_finalize<T, true>(s, tstats, nstat, C, M, x, ws + 2 * C, fa);
-    if (y) launch_apply<T>(s, x, res, y, M, C, coef, relu, mask);
+    if (y) launch_apply<T>(s, x, res, y, M, C, coef, relu, mask, am);
     hip_check(hipGetLastError(), "bn_act forward launch");
     return;
   }
@@ -692,15 +767,16 @@ void fwd_impl(int dev, hipStream_t s, const T* x, const T* res, T* y, int64_t M,
   hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(nb), dim3(blk), shm, s, x, M, C, rpb, part);
   hipLaunchKernelGGL(bn_finalize_fwd_kernel<T>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinK), 0, s, part, nb,
                      C, M, x, gamma, beta, eps, momentum, rmean, rvar, save_mean, save_rstd, coef);
-  if (y) launch_apply<T>(s, x, res, y, M, C, coef, relu, mask);  // y == nullptr: coefficients only
+  if (y) launch_apply<T>(s, x, res, y, M, C, coef, relu, mask, am);  // y == nullptr: coefficients only
   hip_check(hipGetLastError(), "bn_act forward launch");
 }
 
 template <typename T>
 void bwd_impl(hipStream_t s, const T* dy, const uint8_t* mask, const T* x, T* dx, T* dres, int64_t M, int C,
               const float* gamma, const float* mean, const float* rstd, float* dgamma, float* dbeta, float* ws,
-              bool relu, const float* gpart, int64_t npart, const float* coef_in) {
+              bool relu, const float* gpart, int64_t npart, const float* coef_in, uintptr_t amax) {
   constexpr int V = Vec<T>::N;
+  const AmaxOut am = amax_out(dx ? amax : 0, ws + 3 * C);  // the finalize's partials are consumed by then
   check_shape(M, C, V, reinterpret_cast<uintptr_t>(x));
   if (relu && !mask) throw std::invalid_argument("bn_act backward: ReLU needs the forward mask");
   const int G = C / V;
@@ -739,11 +815,11 @@ void bwd_impl(hipStream_t s, const T* dy, const uint8_t* mask, const T* x, T* dx
     return;
   }
   if (relu) {
-    if (dres) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, true>), g, b, 0, s, dy, mask, x, coef, dx, dres, nvec, C);
-    else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, false>), g, b, 0, s, dy, mask, x, coef, dx, dres, nvec, C);
+    if (dres) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, true>), g, b, 0, s, dy, mask, x, coef, dx, dres, nvec, C, am);
+    else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, false>), g, b, 0, s, dy, mask, x, coef, dx, dres, nvec, C, am);
   } else {
-    if (dres) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false, true>), g, b, 0, s, dy, mask, x, coef, dx, dres, nvec, C);
-    else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false, false>), g, b, 0, s, dy, mask, x, coef, dx, dres, nvec, C);
+    if (dres) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false, true>), g, b, 0, s, dy, mask, x, coef, dx, dres, nvec, C, am);
+    else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false, false>), g, b, 0, s, dy, mask, x, coef, dx, dres, nvec, C, am);
   }
   hip_check(hipGetLastError(), "bn_act backward launch");
 }
@@ -757,18 +833,18 @@ int64_t bn_mask_bytes(bool bf16, int64_t M, int C) { (void)bf16; return M * (C /
 void bn_act_fwd(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C,
                 uintptr_t gamma, uintptr_t beta, uintptr_t rmean, uintptr_t rvar, uintptr_t save_mean,
                 uintptr_t save_rstd, uintptr_t ws, float momentum, float eps, bool relu, uintptr_t mask,
-                uintptr_t stats, int64_t nstat) {
+                uintptr_t stats, int64_t nstat, uintptr_t amax) {
   hip_check(hipSetDevice(dev), "hipSetDevice");
   auto F = [](uintptr_t p) { return reinterpret_cast<float*>(p); };
   auto* mk = reinterpret_cast<uint8_t*>(mask);
   if (bf16)
     fwd_impl<uint16_t>(dev, s, reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(res),
                        reinterpret_cast<uint16_t*>(y), M, C, F(gamma), F(beta), F(rmean), F(rvar), F(save_mean),
-                       F(save_rstd), F(ws), momentum, eps, relu, mk, F(stats), nstat);
+                       F(save_rstd), F(ws), momentum, eps, relu, mk, F(stats), nstat, amax);
   else
     fwd_impl<float>(dev, s, reinterpret_cast<const float*>(x), reinterpret_cast<const float*>(res),
                     reinterpret_cast<float*>(y), M, C, F(gamma), F(beta), F(rmean), F(rvar), F(save_mean), F(save_rstd),
-                    F(ws), momentum, eps, relu, mk, F(stats), nstat);
+                    F(ws), momentum, eps, relu, mk, F(stats), nstat, amax);
 }
 
 void bn_act_apply(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C,
@@ -788,7 +864,8 @@ void bn_act_apply(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res,
 
 void bn_act_bwd(int dev, hipStream_t s, bool bf16, uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t dx,
                 uintptr_t dres, int64_t M, int C, uintptr_t gamma, uintptr_t mean, uintptr_t rstd, uintptr_t dgamma,
-                uintptr_t dbeta, uintptr_t ws, bool relu, uintptr_t part, int64_t npart, uintptr_t coef) {
+                uintptr_t dbeta, uintptr_t ws, bool relu, uintptr_t part, int64_t npart, uintptr_t coef,
+                uintptr_t amax) {
   hip_check(hipSetDevice(dev), "hipSetDevice");
   auto F = [](uintptr_t p) { return reinterpret_cast<float*>(p); };
   const auto* mk = reinterpret_cast<const uint8_t*>(mask);
@@ -796,54 +873,59 @@ void bn_act_bwd(int dev, hipStream_t s, bool bf16, uintptr_t dy, uintptr_t mask,
   if (bf16)
     bwd_impl<uint16_t>(s, reinterpret_cast<const uint16_t*>(dy), mk, reinterpret_cast<const uint16_t*>(x),
                        reinterpret_cast<uint16_t*>(dx), reinterpret_cast<uint16_t*>(dres), M, C, F(gamma), F(mean),
-                       F(rstd), F(dgamma), F(dbeta), F(ws), relu, F(part), npart, F(coef));
+                       F(rstd), F(dgamma), F(dbeta), F(ws), relu, F(part), npart, F(coef), amax);
   else
     bwd_impl<float>(s, reinterpret_cast<const float*>(dy), mk, reinterpret_cast<const float*>(x),
                     reinterpret_cast<float*>(dx), reinterpret_cast<float*>(dres), M, C, F(gamma), F(mean), F(rstd),
-                    F(dgamma), F(dbeta), F(ws), relu, F(part), npart, F(coef));
+                    F(dgamma), F(dbeta), F(ws), relu, F(part), npart, F(coef), amax);
 }
 
 template <typename T>
 static void pair_apply_t(hipStream_t s, uintptr_t x1, uintptr_t coef1, uintptr_t x2, uintptr_t coef2, uintptr_t y,
-                         int64_t M, int C, uintptr_t mask) {
+                         int64_t M, int C, uintptr_t mask, uintptr_t amax, uintptr_t scratch) {
   const int G = C / 8, blk = block_for(G);
   const int64_t nvec = M * G;
   hipLaunchKernelGGL(bn_pair_apply_kernel<T>, dim3(apply_grid(nvec, blk)), dim3(blk), 0, s,
                      reinterpret_cast<const T*>(x1), reinterpret_cast<const T*>(x2), reinterpret_cast<T*>(y),
                      reinterpret_cast<const float*>(coef1), reinterpret_cast<const float*>(coef2), nvec, C,
-                     reinterpret_cast<uint8_t*>(mask));
+                     reinterpret_cast<uint8_t*>(mask), amax_out(amax, reinterpret_cast<float*>(scratch)));
 }
 
 template <typename T>
 static void pair_bwd_t(hipStream_t s, uintptr_t dy, uintptr_t mask, uintptr_t x1, uintptr_t coef1, uintptr_t dx1,
-                       uintptr_t x2, uintptr_t coef2, uintptr_t dx2, int64_t M, int C) {
+                       uintptr_t x2, uintptr_t coef2, uintptr_t dx2, int64_t M, int C, uintptr_t amax1, uintptr_t amax2,
+                       uintptr_t scratch) {
   const int G = C / 8, blk = block_for(G);
   const int64_t nvec = M * G;
+  float* sc = reinterpret_cast<float*>(scratch);  // [2][4096]
   hipLaunchKernelGGL(bn_pair_bwd_apply_kernel<T>, dim3(apply_grid(nvec, blk)), dim3(blk), 0, s,
                      reinterpret_cast<const T*>(dy), reinterpret_cast<const uint8_t*>(mask),
                      reinterpret_cast<const T*>(x1), reinterpret_cast<const float*>(coef1), reinterpret_cast<T*>(dx1),
                      reinterpret_cast<const T*>(x2), reinterpret_cast<const float*>(coef2), reinterpret_cast<T*>(dx2),
-                     nvec, C);
+                     nvec, C, amax_out(amax1, sc), amax_out(amax2, sc ? sc + 4096 : nullptr));
 }
 
 void bn_pair_apply(int dev, hipStream_t s, uintptr_t x1, uintptr_t coef1, uintptr_t x2, uintptr_t coef2, uintptr_t y,
-                   int64_t M, int C, uintptr_t mask, bool f32) {
+                   int64_t M, int C, uintptr_t mask, bool f32, uintptr_t amax, uintptr_t scratch) {
   hip_check(hipSetDevice(dev), "hipSetDevice");
   check_shape(M, C, 8, x1);
   check_shape(M, C, 8, x2);
   if (!mask) throw std::invalid_argument("bn_pair_apply: needs the ReLU mask buffer");
-  if (f32) pair_apply_t<float>(s, x1, coef1, x2, coef2, y, M, C, mask);
-  else pair_apply_t<uint16_t>(s, x1, coef1, x2, coef2, y, M, C, mask);
+  if (amax && !scratch) throw std::invalid_argument("bn_pair_apply: amax needs a scratch buffer (4096 floats)");
+  if (f32) pair_apply_t<float>(s, x1, coef1, x2, coef2, y, M, C, mask, amax, scratch);
+  else pair_apply_t<uint16_t>(s, x1, coef1, x2, coef2, y, M, C, mask, amax, scratch);
   hip_check(hipGetLastError(), "bn_pair_apply launch");
 }
 
 void bn_pair_bwd_apply(int dev, hipStream_t s, uintptr_t dy, uintptr_t mask, uintptr_t x1, uintptr_t coef1,
-                       uintptr_t dx1, uintptr_t x2, uintptr_t coef2, uintptr_t dx2, int64_t M, int C, bool f32) {
+                       uintptr_t dx1, uintptr_t x2, uintptr_t coef2, uintptr_t dx2, int64_t M, int C, bool f32,
+                       uintptr_t amax1, uintptr_t amax2, uintptr_t scratch) {
   hip_check(hipSetDevice(dev), "hipSetDevice");
   check_shape(M, C, 8, x1);
   check_shape(M, C, 8, x2);
-  if (f32) pair_bwd_t<float>(s, dy, mask, x1, coef1, dx1, x2, coef2, dx2, M, C);
-  else pair_bwd_t<uint16_t>(s, dy, mask, x1, coef1, dx1, x2, coef2, dx2, M, C);
+  if ((amax1 || amax2) && !scratch) throw std::invalid_argument("bn_pair_bwd_apply: amax needs scratch (8192 floats)");
+  if (f32) pair_bwd_t<float>(s, dy, mask, x1, coef1, dx1, x2, coef2, dx2, M, C, amax1, amax2, scratch);
+  else pair_bwd_t<uint16_t>(s, dy, mask, x1, coef1, dx1, x2, coef2, dx2, M, C, amax1, amax2, scratch);
   hip_check(hipGetLastError(), "bn_pair_bwd_apply launch");
 }
 

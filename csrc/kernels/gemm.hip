@@ -158,6 +158,51 @@ __device__ __forceinline__ void split3(const float (&v)[8], bf16x8& h, bf16x8& m
   m = __builtin_bit_cast(bf16x8, mu);
   l = __builtin_bit_cast(bf16x8, lu);
 }
+// fp32 GEMMs on the fp16 matrix cores ("fp16x3", FM = 11): an operand with a power-of-two
+// scale 2^e (per tensor, from a device-side upper bound amax of |x|: amax * 2^e in [2^13,
+// 2^14), fp16_exp) splits exactly into two fp16 terms, s = x * 2^e = h + l * 2^-11 with h =
+// f16(s) (round to nearest: 11 significant bits) and l = f16((s - h) * 2^11) (the next 11).
+// s - h and (s - h) * 2^11 are exact in fp32, so x is carried to 22 bits (relative error
+// <= 2^-22) wherever s >= 2^-14 (|x| within 2^27 of amax: fp16 normals); smaller values are
+// carried to an absolute error below 2^-48 * amax. A product takes three fp16 MFMAs,
+// hh into one accumulator and hl + lh into a second (scaled back by 2^-11 once, in the
+// epilogue, with the operand scales 2^-(ea + eb)); the dropped ll is < 2^-22 relative — the
+// same order as the bf16x6 split's dropped terms, at half its MFMA count (2.5 PF / 3 = 833 TF
+// peak). Numerics against fp64: tests/test_fp32_path.py.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+// e with amax * 2^e in [2^13, 2^14) (0 for a zero / non-finite bound), clamped to a normal 2^e
+__device__ __forceinline__ int fp16_exp(const float* amax) {
+  const float a = *amax;
+  if (!(a > 0.f) || !(a <= 3.0e38f)) return 0;
+  int x;
+  (void)frexpf(a, &x);  // a = f * 2^x, f in [0.5, 1)
+  return min(116, max(-126, 14 - x));  // 2^(e + 11) stays a normal float
+}
+__device__ __forceinline__ float exp2i(int e) { return __builtin_bit_cast(float, uint32_t(e + 127) << 23); }
+// the lane's 8 fp32 values -> fp16 planes h, l of x * 2^e (s = 2^e, s11 = 2^(e + 11));
+// per pair: v_pk_mul x2, v_cvt_pk_f16_f32 x2, v_cvt_f32_f16 x2, v_pk_fma: 7 VALU
+__device__ __forceinline__ void split2h(const float (&v)[8], float s, float s11, f16x8& h, f16x8& l) {
+  u32x4 hu, lu;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const f32x2 x = {v[2 * p], v[2 * p + 1]};
+    const f16x2 hp = __builtin_convertvector(x * s, f16x2);
+    const f32x2 hf = __builtin_convertvector(hp, f32x2);
+    const f32x2 r = x * s11 - hf * 2048.f;  // 2^11 (x s - h), exact
+    hu[p] = __builtin_bit_cast(uint32_t, hp);
+    lu[p] = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, f16x2));
+  }
+  h = __builtin_bit_cast(f16x8, hu);
+  l = __builtin_bit_cast(f16x8, lu);
+}
+// one fp32 value -> (h, l) fp16 bits of v * s (split2h's arithmetic; weight plans)
+__device__ __forceinline__ void split1h(float v, float s, float s11, uint16_t& h, uint16_t& l) {
+  const _Float16 hh = _Float16(v * s);
+  h = __builtin_bit_cast(uint16_t, hh);
+  l = __builtin_bit_cast(uint16_t, _Float16(v * s11 - float(hh) * 2048.f));
+}
+
 template <int TM, int TN>
 __device__ __forceinline__ void mfma_x3(f32x16 (&hi)[TM][TN], f32x16 (&lo)[TM][TN], const bf16x8 (&ah)[TM],
                                         const bf16x8 (&am)[TM], const bf16x8 (&al)[TM], const bf16x8 (&bh)[TN],
@@ -217,6 +262,9 @@ struct EpiArgs {
   float* flvl;                 // [groups][2][N] group sums
   uint32_t* ftick;             // this launch's tickets [ntn][groups + 1]
   int fgroup;                  // M-tiles per group
+  // fp16x3 (FM 11): device upper bounds of |A| and |B| that set the operand scales
+  const float* amax_a;
+  const float* amax_b;
 };
 
 // write-through (sc1) store: visible to a reader on any XCD without an L2 write-back
@@ -412,7 +460,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
   // wave grid over the tile: 2 x 2 (each wave 64 x 64 of a 128 x 128 tile), or for FM 9
   // (pre-split B) 4 x 1: each wave owns 32 rows x all 128 columns, so every A row is split in
   // registers by exactly one wave (the ready-made B planes are the shared operand)
-  constexpr int WGM = (sizeof(T) == 4 && (FM == 9 || FM == 10)) ? 4 : 2, WGN = NW / WGM;
+  constexpr int WGM = (sizeof(T) == 4 && (FM == 9 || FM == 10 || FM == 11)) ? 4 : 2, WGN = NW / WGM;
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 32, TN = WN / 32;
   constexpr int EPC = epc<T>();                          // elements per 16-B chunk
@@ -423,11 +471,14 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
   // FM 4 (fp32, B pre-split): B arrives as three bf16 planes (h, m, l; plane stride bps
   // elements, made once per step by the weight plan), staged as three 64-B-row images of
   // 32 bf16 per row — the A operand alone is split in registers
-  constexpr bool BSPLIT = F32 && (FM == 4 || FM == 9 || FM == 10);
+  // FM 11 (fp32, fp16x3): B arrives as two fp16 planes (h, l) of the scaled weight, staged the
+  // same way (two 64-B-row images); A is scaled and split in registers (split2h)
+  constexpr bool BSPLIT = F32 && (FM == 4 || FM == 9 || FM == 10 || FM == 11);
+  constexpr int NPL = FM == 11 ? 2 : 3;           // B planes
   constexpr int IBP = BSPLIT ? BN / 16 / NW : 0;  // glds per wave per B plane (16 rows x 64 B)
-  constexpr int NI = BSPLIT ? IA + 3 * IBP : IA + IB;
-  // elements (T) per stage: A rows, then B (fp32 rows, or 3 bf16 plane images = 1.5x the bytes)
-  constexpr int BTILE = BSPLIT ? 3 * BN * 32 / 2 : BN * BK;
+  constexpr int NI = BSPLIT ? IA + NPL * IBP : IA + IB;
+  // elements (T) per stage: A rows, then B (fp32 rows, or NPL 16-bit plane images)
+  constexpr int BTILE = BSPLIT ? NPL * BN * 32 / 2 : BN * BK;
   constexpr int TILE = BM * BK + BTILE;
   static_assert(IA >= 1 && IB >= 1, "tile too small");
   static_assert(!F32 || BKB == 64 || FM == 3 || FM == 4 || FM >= 5, "fp32 tiles stage 64-B rows (FM 3: 128-B)");
@@ -504,7 +555,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
     if constexpr (BSPLIT) {
       uint16_t* Bp = reinterpret_cast<uint16_t*>(Bs);
 #pragma unroll
-      for (int p = 0; p < 3; ++p)
+      for (int p = 0; p < NPL; ++p)
 #pragma unroll
         for (int i = 0; i < IBP; ++i)
           glds(pbp[i] + p * bps + kt * 32, Bp + p * (BN * 32) + (w * IBP + i) * 16 * 32);
@@ -545,6 +596,15 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
 
   const int fr = lane & 31, fh = lane >> 5;
   const int nk = K / BK;
+  // FM 11: operand scales 2^ea (A, applied in the split) and 2^eb (B, applied by the plan)
+  [[maybe_unused]] int ea = 0, eb = 0;
+  [[maybe_unused]] float sa = 1.f, sa11 = 2048.f;
+  if constexpr (F32 && FM == 11) {
+    ea = fp16_exp(ep.amax_a);
+    eb = fp16_exp(ep.amax_b);
+    sa = exp2i(ea);
+    sa11 = exp2i(ea + 11);
+  }
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
     if (s < nk) issue(s, s);
@@ -606,6 +666,38 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pl[sl][j], ah[i], acc[i][j], 0, 0, 0);
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ph[sl][j], al[i], acc[i][j], 0, 0, 0);
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ph[sl][j], ah[i], acc[i][j], 0, 0, 0);
+          }
+      }
+      continue;
+    } else if constexpr (F32 && FM == 11) {
+      // fp16x3: B planes h, l read ready-made; the lane's 8 A floats of k16 step kk (chunks
+      // 4kk + 2fh, +1) scaled and split in registers; hh -> acc, hl + lh -> tacc
+      const uint16_t* Bp = reinterpret_cast<const uint16_t*>(Bs);
+#pragma unroll
+      for (int kk = 0; kk < BK / 16; ++kk) {
+        f16x8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int r = wn * WN + j * 32 + fr;
+          const int o = r * 32 + swz(r, 2 * kk + fh) * 8;
+          bh[j] = *reinterpret_cast<const f16x8*>(Bp + o);
+          bl[j] = *reinterpret_cast<const f16x8*>(Bp + BN * 32 + o);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int r = wm * WM + i * 32 + fr;
+          const float4 x0 = *reinterpret_cast<const float4*>(As + r * BK + swzk<BKB>(r, 4 * kk + 2 * fh) * 4);
+          const float4 x1 = *reinterpret_cast<const float4*>(As + r * BK + swzk<BKB>(r, 4 * kk + 2 * fh + 1) * 4);
+          const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+          split2h(v, sa, sa11, ah[i], al[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bh[j], ah[i], acc[i][j], 0, 0, 0);
+            tacc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bl[j], ah[i], tacc[i][j], 0, 0, 0);
+            tacc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bh[j], al[i], tacc[i][j], 0, 0, 0);
           }
       }
       continue;
@@ -802,7 +894,15 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
     }
   }
 
-  if constexpr (F32 && FM != 0) {  // hh + the five small terms
+  if constexpr (F32 && FM == 11) {  // (hh + 2^-11 (hl + lh)) 2^-(ea + eb), exact scalings
+    const float ia = exp2i(-ea), ib = exp2i(-eb);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) acc[i][j][v] = fmaf(tacc[i][j][v], 1.f / 2048.f, acc[i][j][v]) * ia * ib;
+  } else if constexpr (F32 && FM != 0) {  // hh + the five small terms
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1079,9 +1179,11 @@ __device__ uint32_t g_tn_tickets[kTnTicketSlots * kTnMaxTickets];
 struct TnRed {
   float* out;      // final [N][K] (null: separate split_reduce launches)
   float* mid;      // [groups][N][K] group sums (groups > 1)
-  uint32_t* tick;  // this launch's ticket set: [tiles][groups + 1]
+  uint32_t* tick;  // this launch's tickets: [tiles][groups + 1]
   float beta;
   int ns, groups;
+  const float* amax_y;  // FM 11 (fp16x3): device bounds of |Y| and |X| (operand scales)
+  const float* amax_x;
 };
 
 // sum rows n0..n0+TBN, cols k0..k0+TBK of nsrc [N][K] slices starting at src (slice stride
@@ -1238,8 +1340,18 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y
   const int h = g >> 1;
   const int cbase = 2 * (g & 1) + (p >> 1), cbyte = 4 * (p & 1);  // chunk / element offset in it
   const int fr = lane & 31, fh = lane >> 5;
-  // fp32 split products (FM = 1): the small-term accumulators
+  // fp32 split products (FM = 1, 11): the small-term accumulators
   f32x16 lacc[F32 ? TM : 1][F32 ? TN : 1];
+  [[maybe_unused]] int ey = 0, ex = 0;
+  [[maybe_unused]] float sy = 1.f, sy11 = 2048.f, sx = 1.f, sx11 = 2048.f;
+  if constexpr (F32 && FM == 11) {
+    ey = fp16_exp(red.amax_y);
+    ex = fp16_exp(red.amax_x);
+    sy = exp2i(ey);
+    sy11 = exp2i(ey + 11);
+    sx = exp2i(ex);
+    sx11 = exp2i(ex + 11);
+  }
 #pragma unroll
   for (int i = 0; i < (F32 ? TM : 1); ++i)
 #pragma unroll
@@ -1294,6 +1406,36 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y
           split3(v, bh[j], bm[j], bl[j]);
         }
         mfma_x3<TM, TN>(acc, lacc, ah, am, al, bh, bm, bl, false);
+      }
+    } else if constexpr (F32 && FM == 11) {
+      // fp16x3 (see split2h): the same column reads, each operand scaled and split into fp16
+      // h, l; hh -> acc, hl + lh -> lacc
+#pragma unroll
+      for (int kk = 0; kk < kRows / 16; ++kk) {
+        const int r0 = 16 * kk + 8 * fh;
+        f16x8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          float v[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = Ys[(r0 + e) * TBN + wn * WN + i * 32 + fr];
+          split2h(v, sy, sy11, ah[i], al[i]);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          float v[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = Xs[(r0 + e) * TBK + wk * WK + j * 32 + fr];
+          split2h(v, sx, sx11, bh[j], bl[j]);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+            lacc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], lacc[i][j], 0, 0, 0);
+            lacc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], lacc[i][j], 0, 0, 0);
+          }
       }
     } else if constexpr (F32) {
       // v_mfma_f32_32x32x2_f32: lane (fr, fh) supplies Y[row][n0' + fr] and X[row][k0' + fr]
@@ -1355,6 +1497,14 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] += lacc[i][j];
+  } else if constexpr (F32 && FM == 11) {
+    const float iy = exp2i(-ey), ix = exp2i(-ex);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) acc[i][j][v] = fmaf(lacc[i][j][v], 1.f / 2048.f, acc[i][j][v]) * iy * ix;
   }
   // D[n][k]: column k = lane&31, row n = (v&3) + 8*(v>>2) + 4*(lane>>5)
   float* out = part + int64_t(split) * N * K;
@@ -1682,9 +1832,12 @@ __device__ __forceinline__ void split1(float v, uint16_t& h, uint16_t& m, uint16
 // cast_tile for the pre-split fp32 path: the same copy / transpose, written as three bf16
 // planes (h at p, m at p + plane, l at p + 2 * plane) for the FM 4 GEMMs. wb: planes or
 // null; wt: planes (pt > 0) or plain fp32 (pt == 0: the GEMM reading it splits in registers)
+// f16 (fp16x3 plans): two fp16 planes h, l of the weight scaled by s = 2^e (s11 = 2^(e + 11)),
+// split1h's arithmetic, instead of the three bf16 ones.
 __device__ __forceinline__ void cast_tile_planes(const float* __restrict__ w, int R, int Cc, int T,
                                                  uint16_t* __restrict__ wb, int64_t pb, void* __restrict__ wt_,
-                                                 int64_t pt, const TapMap& map, int cx, int ry, int tap) {
+                                                 int64_t pt, const TapMap& map, int cx, int ry, int tap, bool f16,
+                                                 float s, float s11) {
   __shared__ float tile[32][33];
   const int c0 = cx * 32, r0 = ry * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
@@ -1693,7 +1846,12 @@ __device__ __forceinline__ void cast_tile_planes(const float* __restrict__ w, in
     if (r < R && c < Cc) {
       const int64_t i = (int64_t(r) * T + tap) * Cc + c;
       const float v = w[i];
-      if (wb) {
+      if (wb && f16) {
+        uint16_t h, l;
+        split1h(v, s, s11, h, l);
+        wb[i] = h;
+        wb[pb + i] = l;
+      } else if (wb) {
         uint16_t h, m, l;
         split1(v, h, m, l);
         wb[i] = h;
@@ -1716,6 +1874,13 @@ __device__ __forceinline__ void cast_tile_planes(const float* __restrict__ w, in
         continue;
       }
       uint16_t* wt = static_cast<uint16_t*>(wt_);
+      if (f16) {
+        uint16_t h, l;
+        split1h(tile[tx][y], s, s11, h, l);
+        wt[o] = h;
+        wt[pt + o] = l;
+        continue;
+      }
       uint16_t h, m, l;
       split1(tile[tx][y], h, m, l);
       wt[o] = h;
@@ -1739,7 +1904,9 @@ struct CastJob {
   void* wb;
   void* wt;
   int R, Cc, T, tcx, tcy;  // tiles along Cc and R
-  int f32;                 // outputs: 0 bf16, 1 fp32 (no plain copy), 2 pre-split bf16 planes
+  int f32;                 // outputs: 0 bf16, 1 fp32 (no plain copy), 2 pre-split planes
+  int f16;                 // (f32 == 2) planes are fp16 h, l of the weight scaled by amax's 2^e
+  const float* amax;       // (f16) device upper bound of |w| over the plan
   int64_t block0;
   int64_t pb, pt;          // plane strides (elements) of wb / wt when f32 == 2
   TapMap map;
@@ -1761,9 +1928,16 @@ __global__ __launch_bounds__(256) void cast_batch_kernel(const CastJob* __restri
   const int64_t local = int64_t(blockIdx.x) - J.block0;
   const int per_tap = J.tcx * J.tcy;
   const int tap = int(local / per_tap), rem = int(local % per_tap);
-  if (J.f32 == 2)
+  if (J.f32 == 2) {
+    float sc = 1.f, sc11 = 2048.f;
+    if (J.f16) {
+      const int e = fp16_exp(J.amax);
+      sc = exp2i(e);
+      sc11 = exp2i(e + 11);
+    }
     cast_tile_planes(J.w, J.R, J.Cc, J.T, static_cast<uint16_t*>(J.wb), J.pb, J.wt, J.pt, J.map, rem % J.tcx,
-                     rem / J.tcx, tap);
+                     rem / J.tcx, tap, J.f16 != 0, sc, sc11);
+  }
   else if (J.f32)
     cast_tile<float>(J.w, J.R, J.Cc, J.T, static_cast<float*>(J.wb), static_cast<float*>(J.wt), J.map, rem % J.tcx,
                      rem / J.tcx, tap);
@@ -1973,6 +2147,13 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
       return e && std::string(e) == "acc1";
     }();
     fm = w22 ? 4 : (acc1 ? 10 : 9);
+    if (ep.amax_b) {  // fp16 planes h, l of the scaled weight (fp16x3): A needs its bound too
+      if (!ep.amax_a) throw std::invalid_argument("gemm_nt: fp16 B planes need the A operand's amax bound");
+      check_ptr(B + uintptr_t(bps) * 2, "B plane 1");
+      fm = 11;
+    }
+  } else if (ep.amax_b) {
+    throw std::invalid_argument("gemm_nt: amax_b is the scale of fp16 B planes (bps > 0)");
   }
   const int nk = K / (fm >= 3 ? 32 : nt_bk_of<T>());
   // MPIT_GEMM_STAGES caps the ring depth (A/B measurements). fp32: the 64 KB epilogue tile
@@ -1987,7 +2168,8 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
   }();
   int cap = F32 && N % 128 == 0 ? (fm >= 3 ? 2 : 4) : max_stages;
   if (F32 && f32_stages) cap = f32_stages;
-  const int stages = std::min(cap, nk >= 4 ? 4 : (nk == 3 ? 3 : 2));
+  // (the pre-split kernels, FM >= 4, are built for the 2-deep ring of 128-row tiles only)
+  const int stages = fm >= 4 ? 2 : std::min(cap, nk >= 4 ? 4 : (nk == 3 ? 3 : 2));
   // (kernel templates are named at a non-template call site so their host stubs are emitted)
 #define MPIT_NT_OPT_IN(BM, BN, ST, EPI, CONV, FMV)                                                                 \
   do {                                                                                                             \
@@ -2000,7 +2182,13 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
   } while (0)
 #define MPIT_NT_LAUNCH1(BM, BN, ST, EPI, CONV)                                                                       \
   do {                                                                                                             \
-    if constexpr (F32) {                                                                                           \
+    if constexpr (F32 && BM == 128 && ST == 2) {                                                                 \
+      if (fm == 11) {                                                                                              \
+        if (shm > 65536) MPIT_NT_OPT_IN(BM, BN, ST, EPI, CONV, 11);                                                 \
+        hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, ST, EPI, CONV, 11>), dim3(unsigned(nb)), dim3(256), shm, s, a, \
+                           lda, b, ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g, bps);                          \
+        break;                                                                                                     \
+      }                                                                                                            \
       if (fm >= 5 && fm <= 7) { /* timing ablations (MPIT_F32_ABLATE) */                                        \
         if (fm == 5) {                                                                                             \
           if (shm > 65536) MPIT_NT_OPT_IN(BM, BN, ST, EPI, CONV, 5);                                                \
@@ -2035,6 +2223,9 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
                            lda, b, ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g, bps);                          \
         break;                                                                                                     \
       }                                                                                                            \
+    }                                                                                                              \
+    if constexpr (F32) {                                                                                           \
+      if (fm >= 4) throw std::logic_error("gemm_nt: pre-split kernels run 128-row tiles on a 2-deep ring");        \
       if (fm == 3) {                                                                                               \
         if (shm > 65536) MPIT_NT_OPT_IN(BM, BN, ST, EPI, CONV, 3);                                                  \
         hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, ST, EPI, CONV, 3>), dim3(unsigned(nb)), dim3(256), shm, s, a, \
@@ -2068,7 +2259,7 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
     if (ep.fcoef) fold_plan(ep, dev, s, mtn, ntn);                                                                 \
     /* LDS: the k-tile ring, reused by the epilogue's output tile and reduction table */                      \
     const size_t shm = std::max({size_t(ST) * (size_t(BM) * nt_bkb(BM, BN, fm) +                               \
-                                                (fm == 4 || fm >= 9 ? size_t(BN) * 192 : size_t(BN) * nt_bkb(BM, BN, fm))), \
+                                                (fm == 11 ? size_t(BN) * 128 : fm == 4 || fm >= 9 ? size_t(BN) * 192 : size_t(BN) * nt_bkb(BM, BN, fm))), \
                                  size_t(BM) * BN * sizeof(T), size_t(256) * 8 * 3 * sizeof(float)});          \
     if (geo) MPIT_NT_LAUNCH2(BM, BN, ST, true);                                                           \
     else MPIT_NT_LAUNCH2(BM, BN, ST, false);                                                              \
@@ -2125,6 +2316,10 @@ static void launch_nt(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t
 static EpiArgs epi_args(uintptr_t stats, const BnRed* r, int* mode) {
   EpiArgs ep{};
   *mode = EPI_NONE;
+  if (r) {
+    ep.amax_a = reinterpret_cast<const float*>(r->amax_a);
+    ep.amax_b = reinterpret_cast<const float*>(r->amax_b);
+  }
   if (stats && r && r->part) throw std::invalid_argument("gemm_nt: stats and BN reduction are exclusive");
   if (stats) {
     ep.part = reinterpret_cast<float*>(stats);
@@ -2220,7 +2415,8 @@ int64_t gemm_tn_ws_floats(int dev, int64_t M, int N, int K) {
 
 template <typename T>
 static void launch_tn_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X,
-                        int64_t ldx, uintptr_t out, uintptr_t ws, float beta, const ConvGeo* geo) {
+                        int64_t ldx, uintptr_t out, uintptr_t ws, float beta, const ConvGeo* geo, uintptr_t amax_y,
+                        uintptr_t amax_x) {
   constexpr bool F32 = sizeof(T) == 4;
   constexpr int EPC = epc<T>();
   if (!gemm_tn_supported(M, N, K))
@@ -2255,6 +2451,11 @@ static void launch_tn_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
     return e && std::string(e) == "1";
   }();
   TnRed red{};
+  // fp32 with both operand bounds: fp16x3 (FM 11), else bf16x6 (FM 1)
+  if ((amax_y != 0) != (amax_x != 0)) throw std::invalid_argument("gemm_tn: fp16x3 needs both operand bounds");
+  const int tfm = !F32 || f32_mode() != 1 ? 0 : (amax_y ? 11 : 1);
+  red.amax_y = reinterpret_cast<const float*>(amax_y);
+  red.amax_x = reinterpret_cast<const float*>(amax_x);
   const int ngr = ns > kReduceGroup ? int(tn_groups(ns)) : 1;
   const bool fused = !direct && fused_env && int64_t(ntiles) * (ngr + 1) <= kTnMaxTickets;
   if (fused) {
@@ -2281,7 +2482,7 @@ static void launch_tn_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
     const char* e = std::getenv("MPIT_TN_F32S");
     return e && std::string(e) == "1";
   }();
-  if (F32 && f32_mode() == 1 && f32s && !fused && tbn == 128 && tbk == 128 && (!geo || (!geo->pitch && geo->C % 128 == 0))) {
+  if (F32 && tfm == 1 && f32s && !fused && tbn == 128 && tbk == 128 && (!geo || (!geo->pitch && geo->C % 128 == 0))) {
     const size_t shm = size_t(2) * 3 * 256 * kTsR * 2;
     const auto* yf = reinterpret_cast<const float*>(Y);
     const auto* xf = reinterpret_cast<const float*>(X);
@@ -2306,12 +2507,20 @@ static void launch_tn_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
     size_t shm = size_t(ST) * kRows * (tbn + tbk) * sizeof(T);                                                   \
     if (tn_cap1()) {                                                                                               \
       shm = std::max(shm, kTnCapShm);                                                                              \
-      if (geo && F32 && f32_mode() == 1) MPIT_TN_OPT_IN(A, B, ST, true, F32 ? 1 : 0);                              \
+      if (geo && F32 && tfm == 11) MPIT_TN_OPT_IN(A, B, ST, true, F32 ? 11 : 0);                                   \
+      else if (F32 && tfm == 11) MPIT_TN_OPT_IN(A, B, ST, false, F32 ? 11 : 0);                                    \
+      else if (geo && F32 && f32_mode() == 1) MPIT_TN_OPT_IN(A, B, ST, true, F32 ? 1 : 0);                         \
       else if (F32 && f32_mode() == 1) MPIT_TN_OPT_IN(A, B, ST, false, F32 ? 1 : 0);                               \
       else if (geo) MPIT_TN_OPT_IN(A, B, ST, true, 0);                                                             \
       else MPIT_TN_OPT_IN(A, B, ST, false, 0);                                                                     \
     }                                                                                                              \
-    if (geo && F32 && f32_mode() == 1)                                                                           \
+    if (geo && F32 && tfm == 11)                                                                                   \
+      hipLaunchKernelGGL((gemm_tn_kernel<T, A, B, ST, true, F32 ? 11 : 0>), grid, dim3(256), shm, s, y, ldy, x,    \
+                         ldx, part, M, N, K, rps, ntk, ntiles, g, red);                                            \
+    else if (F32 && tfm == 11)                                                                                     \
+      hipLaunchKernelGGL((gemm_tn_kernel<T, A, B, ST, false, F32 ? 11 : 0>), grid, dim3(256), shm, s, y, ldy, x,   \
+                         ldx, part, M, N, K, rps, ntk, ntiles, g, red);                                            \
+    else if (geo && F32 && f32_mode() == 1)                                                                        \
       hipLaunchKernelGGL((gemm_tn_kernel<T, A, B, ST, true, F32 ? 1 : 0>), grid, dim3(256), shm, s, y, ldy, x,     \
                          ldx, part, M, N, K, rps, ntk, ntiles, g, red);                                            \
     else if (F32 && f32_mode() == 1)                                                                               \
@@ -2358,14 +2567,16 @@ static void launch_tn_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
 }
 
 static void launch_tn(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X,
-                      int64_t ldx, uintptr_t out, uintptr_t ws, float beta, const ConvGeo* geo, bool f32) {
-  if (f32) launch_tn_t<float>(dev, s, M, N, K, Y, ldy, X, ldx, out, ws, beta, geo);
-  else launch_tn_t<uint16_t>(dev, s, M, N, K, Y, ldy, X, ldx, out, ws, beta, geo);
+                      int64_t ldx, uintptr_t out, uintptr_t ws, float beta, const ConvGeo* geo, bool f32,
+                      uintptr_t amax_y = 0, uintptr_t amax_x = 0) {
+  if (f32) launch_tn_t<float>(dev, s, M, N, K, Y, ldy, X, ldx, out, ws, beta, geo, amax_y, amax_x);
+  else if (amax_y || amax_x) throw std::invalid_argument("gemm_tn: operand bounds are for fp32 (fp16x3) calls");
+  else launch_tn_t<uint16_t>(dev, s, M, N, K, Y, ldy, X, ldx, out, ws, beta, geo, 0, 0);
 }
 
 void gemm_tn(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X, int64_t ldx,
-             uintptr_t out, uintptr_t ws, float beta, bool f32) {
-  launch_tn(dev, s, M, N, K, Y, ldy, X, ldx, out, ws, beta, nullptr, f32);
+             uintptr_t out, uintptr_t ws, float beta, bool f32, uintptr_t amax_y, uintptr_t amax_x) {
+  launch_tn(dev, s, M, N, K, Y, ldy, X, ldx, out, ws, beta, nullptr, f32, amax_y, amax_x);
 }
 
 // ------------------------------------------------------------------ convolutions
@@ -2405,13 +2616,14 @@ int64_t conv_wgrad_ws_floats(int dev, int Nb, int H, int W, int C, int Co, int R
 }
 
 void conv_wgrad(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad,
-                uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, float beta, bool f32) {
+                uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, float beta, bool f32, uintptr_t amax_y,
+                uintptr_t amax_x) {
   if (C % 64 || Co % 64) throw std::invalid_argument("conv_wgrad: need C % 64 == 0 and Co % 64 == 0");
   if (int64_t(Nb) * H * W * C >= (int64_t(1) << 31)) throw std::invalid_argument("conv_wgrad: input too large");
   int Ho, Wo;
   const ConvGeo g = conv_geo(H, W, C, R, S, stride, pad, &Ho, &Wo);
   const int64_t M = int64_t(Nb) * Ho * Wo;
-  launch_tn(dev, s, M, Co, R * S * C, dy, Co, x, C, dw, ws, beta, &g, f32);
+  launch_tn(dev, s, M, Co, R * S * C, dy, Co, x, C, dw, ws, beta, &g, f32, amax_y, amax_x);
 }
 
 // Row-tap stem convolution: x is a zero-padded NHWC4 image [Nb][Hp][Wp][4] (bf16 / fp32), the
@@ -2539,7 +2751,7 @@ int64_t conv_dgrad_strided_tiles(int Nb, int H, int W, int C, int Co, int R, int
 
 int64_t cast_job_bytes() { return int64_t(sizeof(CastJob)); }
 
-int64_t cast_jobs_build(uintptr_t host_table, const std::vector<std::array<int64_t, 10>>& specs) {
+int64_t cast_jobs_build(uintptr_t host_table, const std::vector<std::array<int64_t, 11>>& specs) {
   auto* jobs = reinterpret_cast<CastJob*>(host_table);
   int64_t blocks = 0;
   for (size_t k = 0; k < specs.size(); ++k) {
@@ -2547,12 +2759,16 @@ int64_t cast_jobs_build(uintptr_t host_table, const std::vector<std::array<int64
     // q[0] = kind | f32 << 8 (fp32 outputs: transposes only, the plain copy is the master weight)
     //        | 512: wb as three pre-split bf16 planes (else none: the forward reads the master)
     //        | 1024: wt as three pre-split bf16 planes (else fp32)
+    //        | 2048: the planes are fp16x3's two fp16 planes, scaled by the bound at q[10]
     const int kind = int(q[0] & 0xff), Co = int(q[4]), C = int(q[5]), R = int(q[6]), S = int(q[7]);
     const int stride = int(q[8]), pad = int(q[9]);
     CastJob J{};
     J.w = reinterpret_cast<const float*>(q[1]);
     const bool pl_b = (q[0] >> 9) & 1, pl_t = (q[0] >> 10) & 1;
     J.f32 = pl_b || pl_t ? 2 : int((q[0] >> 8) & 1);
+    J.f16 = int((q[0] >> 11) & 1);
+    J.amax = reinterpret_cast<const float*>(q[10]);
+    if (J.f16 && (J.f32 != 2 || !J.amax)) throw std::invalid_argument("cast_jobs_build: fp16 planes need planes and a bound");
     J.wb = (J.f32 == 1 || (J.f32 == 2 && !pl_b)) ? nullptr : reinterpret_cast<void*>(q[2]);
     if (J.f32 == 2) {
       J.pb = int64_t(Co) * R * S * C;

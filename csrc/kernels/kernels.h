@@ -86,7 +86,9 @@ int64_t bn_mask_bytes(bool bf16, int64_t M, int C);
 void bn_act_fwd(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C,
                 uintptr_t gamma, uintptr_t beta, uintptr_t rmean, uintptr_t rvar, uintptr_t save_mean,
                 uintptr_t save_rstd, uintptr_t ws, float momentum, float eps, bool relu, uintptr_t mask,
-                uintptr_t stats = 0, int64_t nstat = 0);
+                uintptr_t stats = 0, int64_t nstat = 0, uintptr_t amax = 0);
+// amax (optional, fp32 [1]): max |y| over the tensor, written by the apply pass (bn_act_bwd:
+// max |dx|; the pair applies: of y / dx1, dx2) — the scale bound of the fp16x3 GEMMs that read it
 // y = act(x*coef[c] + coef[C+c] (+res))  — eval mode / precomputed coefficients
 void bn_act_apply(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C,
                   uintptr_t coef, bool relu);
@@ -95,7 +97,7 @@ void bn_act_apply(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res,
 void bn_act_bwd(int dev, hipStream_t s, bool bf16, uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t dx,
                 uintptr_t dres, int64_t M, int C, uintptr_t gamma, uintptr_t mean, uintptr_t rstd, uintptr_t dgamma,
                 uintptr_t dbeta, uintptr_t ws, bool relu, uintptr_t part = 0, int64_t npart = 0,
-                uintptr_t coef = 0);
+                uintptr_t coef = 0, uintptr_t amax = 0);
 // coef (optional): the apply coefficients [3][C] already computed (the finalize folded into
 // the GEMM that wrote dy, BnRed::fcoef; dgamma / dbeta written there too): apply pass only.
 
@@ -105,9 +107,11 @@ void bn_act_bwd(int dev, hipStream_t s, bool bf16, uintptr_t dy, uintptr_t mask,
 // y = relu(bn1(x1) + bn2(x2)) from the two forward coefficient sets, and the backward
 // dx1 / dx2 from the two backward sets, one pass each.
 void bn_pair_apply(int dev, hipStream_t s, uintptr_t x1, uintptr_t coef1, uintptr_t x2, uintptr_t coef2, uintptr_t y,
-                   int64_t M, int C, uintptr_t mask, bool f32 = false);
+                   int64_t M, int C, uintptr_t mask, bool f32 = false, uintptr_t amax = 0, uintptr_t scratch = 0);
+// scratch: 4096 (pair apply) / 8192 (pair backward) floats when an amax is asked for
 void bn_pair_bwd_apply(int dev, hipStream_t s, uintptr_t dy, uintptr_t mask, uintptr_t x1, uintptr_t coef1,
-                       uintptr_t dx1, uintptr_t x2, uintptr_t coef2, uintptr_t dx2, int64_t M, int C, bool f32 = false);
+                       uintptr_t dx1, uintptr_t x2, uintptr_t coef2, uintptr_t dx2, int64_t M, int C, bool f32 = false,
+                       uintptr_t amax1 = 0, uintptr_t amax2 = 0, uintptr_t scratch = 0);
 
 // ---- MFMA GEMMs for NHWC 1x1 convolutions (gemm.hip), fp32 accumulate -------------------
 // Operands and outputs are bf16 (v_mfma_f32_32x32x16_bf16) or, with f32 = true, fp32
@@ -130,6 +134,9 @@ struct BnRed {
   // fold the BN backward's finalize into the GEMM (single EPI_BNRED launch): coefficients
   // [3][N], dgamma / dbeta [N], from gamma (or 0) and rstd; lvl: gemm_nt_fold_lvl_floats(N)
   uintptr_t fcoef = 0, fgamma = 0, frstd = 0, fdgamma = 0, fdbeta = 0, flvl = 0;
+  // fp32 fp16x3 GEMMs (gemm.hip FM 11): device fp32 upper bounds of |A| and of |B|; amax_b
+  // marks B (bps > 0) as the two fp16 planes of the weight scaled by its bound's 2^e
+  uintptr_t amax_a = 0, amax_b = 0;
 };
 int64_t gemm_nt_fold_lvl_floats(int N);
 bool gemm_nt_supported(int64_t M, int N, int K, bool f32 = false);
@@ -146,8 +153,9 @@ int64_t gemm_tn_ws_floats(int dev, int64_t M, int N, int K);
 // compute units of device `dev`; a stream restricted to the CUs of `mask` (gemm.hip)
 int device_cu_count(int dev);
 uintptr_t stream_create_cu_masked(int dev, const std::vector<uint32_t>& mask);
+// amax_y / amax_x (fp32, both or neither): device bounds of |Y|, |X| -> fp16x3 split products
 void gemm_tn(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X, int64_t ldx,
-             uintptr_t out, uintptr_t ws, float beta, bool f32 = false);
+             uintptr_t out, uintptr_t ws, float beta, bool f32 = false, uintptr_t amax_y = 0, uintptr_t amax_x = 0);
 // fp32 w[R][T][Cc] -> bf16 wb[R][T][Cc] (optional) and bf16 tap-flipped transpose
 // wt[Cc][T-1-t][R] (optional); T = 1 is the plain transpose
 void cast_transpose(int dev, hipStream_t s, uintptr_t w, int R, int Cc, uintptr_t wb, uintptr_t wt, int taps = 1,
@@ -157,7 +165,7 @@ void cast_transpose(int dev, hipStream_t s, uintptr_t w, int R, int Cc, uintptr_
 // parity-class weights (conv_dgrad_strided_weights), 2 = cast only. The table is built on the
 // host (cast_job_bytes() per job) and uploaded once; cast_jobs_run launches it.
 int64_t cast_job_bytes();
-int64_t cast_jobs_build(uintptr_t host_table, const std::vector<std::array<int64_t, 10>>& specs);
+int64_t cast_jobs_build(uintptr_t host_table, const std::vector<std::array<int64_t, 11>>& specs);
 void cast_jobs_run(int dev, hipStream_t s, uintptr_t dev_table, int njobs, int64_t nblocks);
 
 // ---- NHWC RxS convolutions as implicit GEMMs on the same MFMA kernels ----------------
@@ -188,7 +196,8 @@ void relu_bias_bwd(int dev, hipStream_t s, int64_t M, int C, uintptr_t dy, uintp
 // dw [Co,R,S,C] (fp32) = beta*dw + dY^T . im2col(x)   (C % 64 == 0, Co % 64 == 0)
 int64_t conv_wgrad_ws_floats(int dev, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad);
 void conv_wgrad(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad,
-                uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, float beta, bool f32 = false);
+                uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, float beta, bool f32 = false,
+                uintptr_t amax_y = 0, uintptr_t amax_x = 0);
 
 // Row-tap stem conv (7x7 / stride-2 / 3-channel ResNet stem on MFMA): x = zero-padded NHWC4
 // image [Nb][Hp][Wp][4], w = [Co][8][8][4] (bf16, zero-extended kernel), y = [Nb][Ho][Wo][Co];

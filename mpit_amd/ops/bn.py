@@ -26,6 +26,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .._ext import native
+from . import conv as _conv
+from .conv import set_amax
 
 
 def _rows(x: torch.Tensor):
@@ -99,10 +101,19 @@ def tile_stats_of(x: torch.Tensor):
     return ts[0], ts[1]
 
 
+def _want_amax(x: torch.Tensor) -> bool:
+    """fp32 outputs on the GPU carry max |out| for the fp16x3 GEMMs that read them (ops/conv.py)."""
+    return x.is_cuda and x.dtype == torch.float32 and _conv._F32_SPLIT == "f16x3"
+
+
+def _amax_buf(x: torch.Tensor):
+    return torch.empty(1, dtype=torch.float32, device=x.device) if _want_amax(x) else None
+
+
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu, res_slot=None,
-                tstats=None, link=None):
+                tstats=None, link=None, amax=None):
         x = _cl(x)
         if residual is not None:
             residual = _cl(residual).to(x.dtype)
@@ -129,7 +140,8 @@ class _BNActFn(torch.autograd.Function):
                      running_var.data_ptr() if running_var is not None else 0,
                      mean.data_ptr(), rstd.data_ptr(), ws.data_ptr(), float(momentum), float(eps), bool(relu),
                      mask.data_ptr() if mask is not None else 0,
-                     stats=ts[0].data_ptr() if ts is not None else 0, nstat=ts[1] if ts is not None else 0)
+                     stats=ts[0].data_ptr() if ts is not None else 0, nstat=ts[1] if ts is not None else 0,
+                     amax=amax.data_ptr() if amax is not None else 0)
         ctx.save_for_backward(x, mask, w, mean, rstd)
         ctx.link = link
         if link is not None:
@@ -151,6 +163,7 @@ class _BNActFn(torch.autograd.Function):
         dev = x.device.index
         stream = torch.cuda.current_stream(x.device).cuda_stream
         dx = torch.empty_like(x, memory_format=torch.channels_last)
+        amax = _amax_buf(x)
         # residual gradient of act(bn(x) + res) = dy*mask: with a GradSlot consumer it is
         # handed over as (dy, mask) and never written
         park = ctx.has_res and ctx.res_slot is not None and ctx.relu and mask is not None
@@ -176,7 +189,10 @@ class _BNActFn(torch.autograd.Function):
                      dres.data_ptr() if dres is not None else 0, M, C, w.data_ptr() if w is not None else 0,
                      mean.data_ptr(), rstd.data_ptr(), dgamma.data_ptr() if dgamma is not None else 0,
                      dbeta.data_ptr() if dbeta is not None else 0, ws.data_ptr(), bool(ctx.relu),
-                     part=part.data_ptr() if part is not None else 0, npart=npart, coef=coef)
+                     part=part.data_ptr() if part is not None else 0, npart=npart, coef=coef,
+                     amax=amax.data_ptr() if amax is not None else 0)
+        if amax is not None:
+            set_amax(dx, amax)
         if ctx.res_slot is not None:  # the shortcut's gradient is added by the block's first conv
             if park:
                 if not ctx.res_slot.put(dy, mask):
@@ -184,7 +200,7 @@ class _BNActFn(torch.autograd.Function):
             elif not ctx.res_slot.put(dres):
                 raise RuntimeError("GradSlot consumer ran before the BN backward")
             dres = None
-        return dx, dgamma, dbeta, None, None, dres, None, None, None, None, None, None
+        return dx, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None
 
 
 def bn_act_eval(x, weight, bias, running_mean, running_var, eps, residual=None, relu=True):
@@ -262,10 +278,13 @@ class BatchNormAct2d(nn.BatchNorm2d):
         if self.training or not self.track_running_stats:
             momentum, rm, rv = self._train_args()
             link = BNLink() if torch.is_grad_enabled() else None
+            amax = _amax_buf(x)
             y = _BNActFn.apply(x, self.weight, self.bias, rm, rv, residual, momentum, self.eps, self.act,
-                               res_slot, tile_stats_of(x), link)
+                               res_slot, tile_stats_of(x), link, amax)
             if link is not None:
                 y._mpit_bnlink = link
+            if amax is not None:
+                set_amax(y, amax)
             return y
         return bn_act_eval(x, self.weight, self.bias, self.running_mean, self.running_var, self.eps, residual, self.act)
 
@@ -279,7 +298,7 @@ class _BNPairFn(torch.autograd.Function):
     residual-gradient tensor of the unpaired form."""
 
     @staticmethod
-    def forward(ctx, x1, w1, b1, rm1, rv1, x2, w2, b2, rm2, rv2, mom1, eps1, mom2, eps2, ts1, ts2, link):
+    def forward(ctx, x1, w1, b1, rm1, rv1, x2, w2, b2, rm2, rv2, mom1, eps1, mom2, eps2, ts1, ts2, link, amax=None):
         x1, x2 = _cl(x1), _cl(x2).to(x1.dtype)
         M, C = _rows(x1)
         m = native()
@@ -304,8 +323,11 @@ class _BNPairFn(torch.autograd.Function):
             outs.append((wf, mean, rstd, ws))
         y = torch.empty_like(x1, memory_format=torch.channels_last)
         mask = torch.empty(m.bn_mask_bytes(bf16, M, C), dtype=torch.uint8, device=x1.device)
+        # (scratch of the output bound: bn1's workspace past its coefficients)
         m.bn_pair_apply(dev, stream, x1.data_ptr(), outs[0][3].data_ptr(), x2.data_ptr(), outs[1][3].data_ptr(),
-                        y.data_ptr(), M, C, mask.data_ptr(), f32=not bf16)
+                        y.data_ptr(), M, C, mask.data_ptr(), f32=not bf16,
+                        amax=amax.data_ptr() if amax is not None else 0,
+                        scratch=outs[0][3][2 * C:].data_ptr() if amax is not None else 0)
         (wf1, mean1, rstd1, _), (wf2, mean2, rstd2, _) = outs
         ctx.save_for_backward(x1, x2, mask, wf1, mean1, rstd1, wf2, mean2, rstd2)
         ctx.has = (w1 is not None, b1 is not None, w2 is not None, b2 is not None)
@@ -339,11 +361,17 @@ class _BNPairFn(torch.autograd.Function):
             wss.append(ws)
         dx1 = torch.empty_like(x1, memory_format=torch.channels_last)
         dx2 = torch.empty_like(x2, memory_format=torch.channels_last)
+        am1, am2 = _amax_buf(x1), _amax_buf(x1)
         m.bn_pair_bwd_apply(dev, stream, dy.data_ptr(), mask.data_ptr(), x1.data_ptr(), wss[0].data_ptr(),
                             dx1.data_ptr(), x2.data_ptr(), wss[1].data_ptr(), dx2.data_ptr(), M, C,
-                            f32=x1.dtype == torch.float32)
+                            f32=x1.dtype == torch.float32, amax1=am1.data_ptr() if am1 is not None else 0,
+                            amax2=am2.data_ptr() if am2 is not None else 0,
+                            scratch=wss[0][3 * C:].data_ptr() if am1 is not None else 0)
+        if am1 is not None:
+            set_amax(dx1, am1)
+            set_amax(dx2, am2)
         (dg1, db1), (dg2, db2) = grads
-        return (dx1, dg1, db1, None, None, dx2, dg2, db2, None, None, None, None, None, None, None, None, None)
+        return (dx1, dg1, db1, None, None, dx2, dg2, db2, None, None, None, None, None, None, None, None, None, None)
 
 
 def bn_pair(bn1: "BatchNormAct2d", x1: torch.Tensor, bn2: "BatchNormAct2d", x2: torch.Tensor) -> torch.Tensor:
@@ -357,8 +385,11 @@ def bn_pair(bn1: "BatchNormAct2d", x1: torch.Tensor, bn2: "BatchNormAct2d", x2: 
     mom1, rm1, rv1 = bn1._train_args()
     mom2, rm2, rv2 = bn2._train_args()
     link = BNLink() if torch.is_grad_enabled() else None
+    amax = _amax_buf(x1)
     y = _BNPairFn.apply(x1, bn1.weight, bn1.bias, rm1, rv1, x2, bn2.weight, bn2.bias, rm2, rv2, mom1, bn1.eps, mom2,
-                        bn2.eps, tile_stats_of(x1), tile_stats_of(x2), link)
+                        bn2.eps, tile_stats_of(x1), tile_stats_of(x2), link, amax)
     if link is not None:
         y._mpit_bnlink = link
+    if amax is not None:
+        set_amax(y, amax)
     return y

@@ -149,20 +149,117 @@ def mfma_dtype(x: torch.Tensor):
 # activation (round-2 kernels); default: the per-step weight plan writes it pre-split into
 # three bf16 planes and the GEMM splits only the activation (csrc/kernels/gemm.hip FM 4)
 _F32_BSPLIT = os.environ.get("MPIT_F32_BSPLIT", "1") != "0"
-# column width from which a weight operand is pre-split (MPIT_F32_PLANES_N=64: also the
-# N = 64 GEMMs on 128x64 tiles, 2 blocks per CU instead of 3)
-_F32_PLANES_N = int(os.environ.get("MPIT_F32_PLANES_N", "128"))
+# column width from which a weight operand is pre-split (bf16x6: MPIT_F32_PLANES_N=64 also
+# plane the N = 64 GEMMs on 128x64 tiles, 2 blocks per CU instead of 3; the fp16x3 planes are
+# smaller and take every width)
+_F32_PLANES_N = int(os.environ.get("MPIT_F32_PLANES_N",
+                                   "64" if os.environ.get("MPIT_F32_SPLIT", "f16x3") == "f16x3" else "128"))
+
+
+# MPIT_F32_SPLIT: how an fp32 step's GEMMs use the 16-bit matrix cores (csrc/kernels/gemm.hip):
+#   f16x3 (default): operands scaled by a power of two from a device-side bound of |x| and split
+#     into two fp16 terms, 3 fp16 MFMAs per product (FM 11) — the weight plan writes the two
+#     fp16 planes of each weight, the activation / gradient operand is split in registers with
+#     the bound its producer (the BN apply pass) wrote;
+#   bf16x6: three bf16 terms, 6 bf16 MFMAs per product (FM 9 / FM 3, rounds 2-3).
+_F32_SPLIT = os.environ.get("MPIT_F32_SPLIT", "f16x3")
+if _F32_SPLIT not in ("f16x3", "bf16x6"):
+    raise ValueError(f"MPIT_F32_SPLIT={_F32_SPLIT!r}: expected f16x3 or bf16x6")
 
 
 def _bps(w: torch.Tensor, f32: bool) -> int:
-    """Plane stride of a pre-split weight operand ([3, ...] bf16 planes h, m, l) of an fp32
-    GEMM, else 0 (the operand is fp32 / the call is bf16)."""
-    return w[0].numel() if (f32 and w is not None and w.dtype == torch.bfloat16) else 0
+    """Plane stride of a pre-split weight operand of an fp32 GEMM ([3, ...] bf16 planes h, m, l
+    or [2, ...] fp16 planes h, l), else 0 (the operand is fp32 / the call is bf16)."""
+    return w[0].numel() if (f32 and w is not None and w.dtype in (torch.bfloat16, torch.float16)) else 0
+
+
+def _bamax(w: torch.Tensor) -> int:
+    """Device pointer of the bound of |w| that scales fp16 weight planes (0: not fp16 planes)."""
+    if w is None or w.dtype != torch.float16:
+        return 0
+    return w._mpit_wamax.data_ptr()
+
+
+def _f16_exp(amax: torch.Tensor) -> torch.Tensor:
+    """gemm.hip fp16_exp on the host side (tensor ops, no sync): e with amax * 2^e in [2^13, 2^14)."""
+    e = (14 - torch.frexp(amax.float())[1]).clamp(-126, 116)
+    ok = (amax > 0) & torch.isfinite(amax)
+    return torch.where(ok, e, torch.zeros_like(e))
 
 
 def _unsplit(w: torch.Tensor) -> torch.Tensor:
-    """fp32 weight back from its three bf16 planes (exact: w == h + m + l)."""
+    """fp32 weight back from its planes (exact: w == h + m + l, or (h + l / 2^11) / 2^e)."""
+    if w.dtype == torch.float16:
+        s = torch.ldexp(torch.ones_like(w._mpit_wamax), -_f16_exp(w._mpit_wamax))
+        return (w[0].float() + w[1].float() / 2048.0) * s
     return (w[0].float() + w[1].float()) + w[2].float()
+
+
+def f16_planes(w: torch.Tensor, amax: torch.Tensor) -> torch.Tensor:
+    """[2, *w.shape] fp16 planes (h, l) of ``w * 2^e`` for the fp16x3 GEMMs, with e from the bound
+    ``amax`` >= max |w| (gemm.hip split1h's arithmetic on PyTorch ops: the same bits as the
+    weight plan's). ``(h + l / 2^11) / 2^e`` carries w to 2^-22 relative wherever |w| >= 2^-27
+    ``amax``, to 2^-48 ``amax`` absolute below that."""
+    one = torch.ones_like(amax)
+    e = _f16_exp(amax)
+    wf = w.float()
+    h = (wf * torch.ldexp(one, e)).half()
+    lo = (wf * torch.ldexp(one, e + 11) - h.float() * 2048.0).half()
+    p = torch.stack([h, lo])
+    p._mpit_wamax = amax
+    return p
+
+
+def set_amax(t: torch.Tensor, amax: torch.Tensor) -> torch.Tensor:
+    """Attach the device bound ``amax`` ([1] fp32, >= max |t|) to ``t`` (the fp16x3 GEMM operand
+    scale); valid for this storage and version only."""
+    t._mpit_amax = (amax, t.data_ptr(), t._version)
+    return t
+
+
+def amax_of(t: torch.Tensor):
+    """The bound attached to ``t`` by its producer (:func:`set_amax`), or None."""
+    a = getattr(t, "_mpit_amax", None)
+    if a is None or a[1] != t.data_ptr() or a[2] != t._version:
+        return None
+    return a[0]
+
+
+def _amax_arg(t: torch.Tensor, keep: list) -> int:
+    """Device pointer of a bound of |t| for an fp16x3 GEMM: the producer's, else one reduction
+    (the tensor is kept alive in ``keep`` until the launch is queued)."""
+    a = amax_of(t)
+    if a is None:
+        a = torch.linalg.vector_norm(t, float("inf")).reshape(1)
+        COUNTERS["amax_fallback"] += 1
+    keep.append(a)
+    return a.data_ptr()
+
+
+def _split_kw(a: torch.Tensor, w: torch.Tensor, f32: bool, keep: list) -> dict:
+    """GEMM keyword arguments of the weight operand ``w`` (planes) and the operand ``a``."""
+    bps = _bps(w, f32)
+    kw = dict(bps=bps)
+    bam = _bamax(w) if bps else 0
+    if bam:
+        kw.update(amax_a=_amax_arg(a, keep), amax_b=bam)
+    return kw
+
+
+def _wgrad_kw(dy: torch.Tensor, xamax, f32: bool, side, keep: list) -> dict:
+    """fp16x3 operand bounds of a backward-weight GEMM (both producers' bounds, else the bf16x6
+    path: a fallback reduction on the compute stream would not be ordered before the side
+    stream's GEMM); the bound tensors are kept alive for the side stream."""
+    ya = amax_of(dy)
+    if not f32 or _F32_SPLIT != "f16x3" or ya is None or xamax is None:
+        return {}
+    keep += [ya, xamax]
+    _used_on(side, ya, xamax)
+    COUNTERS["wgrad_f16x3"] += 1
+    return dict(amax_y=ya.data_ptr(), amax_x=xamax.data_ptr())
+
+
+COUNTERS = {"amax_fallback": 0, "wgrad_f16x3": 0}
 
 
 def _to(x: torch.Tensor, dt) -> torch.Tensor:
@@ -178,10 +275,12 @@ def tile_stats_to_sums(part: torch.Tensor, M: int, N: int) -> torch.Tensor:
     return torch.stack([(n * mean).sum(0), (m2 + n * mean * mean).sum(0)]).float()
 
 
-def gemm_nt(a: torch.Tensor, b: torch.Tensor, stats: bool = False):
+def gemm_nt(a: torch.Tensor, b: torch.Tensor, stats: bool = False, f16x3: bool = False):
     """``a[M,K] . b[N,K]^T`` in bf16 or fp32 (fp32 accumulate; result in the operands'
     dtype). With ``stats`` also returns the per-column ``[sum, sum of squares]`` of the
-    result as a [2, N] fp32 tensor (from the epilogue's per-tile (mean, M2) partials)."""
+    result as a [2, N] fp32 tensor (from the epilogue's per-tile (mean, M2) partials).
+    ``f16x3`` (fp32): the fp16x3 split products (b as fp16 planes, bounds from reductions)
+    instead of the bf16x6 in-register split."""
     if a.dtype not in (torch.bfloat16, torch.float32) or b.dtype != a.dtype:
         raise TypeError("gemm_nt takes two bf16 or two fp32 operands")
     if a.dim() != 2 or b.dim() != 2 or a.shape[1] != b.shape[1] or a.stride(1) != 1 or b.stride(1) != 1:
@@ -191,15 +290,23 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, stats: bool = False):
     c = torch.empty((M, N), dtype=a.dtype, device=a.device)
     m = native()
     st = torch.empty(m.gemm_nt_stats_floats(M, N), dtype=torch.float32, device=a.device) if stats else None
-    m.gemm_nt(a.device.index, _stream(a), M, N, K, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), c.data_ptr(),
-              N, st.data_ptr() if st is not None else 0, f32=a.dtype == torch.float32)
+    kw, keep = {}, []
+    if f16x3:
+        if a.dtype != torch.float32:
+            raise TypeError("gemm_nt: f16x3 is an fp32 GEMM")
+        b = f16_planes(b.contiguous(), torch.linalg.vector_norm(b, float("inf")).reshape(1))
+        kw = _split_kw(a, b, True, keep)
+    m.gemm_nt(a.device.index, _stream(a), M, N, K, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(-2), c.data_ptr(),
+              N, st.data_ptr() if st is not None else 0, f32=a.dtype == torch.float32, **kw)
     if stats:
         return c, tile_stats_to_sums(st, M, N)
     return c
 
 
-def gemm_tn(y: torch.Tensor, x: torch.Tensor, out: torch.Tensor = None, beta: float = 0.0) -> torch.Tensor:
-    """``out[N,K] = beta*out + y[M,N]^T . x[M,K]`` in fp32 from bf16 or fp32 operands."""
+def gemm_tn(y: torch.Tensor, x: torch.Tensor, out: torch.Tensor = None, beta: float = 0.0,
+            f16x3: bool = False) -> torch.Tensor:
+    """``out[N,K] = beta*out + y[M,N]^T . x[M,K]`` in fp32 from bf16 or fp32 operands
+    (``f16x3``: fp32 operands on the fp16x3 split products, bounds from reductions)."""
     if y.dtype not in (torch.bfloat16, torch.float32) or x.dtype != y.dtype:
         raise TypeError("gemm_tn takes two bf16 or two fp32 operands")
     M, N = y.shape
@@ -214,8 +321,14 @@ def gemm_tn(y: torch.Tensor, x: torch.Tensor, out: torch.Tensor = None, beta: fl
     # split partials; with a single split and beta != 0 the one partial goes through the reduce
     nws = m.gemm_tn_ws_floats(dev, M, N, K) or (N * K if beta != 0.0 else 0)
     ws = torch.empty(nws, dtype=torch.float32, device=y.device) if nws else None
+    kw, keep = {}, []
+    if f16x3:
+        if y.dtype != torch.float32:
+            raise TypeError("gemm_tn: f16x3 is an fp32 GEMM")
+        keep = [torch.linalg.vector_norm(t, float("inf")).reshape(1) for t in (y, x)]
+        kw = dict(amax_y=keep[0].data_ptr(), amax_x=keep[1].data_ptr())
     m.gemm_tn(dev, _stream(y), M, N, K, y.data_ptr(), y.stride(0), x.data_ptr(), x.stride(0), out.data_ptr(),
-              ws.data_ptr() if ws is not None else 0, float(beta), f32=y.dtype == torch.float32)
+              ws.data_ptr() if ws is not None else 0, float(beta), f32=y.dtype == torch.float32, **kw)
     return out
 
 
@@ -355,9 +468,11 @@ class _Conv1x1Fn(torch.autograd.Function):
         if hold is not None:  # batch-norm statistics of y from the accumulators
             st, nt = _tile_stats(co, M, x.device)
             hold.append((st, nt))
+        keep = []
         m.gemm_nt(x.device.index, _stream(x), M, co, ci, x.data_ptr(), ci, wb.data_ptr(), ci, y.data_ptr(), co,
-                  st.data_ptr() if st is not None else 0, f32=f32, bps=_bps(wb, f32))
+                  st.data_ptr() if st is not None else 0, f32=f32, **_split_kw(x, wb, f32, keep))
         ctx.save_for_backward(x, wt)
+        ctx.xamax = amax_of(x) if f32 else None
         ctx.wshape = weight.shape
         ctx.slot = slot
         ctx.link = link
@@ -383,16 +498,17 @@ class _Conv1x1Fn(torch.autograd.Function):
             if ctx.link is not None:  # the producing BN's backward reduction, in the epilogue
                 nt = m.gemm_nt_tiles(M)
                 kw, part, part2, fb = _red_args(ctx.link, ci, nt, x.device, fold=True)
+            keep = []
+            kw.update(_split_kw(dy, wt, f32, keep))
             if extra is not None:  # gradient parked by the block (GradSlot): added in the epilogue
                 extra = _to(extra, dt)
                 if extra.shape != x.shape:
                     raise RuntimeError("GradSlot gradient does not match the convolution input")
                 m.gemm_nt(dev, s, M, ci, co, dy.data_ptr(), co, wt.data_ptr(), co, dx.data_ptr(), ci, 0,
-                          extra.data_ptr(), emask.data_ptr() if emask is not None else 0, f32=f32, bps=_bps(wt, f32),
-                          **kw)
+                          extra.data_ptr(), emask.data_ptr() if emask is not None else 0, f32=f32, **kw)
             else:
                 m.gemm_nt(dev, s, M, ci, co, dy.data_ptr(), co, wt.data_ptr(), co, dx.data_ptr(), ci, 0, f32=f32,
-                          bps=_bps(wt, f32), **kw)
+                          **kw)
             if part is not None:
                 ctx.link.publish(part, nt, dx, part2, fb)
         if ctx.needs_input_grad[1]:
@@ -401,8 +517,10 @@ class _Conv1x1Fn(torch.autograd.Function):
             dw = torch.empty(ctx.wshape, dtype=torch.float32, device=x.device)
             nws = m.gemm_tn_ws_floats(dev, M, co, ci)
             ws = torch.empty(nws, dtype=torch.float32, device=x.device) if nws else None
+            keep = []
             m.gemm_tn(dev, side.cuda_stream if side is not None else s, M, co, ci, dy.data_ptr(), co, x.data_ptr(),
-                      ci, dw.data_ptr(), ws.data_ptr() if ws is not None else 0, 0.0, f32=f32)
+                      ci, dw.data_ptr(), ws.data_ptr() if ws is not None else 0, 0.0, f32=f32,
+                      **_wgrad_kw(dy, ctx.xamax, f32, side, keep))
             _used_on(side, dy, x, dw, ws)
         return dx, dw, None, None, None, None, None
 
@@ -498,8 +616,9 @@ def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None):
             if link is not None:
                 nt = m.gemm_nt_tiles(nb * h * w)
                 kw, part, _, fb = _red_args(link, c, nt, x.device, fold=True)
+            keep = []
             m.conv_fwd(dev, st, nb, ho, wo, co, c, r, s, 1, r - 1 - pad, dz.data_ptr(), wt.data_ptr(),
-                       dx.data_ptr(), f32=f32, bps=_bps(wt, f32), **kw)
+                       dx.data_ptr(), f32=f32, **_split_kw(dz, wt, f32, keep), **kw)
             if part is not None:
                 link.publish(part, nt, dx, None, fb)
         elif wt is not None:
@@ -510,8 +629,9 @@ def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None):
             if link is not None:
                 nt = m.conv_dgrad_strided_tiles(nb, h, w, c, co, r, s, stride, pad)
                 kw, part, _, _ = _red_args(link, c, nt, x.device)
+            keep = []
             m.conv_dgrad_strided(dev, st, nb, h, w, c, co, r, s, stride, pad, dz.data_ptr(), wt.data_ptr(),
-                                 dx.data_ptr(), f32=f32, bps=_bps(wt, f32), **kw)
+                                 dx.data_ptr(), f32=f32, **_split_kw(dz, wt, f32, keep), **kw)
             if part is not None:
                 link.publish(part, nt, dx)
         else:  # MIOpen's NHWC backward-data
@@ -525,8 +645,10 @@ def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None):
         dw = torch.empty((co, c, r, s), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
         nws = m.conv_wgrad_ws_floats(dev, nb, h, w, c, co, r, s, stride, pad)
         ws = torch.empty(nws, dtype=torch.float32, device=x.device) if nws else None
+        keep = []
         m.conv_wgrad(dev, side.cuda_stream if side is not None else st, nb, h, w, c, co, r, s, stride, pad,
-                     dz.data_ptr(), x.data_ptr(), dw.data_ptr(), ws.data_ptr() if ws is not None else 0, 0.0, f32=f32)
+                     dz.data_ptr(), x.data_ptr(), dw.data_ptr(), ws.data_ptr() if ws is not None else 0, 0.0, f32=f32,
+                     **_wgrad_kw(dz, getattr(ctx, "xamax", None), f32, side, keep))
         _used_on(side, dz, x, dw, ws)
     return dx, dw
 
@@ -580,10 +702,13 @@ class _ConvFn(torch.autograd.Function):
         if hold is not None and not relu and b is None:  # batch-norm statistics of y
             st, nt = _tile_stats(co, nb * ho * wo, x.device)
             hold.append((st, nt))
+        keep = []
         native().conv_fwd(x.device.index, _stream(x), nb, h, w, c, co, r, s, stride, pad, x.data_ptr(), wb.data_ptr(),
                           y.data_ptr(), stats=st.data_ptr() if st is not None else 0,
-                          bias=b.data_ptr() if b is not None else 0, relu=bool(relu), f32=f32, bps=_bps(wb, f32))
+                          bias=b.data_ptr() if b is not None else 0, relu=bool(relu), f32=f32,
+                          **_split_kw(x, wb, f32, keep))
         ctx.save_for_backward(x, wb, wt, y if relu else None)
+        ctx.xamax = amax_of(x) if f32 else None
         ctx.geo = (stride, pad, bias is not None, bool(relu))
         ctx.link = link
         return y
@@ -692,6 +817,12 @@ class WeightCastPlan:
         m = native()
         f32 = self.dtype == torch.float32
         planes = f32 and _F32_BSPLIT
+        # fp16x3: two fp16 planes per weight operand, scaled by the bound of |w| over the plan
+        # (self.amax, refreshed by run() before the cast launch)
+        f16p = planes and _F32_SPLIT == "f16x3"
+        npl, pdt = (2, torch.float16) if f16p else (3, torch.bfloat16)
+        self.wlist = []
+        self.amax = None
         for mod in self.model.modules():
             kind = None
             if isinstance(mod, Conv1x1) and mod.stride == (1, 1):
@@ -718,12 +849,15 @@ class WeightCastPlan:
             # would keep the weight's AccumulateGrad node (made at build time, on the stream
             # current then) alive into every step — autograd then warns that the node's stream
             # differs from the step's and inserts a cross-stream wait per weight
+            if f16p and (pl_b or pl_t) and self.amax is None:
+                self.amax = torch.zeros(1, dtype=torch.float32, device=w.device)
             if f32 and not pl_b:
                 wb = _as_rsc(w.detach())
             else:
-                wb = torch.empty(((3,) if pl_b else ()) + (co, r, sw, c), dtype=torch.bfloat16, device=w.device)
-            lt = (3,) if pl_t else ()
-            odt = torch.bfloat16 if pl_t else self.dtype
+                wb = torch.empty(((npl,) if pl_b else ()) + (co, r, sw, c), dtype=pdt if pl_b else torch.bfloat16,
+                                 device=w.device)
+            lt = (npl,) if pl_t else ()
+            odt = pdt if pl_t else self.dtype
             if kind == 0:
                 wt = torch.empty(lt + (c, r, sw, co), dtype=odt, device=w.device)
             elif kind == 1:
@@ -732,13 +866,20 @@ class WeightCastPlan:
             else:
                 wt = None
             if isinstance(mod, Conv1x1):  # the 1x1 path takes 2-D [co, ci] / [ci, co] views
-                wb, wt = wb.reshape(((3,) if pl_b else ()) + (co, c)), wt.view(lt + (c, co))
+                wb, wt = wb.reshape(((npl,) if pl_b else ()) + (co, c)), wt.view(lt + (c, co))
             if f32 and not (pl_b or pl_t) and wt is None:
                 self.mods.append((mod, w.data_ptr(), (wb, wt)))  # nothing to write
                 continue
-            flags = kind | (256 if f32 else 0) | (512 if pl_b else 0) | (1024 if pl_t else 0)
+            if f16p and (pl_b or pl_t):
+                self.wlist.append(w.detach())
+                for t in (wb, wt):
+                    if t is not None and t.dtype == torch.float16:
+                        t._mpit_wamax = self.amax
+            flags = (kind | (256 if f32 else 0) | (512 if pl_b else 0) | (1024 if pl_t else 0)
+                     | (2048 if f16p and (pl_b or pl_t) else 0))
             specs.append([flags, w.data_ptr(), wb.data_ptr() if (pl_b or not f32) else 0,
-                          wt.data_ptr() if wt is not None else 0, co, c, r, sw, mod.stride[0], mod.padding[0]])
+                          wt.data_ptr() if wt is not None else 0, co, c, r, sw, mod.stride[0], mod.padding[0],
+                          self.amax.data_ptr() if (f16p and (pl_b or pl_t)) else 0])
             self.mods.append((mod, w.data_ptr(), (wb, wt)))
         self.njobs = len(specs)
         self.table = None
@@ -757,6 +898,10 @@ class WeightCastPlan:
             self._build()  # parameters moved (FlatParams.rebind)
         if self.table is not None:
             dev = self.table.device
+            if self.wlist:  # the planes' scale: max |w| over the plan's fp16-plane weights
+                with torch.no_grad():
+                    torch.amax(torch.stack(torch._foreach_norm(self.wlist, float("inf"))), 0, keepdim=True,
+                               out=self.amax)
             native().cast_jobs_run(dev.index, torch.cuda.current_stream(dev).cuda_stream, self.table.data_ptr(),
                                    self.njobs, self.nblocks)
         self.valid = True

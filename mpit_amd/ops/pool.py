@@ -11,6 +11,7 @@ import torch
 import torch.nn as nn
 
 from .._ext import native
+from .conv import amax_of, set_amax
 
 
 def _stream(t: torch.Tensor) -> int:
@@ -63,5 +64,9 @@ class MaxPool2dNHWC(nn.MaxPool2d):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.fused(x):
-            return _MaxPoolFn.apply(x, _int(self.kernel_size), _int(self.stride), _int(self.padding))
+            y = _MaxPoolFn.apply(x, _int(self.kernel_size), _int(self.stride), _int(self.padding))
+            a = amax_of(x)
+            if a is not None:  # every output is one of the inputs: the input's bound holds
+                set_amax(y, a)
+            return y
         return super().forward(x)

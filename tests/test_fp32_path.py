@@ -48,6 +48,56 @@ def test_gemm_nt_fp32_vs_fp64(M, N, K):
     assert e < 2e-6
 
 
+def test_f16_planes_carry_22_bits_cpu():
+    """fp16x3 weight planes: (h + l / 2^11) / 2^e == w to 2^-22 relative for |w| 2^e >= 2^-14
+    (within 2^27 of the bound; the scale places the bound in [2^13, 2^14)); smaller values keep
+    their absolute error below 2^-48 of the bound."""
+    torch.manual_seed(0)
+    w = torch.randn(4096) * torch.exp(torch.randn(4096) * 3)
+    amax = w.abs().max().reshape(1)
+    p = C.f16_planes(w, amax)
+    assert p.dtype == torch.float16 and p.shape == (2, 4096)
+    e = int(C._f16_exp(amax).item())
+    assert 2.0 ** 13 <= amax.item() * 2.0 ** e < 2.0 ** 14
+    back = C._unsplit(p)
+    err = (back.double() - w.double()).abs()
+    big = w.abs() * 2.0 ** e >= 2.0 ** -14
+    assert (err[big] <= w.double().abs()[big] * 2.0 ** -22).all()
+    assert (err[~big] <= amax.item() * 2.0 ** -48).all()
+    assert torch.isfinite(p.float()).all()
+
+
+@gpu
+@pytest.mark.parametrize("M,N,K", [(128, 64, 64), (1000, 192, 128), (4096, 256, 512), (333, 64, 1024),
+                                   (12544, 512, 2048), (50176, 128, 576)])
+def test_gemm_nt_f16x3_vs_fp64(M, N, K):
+    """fp16x3 split products (FM 11): within 2x of PyTorch fp32's error against fp64, also for
+    a gradient-sized operand (1e-7 scale: the power-of-two scale keeps it in fp16 range)."""
+    torch.manual_seed(M + N + K)
+    for sa in (1.0, 1e-7):
+        a = torch.randn(M, K, device="cuda") * sa
+        b = torch.randn(N, K, device="cuda") * 0.05
+        ref = a.double().cpu() @ b.double().cpu().t()
+        c = C.gemm_nt(a, b, f16x3=True)
+        lib = a @ b.t()
+        e, el = _rel(c, ref), _rel(lib, ref)
+        assert e <= 2.0 * el + 1e-9, (sa, e, el)
+        assert e < 2e-6
+
+
+@gpu
+@pytest.mark.parametrize("M,N,K", [(64, 64, 64), (1000, 64, 128), (4096, 128, 128), (200704, 256, 64),
+                                   (12544, 512, 2048), (5000, 192, 320)])
+def test_gemm_tn_f16x3_vs_fp64(M, N, K):
+    torch.manual_seed(M % 97 + N + K)
+    y, x = torch.randn(M, N, device="cuda") * 1e-6, torch.relu(torch.randn(M, K, device="cuda"))
+    ref = y.double().cpu().t() @ x.double().cpu()
+    out = C.gemm_tn(y, x, f16x3=True)
+    lib = y.t() @ x
+    e, el = _rel(out, ref), _rel(lib, ref)
+    assert e <= 2.0 * el + 1e-9, (e, el)
+
+
 @gpu
 @pytest.mark.parametrize("M,N,K", [(256, 64, 64), (1000, 128, 192)])
 def test_gemm_nt_fp32_stats(M, N, K):
@@ -196,11 +246,13 @@ def _ref_block(blk, x):
 
 
 @gpu
+@pytest.mark.parametrize("plan", [False, True])
 @pytest.mark.parametrize("inp,planes,stride", [(256, 64, 1), (256, 128, 2)])
-def test_bottleneck_fp32_vs_fp64(inp, planes, stride):
+def test_bottleneck_fp32_vs_fp64(inp, planes, stride, plan):
     """A whole fused bottleneck block in fp32 (GEMM-epilogue BN statistics and backward
     reductions, parked shortcut gradients, bn_pair) against fp64 on the CPU: within 2x of
-    the same block on PyTorch's fp32 ops."""
+    the same block on PyTorch's fp32 ops. With the weight plan (the trainer's setting) every
+    GEMM runs the fp16x3 split products on the bounds the BN passes wrote."""
     from mpit_amd.models.resnet import Bottleneck, conv1x1
     from mpit_amd.ops.bn import BatchNormAct2d
 
@@ -215,10 +267,18 @@ def test_bottleneck_fp32_vs_fp64(inp, planes, stride):
             m.bias.data.uniform_(-0.2, 0.2)
     x = _cl(torch.randn(4, inp, 14, 14, device="cuda"))
     x1 = x.clone().requires_grad_(True)
+    wp = C.WeightCastPlan(blk, torch.float32) if plan else None
+    n16 = C.COUNTERS["wgrad_f16x3"]
+    if wp is not None:
+        wp.run()
     y1 = blk(x1)
     assert y1.dtype == torch.float32
     g = torch.randn(y1.shape, device="cuda")
     y1.backward(g)
+    if wp is not None:
+        wp.invalidate()
+        if C._F32_SPLIT == "f16x3":
+            assert C.COUNTERS["wgrad_f16x3"] > n16  # bounds reached the backward-weight GEMMs
     ours = {n: p.grad.detach().clone() for n, p in blk.named_parameters()}
     ours.update(y=y1.detach(), dx=x1.grad)
     blk.zero_grad(set_to_none=True)
@@ -336,11 +396,19 @@ def test_weight_cast_plan_fp32_planes_exact():
     plan = C.WeightCastPlan(net, torch.float32)
     plan.run()
     torch.cuda.synchronize()
+
+    def same(got, want):  # bf16x6 planes: exact; fp16x3 planes: 22 bits (f16_planes' arithmetic)
+        if got.dtype == torch.float16:
+            assert torch.equal(got, C.f16_planes(want, got._mpit_wamax).view(got.shape))
+            return torch.allclose(C._unsplit(got), want.view(got.shape[1:]), rtol=2.0 ** -22,
+                                  atol=got._mpit_wamax.item() * 2.0 ** -47)
+        return torch.equal(C._unsplit(got).reshape(-1), want.reshape(-1))
+
     for mod, _, (wb, wt) in plan.mods:
         w = mod.weight.detach()
-        if wb.dtype == torch.bfloat16:
-            assert wb.shape[0] == 3 and w.shape[0] % C._F32_PLANES_N == 0
-            assert torch.equal(C._unsplit(wb).reshape(-1), C._as_rsc(w).reshape(-1))
+        if wb.dtype in (torch.bfloat16, torch.float16):
+            assert wb.shape[0] == (2 if wb.dtype == torch.float16 else 3) and w.shape[0] % C._F32_PLANES_N == 0
+            assert same(wb, C._as_rsc(w).contiguous())
         else:
             assert wb.data_ptr() == w.data_ptr()
         if isinstance(mod, C.Conv1x1):
@@ -352,9 +420,12 @@ def test_weight_cast_plan_fp32_planes_exact():
         else:
             _, rt = C.conv_weights(w, True, torch.float32)
         assert (wt is None) == (rt is None)
-        if wt is not None:
-            got = C._unsplit(wt) if wt.dtype == torch.bfloat16 else wt
-            assert torch.equal(got.reshape(-1), rt.reshape(-1))
+        if wt is not None and wt.dtype in (torch.bfloat16, torch.float16):
+            assert same(wt, rt.contiguous())
+        elif wt is not None:
+            assert torch.equal(wt.reshape(-1), rt.reshape(-1))
+    if plan.wlist:  # the plan's bound covers every plane weight
+        assert plan.amax.item() == max(w.abs().max().item() for w in plan.wlist)
 
 
 @gpu
@@ -363,20 +434,23 @@ def test_presplit_weights_bitwise_equal_register_split():
     split of the fp32 weights gives (FM 3): same planes, same MFMA sequence. Two bottleneck
     blocks forward + backward (1x1, 3x3, strided dgrad classes, downsample)."""
     def run(planes):
-        old = C._F32_BSPLIT
-        C._F32_BSPLIT = planes
+        old = C._F32_BSPLIT, C._F32_SPLIT, C._F32_PLANES_N
+        C._F32_BSPLIT, C._F32_SPLIT, C._F32_PLANES_N = planes, "bf16x6", 128  # the bf16x6 kernels
         try:
             net = _bottleneck_net()
             plan = C.WeightCastPlan(net, torch.float32)
         finally:
-            C._F32_BSPLIT = old
+            C._F32_BSPLIT = old[0]
         torch.manual_seed(11)
         x = _cl(torch.randn(4, 256, 14, 14, device="cuda")).requires_grad_(True)
-        plan.run()
-        y = net(x)
-        y.backward(torch.randn_like(y))
-        plan.invalidate()
-        torch.cuda.synchronize()
+        try:
+            plan.run()
+            y = net(x)
+            y.backward(torch.randn_like(y))
+            plan.invalidate()
+            torch.cuda.synchronize()
+        finally:
+            C._F32_SPLIT, C._F32_PLANES_N = old[1], old[2]
         return [y.detach(), x.grad] + [p.grad for p in net.parameters()]
 
     a, b = run(True), run(False)
@@ -409,11 +483,21 @@ def test_convact_weight_plan_bitwise(dt):
         torch.cuda.synchronize()
         return [y.detach().float(), x.grad] + [p.grad.clone() for p in net.parameters()]
 
-    plan = C.WeightCastPlan(net, dt)
-    assert plan.njobs == 3
-    a, b = run(plan), run(None)
-    for u, v in zip(a, b):
-        assert torch.equal(u, v)
+    old = C._F32_SPLIT, C._F32_PLANES_N
+    try:
+        # bitwise: the bf16x6 planes split like the per-call path; fp16x3: within fp32 rounding
+        for mode in ("bf16x6", "f16x3") if dt == torch.float32 else ("bf16x6",):
+            C._F32_SPLIT, C._F32_PLANES_N = mode, 128 if mode == "bf16x6" else 64
+            plan = C.WeightCastPlan(net, dt)
+            assert plan.njobs == 3
+            a, b = run(plan), run(None)
+            for u, v in zip(a, b):
+                if mode == "bf16x6":
+                    assert torch.equal(u, v)
+                else:
+                    assert _rel(u, v) < 1e-5, _rel(u, v)
+    finally:
+        C._F32_SPLIT, C._F32_PLANES_N = old
 
 
 _WGRAD_CHILD = r"""

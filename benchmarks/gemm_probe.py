@@ -6,6 +6,9 @@ runs and tile experiments), bf16 or fp32 (``--f32``: v_mfma_f32_32x32x2_f32).
     python benchmarks/gemm_probe.py [--f32] conv N H W C Co R stride [iters]
     python benchmarks/gemm_probe.py [--f32] wgrad N H W C Co R stride [iters]
     python benchmarks/gemm_probe.py [--f32] dgrad N H W C Co R 1 [iters]      (stride-1 backward-data)
+
+``--f32 --bsplit``: the weight operand as three bf16 planes (bf16x6, FM 9); ``--f32 --f16x3``:
+the fp16x3 split products (FM 11: weight as two fp16 planes, operand bounds from reductions).
 """
 import json
 import os
@@ -36,7 +39,13 @@ def main():
     args = sys.argv[1:]
     f32 = "--f32" in args
     bsplit = "--bsplit" in args  # fp32: weight operand as three pre-split bf16 planes (FM 4)
-    args = [a for a in args if a not in ("--f32", "--bsplit")]
+    f16x3 = "--f16x3" in args
+    args = [a for a in args if a not in ("--f32", "--bsplit", "--f16x3")]
+    from mpit_amd.ops import conv as cops
+
+    def bound(t):
+        return cops.bound_of_value(torch.linalg.vector_norm(t.float(), float("inf")))
+    keep = []
 
     def planes(t):
         t = t.float()
@@ -46,6 +55,10 @@ def main():
         return torch.stack([h, m_, (r - m_.float()).to(torch.bfloat16)]).contiguous()
 
     def bp(t):  # (operand, bps) of a weight operand
+        if f32 and f16x3:
+            p = cops.f16_planes(t.contiguous(), bound(t))
+            keep.append(p)
+            return p, p[0].numel()
         if f32 and bsplit:
             p = planes(t)
             return p, p[0].numel()
@@ -60,8 +73,9 @@ def main():
             a = torch.randn(M, K, device="cuda").to(dt)
             b, bps = bp((torch.randn(N, K, device="cuda") * 0.05).to(dt))
             c = torch.empty(M, N, device="cuda", dtype=dt)
+            kw = dict(amax_a=bound(a).data_ptr(), amax_b=b._mpit_wamax.data_ptr()) if (f32 and f16x3) else {}
             ms = timeit(lambda: m.gemm_nt(0, st, M, N, K, a.data_ptr(), K, b.data_ptr(), K, c.data_ptr(), N, 0,
-                                          f32=f32, bps=bps), it)
+                                          f32=f32, bps=bps, **kw), it)
             by = es * (M * K + N * K + M * N)
         else:
             y = torch.randn(M, N, device="cuda").to(dt)
@@ -69,8 +83,10 @@ def main():
             out = torch.empty(N, K, device="cuda")
             nws = m.gemm_tn_ws_floats(0, M, N, K)
             ws = torch.empty(max(1, nws), device="cuda")
+            keep += [bound(y), bound(x)]
+            kw = dict(amax_y=keep[-2].data_ptr(), amax_x=keep[-1].data_ptr()) if (f32 and f16x3) else {}
             ms = timeit(lambda: m.gemm_tn(0, st, M, N, K, y.data_ptr(), N, x.data_ptr(), K, out.data_ptr(),
-                                          ws.data_ptr(), 0.0, f32=f32), it)
+                                          ws.data_ptr(), 0.0, f32=f32, **kw), it)
             by = es * (M * K + M * N) + 4 * N * K
         fl = 2.0 * M * N * K
     else:
@@ -81,20 +97,25 @@ def main():
         x = torch.randn(Nb, H, W, C, device="cuda").to(dt)
         w, wbps = bp((torch.randn(Co, R, R, C, device="cuda") * 0.05).to(dt))
         y = torch.randn(Nb, Ho, Wo, Co, device="cuda").to(dt)
+        keep += [bound(x), bound(y)]
+        fx = f32 and f16x3
         if kind == "conv":
+            kw = dict(amax_a=keep[-2].data_ptr(), amax_b=w._mpit_wamax.data_ptr()) if fx else {}
             ms = timeit(lambda: m.conv_fwd(0, st, Nb, H, W, C, Co, R, R, S, pad, x.data_ptr(), w.data_ptr(),
-                                           y.data_ptr(), f32=f32, bps=wbps), it)
+                                           y.data_ptr(), f32=f32, bps=wbps, **kw), it)
         elif kind == "dgrad":  # stride-1 backward-data = forward conv of dy with the transposed weight
             wt, tbps = bp((torch.randn(C, R, R, Co, device="cuda") * 0.05).to(dt))
             dx = torch.empty_like(x)
+            kw = dict(amax_a=keep[-1].data_ptr(), amax_b=wt._mpit_wamax.data_ptr()) if fx else {}
             ms = timeit(lambda: m.conv_fwd(0, st, Nb, Ho, Wo, Co, C, R, R, 1, R - 1 - pad, y.data_ptr(),
-                                           wt.data_ptr(), dx.data_ptr(), f32=f32, bps=tbps), it)
+                                           wt.data_ptr(), dx.data_ptr(), f32=f32, bps=tbps, **kw), it)
         else:
             dw = torch.empty(Co, R, R, C, device="cuda")
             nws = m.conv_wgrad_ws_floats(0, Nb, H, W, C, Co, R, R, S, pad)
             ws = torch.empty(max(1, nws), device="cuda")
+            kw = dict(amax_y=keep[-1].data_ptr(), amax_x=keep[-2].data_ptr()) if fx else {}
             ms = timeit(lambda: m.conv_wgrad(0, st, Nb, H, W, C, Co, R, R, S, pad, y.data_ptr(), x.data_ptr(),
-                                             dw.data_ptr(), ws.data_ptr(), 0.0, f32=f32), it)
+                                             dw.data_ptr(), ws.data_ptr(), 0.0, f32=f32, **kw), it)
         fl = 2.0 * Nb * Ho * Wo * Co * R * R * C
         by = es * (x.numel() + (w[0].numel() if wbps else w.numel()) + y.numel())
     print(json.dumps({"args": sys.argv[1:], "ms": round(ms, 4), "tflops": round(fl / ms / 1e9, 1),

@@ -136,10 +136,10 @@ PYBIND11_MODULE(_mpit, m) {
          uintptr_t red_mask, uintptr_t red_mean, int64_t red_row0, uintptr_t red_part2, uintptr_t red_x2,
          uintptr_t red_mean2, bool f32, uintptr_t fold_coef, uintptr_t fold_gamma, uintptr_t fold_rstd,
          uintptr_t fold_dgamma, uintptr_t fold_dbeta, uintptr_t fold_lvl, int64_t bps, uintptr_t amax_a,
-         uintptr_t amax_b) {
+         uintptr_t amax_b, uintptr_t fold_zero) {
         BnRed r{red_part, red_x, red_mask, red_mean, red_row0, red_part2, red_x2, red_mean2};
         r.fcoef = fold_coef; r.fgamma = fold_gamma; r.frstd = fold_rstd;
-        r.fdgamma = fold_dgamma; r.fdbeta = fold_dbeta; r.flvl = fold_lvl;
+        r.fdgamma = fold_dgamma; r.fdbeta = fold_dbeta; r.flvl = fold_lvl; r.fzero = fold_zero;
         r.amax_a = amax_a; r.amax_b = amax_b;
         gemm_nt(dev, S(s), M, N, K, A, lda, B, ldb, C, ldc, stats, cin, cmask, &r, f32, bps);
       },
@@ -149,8 +149,9 @@ PYBIND11_MODULE(_mpit, m) {
       py::arg("red_mean") = 0, py::arg("red_row0") = 0, py::arg("red_part2") = 0, py::arg("red_x2") = 0,
       py::arg("red_mean2") = 0, py::arg("f32") = false, py::arg("fold_coef") = 0, py::arg("fold_gamma") = 0,
       py::arg("fold_rstd") = 0, py::arg("fold_dgamma") = 0, py::arg("fold_dbeta") = 0, py::arg("fold_lvl") = 0,
-      py::arg("bps") = 0, py::arg("amax_a") = 0, py::arg("amax_b") = 0);
+      py::arg("bps") = 0, py::arg("amax_a") = 0, py::arg("amax_b") = 0, py::arg("fold_zero") = 0);
   m.def("gemm_nt_fold_lvl_floats", &gemm_nt_fold_lvl_floats);
+  m.def("bound_floats", [] { return kBoundFloats; });
   m.def("gemm_tn_supported", &gemm_tn_supported);
   m.def("gemm_tn_ws_floats", &gemm_tn_ws_floats);
   m.def("device_cu_count", &device_cu_count);
@@ -198,10 +199,10 @@ PYBIND11_MODULE(_mpit, m) {
          uintptr_t red_x, uintptr_t red_mask, uintptr_t red_mean, int64_t red_row0, uintptr_t red_part2,
          uintptr_t red_x2, uintptr_t red_mean2, bool f32, uintptr_t fold_coef, uintptr_t fold_gamma,
          uintptr_t fold_rstd, uintptr_t fold_dgamma, uintptr_t fold_dbeta, uintptr_t fold_lvl, int64_t bps,
-         uintptr_t amax_a, uintptr_t amax_b) {
+         uintptr_t amax_a, uintptr_t amax_b, uintptr_t fold_zero) {
         BnRed r{red_part, red_x, red_mask, red_mean, red_row0, red_part2, red_x2, red_mean2};
         r.fcoef = fold_coef; r.fgamma = fold_gamma; r.frstd = fold_rstd;
-        r.fdgamma = fold_dgamma; r.fdbeta = fold_dbeta; r.flvl = fold_lvl;
+        r.fdgamma = fold_dgamma; r.fdbeta = fold_dbeta; r.flvl = fold_lvl; r.fzero = fold_zero;
         r.amax_a = amax_a; r.amax_b = amax_b;
         conv_fwd(dev, S(s), Nb, H, W, C, Co, R, S_, stride, pad, x, w, y, stats, cin, bias, relu, &r, f32, bps);
       },
@@ -212,7 +213,7 @@ PYBIND11_MODULE(_mpit, m) {
       py::arg("red_part2") = 0, py::arg("red_x2") = 0, py::arg("red_mean2") = 0, py::arg("f32") = false,
       py::arg("fold_coef") = 0, py::arg("fold_gamma") = 0, py::arg("fold_rstd") = 0, py::arg("fold_dgamma") = 0,
       py::arg("fold_dbeta") = 0, py::arg("fold_lvl") = 0, py::arg("bps") = 0, py::arg("amax_a") = 0,
-      py::arg("amax_b") = 0);
+      py::arg("amax_b") = 0, py::arg("fold_zero") = 0);
   m.def("conv_dgrad_strided_wfloats", &conv_dgrad_strided_wfloats);
   m.def(
       "conv_dgrad_strided_weights",

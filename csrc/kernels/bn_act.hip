@@ -79,28 +79,15 @@ inline int block_for(int G) { return G >= 256 ? G : (256 / G) * G; }
 // ---------------------------------------------------------------- output bound (fp16x3)
 // An apply kernel that produces the next convolution's fp32 GEMM operand also writes max|out|
 // over the whole tensor: the fp16x3 GEMMs (gemm.hip FM 11) derive the operand's power-of-two
-// scale from it. Each block writes its maximum (write-through) to scratch[blockIdx], takes a
-// ticket, and the launch's last block reduces scratch into *amax and resets the ticket — no
-// pre-zeroed output, no host round trip. Ticket sets rotate per launch over kAmaxSlots
-// (launches in flight at once: the BN kernels run on one stream; two per pair launch).
-constexpr int kAmaxSlots = 64;
-__device__ uint32_t g_amax_tickets[kAmaxSlots];
-
+// scale from it. Each block reduces its maximum and issues ONE atomic max (no return value:
+// nothing waits on it) into slot blockIdx % kBoundSlots of the bound (kernels.h; one address
+// took 4096 serialised atomics per pass: +20 us a call), which the kernel that ran before the apply on the same
+// stream set to zero — the finalize that wrote the apply coefficients (FinArgs::zero, the
+// GEMM's folded finalize: EpiArgs::fzero) or, on the paths without one, a 4-byte memset.
+// |out| >= 0, so the float bits order like unsigned integers.
 struct AmaxOut {
-  float* amax;      // null: not wanted
-  float* scratch;   // >= gridDim.x floats
-  uint32_t* tick;
+  float* amax;  // null: not wanted
 };
-
-AmaxOut amax_out(uintptr_t amax, float* scratch) {
-  AmaxOut o{reinterpret_cast<float*>(amax), scratch, nullptr};
-  if (!amax) return o;
-  static std::atomic<uint32_t> launches{0};
-  uint32_t* base = nullptr;
-  hip_check(hipGetSymbolAddress(reinterpret_cast<void**>(&base), HIP_SYMBOL(g_amax_tickets)), "amax ticket symbol");
-  o.tick = base + launches.fetch_add(1) % kAmaxSlots;
-  return o;
-}
 
 __device__ __forceinline__ float block_max(float m, float* red /* >= 16 floats of LDS */) {
 #pragma unroll
@@ -116,23 +103,9 @@ __device__ __forceinline__ float block_max(float m, float* red /* >= 16 floats o
 
 __device__ __forceinline__ void amax_finish(float m, const AmaxOut& o) {
   __shared__ float red[16];
-  __shared__ uint32_t prev;
   const float b = block_max(m, red);
-  if (threadIdx.x == 0) {
-    __hip_atomic_store(&o.scratch[blockIdx.x], b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    prev = atomicAdd(o.tick, 1u);
-  }
-  __syncthreads();
-  if (prev != gridDim.x - 1) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  float r = 0.f;
-  for (int k = threadIdx.x; k < int(gridDim.x); k += blockDim.x) r = fmaxf(r, o.scratch[k]);
-  r = block_max(r, red);
-  if (threadIdx.x == 0) {
-    *o.amax = r;
-    __hip_atomic_store(o.tick, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  if (threadIdx.x == 0)
+    atomicMax(reinterpret_cast<unsigned int*>(o.amax + (blockIdx.x % kBoundSlots) * kBoundStride), __float_as_uint(b));
 }
 
 // ---------------------------------------------------------------- forward: statistics
@@ -302,6 +275,7 @@ struct FinArgs {
   float* dgamma;
   float* dbeta;
   float* coef;
+  float* zero;  // set to 0 by the finalizing block (an output bound the apply pass then raises)
 };
 
 template <typename T, bool CHAN, int kTileLanes>
@@ -374,6 +348,7 @@ __global__ __launch_bounds__(64 * kTileLanes) void bn_tiles_finalize_kernel(cons
   sb[kl][cl] = b;
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_store(&tickets[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x < kBoundSlots && blockIdx.x == 0 && fa.zero) fa.zero[threadIdx.x * kBoundStride] = 0.f;
   if (kl != 0 || c >= C) return;
 #pragma unroll
   for (int k = 1; k < kTileLanes; ++k) {
@@ -737,7 +712,9 @@ void fwd_impl(int dev, hipStream_t s, const T* x, const T* res, T* y, int64_t M,
               float momentum, float eps, bool relu, uint8_t* mask, const float* tstats, int64_t nstat,
               uintptr_t amax) {
   constexpr int V = Vec<T>::N;
-  const AmaxOut am = amax_out(y ? amax : 0, ws + 2 * C);  // the finalize's level buffer is free by then
+  // amax: zeroed by the finalize below (tile statistics) or a memset, raised by the apply pass;
+  // with y == nullptr (coefficients only, bn_pair) only the zeroing happens
+  const AmaxOut am{y ? reinterpret_cast<float*>(amax) : nullptr};
   check_shape(M, C, V, reinterpret_cast<uintptr_t>(x));
   const int G = C / V;
   const int blk = block_for(G);
@@ -754,6 +731,7 @@ void fwd_impl(int dev, hipStream_t s, const T* x, const T* res, T* y, int64_t M,
     fa.save_mean = save_mean;
     fa.save_rstd = save_rstd;
     fa.coef = coef;
+    fa.zero = reinterpret_cast<float*>(amax);
     launch_tiles_finalize<T, true>(s, tstats, nstat, C, M, x, ws + 2 * C, fa);
     if (y) launch_apply<T>(s, x, res, y, M, C, coef, relu, mask, am);
     hip_check(hipGetLastError(), "bn_act forward launch");
@@ -767,6 +745,7 @@ void fwd_impl(int dev, hipStream_t s, const T* x, const T* res, T* y, int64_t M,
   hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(nb), dim3(blk), shm, s, x, M, C, rpb, part);
   hipLaunchKernelGGL(bn_finalize_fwd_kernel<T>, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinK), 0, s, part, nb,
                      C, M, x, gamma, beta, eps, momentum, rmean, rvar, save_mean, save_rstd, coef);
+  if (amax) hip_check(hipMemsetAsync(reinterpret_cast<void*>(amax), 0, kBoundFloats * sizeof(float), s), "amax zero");
   if (y) launch_apply<T>(s, x, res, y, M, C, coef, relu, mask, am);  // y == nullptr: coefficients only
   hip_check(hipGetLastError(), "bn_act forward launch");
 }
@@ -776,7 +755,9 @@ void bwd_impl(hipStream_t s, const T* dy, const uint8_t* mask, const T* x, T* dx
               const float* gamma, const float* mean, const float* rstd, float* dgamma, float* dbeta, float* ws,
               bool relu, const float* gpart, int64_t npart, const float* coef_in, uintptr_t amax) {
   constexpr int V = Vec<T>::N;
-  const AmaxOut am = amax_out(dx ? amax : 0, ws + 3 * C);  // the finalize's partials are consumed by then
+  // amax: zeroed by the finalize (or, given coefficients, by the GEMM that folded it), raised
+  // by the apply pass; dx == nullptr: coefficients (and the zeroing) only
+  const AmaxOut am{dx ? reinterpret_cast<float*>(amax) : nullptr};
   check_shape(M, C, V, reinterpret_cast<uintptr_t>(x));
   if (relu && !mask) throw std::invalid_argument("bn_act backward: ReLU needs the forward mask");
   const int G = C / V;
@@ -797,6 +778,7 @@ void bwd_impl(hipStream_t s, const T* dy, const uint8_t* mask, const T* x, T* dx
     fa.dgamma = dgamma;
     fa.dbeta = dbeta;
     fa.coef = ws;
+    fa.zero = reinterpret_cast<float*>(amax);
     launch_tiles_finalize<T, false>(s, gpart, npart, C, M, x, part, fa);
   } else {
     if (relu)
@@ -807,6 +789,7 @@ void bwd_impl(hipStream_t s, const T* dy, const uint8_t* mask, const T* x, T* dx
                          part);
     hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kFinCh * kFinK), 0, s, part, nb,
                        C, M, gamma, mean, rstd, dgamma, dbeta, ws);
+    if (amax) hip_check(hipMemsetAsync(reinterpret_cast<void*>(amax), 0, kBoundFloats * sizeof(float), s), "amax zero");
   }
   const int64_t nvec = M * G;
   const dim3 g(apply_grid(nvec, blk)), b(blk);
@@ -888,7 +871,7 @@ static void pair_apply_t(hipStream_t s, uintptr_t x1, uintptr_t coef1, uintptr_t
   hipLaunchKernelGGL(bn_pair_apply_kernel<T>, dim3(apply_grid(nvec, blk)), dim3(blk), 0, s,
                      reinterpret_cast<const T*>(x1), reinterpret_cast<const T*>(x2), reinterpret_cast<T*>(y),
                      reinterpret_cast<const float*>(coef1), reinterpret_cast<const float*>(coef2), nvec, C,
-                     reinterpret_cast<uint8_t*>(mask), amax_out(amax, reinterpret_cast<float*>(scratch)));
+                     reinterpret_cast<uint8_t*>(mask), AmaxOut{reinterpret_cast<float*>(amax)});
 }
 
 template <typename T>
@@ -897,12 +880,12 @@ static void pair_bwd_t(hipStream_t s, uintptr_t dy, uintptr_t mask, uintptr_t x1
                        uintptr_t scratch) {
   const int G = C / 8, blk = block_for(G);
   const int64_t nvec = M * G;
-  float* sc = reinterpret_cast<float*>(scratch);  // [2][4096]
+
   hipLaunchKernelGGL(bn_pair_bwd_apply_kernel<T>, dim3(apply_grid(nvec, blk)), dim3(blk), 0, s,
                      reinterpret_cast<const T*>(dy), reinterpret_cast<const uint8_t*>(mask),
                      reinterpret_cast<const T*>(x1), reinterpret_cast<const float*>(coef1), reinterpret_cast<T*>(dx1),
                      reinterpret_cast<const T*>(x2), reinterpret_cast<const float*>(coef2), reinterpret_cast<T*>(dx2),
-                     nvec, C, amax_out(amax1, sc), amax_out(amax2, sc ? sc + 4096 : nullptr));
+                     nvec, C, AmaxOut{reinterpret_cast<float*>(amax1)}, AmaxOut{reinterpret_cast<float*>(amax2)});
 }
 
 void bn_pair_apply(int dev, hipStream_t s, uintptr_t x1, uintptr_t coef1, uintptr_t x2, uintptr_t coef2, uintptr_t y,
@@ -911,7 +894,6 @@ void bn_pair_apply(int dev, hipStream_t s, uintptr_t x1, uintptr_t coef1, uintpt
   check_shape(M, C, 8, x1);
   check_shape(M, C, 8, x2);
   if (!mask) throw std::invalid_argument("bn_pair_apply: needs the ReLU mask buffer");
-  if (amax && !scratch) throw std::invalid_argument("bn_pair_apply: amax needs a scratch buffer (4096 floats)");
   if (f32) pair_apply_t<float>(s, x1, coef1, x2, coef2, y, M, C, mask, amax, scratch);
   else pair_apply_t<uint16_t>(s, x1, coef1, x2, coef2, y, M, C, mask, amax, scratch);
   hip_check(hipGetLastError(), "bn_pair_apply launch");
@@ -923,7 +905,6 @@ void bn_pair_bwd_apply(int dev, hipStream_t s, uintptr_t dy, uintptr_t mask, uin
   hip_check(hipSetDevice(dev), "hipSetDevice");
   check_shape(M, C, 8, x1);
   check_shape(M, C, 8, x2);
-  if ((amax1 || amax2) && !scratch) throw std::invalid_argument("bn_pair_bwd_apply: amax needs scratch (8192 floats)");
   if (f32) pair_bwd_t<float>(s, dy, mask, x1, coef1, dx1, x2, coef2, dx2, M, C, amax1, amax2, scratch);
   else pair_bwd_t<uint16_t>(s, dy, mask, x1, coef1, dx1, x2, coef2, dx2, M, C, amax1, amax2, scratch);
   hip_check(hipGetLastError(), "bn_pair_bwd_apply launch");

@@ -173,7 +173,9 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 // e with amax * 2^e in [2^13, 2^14) (0 for a zero / non-finite bound), clamped to a normal 2^e
 __device__ __forceinline__ int fp16_exp(const float* amax) {
-  const float a = *amax;
+  float a = amax[0];  // the bound: max over its kBoundSlots slots (kernels.h)
+#pragma unroll
+  for (int k = 1; k < kBoundSlots; ++k) a = fmaxf(a, amax[k * kBoundStride]);
   if (!(a > 0.f) || !(a <= 3.0e38f)) return 0;
   int x;
   (void)frexpf(a, &x);  // a = f * 2^x, f in [0.5, 1)
@@ -262,6 +264,7 @@ struct EpiArgs {
   float* flvl;                 // [groups][2][N] group sums
   uint32_t* ftick;             // this launch's tickets [ntn][groups + 1]
   int fgroup;                  // M-tiles per group
+  float* fzero;                // set to 0 by the finalizing block of column tile 0 (or null)
   // fp16x3 (FM 11): device upper bounds of |A| and |B| that set the operand scales
   const float* amax_a;
   const float* amax_b;
@@ -404,6 +407,7 @@ __device__ __forceinline__ void bnred_fold(const EpiArgs& ep, void* smem, int64_
   sd[(L + kl) * BN + cl] = b;
   __syncthreads();
   if (t == 0) __hip_atomic_store(&tk[ngr], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t < kBoundSlots && nt == 0 && ep.fzero) ep.fzero[t * kBoundStride] = 0.f;
   if (kl != 0) return;
   a = b = 0;
 #pragma unroll
@@ -2338,6 +2342,7 @@ static EpiArgs epi_args(uintptr_t stats, const BnRed* r, int* mode) {
       ep.fdgamma = reinterpret_cast<float*>(r->fdgamma);
       ep.fdbeta = reinterpret_cast<float*>(r->fdbeta);
       ep.flvl = reinterpret_cast<float*>(r->flvl);
+      ep.fzero = reinterpret_cast<float*>(r->fzero);
     }
     if (r->part2) {
       if (!r->x2 || !r->mean2) throw std::invalid_argument("gemm_nt: second BN reduction needs x2 and mean2");

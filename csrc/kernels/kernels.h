@@ -87,8 +87,11 @@ void bn_act_fwd(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res, u
                 uintptr_t gamma, uintptr_t beta, uintptr_t rmean, uintptr_t rvar, uintptr_t save_mean,
                 uintptr_t save_rstd, uintptr_t ws, float momentum, float eps, bool relu, uintptr_t mask,
                 uintptr_t stats = 0, int64_t nstat = 0, uintptr_t amax = 0);
-// amax (optional, fp32 [1]): max |y| over the tensor, written by the apply pass (bn_act_bwd:
-// max |dx|; the pair applies: of y / dx1, dx2) — the scale bound of the fp16x3 GEMMs that read it
+// amax (optional, fp32 [1]): max |y| over the tensor (bn_act_bwd: max |dx|), the scale bound of the
+// fp16x3 GEMMs that read it: zeroed by this call's finalize, raised by its apply pass. With
+// y / dx null (the coefficient-only calls of a bn_pair) amax is only zeroed, for the pair
+// apply that follows. Given coefficients (bn_act_bwd coef), the GEMM that folded the finalize
+// zeroed it (BnRed::fzero).
 // y = act(x*coef[c] + coef[C+c] (+res))  — eval mode / precomputed coefficients
 void bn_act_apply(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C,
                   uintptr_t coef, bool relu);
@@ -108,7 +111,8 @@ void bn_act_bwd(int dev, hipStream_t s, bool bf16, uintptr_t dy, uintptr_t mask,
 // dx1 / dx2 from the two backward sets, one pass each.
 void bn_pair_apply(int dev, hipStream_t s, uintptr_t x1, uintptr_t coef1, uintptr_t x2, uintptr_t coef2, uintptr_t y,
                    int64_t M, int C, uintptr_t mask, bool f32 = false, uintptr_t amax = 0, uintptr_t scratch = 0);
-// scratch: 4096 (pair apply) / 8192 (pair backward) floats when an amax is asked for
+// amax / amax1 / amax2: raised by the pass (zeroed beforehand: the bn_act_fwd / bwd coefficient
+// calls of the pair zero them); scratch: unused (kept for the call signature)
 void bn_pair_bwd_apply(int dev, hipStream_t s, uintptr_t dy, uintptr_t mask, uintptr_t x1, uintptr_t coef1,
                        uintptr_t dx1, uintptr_t x2, uintptr_t coef2, uintptr_t dx2, int64_t M, int C, bool f32 = false,
                        uintptr_t amax1 = 0, uintptr_t amax2 = 0, uintptr_t scratch = 0);
@@ -127,6 +131,10 @@ void bn_pair_bwd_apply(int dev, hipStream_t s, uintptr_t dy, uintptr_t mask, uin
 // 128-row tile at part[row0 + tile][2][N] — bn_act_bwd(part, npart) then skips its pass.
 // x2 / mean2 / part2 (optional): a second BN fed by the same gradient (the downsample
 // shortcut's BN of a bn_pair): its (sum dz, sum dz*(x2-mean2)) go to part2.
+// Output bounds (fp16x3 operand scales): kBoundSlots fp32 maxima kBoundStride floats apart
+// (one 128-B line each, so the producers' one-atomic-per-block maxima spread over 16 lines
+// instead of serialising on one address); the bound is the max over the slots.
+constexpr int kBoundSlots = 16, kBoundStride = 32, kBoundFloats = kBoundSlots * kBoundStride;
 struct BnRed {
   uintptr_t part = 0, x = 0, mask = 0, mean = 0;
   int64_t row0 = 0;
@@ -137,6 +145,9 @@ struct BnRed {
   // fp32 fp16x3 GEMMs (gemm.hip FM 11): device fp32 upper bounds of |A| and of |B|; amax_b
   // marks B (bps > 0) as the two fp16 planes of the weight scaled by its bound's 2^e
   uintptr_t amax_a = 0, amax_b = 0;
+  // with fcoef: an output bound the folded finalize sets to zero (the BN backward's apply pass
+  // then raises it to max |dx|)
+  uintptr_t fzero = 0;
 };
 int64_t gemm_nt_fold_lvl_floats(int N);
 bool gemm_nt_supported(int64_t M, int N, int K, bool f32 = false);

@@ -107,7 +107,7 @@ def _want_amax(x: torch.Tensor) -> bool:
 
 
 def _amax_buf(x: torch.Tensor):
-    return torch.empty(1, dtype=torch.float32, device=x.device) if _want_amax(x) else None
+    return torch.empty(_conv.BOUND_FLOATS, dtype=torch.float32, device=x.device) if _want_amax(x) else None
 
 
 class _BNActFn(torch.autograd.Function):
@@ -163,7 +163,6 @@ class _BNActFn(torch.autograd.Function):
         dev = x.device.index
         stream = torch.cuda.current_stream(x.device).cuda_stream
         dx = torch.empty_like(x, memory_format=torch.channels_last)
-        amax = _amax_buf(x)
         # residual gradient of act(bn(x) + res) = dy*mask: with a GradSlot consumer it is
         # handed over as (dy, mask) and never written
         park = ctx.has_res and ctx.res_slot is not None and ctx.relu and mask is not None
@@ -178,12 +177,17 @@ class _BNActFn(torch.autograd.Function):
         coef = 0
         if part is not None:
             COUNTERS["bwd_linked"] += 1
+        # the output bound of dx (fp16x3 GEMM operand): zeroed by the folded finalize, else by
+        # this call's own finalize
+        amax = _amax_buf(x)
         if fold is not None:
             COUNTERS["bwd_folded"] += 1
             coef = fold[0].data_ptr()
             dgamma = fold[1] if ctx.has_w else None
             dbeta = fold[2] if ctx.has_b else None
             part, npart = None, 0
+            if amax is not None:
+                amax = fold[3]
         m.bn_act_bwd(dev, stream, x.dtype == torch.bfloat16, dy.data_ptr(),
                      mask.data_ptr() if mask is not None else 0, x.data_ptr(), dx.data_ptr(),
                      dres.data_ptr() if dres is not None else 0, M, C, w.data_ptr() if w is not None else 0,
@@ -315,19 +319,20 @@ class _BNPairFn(torch.autograd.Function):
             ts = ts if (ts is not None and ts[1] == m.gemm_nt_tiles(M)) else None
             if ts is not None:
                 COUNTERS["fwd_tile_stats"] += 1
+            # (the first call also zeroes the pair's output bound, raised by the pair apply)
             m.bn_act_fwd(dev, stream, bf16, x.data_ptr(), 0, 0, M, C, wf.data_ptr() if wf is not None else 0,
                          bf.data_ptr() if bf is not None else 0, rm.data_ptr() if rm is not None else 0,
                          rv.data_ptr() if rv is not None else 0, mean.data_ptr(), rstd.data_ptr(), ws.data_ptr(),
                          float(mom), float(eps), False, 0, stats=ts[0].data_ptr() if ts is not None else 0,
-                         nstat=ts[1] if ts is not None else 0)
+                         nstat=ts[1] if ts is not None else 0,
+                         amax=amax.data_ptr() if (amax is not None and not outs) else 0)
             outs.append((wf, mean, rstd, ws))
         y = torch.empty_like(x1, memory_format=torch.channels_last)
         mask = torch.empty(m.bn_mask_bytes(bf16, M, C), dtype=torch.uint8, device=x1.device)
         # (scratch of the output bound: bn1's workspace past its coefficients)
         m.bn_pair_apply(dev, stream, x1.data_ptr(), outs[0][3].data_ptr(), x2.data_ptr(), outs[1][3].data_ptr(),
                         y.data_ptr(), M, C, mask.data_ptr(), f32=not bf16,
-                        amax=amax.data_ptr() if amax is not None else 0,
-                        scratch=outs[0][3][2 * C:].data_ptr() if amax is not None else 0)
+                        amax=amax.data_ptr() if amax is not None else 0)
         (wf1, mean1, rstd1, _), (wf2, mean2, rstd2, _) = outs
         ctx.save_for_backward(x1, x2, mask, wf1, mean1, rstd1, wf2, mean2, rstd2)
         ctx.has = (w1 is not None, b1 is not None, w2 is not None, b2 is not None)
@@ -348,25 +353,25 @@ class _BNPairFn(torch.autograd.Function):
             COUNTERS["bwd_linked"] += 2
         f32 = dict(dtype=torch.float32, device=x1.device)
         grads, wss = [], []
-        for x, wf, mean, rstd, p, hw, hb in ((x1, wf1, mean1, rstd1, part, ctx.has[0], ctx.has[1]),
-                                            (x2, wf2, mean2, rstd2, part2, ctx.has[2], ctx.has[3])):
+        am1, am2 = _amax_buf(x1), _amax_buf(x1)  # bounds of dx1, dx2: zeroed by the two finalizes
+        for x, wf, mean, rstd, p, hw, hb, am in ((x1, wf1, mean1, rstd1, part, ctx.has[0], ctx.has[1], am1),
+                                                (x2, wf2, mean2, rstd2, part2, ctx.has[2], ctx.has[3], am2)):
             dg = torch.empty(C, **f32) if hw else None
             db = torch.empty(C, **f32) if hb else None
             ws = torch.empty(m.bn_workspace_floats(C), **f32)
             m.bn_act_bwd(dev, stream, x1.dtype == torch.bfloat16, dy.data_ptr(), mask.data_ptr(), x.data_ptr(), 0, 0, M, C,
                          wf.data_ptr() if wf is not None else 0, mean.data_ptr(), rstd.data_ptr(),
                          dg.data_ptr() if dg is not None else 0, db.data_ptr() if db is not None else 0, ws.data_ptr(),
-                         True, part=p.data_ptr() if p is not None else 0, npart=npart if p is not None else 0)
+                         True, part=p.data_ptr() if p is not None else 0, npart=npart if p is not None else 0,
+                         amax=am.data_ptr() if am is not None else 0)
             grads.append((dg, db))
             wss.append(ws)
         dx1 = torch.empty_like(x1, memory_format=torch.channels_last)
         dx2 = torch.empty_like(x2, memory_format=torch.channels_last)
-        am1, am2 = _amax_buf(x1), _amax_buf(x1)
         m.bn_pair_bwd_apply(dev, stream, dy.data_ptr(), mask.data_ptr(), x1.data_ptr(), wss[0].data_ptr(),
                             dx1.data_ptr(), x2.data_ptr(), wss[1].data_ptr(), dx2.data_ptr(), M, C,
                             f32=x1.dtype == torch.float32, amax1=am1.data_ptr() if am1 is not None else 0,
-                            amax2=am2.data_ptr() if am2 is not None else 0,
-                            scratch=wss[0][3 * C:].data_ptr() if am1 is not None else 0)
+                            amax2=am2.data_ptr() if am2 is not None else 0)
         if am1 is not None:
             set_amax(dx1, am1)
             set_amax(dx2, am2)

@@ -187,11 +187,16 @@ def _f16_exp(amax: torch.Tensor) -> torch.Tensor:
     return torch.where(ok, e, torch.zeros_like(e))
 
 
+def _exp2i(e: torch.Tensor) -> torch.Tensor:
+    """2^e (integer e in [-126, 127]) as an exact fp32 tensor (gemm.hip exp2i: the exponent field;
+    torch.ldexp goes through pow and need not be exact)."""
+    return ((e.to(torch.int32) + 127) << 23).view(torch.float32)
+
+
 def _unsplit(w: torch.Tensor) -> torch.Tensor:
     """fp32 weight back from its planes (exact: w == h + m + l, or (h + l / 2^11) / 2^e)."""
     if w.dtype == torch.float16:
-        s = torch.ldexp(torch.ones_like(w._mpit_wamax), -_f16_exp(w._mpit_wamax))
-        return (w[0].float() + w[1].float() / 2048.0) * s
+        return (w[0].float() + w[1].float() / 2048.0) * _exp2i(-_f16_exp(bound_value(w._mpit_wamax)))
     return (w[0].float() + w[1].float()) + w[2].float()
 
 
@@ -200,14 +205,31 @@ def f16_planes(w: torch.Tensor, amax: torch.Tensor) -> torch.Tensor:
     ``amax`` >= max |w| (gemm.hip split1h's arithmetic on PyTorch ops: the same bits as the
     weight plan's). ``(h + l / 2^11) / 2^e`` carries w to 2^-22 relative wherever |w| >= 2^-27
     ``amax``, to 2^-48 ``amax`` absolute below that."""
-    one = torch.ones_like(amax)
-    e = _f16_exp(amax)
+    e = _f16_exp(bound_value(amax) if amax.numel() > 1 else amax)
     wf = w.float()
-    h = (wf * torch.ldexp(one, e)).half()
-    lo = (wf * torch.ldexp(one, e + 11) - h.float() * 2048.0).half()
+    h = (wf * _exp2i(e)).half()
+    lo = (wf * _exp2i(e + 11) - h.float() * 2048.0).half()
     p = torch.stack([h, lo])
     p._mpit_wamax = amax
     return p
+
+
+# an output bound on the device: 16 fp32 slots 32 floats apart (csrc/kernels/kernels.h
+# kBoundSlots); producers raise one slot per block, consumers take the max over the slots
+BOUND_SLOTS, BOUND_STRIDE = 16, 32
+BOUND_FLOATS = BOUND_SLOTS * BOUND_STRIDE
+
+
+def bound_value(amax: torch.Tensor) -> torch.Tensor:
+    """The bound a slotted buffer holds ([1] tensor)."""
+    return amax[:BOUND_FLOATS].view(BOUND_SLOTS, BOUND_STRIDE)[:, 0].amax().reshape(1)
+
+
+def bound_of_value(v: torch.Tensor) -> torch.Tensor:
+    """A slotted bound buffer holding the [1] tensor ``v``."""
+    b = torch.zeros(BOUND_FLOATS, dtype=torch.float32, device=v.device)
+    b[:1].copy_(v.reshape(1))
+    return b
 
 
 def set_amax(t: torch.Tensor, amax: torch.Tensor) -> torch.Tensor:
@@ -230,7 +252,7 @@ def _amax_arg(t: torch.Tensor, keep: list) -> int:
     (the tensor is kept alive in ``keep`` until the launch is queued)."""
     a = amax_of(t)
     if a is None:
-        a = torch.linalg.vector_norm(t, float("inf")).reshape(1)
+        a = bound_of_value(torch.linalg.vector_norm(t, float("inf")))
         COUNTERS["amax_fallback"] += 1
     keep.append(a)
     return a.data_ptr()
@@ -294,7 +316,7 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, stats: bool = False, f16x3: bool =
     if f16x3:
         if a.dtype != torch.float32:
             raise TypeError("gemm_nt: f16x3 is an fp32 GEMM")
-        b = f16_planes(b.contiguous(), torch.linalg.vector_norm(b, float("inf")).reshape(1))
+        b = f16_planes(b.contiguous(), bound_of_value(torch.linalg.vector_norm(b, float("inf"))))
         kw = _split_kw(a, b, True, keep)
     m.gemm_nt(a.device.index, _stream(a), M, N, K, a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(-2), c.data_ptr(),
               N, st.data_ptr() if st is not None else 0, f32=a.dtype == torch.float32, **kw)
@@ -325,7 +347,7 @@ def gemm_tn(y: torch.Tensor, x: torch.Tensor, out: torch.Tensor = None, beta: fl
     if f16x3:
         if y.dtype != torch.float32:
             raise TypeError("gemm_tn: f16x3 is an fp32 GEMM")
-        keep = [torch.linalg.vector_norm(t, float("inf")).reshape(1) for t in (y, x)]
+        keep = [bound_of_value(torch.linalg.vector_norm(t, float("inf"))) for t in (y, x)]
         kw = dict(amax_y=keep[0].data_ptr(), amax_x=keep[1].data_ptr())
     m.gemm_tn(dev, _stream(y), M, N, K, y.data_ptr(), y.stride(0), x.data_ptr(), x.stride(0), out.data_ptr(),
               ws.data_ptr() if ws is not None else 0, float(beta), f32=y.dtype == torch.float32, **kw)
@@ -366,12 +388,14 @@ def _red_args(link, c: int, ntiles: int, device, fold: bool = False):
         part2 = torch.empty(ntiles * 2 * c, dtype=torch.float32, device=device)
         kw.update(red_part2=part2.data_ptr(), red_x2=link.x2.data_ptr(), red_mean2=link.mean2.data_ptr())
     elif fold and _BN_FOLD and link.rstd is not None:
-        buf = torch.empty(5 * c + native().gemm_nt_fold_lvl_floats(c), dtype=torch.float32, device=device)
-        coef, dgamma, dbeta, lvl = buf[: 3 * c], buf[3 * c: 4 * c], buf[4 * c: 5 * c], buf[5 * c:]
+        nl = native().gemm_nt_fold_lvl_floats(c)
+        buf = torch.empty(5 * c + nl + BOUND_FLOATS, dtype=torch.float32, device=device)
+        coef, dgamma, dbeta, lvl = buf[: 3 * c], buf[3 * c: 4 * c], buf[4 * c: 5 * c], buf[5 * c: 5 * c + nl]
+        amax = buf[5 * c + nl:]  # the BN backward's output bound: zeroed by the fold, raised by its apply
         kw.update(fold_coef=coef.data_ptr(), fold_gamma=link.w.data_ptr() if link.w is not None else 0,
                   fold_rstd=link.rstd.data_ptr(), fold_dgamma=dgamma.data_ptr(), fold_dbeta=dbeta.data_ptr(),
-                  fold_lvl=lvl.data_ptr())
-        fb = (coef, dgamma, dbeta)
+                  fold_lvl=lvl.data_ptr(), fold_zero=amax.data_ptr())
+        fb = (coef, dgamma, dbeta, amax)
     return kw, part, part2, fb
 
 
@@ -449,8 +473,12 @@ class _ParkGradFn(torch.autograd.Function):
 
 def park_grad(x: torch.Tensor, slot: GradSlot) -> torch.Tensor:
     """Identity whose backward parks the incoming gradient in ``slot`` for a later
-    GEMM epilogue to add (see :class:`GradSlot`)."""
-    return _ParkGradFn.apply(x, slot)
+    GEMM epilogue to add (see :class:`GradSlot`). The view keeps x's output bound."""
+    v = _ParkGradFn.apply(x, slot)
+    a = amax_of(x)
+    if a is not None:
+        set_amax(v, a)
+    return v
 
 
 class _Conv1x1Fn(torch.autograd.Function):
@@ -850,7 +878,7 @@ class WeightCastPlan:
             # current then) alive into every step — autograd then warns that the node's stream
             # differs from the step's and inserts a cross-stream wait per weight
             if f16p and (pl_b or pl_t) and self.amax is None:
-                self.amax = torch.zeros(1, dtype=torch.float32, device=w.device)
+                self.amax = torch.zeros(BOUND_FLOATS, dtype=torch.float32, device=w.device)  # value in slot 0
             if f32 and not pl_b:
                 wb = _as_rsc(w.detach())
             else:
@@ -901,7 +929,7 @@ class WeightCastPlan:
             if self.wlist:  # the planes' scale: max |w| over the plan's fp16-plane weights
                 with torch.no_grad():
                     torch.amax(torch.stack(torch._foreach_norm(self.wlist, float("inf"))), 0, keepdim=True,
-                               out=self.amax)
+                               out=self.amax[:1])
             native().cast_jobs_run(dev.index, torch.cuda.current_stream(dev).cuda_stream, self.table.data_ptr(),
                                    self.njobs, self.nblocks)
         self.valid = True

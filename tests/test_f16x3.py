@@ -1,0 +1,146 @@
+"""fp16x3 split products for the fp32 GEMMs (csrc/kernels/gemm.hip FM 11): the power-of-two
+operand scales come from device-side bounds of |x| that the producers write — the BN apply
+passes (forward y, backward dx, the bn_pair passes, the finalize folded into a backward-data
+GEMM) and the weight plan. A bound below the true max |x| would overflow the fp16 planes, so
+every producer's bound is checked to equal max |x| exactly."""
+import pytest
+import torch
+
+from mpit_amd.ops import conv as C
+
+gpu = pytest.mark.gpu
+
+
+def _cl(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+def test_exp2i_exact_cpu():
+    e = torch.arange(-126, 128)
+    got = C._exp2i(e)
+    want = torch.tensor([2.0 ** int(k) for k in e.tolist()], dtype=torch.float64)
+    assert torch.equal(got.double(), want)
+
+
+def test_f16_exp_places_bound_cpu():
+    for a in (1e-30, 3e-8, 0.0625, 0.07, 1.0, 13.5, 1e6, 3e38):
+        e = int(C._f16_exp(torch.tensor([a])).item())
+        assert 2.0 ** 13 <= a * 2.0 ** e < 2.0 ** 14 or e in (-126, 116), (a, e)
+    assert int(C._f16_exp(torch.tensor([0.0])).item()) == 0
+    assert int(C._f16_exp(torch.tensor([float("inf")])).item()) == 0
+
+
+def test_f16_planes_match_exact_split_cpu():
+    """f16_planes == the exact residual split, element by element (h = RNE(s), l = RNE(2^11 (s - h)))."""
+    torch.manual_seed(1)
+    w = torch.randn(2000) * 0.05
+    amax = C.bound_of_value(w.abs().max())
+    p = C.f16_planes(w, amax)
+    e = int(C._f16_exp(C.bound_value(amax)).item())
+    s = w.double() * 2.0 ** e
+    h = s.half().double()
+    assert torch.equal(p[0].double(), h)
+    assert torch.equal(p[1].double(), ((s - h) * 2048).half().double())
+
+
+def test_park_grad_keeps_bound_cpu():
+    x = torch.randn(4, 8)
+    a = C.bound_of_value(x.abs().max())
+    C.set_amax(x, a)
+    v = C.park_grad(x, C.GradSlot())
+    assert C.amax_of(v) is a
+    x.add_(1.0)  # a new version: the bound no longer holds
+    assert C.amax_of(x) is None
+
+
+def _bound(t):
+    a = C.amax_of(t)
+    assert a is not None, "no bound attached"
+    return C.bound_value(a).item()
+
+
+@gpu
+@pytest.mark.parametrize("res,relu", [(False, True), (True, True), (False, False)])
+def test_bn_forward_backward_bounds_exact(res, relu):
+    from mpit_amd.ops.bn import BatchNormAct2d
+
+    torch.manual_seed(3)
+    bn = BatchNormAct2d(64, act=relu).cuda()
+    bn.weight.data.uniform_(0.5, 2.0)
+    bn.bias.data.uniform_(-1.0, 1.0)
+    x = _cl(torch.randn(4, 64, 9, 9, device="cuda") * 3).requires_grad_(True)
+    r = _cl(torch.randn(4, 64, 9, 9, device="cuda")) if res else None
+    got = []
+    x.register_hook(lambda g: got.append(g))
+    y = bn(x, r)
+    torch.cuda.synchronize()
+    assert _bound(y) == y.detach().abs().max().item()
+    y.backward(torch.randn_like(y) * 1e-6)
+    torch.cuda.synchronize()
+    assert _bound(got[0]) == got[0].abs().max().item()
+
+
+@gpu
+def test_bn_pair_bounds_exact():
+    from mpit_amd.ops.bn import BatchNormAct2d, bn_pair
+
+    torch.manual_seed(4)
+    b1, b2 = BatchNormAct2d(128).cuda(), BatchNormAct2d(128, act=False).cuda()
+    x1 = _cl(torch.randn(2, 128, 7, 7, device="cuda")).requires_grad_(True)
+    x2 = _cl(torch.randn(2, 128, 7, 7, device="cuda")).requires_grad_(True)
+    g1, g2 = [], []
+    x1.register_hook(lambda g: g1.append(g))
+    x2.register_hook(lambda g: g2.append(g))
+    y = bn_pair(b1, x1, b2, x2)
+    torch.cuda.synchronize()
+    assert _bound(y) == y.detach().abs().max().item()
+    y.backward(torch.randn_like(y))
+    torch.cuda.synchronize()
+    assert _bound(g1[0]) == g1[0].abs().max().item()
+    assert _bound(g2[0]) == g2[0].abs().max().item()
+
+
+@gpu
+def test_folded_finalize_bound_exact():
+    """BN -> Conv1x1: the conv's backward-data GEMM folds the BN backward's finalize and zeroes
+    the bound that the BN's apply pass then raises to max |dx|; repeated steps reuse nothing stale."""
+    from mpit_amd.ops.bn import COUNTERS, BatchNormAct2d
+
+    torch.manual_seed(5)
+    bn = BatchNormAct2d(128).cuda()
+    conv = C.Conv1x1(128, 256).cuda().to(memory_format=torch.channels_last)
+    for step in range(3):
+        x = _cl(torch.randn(2, 128, 14, 14, device="cuda") * (10.0 ** -step)).requires_grad_(True)
+        got = []
+        x.register_hook(lambda g: got.append(g))
+        n0 = COUNTERS["bwd_folded"]
+        z = conv(bn(x))
+        z.backward(torch.randn_like(z))
+        torch.cuda.synchronize()
+        assert COUNTERS["bwd_folded"] == n0 + 1
+        assert _bound(got[0]) == got[0].abs().max().item()
+
+
+@gpu
+def test_resnet50_f16x3_step_uses_producer_bounds():
+    """One fp32 ResNet-50 step through the weight plan: every fp16x3 GEMM operand has its
+    producer's bound (no fallback reduction), and the backward-weight GEMMs run fp16x3."""
+    from mpit_amd.models.resnet import resnet50
+
+    if C._F32_SPLIT != "f16x3":
+        pytest.skip("MPIT_F32_SPLIT=bf16x6")
+    torch.manual_seed(0)
+    net = resnet50(num_classes=10).cuda().to(memory_format=torch.channels_last)
+    plan = C.WeightCastPlan(net, torch.float32)
+    x = _cl(torch.randn(4, 3, 64, 64, device="cuda"))
+    f0, w0 = C.COUNTERS["amax_fallback"], C.COUNTERS["wgrad_f16x3"]
+    plan.run()
+    out = net(x)
+    out.float().sum().backward()
+    plan.invalidate()
+    torch.cuda.synchronize()
+    assert C.COUNTERS["amax_fallback"] == f0
+    assert C.COUNTERS["wgrad_f16x3"] - w0 == 52  # every conv but the stem
+    for m in net.modules():
+        if isinstance(m, torch.nn.Conv2d):
+            assert torch.isfinite(m.weight.grad).all()

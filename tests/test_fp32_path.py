@@ -55,7 +55,7 @@ def test_f16_planes_carry_22_bits_cpu():
     torch.manual_seed(0)
     w = torch.randn(4096) * torch.exp(torch.randn(4096) * 3)
     amax = w.abs().max().reshape(1)
-    p = C.f16_planes(w, amax)
+    p = C.f16_planes(w, C.bound_of_value(amax))
     assert p.dtype == torch.float16 and p.shape == (2, 4096)
     e = int(C._f16_exp(amax).item())
     assert 2.0 ** 13 <= amax.item() * 2.0 ** e < 2.0 ** 14
@@ -401,7 +401,7 @@ def test_weight_cast_plan_fp32_planes_exact():
         if got.dtype == torch.float16:
             assert torch.equal(got, C.f16_planes(want, got._mpit_wamax).view(got.shape))
             return torch.allclose(C._unsplit(got), want.view(got.shape[1:]), rtol=2.0 ** -22,
-                                  atol=got._mpit_wamax.item() * 2.0 ** -47)
+                                  atol=C.bound_value(got._mpit_wamax).item() * 2.0 ** -47)
         return torch.equal(C._unsplit(got).reshape(-1), want.reshape(-1))
 
     for mod, _, (wb, wt) in plan.mods:
@@ -425,7 +425,7 @@ def test_weight_cast_plan_fp32_planes_exact():
         elif wt is not None:
             assert torch.equal(wt.reshape(-1), rt.reshape(-1))
     if plan.wlist:  # the plan's bound covers every plane weight
-        assert plan.amax.item() == max(w.abs().max().item() for w in plan.wlist)
+        assert C.bound_value(plan.amax).item() == max(w.abs().max().item() for w in plan.wlist)
 
 
 @gpu

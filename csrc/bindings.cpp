@@ -247,18 +247,22 @@ PYBIND11_MODULE(_mpit, m) {
   m.def(
       "conv_stem_fwd",
       [](int dev, uintptr_t s, int Nb, int Hp, int Wp, int Co, int Ho, int Wo, int stride, uintptr_t x, uintptr_t w,
-         uintptr_t y, uintptr_t stats, bool f32) { conv_stem_fwd(dev, S(s), Nb, Hp, Wp, Co, Ho, Wo, stride, x, w, y, stats, f32); },
+         uintptr_t y, uintptr_t stats, bool f32, int64_t bps, uintptr_t amax_a, uintptr_t amax_b) {
+        conv_stem_fwd(dev, S(s), Nb, Hp, Wp, Co, Ho, Wo, stride, x, w, y, stats, f32, bps, amax_a, amax_b);
+      },
       py::arg("dev"), py::arg("stream"), py::arg("Nb"), py::arg("Hp"), py::arg("Wp"), py::arg("Co"), py::arg("Ho"),
       py::arg("Wo"), py::arg("stride"), py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stats"),
-      py::arg("f32") = false);
+      py::arg("f32") = false, py::arg("bps") = 0, py::arg("amax_a") = 0, py::arg("amax_b") = 0);
   m.def("conv_stem_wgrad_ws_floats", &conv_stem_wgrad_ws_floats);
   m.def(
       "conv_stem_wgrad",
       [](int dev, uintptr_t s, int Nb, int Hp, int Wp, int Co, int Ho, int Wo, int stride, uintptr_t dy, uintptr_t x,
-         uintptr_t dw, uintptr_t ws, bool f32) { conv_stem_wgrad(dev, S(s), Nb, Hp, Wp, Co, Ho, Wo, stride, dy, x, dw, ws, f32); },
+         uintptr_t dw, uintptr_t ws, bool f32, uintptr_t amax_y, uintptr_t amax_x) {
+        conv_stem_wgrad(dev, S(s), Nb, Hp, Wp, Co, Ho, Wo, stride, dy, x, dw, ws, f32, amax_y, amax_x);
+      },
       py::arg("dev"), py::arg("stream"), py::arg("Nb"), py::arg("Hp"), py::arg("Wp"), py::arg("Co"), py::arg("Ho"),
       py::arg("Wo"), py::arg("stride"), py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("ws"),
-      py::arg("f32") = false);
+      py::arg("f32") = false, py::arg("amax_y") = 0, py::arg("amax_x") = 0);
   m.def("conv_wgrad_ws_floats", &conv_wgrad_ws_floats);
   m.def(
       "conv_wgrad",

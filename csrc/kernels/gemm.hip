@@ -2132,7 +2132,7 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
     return v == "nosplit" ? 5 : v == "splitA" ? 6 : v == "splitB" ? 7 : 0;
   }();
   int fm = !F32 || f32_mode() != 1 ? 0
-           : (f32_bk == 32 && K % 32 == 0 && (!geo || (geo->C % 32 == 0 && !geo->pitch)) ? 3 : 1);
+           : (f32_bk == 32 && K % 32 == 0 && (!geo || (geo->C % 32 == 0 && (!geo->pitch || bps > 0))) ? 3 : 1);
   if (fm == 3 && ablate) fm = ablate;
   if (bps > 0) {  // B is three pre-split bf16 planes: only the FM 4 kernels read that
     if (!F32 || fm != 3 || ablate || bps < int64_t(N) * ldb || ldb % 8)
@@ -2642,12 +2642,17 @@ static ConvGeo stem_geo(int Nb, int Hp, int Wp, int Ho, int Wo, int stride) {
 }
 
 void conv_stem_fwd(int dev, hipStream_t s, int Nb, int Hp, int Wp, int Co, int Ho, int Wo, int stride, uintptr_t x,
-                   uintptr_t w, uintptr_t y, uintptr_t stats, bool f32) {
+                   uintptr_t w, uintptr_t y, uintptr_t stats, bool f32, int64_t bps, uintptr_t amax_a,
+                   uintptr_t amax_b) {
   if (Co % 64) throw std::invalid_argument("conv_stem_fwd: need Co % 64 == 0");
   const ConvGeo g = stem_geo(Nb, Hp, Wp, Ho, Wo, stride);
   int mode;
-  const EpiArgs ep = epi_args(stats, nullptr, &mode);
-  launch_nt(dev, s, int64_t(Nb) * Ho * Wo, Co, kStemK, x, kStemTap, w, kStemK, y, Co, 0, 0, &g, ep, mode, f32);
+  BnRed r{};
+  r.amax_a = amax_a;
+  r.amax_b = amax_b;
+  const EpiArgs ep = epi_args(stats, &r, &mode);
+  launch_nt(dev, s, int64_t(Nb) * Ho * Wo, Co, kStemK, x, kStemTap, w, kStemK, y, Co, 0, 0, &g, ep, mode, f32, 0, false,
+            bps);
 }
 
 int64_t conv_stem_wgrad_ws_floats(int dev, int Nb, int Ho, int Wo, int Co) {
@@ -2658,10 +2663,10 @@ int64_t conv_stem_wgrad_ws_floats(int dev, int Nb, int Ho, int Wo, int Co) {
 }
 
 void conv_stem_wgrad(int dev, hipStream_t s, int Nb, int Hp, int Wp, int Co, int Ho, int Wo, int stride, uintptr_t dy,
-                     uintptr_t x, uintptr_t dw, uintptr_t ws, bool f32) {
+                     uintptr_t x, uintptr_t dw, uintptr_t ws, bool f32, uintptr_t amax_y, uintptr_t amax_x) {
   if (Co % 64) throw std::invalid_argument("conv_stem_wgrad: need Co % 64 == 0");
   const ConvGeo g = stem_geo(Nb, Hp, Wp, Ho, Wo, stride);
-  launch_tn(dev, s, int64_t(Nb) * Ho * Wo, Co, kStemK, dy, Co, x, kStemTap, dw, ws, 0.f, &g, f32);
+  launch_tn(dev, s, int64_t(Nb) * Ho * Wo, Co, kStemK, dy, Co, x, kStemTap, dw, ws, 0.f, &g, f32, amax_y, amax_x);
 }
 
 static void launch_cast(int dev, hipStream_t s, uintptr_t w, int R, int Cc, uintptr_t wb, uintptr_t wt, int taps,

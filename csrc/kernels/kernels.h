@@ -214,10 +214,14 @@ void conv_wgrad(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int
 // image [Nb][Hp][Wp][4], w = [Co][8][8][4] (bf16, zero-extended kernel), y = [Nb][Ho][Wo][Co];
 // dw = [Co][8][8][4] fp32; stats: BN statistics of y as conv_fwd
 void conv_stem_fwd(int dev, hipStream_t s, int Nb, int Hp, int Wp, int Co, int Ho, int Wo, int stride, uintptr_t x,
-                   uintptr_t w, uintptr_t y, uintptr_t stats, bool f32 = false);
+                   uintptr_t w, uintptr_t y, uintptr_t stats, bool f32 = false, int64_t bps = 0, uintptr_t amax_a = 0,
+                   uintptr_t amax_b = 0);
+// (fp32 fp16x3: w as two fp16 planes of plane stride bps with bound amax_b, the image's bound amax_a;
+// the wgrad's amax_y / amax_x as gemm_tn)
 int64_t conv_stem_wgrad_ws_floats(int dev, int Nb, int Ho, int Wo, int Co);
 void conv_stem_wgrad(int dev, hipStream_t s, int Nb, int Hp, int Wp, int Co, int Ho, int Wo, int stride, uintptr_t dy,
-                     uintptr_t x, uintptr_t dw, uintptr_t ws, bool f32 = false);
+                     uintptr_t x, uintptr_t dw, uintptr_t ws, bool f32 = false, uintptr_t amax_y = 0,
+                     uintptr_t amax_x = 0);
 
 // ---- NHWC bf16 / fp32 max pooling with a uint8 argmax per output element (pool.hip) ---
 // x [N,H,W,C] -> y, idx [N,Ho,Wo,C]; dx [N,H,W,C] gathered from dy + idx (no atomics).

@@ -1047,8 +1047,15 @@ class _StemConvFn(torch.autograd.Function):
         if hold is not None:
             st, nt = _tile_stats(co, nb * ho * wo, x.device)
             hold.append((st, nt))
+        kw, ctx.xbound = {}, None
+        if f32 and _F32_SPLIT == "f16x3":
+            # fp16x3: the image's bound (the padded copy only adds zeros) and the packed weight as
+            # two fp16 planes; the row-tap GEMM then runs 32-deep tiles, one kernel row each
+            ctx.xbound = bound_of_value(torch.linalg.vector_norm(x, float("inf")))
+            wb = f16_planes(wb.reshape(co, -1), bound_of_value(torch.linalg.vector_norm(weight.detach(), float("inf"))))
+            kw = dict(bps=wb[0].numel(), amax_a=ctx.xbound.data_ptr(), amax_b=wb._mpit_wamax.data_ptr())
         native().conv_stem_fwd(x.device.index, _stream(x), nb, hp, wp, co, ho, wo, stride, xp.data_ptr(),
-                               wb.data_ptr(), y.data_ptr(), st.data_ptr() if st is not None else 0, f32=f32)
+                               wb.data_ptr(), y.data_ptr(), st.data_ptr() if st is not None else 0, f32=f32, **kw)
         ctx.save_for_backward(xp)
         ctx.geo = (nb, hp, wp, co, ho, wo, stride, tuple(weight.shape))
         ctx.pack = ent
@@ -1071,8 +1078,11 @@ class _StemConvFn(torch.autograd.Function):
             dwp = torch.empty((co, 8, 8, 4), dtype=torch.float32, device=xp.device)
             nws = m.conv_stem_wgrad_ws_floats(dev, nb, ho, wo, co)
             ws = torch.empty(nws, dtype=torch.float32, device=xp.device) if nws else None
+            ya = amax_of(dy)
+            kw = dict(amax_y=ya.data_ptr(), amax_x=ctx.xbound.data_ptr()) if (
+                ya is not None and ctx.xbound is not None) else {}
             m.conv_stem_wgrad(dev, _stream(xp), nb, hp, wp, co, ho, wo, stride, dy.data_ptr(), xp.data_ptr(),
-                              dwp.data_ptr(), ws.data_ptr() if ws is not None else 0, f32=dt == torch.float32)
+                              dwp.data_ptr(), ws.data_ptr() if ws is not None else 0, f32=dt == torch.float32, **kw)
             _, c, r, s = wshape
             dw = dwp[:, :r, :s, :c].permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
         if ctx.pack is not None:

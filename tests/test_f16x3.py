@@ -144,3 +144,39 @@ def test_resnet50_f16x3_step_uses_producer_bounds():
     for m in net.modules():
         if isinstance(m, torch.nn.Conv2d):
             assert torch.isfinite(m.weight.grad).all()
+
+
+@gpu
+def test_stem_f16x3_vs_fp64():
+    """The row-tap stem on fp16x3 (32-deep tiles, one kernel row per k-tile), forward and, with
+    the stem BN's backward bound on dy, the backward-weight GEMM: within 2x of PyTorch fp32."""
+    import torch.nn.functional as F
+
+    from mpit_amd.ops.bn import BatchNormAct2d
+
+    torch.manual_seed(6)
+    conv = C.StemConv(3, 64, 7, 2, 3).cuda().to(memory_format=torch.channels_last)
+    bn = BatchNormAct2d(64).cuda()
+    x = _cl(torch.randn(4, 3, 64, 64, device="cuda"))
+    assert conv.fused(x)
+    y = bn(conv(x))
+    g = torch.randn_like(y)
+    y.backward(g)
+
+    def ref(dev, dt):
+        xx = x.to(dev, dt)
+        ww = conv.weight.detach().to(dev, dt).clone().requires_grad_(True)
+        z = F.conv2d(xx, ww, stride=2, padding=3)
+        yy = F.relu(F.batch_norm(z, None, None, bn.weight.detach().to(dev, dt), bn.bias.detach().to(dev, dt),
+                                 training=True, eps=bn.eps))
+        yy.backward(g.to(dev, dt))
+        return yy.detach(), ww.grad
+
+    (yr, gr), (yl, gl) = ref("cpu", torch.float64), ref("cuda", torch.float32)
+
+    def rel(a, b):
+        a, b = a.double().cpu(), b.double().cpu()
+        return ((a - b).norm() / b.norm()).item()
+
+    assert rel(y, yr) <= 2 * rel(yl, yr) + 1e-9
+    assert rel(conv.weight.grad, gr) <= 2 * rel(gl, gr) + 1e-9

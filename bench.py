@@ -63,7 +63,9 @@ def _make(a, mp_train, amp: bool, topology: str, servers: int, ps_id: int):
     cfg = mp_train.TrainConfig(model=a.model, batch=a.batch, optimizer=a.optimizer, topology=topology,
                                servers=servers, su=a.su, lr=lr, mva=mva, mom=0.0, amp=amp,
                                channels_last=not a.no_channels_last, datapath=a.datapath, staleness=a.staleness,
-                               wire_dtype=a.wire, extra={"ps_id": ps_id, "shards_per_server": a.emulate_shards})
+                               wire_dtype=a.wire, extra={"ps_id": ps_id, "shards_per_server": a.emulate_shards,
+                                                         # timed loop: step() back to back, then sync()
+                                                         "defer_ps_wait": True})
     return mp_train.Trainer(cfg)
 
 

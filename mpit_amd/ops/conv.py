@@ -1051,7 +1051,10 @@ class _StemConvFn(torch.autograd.Function):
         if f32 and _F32_SPLIT == "f16x3":
             # fp16x3: the image's bound (the padded copy only adds zeros) and the packed weight as
             # two fp16 planes; the row-tap GEMM then runs 32-deep tiles, one kernel row each
-            ctx.xbound = bound_of_value(torch.linalg.vector_norm(x, float("inf")))
+            ctx.xbound = amax_of(x)  # kept on the input while it is unchanged (a reused batch)
+            if ctx.xbound is None:
+                ctx.xbound = bound_of_value(torch.linalg.vector_norm(x, float("inf")))
+                set_amax(x, ctx.xbound)
             wb = f16_planes(wb.reshape(co, -1), bound_of_value(torch.linalg.vector_norm(weight.detach(), float("inf"))))
             kw = dict(bps=wb[0].numel(), amax_a=ctx.xbound.data_ptr(), amax_b=wb._mpit_wamax.data_ptr())
         native().conv_stem_fwd(x.device.index, _stream(x), nb, hp, wp, co, ho, wo, stride, xp.data_ptr(),

@@ -80,9 +80,15 @@ def downpour(opfunc, w, config, state=None):
             pusher.abort()  # no pushes of half-computed shards
             raise
         pusher.finish()
-        t0 = time.perf_counter()
-        pc.wait()
-        state["dusync"] += time.perf_counter() - t0
+        if config.get("defer_wait"):
+            # the caller retires the pulls right before its next read of w (mpit_amd/train.py
+            # Trainer._feval / sync): the host's step bookkeeping then overlaps the servers'
+            # apply + pull instead of following the reply
+            state["wait_pending"] = True
+        else:
+            t0 = time.perf_counter()
+            pc.wait()
+            state["dusync"] += time.perf_counter() - t0
         state["pversion"] = pv + 1
         return w, [fx]
     fx, dfdx = opfunc(w)

@@ -137,6 +137,11 @@ class Trainer:
                 from .parallel.overlap import ShardPusher
 
                 self.opt_config["pusher"] = ShardPusher(self.flat, self.pc)
+                # defer the wait for the last shards' replies to the next read of w (cfg.extra
+                # "defer_ps_wait": bench.py; MPIT_DEFER_PS_WAIT=0/1 overrides): step() then
+                # returns with pulls in flight — read w only after sync() / the next step
+                dw = os.environ.get("MPIT_DEFER_PS_WAIT")
+                self.opt_config["defer_wait"] = (dw == "1") if dw is not None else bool(cfg.extra.get("defer_ps_wait", False))
         # bf16 casts of every MFMA conv weight in one launch per step (ops/conv.py)
         self.wcast = None
         if self.on_gpu and cfg.extra.get("batched_weight_casts", True):
@@ -202,7 +207,17 @@ class Trainer:
             pass  # dedicated server rank: serve until the workers stop (see run_server)
 
     # ------------------------------------------------------------------ step
+    def _retire_deferred(self):
+        """Wait for the pulls a deferred Downpour step left in flight (optim/distributed.py)."""
+        st = getattr(self, "state", None)
+        if st is not None and st.get("wait_pending"):
+            t0 = time.perf_counter()
+            self.pc.wait()
+            st["dusync"] = st.get("dusync", 0.0) + time.perf_counter() - t0
+            st["wait_pending"] = False
+
     def _feval(self, w):
+        self._retire_deferred()  # the previous step's pulls land in w before anything reads it
         if not getattr(self, "steal", False):
             self.flat.zero_grad()
         if self.wcast is not None:  # the weights as they are now, for this forward/backward only
@@ -381,6 +396,8 @@ class Trainer:
         deliberately leaves its last elastic push in flight, asyncsgd/optim-eamsgd.lua:65-67)."""
         if self.pc is not None:
             self.pc.wait()
+            if getattr(self, "state", None) is not None:
+                self.state["wait_pending"] = False
 
     def run_server(self):
         """Block a dedicated server rank until all workers sent stop."""
@@ -394,6 +411,7 @@ class Trainer:
             self.ps_server.wait_done()
 
     def sync(self):
+        self._retire_deferred()
         if self.on_gpu:
             torch.cuda.synchronize()
 

@@ -695,9 +695,6 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
           const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
           split2h(v, sa, sa11, ah[i], al[i]);
         }
-#ifdef MPIT_F16X3_PRIO
-        __builtin_amdgcn_s_setprio(1);
-#endif
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -706,9 +703,6 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
             tacc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bl[j], ah[i], tacc[i][j], 0, 0, 0);
             tacc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bh[j], al[i], tacc[i][j], 0, 0, 0);
           }
-#ifdef MPIT_F16X3_PRIO
-        __builtin_amdgcn_s_setprio(0);
-#endif
       }
       continue;
     } else if constexpr (BSPLIT) {
@@ -2179,12 +2173,7 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
   int cap = F32 && N % 128 == 0 ? (fm >= 3 ? 2 : 4) : max_stages;
   if (F32 && f32_stages) cap = f32_stages;
   // (the pre-split kernels, FM >= 4, are built for the 2-deep ring of 128-row tiles only)
-  // MPIT_F16X3_STAGES=3: the fp16x3 kernels on a 3-deep ring (96 KB: one block per CU) — A/B knob
-  static const int f16x3_stages = [] {
-    const char* e = std::getenv("MPIT_F16X3_STAGES");
-    return e && std::atoi(e) == 3 ? 3 : 2;
-  }();
-  const int stages = fm == 11 ? f16x3_stages : fm >= 4 ? 2 : std::min(cap, nk >= 4 ? 4 : (nk == 3 ? 3 : 2));
+  const int stages = fm >= 4 ? 2 : std::min(cap, nk >= 4 ? 4 : (nk == 3 ? 3 : 2));
   // (kernel templates are named at a non-template call site so their host stubs are emitted)
 #define MPIT_NT_OPT_IN(BM, BN, ST, EPI, CONV, FMV)                                                                 \
   do {                                                                                                             \
@@ -2197,14 +2186,6 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
   } while (0)
 #define MPIT_NT_LAUNCH1(BM, BN, ST, EPI, CONV)                                                                       \
   do {                                                                                                             \
-    if constexpr (F32 && BM == 128 && ST == 3) {                                                                 \
-      if (fm == 11) {                                                                                              \
-        if (shm > 65536) MPIT_NT_OPT_IN(BM, BN, ST, EPI, CONV, 11);                                                 \
-        hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, ST, EPI, CONV, 11>), dim3(unsigned(nb)), dim3(256), shm, s, a, \
-                           lda, b, ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g, bps);                          \
-        break;                                                                                                     \
-      }                                                                                                            \
-    }                                                                                                              \
     if constexpr (F32 && BM == 128 && ST == 2) {                                                                 \
       if (fm == 11) {                                                                                              \
         if (shm > 65536) MPIT_NT_OPT_IN(BM, BN, ST, EPI, CONV, 11);                                                 \

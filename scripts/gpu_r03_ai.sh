@@ -32,4 +32,6 @@ print("shape | " + " | ".join(vs))
 for a in dict.fromkeys(r["a"] for r in rows):
     print(a, "|", " | ".join(f"{max(t[(a, v)]):.1f}" for v in vs))
 PY
+timeout -k 10 500 python -u -m pytest tests/test_overlap.py -m gpu -q --timeout 450 --timeout-method thread > $O/overlap.log 2>&1
+rc=$?; tail -2 $O/overlap.log; [ $rc -ne 0 ] && { grep -E "FAILED|Error|DIFF" $O/overlap.log | head; exit 1; }
 echo ALL OK

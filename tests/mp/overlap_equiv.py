@@ -5,7 +5,9 @@ bit-identical parameters to the non-overlapped path (push + pull after the backw
 Run under torch.distributed.run with 3 ranks: 2 dedicated servers, 1 worker. For each
 precision (fp32, bf16 autocast) two PS instances train the same model from the same init on
 the same data, one with overlap, one without; the final pulled parameters are compared
-bit for bit (int64 sums of the fp32 words and an exact tensor compare on the worker)."""
+bit for bit (int64 sums of the fp32 words and an exact tensor compare on the worker). A third
+instance runs the overlap with the deferred wait (the last pulls retired at the next forward,
+extra["defer_ps_wait"], what bench.py runs) and must match too."""
 import os
 import sys
 
@@ -26,10 +28,11 @@ results = {}
 ps_id = 0
 for amp in (False, True):
     finals = {}
-    for overlap in (True, False):
+    for arm in ("overlap", "plain", "defer"):
+        overlap = arm != "plain"
         tr = Trainer(TrainConfig(model=model, batch=8, num_classes=10, optimizer="downpour", topology="dedicated",
                                  servers=2, lr=0.05, amp=amp,
-                                 extra={"ps_id": ps_id, "overlap_push": overlap}))
+                                 extra={"ps_id": ps_id, "overlap_push": overlap, "defer_ps_wait": arm == "defer"}))
         ps_id += 1
         if tr.is_worker:
             assert ("pusher" in tr.opt_config) == overlap
@@ -37,18 +40,21 @@ for amp in (False, True):
         chk = tr.verify_ps()
         assert chk["ok"], chk
         if tr.is_worker:
-            finals[overlap] = tr.flat.flat.detach().clone()
+            finals[arm] = tr.flat.flat.detach().clone()
             names = [(n, off, p.numel()) for (n, p), off in zip(tr.model.named_parameters(), tr.flat.offsets)]
         tr.stop()
-    if finals:
-        a, b = finals[True], finals[False]
+    for arm in ("overlap", "defer"):
+        if not finals:
+            break
+        a, b = finals[arm], finals["plain"]
         same = bool(torch.equal(a.view(torch.int32), b.view(torch.int32)))
         diff = float((a - b).abs().max())
-        results["bf16" if amp else "fp32"] = (same, diff)
+        key = ("bf16" if amp else "fp32") + ("" if arm == "overlap" else "_defer")
+        results[key] = (same, diff)
         if not same:  # which parameters differ (diagnostics)
             bad = [(n, float((a[o:o + k] - b[o:o + k]).abs().max())) for n, o, k in names
                    if not torch.equal(a[o:o + k], b[o:o + k])]
-            print(f"DIFF {'bf16' if amp else 'fp32'} {len(bad)}/{len(names)}: {bad[:12]}", flush=True)
+            print(f"DIFF {key} {len(bad)}/{len(names)}: {bad[:12]}", flush=True)
 allr = [r for r in W.allgather_obj(results) if r]
 if W.Get_rank() == 0:
     print("RESULT", allr, flush=True)

@@ -68,13 +68,14 @@ def test_shard_pusher_matches_one_shot_gather():
 def test_overlap_equals_non_overlapped_on_gpu_three_ranks():
     """1 worker + 2 dedicated servers on the box's GPU: ResNet-18 Downpour steps with the
     refreshed shards written into the model during the backward give exactly the parameters
-    of pushing / pulling after the backward, in fp32 and in bf16 autocast."""
+    of pushing / pulling after the backward, in fp32 and in bf16 autocast — also with the
+    last pulls' wait deferred to the next forward (defer_ps_wait)."""
     out = run_ranks("overlap_equiv.py", 3, {"MPIT_WGRAD_STREAM": "force"}, timeout=400)
     m = re.search(r"RESULT (.*)", out)
     assert m, out[-3000:]
     res = eval(m.group(1))
     assert len(res) == 1, res
-    for prec in ("fp32", "bf16"):
+    for prec in ("fp32", "bf16", "fp32_defer", "bf16_defer"):
         same, diff = res[0][prec]
         assert same, (prec, diff)
 

@@ -176,9 +176,12 @@ PYBIND11_MODULE(_mpit, m) {
   m.def("cast_jobs_build", [](uintptr_t table, std::vector<std::array<int64_t, 11>> specs) {
     return cast_jobs_build(table, specs);
   });
-  m.def("cast_jobs_run", [](int dev, uintptr_t s, uintptr_t table, int njobs, int64_t nblocks) {
-    cast_jobs_run(dev, S(s), table, njobs, nblocks);
-  });
+  m.def(
+      "cast_jobs_run",
+      [](int dev, uintptr_t s, uintptr_t table, int njobs, int64_t nblocks, uintptr_t amax) {
+        cast_jobs_run(dev, S(s), table, njobs, nblocks, amax);
+      },
+      py::arg("dev"), py::arg("s"), py::arg("table"), py::arg("njobs"), py::arg("nblocks"), py::arg("amax") = 0);
   m.def(
       "maxpool_fwd",
       [](int dev, uintptr_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t x, uintptr_t y,

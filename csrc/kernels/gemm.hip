@@ -1916,6 +1916,43 @@ struct CastJob {
   TapMap map;
 };
 
+// The fp16-plane jobs' bound, max |w| over every such weight of the plan (one pass before
+// cast_batch_kernel, which derives the planes' scale from it): block b of job j (the same
+// block -> job map) strides over the job's R * Cc * T weights, reduces its maximum and issues
+// ONE fire-and-forget atomic max into slot b % kBoundSlots of J.amax (zeroed by the launch).
+// Replaces the per-step torch _foreach_norm + stack + amax chain (several launches with host
+// gaps between them at the step boundary).
+__global__ __launch_bounds__(256) void cast_amax_kernel(const CastJob* __restrict__ jobs, int njobs, int64_t nblocks) {
+  __shared__ int jsel;
+  __shared__ float red[4];
+  if (threadIdx.x == 0) {
+    int lo = 0, hi = njobs - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (jobs[mid].block0 <= int64_t(blockIdx.x)) lo = mid;
+      else hi = mid - 1;
+    }
+    jsel = lo;
+  }
+  __syncthreads();
+  const CastJob& J = jobs[jsel];
+  if (!(J.f32 == 2 && J.f16)) return;  // uniform per block
+  const int64_t nbj = (jsel + 1 < njobs ? jobs[jsel + 1].block0 : nblocks) - J.block0;
+  const int64_t n = int64_t(J.R) * J.Cc * J.T;
+  float m = 0.f;
+  for (int64_t i = (int64_t(blockIdx.x) - J.block0) * 256 + threadIdx.x; i < n; i += nbj * 256)
+    m = fmaxf(m, fabsf(J.w[i]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float b = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    atomicMax(reinterpret_cast<unsigned int*>(const_cast<float*>(J.amax) + (blockIdx.x % kBoundSlots) * kBoundStride),
+              __float_as_uint(b));
+  }
+}
+
 __global__ __launch_bounds__(256) void cast_batch_kernel(const CastJob* __restrict__ jobs, int njobs) {
   __shared__ int jsel;
   if (threadIdx.x == 0) {
@@ -2809,9 +2846,14 @@ int64_t cast_jobs_build(uintptr_t host_table, const std::vector<std::array<int64
   return blocks;
 }
 
-void cast_jobs_run(int dev, hipStream_t s, uintptr_t dev_table, int njobs, int64_t nblocks) {
+void cast_jobs_run(int dev, hipStream_t s, uintptr_t dev_table, int njobs, int64_t nblocks, uintptr_t amax) {
   if (njobs <= 0 || nblocks <= 0) return;
   hip_check(hipSetDevice(dev), "hipSetDevice");
+  if (amax) {  // the fp16-plane jobs' bound (every such job points at this buffer)
+    hip_check(hipMemsetAsync(reinterpret_cast<void*>(amax), 0, kBoundFloats * sizeof(float), s), "cast amax zero");
+    hipLaunchKernelGGL(cast_amax_kernel, dim3(unsigned(nblocks)), dim3(256), 0, s,
+                       reinterpret_cast<const CastJob*>(dev_table), njobs, nblocks);
+  }
   hipLaunchKernelGGL(cast_batch_kernel, dim3(unsigned(nblocks)), dim3(256), 0, s,
                      reinterpret_cast<const CastJob*>(dev_table), njobs);
   hip_check(hipGetLastError(), "cast_batch launch");

@@ -177,7 +177,7 @@ void cast_transpose(int dev, hipStream_t s, uintptr_t w, int R, int Cc, uintptr_
 // host (cast_job_bytes() per job) and uploaded once; cast_jobs_run launches it.
 int64_t cast_job_bytes();
 int64_t cast_jobs_build(uintptr_t host_table, const std::vector<std::array<int64_t, 11>>& specs);
-void cast_jobs_run(int dev, hipStream_t s, uintptr_t dev_table, int njobs, int64_t nblocks);
+void cast_jobs_run(int dev, hipStream_t s, uintptr_t dev_table, int njobs, int64_t nblocks, uintptr_t amax = 0);
 
 // ---- NHWC RxS convolutions as implicit GEMMs on the same MFMA kernels ----------------
 // x [Nb,H,W,C], w [Co,R,S,C] (bf16), y [Nb,Ho,Wo,Co] (bf16); stats / cin as gemm_nt.

@@ -878,7 +878,7 @@ class WeightCastPlan:
             # current then) alive into every step — autograd then warns that the node's stream
             # differs from the step's and inserts a cross-stream wait per weight
             if f16p and (pl_b or pl_t) and self.amax is None:
-                self.amax = torch.zeros(BOUND_FLOATS, dtype=torch.float32, device=w.device)  # value in slot 0
+                self.amax = torch.zeros(BOUND_FLOATS, dtype=torch.float32, device=w.device)  # slotted bound
             if f32 and not pl_b:
                 wb = _as_rsc(w.detach())
             else:
@@ -926,12 +926,10 @@ class WeightCastPlan:
             self._build()  # parameters moved (FlatParams.rebind)
         if self.table is not None:
             dev = self.table.device
-            if self.wlist:  # the planes' scale: max |w| over the plan's fp16-plane weights
-                with torch.no_grad():
-                    torch.amax(torch.stack(torch._foreach_norm(self.wlist, float("inf"))), 0, keepdim=True,
-                               out=self.amax[:1])
+            # fp16 planes: the same launch sequence first writes their scale's bound, max |w| over
+            # the plan's fp16-plane weights, into self.amax (gemm.hip cast_amax_kernel)
             native().cast_jobs_run(dev.index, torch.cuda.current_stream(dev).cuda_stream, self.table.data_ptr(),
-                                   self.njobs, self.nblocks)
+                                   self.njobs, self.nblocks, self.amax.data_ptr() if self.wlist else 0)
         self.valid = True
 
     def invalidate(self):

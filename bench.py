@@ -17,9 +17,18 @@ over ranks.
 
 Precision: the headline is **fp32** — the reference trains fp32 Float/CudaTensors
 (asyncsgd/glaunch.lua:11, BiCNN/plaunch.lua:200) — with fp32 weights, activations and
-gradients on the hand-written gfx950 kernels (every GEMM-shaped op as exact bf16x6 split
-products on the bf16 MFMA, ops/conv.py). bf16 autocast (fp32 master
-weights) is reported as the secondary field ``secondary.bf16_autocast`` of the same job.
+gradients on the hand-written gfx950 kernels. Every GEMM-shaped op runs as fp16x3 split
+products on the fp16 MFMA (``"fp32_gemm": "fp16x3"`` in the JSON; ops/conv.py,
+csrc/kernels/gemm.hip FM 11): each operand is scaled by a power of two from a device-side
+bound and split exactly into two fp16 planes (22 significant bits), three MFMAs per product
+with fp32 accumulation. Measured closer to fp64 than PyTorch's fp32 GEMMs on every
+ResNet-50 shape (tests/test_fp32_path.py). ``MPIT_F32_SPLIT=bf16x6`` selects the 6-MFMA bf16
+split instead. bf16 autocast (fp32 master weights) is reported as the secondary field
+``secondary.bf16_autocast`` of the same job.
+
+The last pulls of a step are waited for at the end of that step (the reference's
+push, pull, wait: asyncsgd/optim-downpour.lua:50-53); ``--defer-ps-wait`` retires them at
+the next step's first read of the weights instead (measured slower, off by default).
 
 Also reported, outside the timed region (``--no-secondary`` skips them):
 * ``ps_check``: after the run every worker pulls every shard again and the exact bit-sums
@@ -64,9 +73,15 @@ def _make(a, mp_train, amp: bool, topology: str, servers: int, ps_id: int):
                                servers=servers, su=a.su, lr=lr, mva=mva, mom=0.0, amp=amp,
                                channels_last=not a.no_channels_last, datapath=a.datapath, staleness=a.staleness,
                                wire_dtype=a.wire, extra={"ps_id": ps_id, "shards_per_server": a.emulate_shards,
-                                                         # timed loop: step() back to back, then sync()
-                                                         "defer_ps_wait": True})
+                                                         "defer_ps_wait": a.defer_ps_wait})
     return mp_train.Trainer(cfg)
+
+
+def _fp32_gemm() -> str:
+    """How the fp32 step's GEMMs use the matrix cores (ops/conv.py MPIT_F32_SPLIT)."""
+    from mpit_amd.ops import conv
+
+    return conv._F32_SPLIT
 
 
 def _devices(W, tr) -> list:
@@ -128,6 +143,9 @@ def main(argv=None) -> int:
                     help="K > 1: split the (single) server's shard into K shards, each pushed from inside the "
                          "backward and served through the remote-client pipeline (link stream, inbox / outbox) — "
                          "one GPU carrying the per-worker shard traffic of an N=K job (diagnostic, not the headline)")
+    ap.add_argument("--defer-ps-wait", action="store_true",
+                    help="retire a step's last pulls at the next step's first weight read instead of at the "
+                         "end of the step (profiles/defer_ps_wait_ab_r03.md: slower; off by default)")
     ap.add_argument("--miopen-find", action="store_true",
                     help="exhaustive MIOpen algorithm search for what still runs on MIOpen (the fc layer)")
     a = ap.parse_args(argv)
@@ -213,7 +231,8 @@ def main(argv=None) -> int:
             "data": f"synthetic (random images {shape[0]}x{shape[1]}x{shape[2]}, random labels, random-init weights)",
             "config": {"model": a.model, "global_batch": a.batch * nworkers, "seq_len": None, "image_size": shape[-1],
                        "parallelism": par, "optimizer": a.optimizer, "su": a.su, "per_gpu_batch": a.batch,
-                       "master_weights": "fp32", "loss_last": lossv},
+                       "master_weights": "fp32", "loss_last": lossv, "defer_ps_wait": a.defer_ps_wait},
+            "fp32_gemm": _fp32_gemm() if not (tr.on_gpu and amp) else None,
             "world": st.world, "shared_devices": st.shared_devices, "devices": devices, "rccl": rccl,
             "ps_check": check,
             **({"emulate_shards": a.emulate_shards} if a.emulate_shards > 1 else {}),

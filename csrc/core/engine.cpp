@@ -48,7 +48,11 @@ void futex_wait(void* addr, uint32_t expect, int64_t timeout_us, bool shared) {
 }
 
 double Engine::wait_timeout_s() {
-  static const double t = env_seconds("MPIT_WAIT_TIMEOUT_S", 600.0);
+  // 0 (default) = never: MPI's blocking calls have no deadline either, and a rank may
+  // legitimately sit in Barrier / Wait for hours (a BiCNN rank outside the active set, a fast
+  // goot worker at the final Barrier). Dead peers are caught by check_peers + the abort flag;
+  // tests opt in to a deadline.
+  static const double t = env_seconds("MPIT_WAIT_TIMEOUT_S", 0.0);
   return t;
 }
 
@@ -835,13 +839,17 @@ bool Engine::idle_deep_ok() {
   return true;
 }
 
-void Engine::park(int64_t timeout_us) {
+void Engine::park(int64_t timeout_us, uint64_t last_act) {
   RankInfo& ri = seg_->hdr()->ranks[rank_];
   const uint32_t v = ri.doorbell.load(std::memory_order_seq_cst);
   ri.sleeping.store(1, std::memory_order_seq_cst);
   std::atomic_thread_fence(std::memory_order_seq_cst);
-  // final re-check after announcing: incoming headers / bulk bytes, local requests
-  bool work = seg_->hdr()->abort_flag.load(std::memory_order_seq_cst) != 0 || !running_.load();
+  // final re-check after announcing: local activity since the idle check (a kick() between
+  // idle_deep_ok() and the store above saw sleeping == 0 and rang nobody: its seq_cst
+  // fetch_add on activity_ precedes its fence, so it is visible here), incoming headers /
+  // bulk bytes, abort
+  bool work = activity_.load(std::memory_order_seq_cst) != last_act ||
+              seg_->hdr()->abort_flag.load(std::memory_order_seq_cst) != 0 || !running_.load();
   for (int s = 0; s < world_ && !work; ++s) {
     Ring* rg = seg_->ring(s, rank_);
     BulkHdr* b = seg_->bulk(s, rank_);
@@ -896,7 +904,7 @@ void Engine::progress_loop() {
     } else if (idle < 256 + yields) {
       std::this_thread::yield();
     } else if (deep && idle_deep_ok()) {
-      park(50000);
+      park(50000, last_act);
     } else {
       std::this_thread::sleep_for(std::chrono::microseconds(20));
     }

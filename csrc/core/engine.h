@@ -190,7 +190,7 @@ class Engine {
   void check_abort();
   void publish_abort(const std::string& why, int code);
   bool idle_deep_ok();
-  void park(int64_t timeout_us);
+  void park(int64_t timeout_us, uint64_t last_act);
   bool push_msg_locked(int dst, const Msg& m);
   int64_t bulk_write_locked(int dst, const uint8_t* p, int64_t n);
   int64_t bulk_read(int src, uint8_t* p, int64_t n);

@@ -61,6 +61,7 @@ PSServer::PSServer(Engine& eng, int ps_id, Window& rx, Window& tx, std::vector<i
       if (std::atoi(r) != eng_.rank()) fault_kind_ = 0;
   }
   clock_.assign(clients_.size(), 0);
+  tpush_.assign(clients_.size(), 0);
   if (device_) {
     hipp(hipSetDevice(eng_.device()), "hipSetDevice");
     int lo = 0, hi = 0;
@@ -321,15 +322,25 @@ std::vector<uintptr_t> PSServer::rule_ptrs(const void* g, void* out, Sub sb) con
   return ptrs;
 }
 
-void PSServer::apply_rule(const void* g, void* out, Sub sb) {
+void PSServer::apply_rule(const void* g, void* out, Sub sb, int ci) {
   const int dev = device_ ? eng_.device() : -1;
   const uint32_t bf = grad_bf16_ ? 2u : 0u;
   const int v = out ? kOut : 0;
   const std::vector<uintptr_t> ptrs = rule_ptrs(g, out, sb);
   ServerRule r = rule_;  // progress thread only; lr may be changed concurrently (set_lr)
   r.lr = lr_.load(std::memory_order_relaxed);
-  // the rule's step counter advances once per client push: on its first piece
-  const bool first = sb.o == 0;
+  // the rule's step counter advances once per client push, on its first piece; the later
+  // pieces of that push (split shard entries) reuse the step their first piece took, even
+  // when another client's push arrived in between
+  int64_t tc = 0;
+  if (r.kind >= 2) {
+    if (sb.o == 0) {
+      tc = t_.fetch_add(1) + 1;
+      if (ci >= 0) tpush_[size_t(ci)] = tc;
+    } else {
+      tc = ci >= 0 && tpush_[size_t(ci)] > 0 ? tpush_[size_t(ci)] : t_.load();
+    }
+  }
   switch (r.kind) {
     case 0:
       ew_update(kApply, v, dev, stream_, sb.n, ptrs, bf, {r.a});
@@ -338,26 +349,22 @@ void PSServer::apply_rule(const void* g, void* out, Sub sb) {
       ew_update(kRMSProp, v | kAdd, dev, stream_, sb.n, ptrs, bf, {r.decay, r.lr, r.mom, r.eps});
       break;
     case 2: {  // BiCNN/pserver.lua:147-154: bias correction on floor(t/stepDiv)+1
-      if (first) ++t_;
-      const double k = double(t_.load() / std::max<int64_t>(1, r.step_div) + 1);
+      const double k = double(tc / std::max<int64_t>(1, r.step_div) + 1);
       const double lr_t = r.lr * std::sqrt(1.0 - std::pow(double(r.b2), k)) / (1.0 - std::pow(double(r.b1), k));
       ew_update(kAdam, v, dev, stream_, sb.n, ptrs, bf, {r.b1, r.b2, r.eps, float(lr_t)});
       break;
     }
     case 3: {  // BiCNN/pserver.lua:163-170
-      if (first) ++t_;
-      const double lr_t = r.lr / (1.0 - std::pow(double(r.b1), double(t_.load())));
+      const double lr_t = r.lr / (1.0 - std::pow(double(r.b1), double(tc)));
       ew_update(kAdamax, v, dev, stream_, sb.n, ptrs, bf, {r.b1, r.b2, r.eps, float(lr_t)});
       break;
     }
     case 4: {  // BiCNN/pserver.lua:177-182 (clr on the count before this push)
-      const int64_t t = first ? t_.fetch_add(1) : t_.load() - 1;
-      const float clr = float(r.lr / (1.0 + double(t) * r.lrd));
+      const float clr = float(r.lr / (1.0 + double(tc - 1) * r.lrd));
       ew_update(kAdagrad, v, dev, stream_, sb.n, ptrs, bf, {r.eps, clr});
       break;
     }
     case 5:  // BiCNN/pserver.lua:189-193
-      if (first) ++t_;
       ew_update(kAdadelta, v, dev, stream_, sb.n, ptrs, bf, {r.rho, r.eps, r.lr});
       break;
   }
@@ -466,7 +473,7 @@ void PSServer::do_grad(int c, bool pull, Sub sb) {
     hipp(hipEventRecord(ev_in_[k], cs), "record inbox full");
     hipp(hipStreamWaitEvent(stream_, ev_in_[k], 0), "update waits inbox");
     if (push_back) hipp(hipStreamWaitEvent(stream_, ev_out_[k], 0), "update waits outbox free");
-    apply_rule(in, push_back ? out : nullptr, sb);
+    apply_rule(in, push_back ? out : nullptr, sb, ci);
     hipp(hipEventRecord(ev_up_[k], stream_), "record update");
     hipp(hipStreamWaitEvent(cs, ev_up_[k], 0), "link waits update");  // inbox reusable after this
     if (push_back) {
@@ -501,7 +508,7 @@ void PSServer::do_grad(int c, bool pull, Sub sb) {
       g = ib;
     }
   }
-  apply_rule(g, fused_out, sb);
+  apply_rule(g, fused_out, sb, ci);
   if (pull && !defer_pull && !fused_out) copy_out(c, sb);
   {
     std::lock_guard<std::mutex> lk(mu_);
@@ -609,6 +616,19 @@ PSClient::PSClient(Engine& eng, int ps_id, std::vector<int> servers, std::vector
 
 PSClient::~PSClient() {
   if (hook_ >= 0) eng_.remove_hook(hook_);
+  // gates never retired (the client went away with pushes queued): release their events
+  // and their pending count, or deep parking stays disabled for the rest of the process
+  std::deque<GateQueue::Gate> left;
+  {
+    std::lock_guard<std::mutex> l(gq_->mu);
+    left.swap(gq_->q);
+  }
+  for (auto& g : left)
+    if (g.ev) {
+      hipEventSynchronize(g.ev);
+      eng_.put_event(g.ev);
+      eng_.gpu_pending_add(-1);
+    }
 }
 
 void PSClient::start() {
@@ -627,12 +647,15 @@ void PSClient::gate(hipStream_t s, std::function<void()> send) {
     g.ev = eng_.get_event();
     Engine::record_event(g.ev, s);
   }
+  // count the pending GPU event BEFORE the gate becomes visible to the progress hook: the
+  // hook may pop it (and decrement) right after the push, and an under-count while another
+  // gate is outstanding would let the progress thread park with an event still to poll
+  if (g.ev) eng_.gpu_pending_add(1);
   {
     std::lock_guard<std::mutex> l(gq_->mu);
     gq_->q.push_back(g);
   }
-  if (g.ev) eng_.gpu_pending_add(1);
-  else eng_.kick();
+  if (!g.ev) eng_.kick();
 }
 
 // the message of shard entry k: whole-shard entries carry no piece (aux2 = 0)
@@ -694,9 +717,11 @@ void PSClient::on_reply(const Msg&) {
 // MPIT_WAIT_SPIN_US > 0 polls (pause) for up to that long before the futex sleep, keeping
 // the core awake for the step start that follows (device clients only). Measured within
 // noise of sleeping at once (profiles/step_start_host_r02.md): default 0.
-// MPIT_PS_TIMEOUT_S (default 300, 0 = never): a reply missing that long means a server is
+// MPIT_PS_TIMEOUT_S (default 0 = never, opt-in): a reply missing that long means a server is
 // gone or stuck — raise with what is missing instead of hanging the job (a server that
-// fails raises the job-wide abort itself, Engine::fatal; this covers the silent cases).
+// fails raises the job-wide abort itself, Engine::fatal; a dead server process is caught by
+// the peer check). Off by default: an SSP-deferred pull may wait on a slow straggler for
+// as long as that straggler takes, as the reference's blocking MPI calls do.
 void PSClient::wait() {
   static const int64_t spin_us = [] {
     const char* e = std::getenv("MPIT_WAIT_SPIN_US");
@@ -704,7 +729,7 @@ void PSClient::wait() {
   }();
   static const double timeout_s = [] {
     const char* e = std::getenv("MPIT_PS_TIMEOUT_S");
-    return e ? std::max(0.0, std::atof(e)) : 300.0;
+    return e ? std::max(0.0, std::atof(e)) : 0.0;
   }();
   const auto t0 = std::chrono::steady_clock::now();
   if (spin_us > 0 && eng_.device() >= 0) {  // GPU workers only (CPU ranks share few cores)

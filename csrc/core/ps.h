@@ -114,7 +114,7 @@ class PSServer {
   void do_param(int c, bool from_rx, Sub sb);
   void do_grad(int c, bool pull, Sub sb);
   void do_pull(int c, Sub sb);
-  void apply_rule(const void* g, void* out, Sub sb);
+  void apply_rule(const void* g, void* out, Sub sb, int ci);
   std::vector<uintptr_t> rule_ptrs(const void* g, void* out, Sub sb) const;
   // gradient pieces of the direct (non-link) path that arrive in one progress sweep are
   // applied together: ONE multi-segment launch (ew_update_multi) instead of one per piece.
@@ -189,6 +189,7 @@ class PSServer {
   std::vector<Msg> backlog_;      // grads / pulls that arrived before that push
   std::atomic<int64_t> t_{0};  // rule step counter (adam / adamax / adagrad / adadelta)
   std::vector<int64_t> clock_;  // pushes received per client (SSP)
+  std::vector<int64_t> tpush_;  // per client: the rule step its current push took (split entries)
   std::deque<std::pair<int, Sub>> deferred_;  // pulls (client, piece) waiting for stragglers
   mutable std::mutex mu_;
   std::condition_variable cv_;

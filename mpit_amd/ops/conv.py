@@ -165,6 +165,9 @@ _F32_PLANES_N = int(os.environ.get("MPIT_F32_PLANES_N",
 _F32_SPLIT = os.environ.get("MPIT_F32_SPLIT", "f16x3")
 if _F32_SPLIT not in ("f16x3", "bf16x6"):
     raise ValueError(f"MPIT_F32_SPLIT={_F32_SPLIT!r}: expected f16x3 or bf16x6")
+# MPIT_WPLAN_TORCH_BOUND=1 (A/B): the weight plan's fp16-plane bound by torch launches
+# (foreach_norm + amax into slot 0) instead of gemm.hip cast_amax_kernel
+_WPLAN_TORCH_BOUND = os.environ.get("MPIT_WPLAN_TORCH_BOUND", "0") == "1"
 
 
 def _bps(w: torch.Tensor, f32: bool) -> int:
@@ -926,10 +929,16 @@ class WeightCastPlan:
             self._build()  # parameters moved (FlatParams.rebind)
         if self.table is not None:
             dev = self.table.device
+            native_bound = bool(self.wlist) and not _WPLAN_TORCH_BOUND
+            if self.wlist and _WPLAN_TORCH_BOUND:  # A/B: the bound by torch launches, slot 0 only
+                with torch.no_grad():
+                    self.amax.zero_()
+                    torch.amax(torch.stack(torch._foreach_norm(self.wlist, float("inf"))), 0, keepdim=True,
+                               out=self.amax[:1])
             # fp16 planes: the same launch sequence first writes their scale's bound, max |w| over
             # the plan's fp16-plane weights, into self.amax (gemm.hip cast_amax_kernel)
             native().cast_jobs_run(dev.index, torch.cuda.current_stream(dev).cuda_stream, self.table.data_ptr(),
-                                   self.njobs, self.nblocks, self.amax.data_ptr() if self.wlist else 0)
+                                   self.njobs, self.nblocks, self.amax.data_ptr() if native_bound else 0)
         self.valid = True
 
     def invalidate(self):

@@ -1,0 +1,127 @@
+#!/usr/bin/env python3
+"""One parameterised runner for every GPU-box job (replaces the per-letter gpu_r0*_*.sh files).
+
+    gpurun --timeout 1200 -- python3 scripts/gpu.py <outdir> <step> [<step> ...]
+
+Writes everything under gpurun_out/<outdir>/. Steps run in order, each under its own
+``timeout -k 10``; the first failing step (non-zero exit, time limit, abort, segfault) ends
+the run with that step's exit code — nothing else touches the GPU after it.
+
+Steps:
+  smoke                 __graft_entry__.smoke()                         -> smoke.log
+  tier                  pytest -m gpu (whole GPU tier)                  -> pytest_gpu.log
+  pytest:<args>         pytest <args> (e.g. pytest:tests/test_overlap.py) -> pytest_<n>.log
+  bench                 bench.py defaults (fp32 headline + bf16 secondary) -> bench.json
+  bench:<args>          bench.py <args> (comma separated)               -> bench_<n>.json
+  prof:<name>:<args>    rocprofv3 --kernel-trace of bench.py <args> + stream table -> streams_<name>.md
+  mp:<script>:<n>[:K=V;K=V] tests/mp/<script> on n ranks with extra env   -> mp_<script>_<n>.log
+  py:<file>[:args]      python3 <file> <args> (benchmarks/ probes)      -> py_<n>.log
+"""
+from __future__ import annotations
+
+import os
+import shlex
+import subprocess
+import sys
+import time
+
+ROOT = os.environ.get("GRAFT_REPO_ROOT") or os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PY = sys.executable
+
+
+def _run(out: str, name: str, cmd, limit: int, env=None, stdout_file=None) -> int:
+    log = os.path.join(out, name)
+    e = dict(os.environ)
+    e.setdefault("TMPDIR", "/tmp")
+    e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    e["PYTHONPATH"] = ROOT + os.pathsep + e.get("PYTHONPATH", "")
+    e.update(env or {})
+    full = ["timeout", "-k", "10", str(limit)] + cmd
+    t0 = time.time()
+    print(f"[gpu.py] {name}: {' '.join(shlex.quote(c) for c in cmd)}", flush=True)
+    if stdout_file:
+        with open(os.path.join(out, stdout_file), "w") as so, open(log, "w") as se:
+            rc = subprocess.call(full, stdout=so, stderr=se, env=e, cwd=ROOT)
+    else:
+        with open(log, "w") as f:
+            rc = subprocess.call(full, stdout=f, stderr=subprocess.STDOUT, env=e, cwd=ROOT)
+    print(f"[gpu.py] {name}: rc={rc} in {time.time() - t0:.1f}s", flush=True)
+    if rc != 0:
+        try:
+            with open(log) as f:
+                print("".join(f.readlines()[-40:]), flush=True)
+        except OSError:
+            pass
+    return rc
+
+
+def _tail(path: str, n: int = 3) -> str:
+    try:
+        with open(path) as f:
+            return "".join(f.readlines()[-n:]).rstrip()
+    except OSError:
+        return ""
+
+
+def main(argv) -> int:
+    if len(argv) < 2:
+        print(__doc__)
+        return 2
+    out = os.path.join(ROOT, "gpurun_out", argv[0])
+    os.makedirs(out, exist_ok=True)
+    pyt = [PY, "-u", "-m", "pytest", "-x", "-v", "--timeout", "120", "--timeout-method", "thread"]
+    for i, step in enumerate(argv[1:]):
+        kind, _, rest = step.partition(":")
+        if kind == "smoke":
+            rc = _run(out, "smoke.log", [PY, "-u", "-c", "import __graft_entry__ as g; g.smoke()"], 300)
+            print(_tail(os.path.join(out, "smoke.log"), 1))
+        elif kind == "tier":
+            rc = _run(out, "pytest_gpu.log", pyt + ["tests", "-m", "gpu"] + (rest.split(",") if rest else []), 1000)
+            print(_tail(os.path.join(out, "pytest_gpu.log"), 2))
+        elif kind == "pytest":
+            rc = _run(out, f"pytest_{i}.log", pyt + rest.split(","), 900)
+            print(_tail(os.path.join(out, f"pytest_{i}.log"), 2))
+        elif kind == "bench":
+            args = rest.split(",") if rest else []
+            rc = _run(out, f"bench_{i}.err", [PY, "-u", "bench.py"] + args, 600, stdout_file=f"bench_{i}.json")
+            print(_tail(os.path.join(out, f"bench_{i}.json"), 1)[:600])
+        elif kind == "prof":
+            name, _, args = rest.partition(":")
+            d = os.path.join(out, f"prof_{name}")
+            rc = _run(out, f"prof_{name}.log", ["rocprofv3", "--kernel-trace", "--stats", "-d", d, "-o", "t",
+                                               "--output-format", "csv", "--", PY, "bench.py"]
+                      + (args.split(",") if args else []), 600)
+            if rc == 0:
+                rc = _run(out, f"streams_{name}.log", [PY, "scripts/stream_summary.py", d,
+                                                       os.path.join(out, f"streams_{name}.md"), "cast_batch_kernel", "3"], 300)
+                for root, _, files in os.walk(d):
+                    for fn in files:
+                        p = os.path.join(root, fn)
+                        if fn.endswith("kernel_trace.csv") and os.path.getsize(p) > 40 << 20:
+                            os.remove(p)
+        elif kind == "mp":
+            parts = rest.split(":")
+            script, n = parts[0], parts[1]
+            env = dict(kv.split("=", 1) for kv in parts[2].split(";")) if len(parts) > 2 and parts[2] else {}
+            port = str(29500 + (os.getpid() + i) % 2000)
+            rc = _run(out, f"mp_{script}_{n}_{i}.log",
+                      [PY, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+                       "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join("tests", "mp", script)],
+                      500, env=env)
+            print(_tail(os.path.join(out, f"mp_{script}_{n}_{i}.log"), 6))
+        elif kind == "py":
+            f, _, args = rest.partition(":")
+            rc = _run(out, f"py_{i}.log", [PY, "-u", f] + (args.split(",") if args else []), 600)
+            print(_tail(os.path.join(out, f"py_{i}.log"), 8))
+        else:
+            print(f"[gpu.py] unknown step {step!r}")
+            return 2
+        if rc != 0:
+            print(f"[gpu.py] STOP after {step!r} (rc={rc})", flush=True)
+            return rc if rc > 0 else 1
+    print("[gpu.py] ALL OK", flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main(sys.argv[1:]))

@@ -63,3 +63,26 @@ def test_stuck_server_times_out():
     assert any("MPIT_PS_TIMEOUT_S" in o for o in outs), outs
     assert not any("should not get here" in o for o in outs)
     assert dt < 60, dt
+
+
+def _run_barrier_sleep(env_extra, n=2, timeout=90):
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = {k: v for k, v in os.environ.items() if k != "MPIT_WAIT_TIMEOUT_S"}
+        env.update(RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), MPIT_CPU_ONLY="1", PYTHONPATH=ROOT, **env_extra)
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "mp", "barrier_sleep.py")], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    outs = [p.communicate(timeout=timeout)[0] for p in procs]
+    return [p.returncode for p in procs], outs
+
+
+def test_long_barrier_has_no_default_deadline():
+    """a rank legitimately waiting in Barrier longer than any deadline must
+    not kill the job by default (MPI blocks without one); the deadline is opt-in."""
+    rcs, outs = _run_barrier_sleep({"T_SLEEP": "4"})
+    assert rcs == [0, 0], (rcs, outs)
+    assert all("barrier passed" in o for o in outs), outs
+    rcs, outs = _run_barrier_sleep({"T_SLEEP": "6", "MPIT_WAIT_TIMEOUT_S": "1"})
+    assert rcs[0] != 0 and "MPIT_WAIT_TIMEOUT_S" in outs[0], (rcs, outs)

@@ -171,6 +171,20 @@ def main(argv=None) -> int:
     W = mp.COMM_WORLD()
     amp = a.dtype == "bf16"
     tr = _make(a, mp_train, amp, a.topology, a.servers, 0)
+    preflight = None
+    if world > 1 and (tr.pc is not None or tr.ps_server is not None):
+        # every (worker, server) data path exercised once BEFORE the timed region: peer
+        # access per pair, one pull of every shard, exact bit-sums against the owning server
+        # (asyncsgd/ptest.lua's ping-pong before training). A broken pair ends the run here,
+        # named, instead of surfacing as a wrong ps_check after timing.
+        preflight = tr.preflight()
+        if not preflight["ok"]:
+            if W.Get_rank() == 0:
+                print(f"bench.py: pre-flight failed: no peer access {preflight['no_peer']}, pulled shard bits "
+                      f"differ for (worker, server) {preflight['mismatches']}; devices {preflight['devices']}",
+                      file=sys.stderr, flush=True)
+            mp.Finalize()
+            return 3
     secs, loss = mp_train.timed_steps(tr, a.steps, a.warmup)
     nworkers = len(tr.cranks)
     shape = INPUT_SHAPES.get(a.model, (3, 224, 224))
@@ -234,7 +248,7 @@ def main(argv=None) -> int:
                        "master_weights": "fp32", "loss_last": lossv, "defer_ps_wait": a.defer_ps_wait},
             "fp32_gemm": _fp32_gemm() if not (tr.on_gpu and amp) else None,
             "world": st.world, "shared_devices": st.shared_devices, "devices": devices, "rccl": rccl,
-            "ps_check": check,
+            "ps_check": check, "preflight": preflight,
             **({"emulate_shards": a.emulate_shards} if a.emulate_shards > 1 else {}),
             "secondary": secondary,
             "secondary_s": round(time.perf_counter() - t_sec, 2),

@@ -55,7 +55,11 @@ PSServer::PSServer(Engine& eng, int ps_id, Window& rx, Window& tx, std::vector<i
   if (const char* e = std::getenv("MPIT_PS_FAULT")) {
     const std::string f(e);
     const std::string kind = f.substr(0, f.find(':'));
-    fault_kind_ = kind == "grad" ? 1 : kind == "pull" ? 2 : kind == "param" ? 3 : kind == "drop" ? 4 : 0;
+    fault_kind_ = kind == "grad" ? 1 : kind == "pull" ? 2 : kind == "param" ? 3 : kind == "drop" ? 4
+                  : kind == "badpull" ? 5 : 0;
+    // badpull: every pull this server serves to client MPIT_PS_FAULT_CLIENT arrives with a
+    // corrupted first word (a broken (worker, server) data path for the pre-flight check)
+    if (const char* c = std::getenv("MPIT_PS_FAULT_CLIENT")) fault_client_ = std::atoi(c);
     if (f.find(':') != std::string::npos) fault_at_ = std::max(1, std::atoi(f.c_str() + f.find(':') + 1));
     if (const char* r = std::getenv("MPIT_PS_FAULT_RANK"))
       if (std::atoi(r) != eng_.rank()) fault_kind_ = 0;
@@ -68,8 +72,15 @@ PSServer::PSServer(Engine& eng, int ps_id, Window& rx, Window& tx, std::vector<i
     hipp(hipDeviceGetStreamPriorityRange(&lo, &hi), "priority range");
     hipp(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi), "server stream");
     if (datapath_ == 2) {
+      // link streams: at most 2 by default (MPIT_PS_LINK_STREAMS=k overrides), shared
+      // round-robin by the clients. A co-located N=8 process already holds the compute,
+      // priority, side, server, engine and RCCL streams; one link stream per client would
+      // put 7 more on the 4 hardware queues a process gets (GPU_MAX_HW_QUEUES), and queue
+      // oversubscription is what collapsed the 8-rank rehearsal
+      // (profiles/collapse_8rank_1gpu_r03.md). The per-client events keep every client's
+      // inbox / update / outbox order whatever stream it shares.
       const size_t nc = clients_.size();
-      size_t nl = nc;
+      size_t nl = std::min<size_t>(nc, 2);
       if (const char* e = std::getenv("MPIT_PS_LINK_STREAMS"))
         if (std::atoi(e) > 0) nl = std::min(nc, size_t(std::atoi(e)));
       cstream_.resize(std::max<size_t>(nl, 1));
@@ -426,6 +437,7 @@ void PSServer::do_pull(int c, Sub sb) {
     hipp(hipEventRecord(ev_up_[size_t(ci)], stream_), "record snapshot");
     hipp(hipStreamWaitEvent(cs, ev_up_[size_t(ci)], 0), "link waits snapshot");
     hipp(hipMemcpyAsync(dst, out, size_t(sb.n) * 4, hipMemcpyDefault, cs), "param push (link)");
+    if (fault_kind_ == 5 && c == fault_client_) hipp(hipMemsetAsync(dst, 0x7f, 4, cs), "injected bad pull");
     hipp(hipEventRecord(ev_out_[size_t(ci)], cs), "record outbox sent");
     {
       std::lock_guard<std::mutex> g(mu_);
@@ -435,6 +447,11 @@ void PSServer::do_pull(int c, Sub sb) {
     return;
   }
   copy_out(c, sb);
+  if (fault_kind_ == 5 && c == fault_client_ && sb.n > 0) {
+    uint8_t* dst = reinterpret_cast<uint8_t*>(rx_.remote_ptr(member_of(c))) + (off_ + sb.o) * 4;
+    if (device_) hipp(hipMemsetAsync(dst, 0x7f, 4, stream_), "injected bad pull");
+    else std::memset(dst, 0x7f, 4);
+  }
   {
     std::lock_guard<std::mutex> g(mu_);
     ++stats_.pulls;

@@ -180,7 +180,7 @@ class PSServer {
   // fault injection (tests of the fail-fast path): MPIT_PS_FAULT=grad|pull|param[:N] throws
   // in the Nth such request, drop[:N] silently ignores gradient pushes from the Nth on;
   // MPIT_PS_FAULT_RANK=r limits it to the server on rank r
-  int fault_kind_ = 0, fault_at_ = 1;
+  int fault_kind_ = 0, fault_at_ = 1, fault_client_ = -1;
   std::atomic<int> fault_seen_{0};
   std::atomic<int> stopped_{0};
   std::atomic<int64_t> version_{0};

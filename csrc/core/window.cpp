@@ -128,7 +128,14 @@ void Window::connect(const std::vector<std::string>& blobs, const std::vector<in
     if (!r.device) {
       r.ptr = static_cast<uint8_t*>(r.map) + kCtl;
     } else if (b.bytes > 0 && eng_.device() >= 0) {
-      r.ptr = static_cast<uint8_t*>(eng_.open_ipc(b.world_rank, b.handle)) + b.offset;
+      try {
+        r.ptr = static_cast<uint8_t*>(eng_.open_ipc(b.world_rank, b.handle)) + b.offset;
+      } catch (const std::exception& e) {
+        // name the pair: which rank (device) could not map whose window (device)
+        throw std::runtime_error("mpit: rank " + std::to_string(eng_.rank()) + " (device " +
+                                 std::to_string(eng_.device()) + ") could not map window " + std::to_string(id_) +
+                                 " of rank " + std::to_string(b.world_rank) + ": " + e.what());
+      }
     }
   }
 }

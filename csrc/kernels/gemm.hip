@@ -2081,35 +2081,43 @@ static bool gemm_log() {
 // group size (M-tiles) and ticket set of a folded BN finalize: <= kFoldMaxGroups groups of
 // >= 16 M-tiles. Ticket counters are reset to zero by their last user, so a set is free
 // once its launch retired — guaranteed only for launches of the SAME stream (stream
-// order). Each (device, stream) therefore owns its own group of kFoldPerStream sets and
-// rotates within it; two folded GEMMs in flight on different streams never share a set.
+// order). Each (device, stream) therefore owns its own kFoldPerStream sets (the first
+// kFoldStreams streams of a device in the static table, later ones in a zeroed allocation
+// of their own: no process-lifetime cap on the streams a process may fold from, e.g. one
+// priority stream per Trainer) and rotates within them; two folded GEMMs in flight on
+// different streams never share a set.
 static void fold_plan(EpiArgs& ep, int dev, hipStream_t s, int64_t mtn, int ntn) {
   const int64_t fg = std::max<int64_t>(16, (mtn + kFoldMaxGroups - 1) / kFoldMaxGroups);
   const int64_t ngr = (mtn + fg - 1) / fg;
   if (int64_t(ntn) * (ngr + 1) > kFoldMax) throw std::invalid_argument("gemm_nt: BN fold ticket table too small");
   struct Group {
-    int index;
+    uint32_t* sets;  // kFoldPerStream * kFoldMax counters
     uint32_t next;
   };
   static std::mutex mu;
   static std::map<std::pair<int, hipStream_t>, Group> groups;
-  static std::map<int, int> used;  // groups handed out per device
-  uint32_t slot;
+  static std::map<int, int> used;  // static-table groups handed out per device
+  uint32_t* set = nullptr;
   {
     std::lock_guard<std::mutex> g(mu);
     auto it = groups.find({dev, s});
     if (it == groups.end()) {
       int& u = used[dev];
-      if (u >= kFoldStreams)
-        throw std::runtime_error("gemm_nt: the BN finalize fold was used from more than " +
-                                 std::to_string(kFoldStreams) + " streams of one device (MPIT_BN_FOLD=0 disables it)");
-      it = groups.emplace(std::make_pair(dev, s), Group{u++, 0}).first;
+      uint32_t* sets = nullptr;
+      if (u < kFoldStreams) {
+        uint32_t* base = nullptr;
+        hip_check(hipGetSymbolAddress(reinterpret_cast<void**>(&base), HIP_SYMBOL(g_fold_tickets)), "fold ticket symbol");
+        sets = base + size_t(u++) * kFoldPerStream * kFoldMax;
+      } else {
+        const size_t bytes = size_t(kFoldPerStream) * kFoldMax * sizeof(uint32_t);
+        hip_check(hipMalloc(reinterpret_cast<void**>(&sets), bytes), "fold ticket sets");
+        hip_check(hipMemsetAsync(sets, 0, bytes, s), "fold ticket sets zero");
+      }
+      it = groups.emplace(std::make_pair(dev, s), Group{sets, 0}).first;
     }
-    slot = uint32_t(it->second.index * kFoldPerStream) + (it->second.next++ % kFoldPerStream);
+    set = it->second.sets + size_t(it->second.next++ % kFoldPerStream) * kFoldMax;
   }
-  uint32_t* base = nullptr;
-  hip_check(hipGetSymbolAddress(reinterpret_cast<void**>(&base), HIP_SYMBOL(g_fold_tickets)), "fold ticket symbol");
-  ep.ftick = base + size_t(slot) * kFoldMax;
+  ep.ftick = set;
   ep.fgroup = int(fg);
 }
 

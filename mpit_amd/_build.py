@@ -89,11 +89,42 @@ def _jobs(san=None, build_dir=BUILD) -> list[tuple[str, str, list[str]]]:
     return jobs
 
 
-def _stale(src: str, obj: str, hdr_mtime: float) -> bool:
+_INC = None
+
+
+def _includes(path: str, seen: set) -> set:
+    """Project headers ``path`` includes, transitively (``#include "..."`` resolved against the
+    including file's directory, then csrc/)."""
+    global _INC
+    if _INC is None:
+        import re
+
+        _INC = re.compile(r'^\s*#\s*include\s*"([^"]+)"', re.M)
+    try:
+        with open(path) as f:
+            text = f.read()
+    except OSError:
+        return seen
+    for name in _INC.findall(text):
+        for base in (os.path.dirname(path), CSRC):
+            h = os.path.normpath(os.path.join(base, name))
+            if os.path.exists(h):
+                if h not in seen:
+                    seen.add(h)
+                    _includes(h, seen)
+                break
+    return seen
+
+
+def _stale(src: str, obj: str, hdr_mtime: float = None) -> bool:
+    """An object is stale when its source or any project header it includes (transitively) is
+    newer: editing csrc/core/ps.h no longer recompiles the kernel files."""
     if not os.path.exists(obj):
         return True
     t = os.path.getmtime(obj)
-    return os.path.getmtime(src) > t or hdr_mtime > t
+    deps = _includes(src, set())
+    newest = max([os.path.getmtime(src)] + [os.path.getmtime(h) for h in deps])
+    return newest > t
 
 
 def build(jobs: int = 8, force: bool = False, verbose: bool = False, sanitize: str = None) -> str:

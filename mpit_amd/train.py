@@ -391,6 +391,35 @@ class Trainer:
         return {"ok": not bad and len(srv) == len(self.sranks), "shards": len(self.sranks),
                 "workers": sum(v["worker"] is not None for v in allv), "mismatches": bad[:8]}
 
+    def preflight(self) -> dict:
+        """Collective check of every (worker, server) data path BEFORE a timed run (bench.py),
+        the job's version of the reference's per-rank-GPU ping-pong (asyncsgd/ptest.lua:40-65):
+
+        * ``devices``: each rank's GPU, and ``no_peer``: the (worker, server) pairs on distinct
+          devices without peer access (a server's kernels read the worker's gradient window
+          and write its parameter window directly); the windows themselves were mapped when
+          the PS started — a mapping failure has already raised naming its pair
+          (csrc/core/window.cpp);
+        * the pull check of :meth:`verify_ps`: every worker pulls every shard once and the
+          exact bit-sums must equal the owning server's; ``mismatches`` names the failing
+          (worker, server) pairs.
+
+        Returns the report on every rank; ``ok`` is False when any pair failed."""
+        W = COMM_WORLD()
+        dev = self.device.index if self.on_gpu else None
+        devs = W.allgather_obj(dev)
+        no_peer = []
+        if self.on_gpu and self.pc is not None:
+            for s in self.sranks:
+                d = devs[s]
+                if d is not None and d != dev and not torch.cuda.can_device_access_peer(d, dev):
+                    no_peer.append((self.rank, s))
+        no_peer = sorted({tuple(p) for lst in W.allgather_obj(no_peer) for p in lst})
+        chk = self.verify_ps() if (self.pc is not None or self.ps_server is not None) else {"ok": True, "mismatches": []}
+        bad = [tuple(p) for p in chk.get("mismatches", [])]
+        return {"ok": bool(chk["ok"]) and not no_peer, "devices": devs, "no_peer": [list(p) for p in no_peer],
+                "mismatches": [list(p) for p in bad], "shards": chk.get("shards"), "workers": chk.get("workers")}
+
     def retire_pushes(self):
         """Wait until every push / pull this worker issued has been acknowledged (EAMSGD
         deliberately leaves its last elastic push in flight, asyncsgd/optim-eamsgd.lua:65-67)."""

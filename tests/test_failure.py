@@ -86,3 +86,19 @@ def test_long_barrier_has_no_default_deadline():
     assert all("barrier passed" in o for o in outs), outs
     rcs, outs = _run_barrier_sleep({"T_SLEEP": "6", "MPIT_WAIT_TIMEOUT_S": "1"})
     assert rcs[0] != 0 and "MPIT_WAIT_TIMEOUT_S" in outs[0], (rcs, outs)
+
+
+def test_preflight_names_the_broken_pair():
+    """Verdict r03 #5: the pre-timing check pulls every shard once and names the (worker,
+    server) pair whose pulled bits differ from the server's; a healthy job reports ok."""
+    import re
+
+    from mp_util import run_ranks
+
+    out = run_ranks("preflight_check.py", 3, {"MPIT_CPU_ONLY": "1"}, timeout=240)
+    rep = eval(re.search(r"PREFLIGHT (.*)", out).group(1))
+    assert rep["ok"] and rep["mismatches"] == [] and rep["shards"] == 3 and rep["workers"] == 3, rep
+    out = run_ranks("preflight_check.py", 3, {"MPIT_CPU_ONLY": "1", "MPIT_PS_FAULT": "badpull",
+                                              "MPIT_PS_FAULT_RANK": "1", "MPIT_PS_FAULT_CLIENT": "2"}, timeout=240)
+    rep = eval(re.search(r"PREFLIGHT (.*)", out).group(1))
+    assert not rep["ok"] and rep["mismatches"] == [[2, 1]], rep

@@ -131,7 +131,10 @@ def main(argv=None) -> int:
     ap.add_argument("--lr", type=float, default=0.05,
                     help="learning rate; Downpour divides it by the number of workers (every worker's "
                          "push is applied, so N pushes per round then add up to one step of this size)")
-    ap.add_argument("--datapath", type=int, default=2)
+    ap.add_argument("--datapath", type=int, default=2,
+                    help="PS data plane: 2 = one-sided xGMI peer copies on per-client link streams (default), "
+                         "0 = fused remote kernel, 1 = serial SDMA, 3 = two-sided RCCL send/recv (the automatic "
+                         "fallback when the pre-flight check finds a broken peer mapping)")
     ap.add_argument("--staleness", type=int, default=-1, help="bounded staleness (SSP); -1 = fully async")
     ap.add_argument("--wire", default="fp32", choices=["fp32", "bf16"], help="EASGD elastic-difference dtype")
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
@@ -170,14 +173,32 @@ def main(argv=None) -> int:
     mp.Init()
     W = mp.COMM_WORLD()
     amp = a.dtype == "bf16"
-    tr = _make(a, mp_train, amp, a.topology, a.servers, 0)
+    from mpit_amd.parallel.ps import PSMapError
+
+    fallback = None
+    try:
+        tr = _make(a, mp_train, amp, a.topology, a.servers, 0)
+    except PSMapError as e:  # a peer window could not be mapped (every rank raised it)
+        if a.datapath == 3:
+            raise
+        fallback = {"from_datapath": a.datapath, "reason": f"window mapping: {e}"}
+        a.datapath = 3
+        tr = _make(a, mp_train, amp, a.topology, a.servers, 2)
     preflight = None
     if world > 1 and (tr.pc is not None or tr.ps_server is not None):
         # every (worker, server) data path exercised once BEFORE the timed region: peer
         # access per pair, one pull of every shard, exact bit-sums against the owning server
-        # (asyncsgd/ptest.lua's ping-pong before training). A broken pair ends the run here,
-        # named, instead of surfacing as a wrong ps_check after timing.
+        # (asyncsgd/ptest.lua's ping-pong before training). A broken one-sided path switches
+        # the job to the two-sided RCCL data plane (datapath 3, csrc/core/link.h) and checks
+        # again; a pair still broken ends the run here, named, before any timing.
         preflight = tr.preflight()
+        if not preflight["ok"] and a.datapath != 3:
+            fallback = {"from_datapath": a.datapath, "reason": f"pre-flight: no peer access {preflight['no_peer']}, "
+                                                                 f"pulled shard bits differ {preflight['mismatches']}"}
+            tr.stop()
+            a.datapath = 3
+            tr = _make(a, mp_train, amp, a.topology, a.servers, 2)
+            preflight = tr.preflight()
         if not preflight["ok"]:
             if W.Get_rank() == 0:
                 print(f"bench.py: pre-flight failed: no peer access {preflight['no_peer']}, pulled shard bits "
@@ -185,6 +206,8 @@ def main(argv=None) -> int:
                       file=sys.stderr, flush=True)
             mp.Finalize()
             return 3
+        if fallback is not None:
+            preflight["fallback"] = fallback
     secs, loss = mp_train.timed_steps(tr, a.steps, a.warmup)
     nworkers = len(tr.cranks)
     shape = INPUT_SHAPES.get(a.model, (3, 224, 224))
@@ -245,7 +268,8 @@ def main(argv=None) -> int:
             "data": f"synthetic (random images {shape[0]}x{shape[1]}x{shape[2]}, random labels, random-init weights)",
             "config": {"model": a.model, "global_batch": a.batch * nworkers, "seq_len": None, "image_size": shape[-1],
                        "parallelism": par, "optimizer": a.optimizer, "su": a.su, "per_gpu_batch": a.batch,
-                       "master_weights": "fp32", "loss_last": lossv, "defer_ps_wait": a.defer_ps_wait},
+                       "master_weights": "fp32", "loss_last": lossv, "defer_ps_wait": a.defer_ps_wait,
+                       "datapath": a.datapath},
             "fp32_gemm": _fp32_gemm() if not (tr.on_gpu and amp) else None,
             "world": st.world, "shared_devices": st.shared_devices, "devices": devices, "rccl": rccl,
             "ps_check": check, "preflight": preflight,

@@ -354,12 +354,13 @@ PYBIND11_MODULE(_mpit, m) {
            py::keep_alive<1, 2>())
       .def("blob", [](Window& w) { return py::bytes(w.blob()); })
       .def("connect",
-           [](Window& w, std::vector<py::bytes> blobs, std::vector<int> ranks) {
+           [](Window& w, std::vector<py::bytes> blobs, std::vector<int> ranks, bool map_remote) {
              std::vector<std::string> b;
              for (auto& x : blobs) b.push_back(std::string(x));
              py::gil_scoped_release r;
-             w.connect(b, ranks);
-           })
+             w.connect(b, ranks, map_remote);
+           },
+           py::arg("blobs"), py::arg("ranks"), py::arg("map_remote") = true)
       .def("unlink_names", &Window::unlink_names)
       .def_property_readonly("local_ptr", &Window::local_ptr)
       .def_property_readonly("bytes", &Window::bytes)
@@ -406,6 +407,7 @@ PYBIND11_MODULE(_mpit, m) {
       .def("set_counters", &PSServer::set_counters)
       .def("set_lr", &PSServer::set_lr)
       .def("sync", &PSServer::sync, py::call_guard<py::gil_scoped_release>())
+      .def("set_link", &PSServer::set_link, py::keep_alive<1, 2>())
       .def("stats", [](PSServer& s) {
         auto st = s.stats();
         return py::dict(py::arg("grads") = st.grads, py::arg("pulls") = st.pulls,
@@ -425,5 +427,24 @@ PYBIND11_MODULE(_mpit, m) {
       .def("wait", &PSClient::wait, py::call_guard<py::gil_scoped_release>())
       .def("test", &PSClient::test)
       .def("pending", &PSClient::pending)
-      .def("replies", &PSClient::replies);
+      .def("replies", &PSClient::replies)
+      .def("set_link", &PSClient::set_link, py::keep_alive<1, 2>());
+
+  py::class_<PsLink>(m, "PsLink")
+      .def(py::init<Engine&, int, std::vector<int>, std::vector<int>, bool>(), py::keep_alive<1, 2>())
+      .def_property_readonly("device", &PsLink::device)
+      .def("make_ids",
+           [](PsLink& l) {
+             py::list out;
+             for (auto& [c, id] : l.make_ids()) out.append(py::make_tuple(c, py::bytes(id)));
+             return out;
+           })
+      .def("connect",
+           [](PsLink& l, std::vector<std::tuple<int, int, py::bytes>> ids) {
+             std::vector<std::tuple<int, int, std::string>> v;
+             for (auto& [s, c, b] : ids) v.emplace_back(s, c, std::string(b));
+             py::gil_scoped_release r;
+             l.connect(v);
+           })
+      .def("stats", [](PsLink& l) { return py::dict(py::arg("bytes_sent") = l.bytes_sent(), py::arg("bytes_recv") = l.bytes_recv()); });
 }

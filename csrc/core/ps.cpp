@@ -57,8 +57,9 @@ PSServer::PSServer(Engine& eng, int ps_id, Window& rx, Window& tx, std::vector<i
     const std::string kind = f.substr(0, f.find(':'));
     fault_kind_ = kind == "grad" ? 1 : kind == "pull" ? 2 : kind == "param" ? 3 : kind == "drop" ? 4
                   : kind == "badpull" ? 5 : 0;
-    // badpull: every pull this server serves to client MPIT_PS_FAULT_CLIENT arrives with a
-    // corrupted first word (a broken (worker, server) data path for the pre-flight check)
+    // badpull: every one-sided pull (datapaths 0-2) this server serves to client
+    // MPIT_PS_FAULT_CLIENT arrives with a corrupted first word (a broken (worker, server)
+    // peer path for the pre-flight check; the two-sided datapath 3 stays intact)
     if (const char* c = std::getenv("MPIT_PS_FAULT_CLIENT")) fault_client_ = std::atoi(c);
     if (f.find(':') != std::string::npos) fault_at_ = std::max(1, std::atoi(f.c_str() + f.find(':') + 1));
     if (const char* r = std::getenv("MPIT_PS_FAULT_RANK"))
@@ -71,7 +72,7 @@ PSServer::PSServer(Engine& eng, int ps_id, Window& rx, Window& tx, std::vector<i
     int lo = 0, hi = 0;
     hipp(hipDeviceGetStreamPriorityRange(&lo, &hi), "priority range");
     hipp(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi), "server stream");
-    if (datapath_ == 2) {
+    if (datapath_ == 2 || datapath_ == 3) {
       // link streams: at most 2 by default (MPIT_PS_LINK_STREAMS=k overrides), shared
       // round-robin by the clients. A co-located N=8 process already holds the compute,
       // priority, side, server, engine and RCCL streams; one link stream per client would
@@ -128,6 +129,7 @@ void PSServer::finish_on(hipStream_t s, std::function<void()> then) {
 }
 
 void PSServer::start() {
+  if (datapath_ == 3 && !link_) throw std::invalid_argument("mpit: PS datapath 3 needs its link (set_link)");
   if (batch_ && device_ && (rule_.kind == 0 || rule_.kind == 1)) {
     fg_ = std::make_shared<FlushGate>();
     fg_->s = this;
@@ -142,7 +144,7 @@ void PSServer::start() {
 }
 
 bool PSServer::batchable(int c) const {
-  return fg_ && datapath_ != 1 && !pipelined(client_index(c), c);
+  return fg_ && datapath_ != 1 && !pipelined(client_index(c), c) && !messaged(client_index(c), c);
 }
 
 void PSServer::queue_grad(int c, bool pull, Sub sb) {
@@ -268,13 +270,24 @@ void PSServer::on_msg(const Msg& m) {
       break;
     case kTagParam: {
       const Sub sb = sub_of(m);
-      do_param(m.src, (m.aux0 & kPsFromRx) != 0, sb);
-      if (init_rank_ >= 0 && m.src == init_rank_ && (init_left_ -= sb.n) <= 0) {
-        init_rank_ = -1;
-        std::vector<Msg> later;
-        later.swap(backlog_);
-        for (auto& x : later) on_msg(x);
+      const bool init_piece = init_rank_ >= 0 && m.src == init_rank_;
+      auto init_done = [this, sb] {
+        if ((init_left_ -= sb.n) <= 0) {
+          init_rank_ = -1;
+          std::vector<Msg> later;
+          later.swap(backlog_);
+          for (auto& x : later) on_msg(x);
+        }
+      };
+      if (init_piece && !device_ && messaged(client_index(m.src), m.src)) {
+        // host link: the shard holds the initial parameters only once their message landed
+        TraceRange tr("ps_server_param");
+        maybe_fault(3);
+        param_msg(m.src, client_index(m.src), (m.aux0 & kPsFromRx) != 0, sb, init_done);
+        break;
       }
+      do_param(m.src, (m.aux0 & kPsFromRx) != 0, sb);
+      if (init_piece) init_done();
       break;
     }
     case kTagGrad:
@@ -385,6 +398,10 @@ void PSServer::apply_rule(const void* g, void* out, Sub sb, int ci) {
 void PSServer::do_param(int c, bool from_rx, Sub sb) {
   TraceRange tr("ps_server_param");
   maybe_fault(3);
+  if (messaged(client_index(c), c)) {
+    param_msg(c, client_index(c), from_rx, sb);
+    return;
+  }
   const int m = member_of(c);
   const Window& w = from_rx ? rx_ : tx_;  // rx is always fp32
   const bool bf = grad_bf16_ && !from_rx;
@@ -424,6 +441,10 @@ void PSServer::do_pull(int c, Sub sb) {
   TraceRange tr("ps_server_pull");
   maybe_fault(2);
   const int ci = client_index(c);
+  if (messaged(ci, c)) {
+    pull_msg(c, ci, sb);
+    return;
+  }
   if (pipelined(ci, c)) {
     // snapshot the piece in update order on stream_, push it over the client's link
     hipp(hipSetDevice(eng_.device()), "hipSetDevice");
@@ -475,6 +496,10 @@ void PSServer::do_grad(int c, bool pull, Sub sb) {
       for (auto x : clock_) mn = std::min(mn, x);
       defer_pull = clock_[size_t(ci)] - mn > staleness_;
     }
+  }
+  if (messaged(ci, c)) {
+    grad_msg(c, ci, pull, defer_pull, sb);
+    return;
   }
   if (!device_ && tx_.remote_device(m)) throw std::runtime_error("mpit: host server cannot read a device tx window");
   if (pipelined(ci, c)) {
@@ -541,6 +566,126 @@ void PSServer::do_grad(int c, bool pull, Sub sb) {
     if (pull && !defer_pull) reply(c, kTagSendParam);
   });
   release_deferred();
+}
+
+// ---- datapath 3: the shard's data as two-sided messages with a remote client (link.h) -----
+// Device: the same staging and stream choreography as the link-stream path of datapath 2,
+// with the peer copies replaced by RCCL recv / send on the client's link stream. Host (no
+// GPU): per-message buffers, each step a continuation once the previous one's transfer is
+// done (PsLink::then), in arrival order per client.
+
+void PSServer::grad_msg(int c, int ci, bool pull, bool defer_pull, Sub sb) {
+  const int64_t es = grad_bf16_ ? 2 : 4;
+  const bool push_back = pull && !defer_pull;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    ++stats_.grads;
+    if (push_back) ++stats_.pulls;
+    if (defer_pull) {
+      deferred_.push_back({c, sb});
+      ++stats_.deferred;
+    }
+  }
+  if (device_) {
+    hipp(hipSetDevice(eng_.device()), "hipSetDevice");
+    const size_t k = size_t(ci);
+    hipStream_t cs = link(ci);
+    uint8_t* in = stage_ + k * size_t(len_) * 8 + size_t(sb.o * es);
+    uint8_t* out = stage_ + k * size_t(len_) * 8 + size_t(len_) * 4 + size_t(sb.o) * 4;
+    link_->recv(c, true, in, sb.n * es, cs);
+    hipp(hipEventRecord(ev_in_[k], cs), "record inbox full");
+    hipp(hipStreamWaitEvent(stream_, ev_in_[k], 0), "update waits inbox");
+    if (push_back) hipp(hipStreamWaitEvent(stream_, ev_out_[k], 0), "update waits outbox free");
+    apply_rule(in, push_back ? out : nullptr, sb, ci);
+    hipp(hipEventRecord(ev_up_[k], stream_), "record update");
+    hipp(hipStreamWaitEvent(cs, ev_up_[k], 0), "link waits update");
+    if (push_back) {
+      link_->send(c, true, out, sb.n * 4, cs);
+      hipp(hipEventRecord(ev_out_[k], cs), "record outbox sent");
+    }
+    link_->then(c, true, cs, [this, c, push_back] {
+      reply(c, kTagGradTail);
+      if (push_back) reply(c, kTagSendParam);
+    });
+  } else {
+    auto in = std::make_shared<std::vector<uint8_t>>(size_t(sb.n * es));
+    link_->recv(c, true, in->data(), sb.n * es, nullptr);
+    link_->then(c, true, nullptr, [this, c, ci, sb, in, push_back] {
+      auto out = push_back ? std::make_shared<std::vector<uint8_t>>(size_t(sb.n) * 4) : nullptr;
+      apply_rule(in->data(), out ? out->data() : nullptr, sb, ci);
+      if (out) link_->send(c, true, out->data(), sb.n * 4, nullptr);
+      link_->then(c, true, nullptr, [this, c, out, push_back] {
+        reply(c, kTagGradTail);
+        if (push_back) reply(c, kTagSendParam);
+      });
+    });
+  }
+  release_deferred();
+}
+
+void PSServer::pull_msg(int c, int ci, Sub sb) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    ++stats_.pulls;
+  }
+  if (device_) {
+    hipp(hipSetDevice(eng_.device()), "hipSetDevice");
+    const size_t k = size_t(ci);
+    hipStream_t cs = link(ci);
+    uint8_t* out = stage_ + k * size_t(len_) * 8 + size_t(len_) * 4 + size_t(sb.o) * 4;
+    const uint8_t* src = static_cast<const uint8_t*>(p_) + sb.o * 4;
+    // the snapshot in update order on stream_, sent on the client's link stream
+    hipp(hipStreamWaitEvent(stream_, ev_out_[k], 0), "wait outbox free");
+    ew_update(kCopy, 0, eng_.device(), stream_, sb.n, {reinterpret_cast<uintptr_t>(out), reinterpret_cast<uintptr_t>(src)},
+              0u, {1.f});
+    hipp(hipEventRecord(ev_up_[k], stream_), "record snapshot");
+    hipp(hipStreamWaitEvent(cs, ev_up_[k], 0), "link waits snapshot");
+    link_->send(c, true, out, sb.n * 4, cs);
+    hipp(hipEventRecord(ev_out_[k], cs), "record outbox sent");
+    link_->then(c, true, cs, [this, c] { reply(c, kTagSendParam); });
+    return;
+  }
+  // host: snapshot once every earlier message of this client has been applied
+  link_->then(c, true, nullptr, [this, c, sb] {
+    auto out = std::make_shared<std::vector<uint8_t>>(size_t(sb.n) * 4);
+    std::memcpy(out->data(), static_cast<const uint8_t*>(p_) + sb.o * 4, size_t(sb.n) * 4);
+    link_->send(c, true, out->data(), sb.n * 4, nullptr);
+    link_->then(c, true, nullptr, [this, c, out] { reply(c, kTagSendParam); });
+  });
+}
+
+void PSServer::param_msg(int c, int ci, bool from_rx, Sub sb, std::function<void()> after) {
+  const bool bf = grad_bf16_ && !from_rx;
+  const int64_t es = bf ? 2 : 4;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    ++stats_.param_pushes;
+  }
+  if (device_) {
+    hipp(hipSetDevice(eng_.device()), "hipSetDevice");
+    const size_t k = size_t(ci);
+    hipStream_t cs = link(ci);
+    uint8_t* in = stage_ + k * size_t(len_) * 8 + size_t(sb.o * es);
+    link_->recv(c, true, in, sb.n * es, cs);
+    hipp(hipEventRecord(ev_in_[k], cs), "record inbox full");
+    hipp(hipStreamWaitEvent(stream_, ev_in_[k], 0), "copy waits inbox");
+    ew_update(kCopy, 0, eng_.device(), stream_, sb.n,
+              {reinterpret_cast<uintptr_t>(static_cast<uint8_t*>(p_) + sb.o * 4), reinterpret_cast<uintptr_t>(in)},
+              bf ? 2u : 0u, {1.f});
+    hipp(hipEventRecord(ev_up_[k], stream_), "record copy");
+    hipp(hipStreamWaitEvent(cs, ev_up_[k], 0), "link waits copy");
+    finish([this, c] { reply(c, kTagParamTail); });
+    return;
+  }
+  auto in = std::make_shared<std::vector<uint8_t>>(size_t(sb.n * es));
+  link_->recv(c, true, in->data(), sb.n * es, nullptr);
+  link_->then(c, true, nullptr, [this, c, sb, in, bf, after] {
+    ew_update(kCopy, 0, -1, nullptr, sb.n,
+              {reinterpret_cast<uintptr_t>(static_cast<uint8_t*>(p_) + sb.o * 4), reinterpret_cast<uintptr_t>(in->data())},
+              bf ? 2u : 0u, {1.f});
+    reply(c, kTagParamTail);
+    if (after) after();
+  });
 }
 
 void PSServer::release_deferred() {
@@ -633,6 +778,11 @@ PSClient::PSClient(Engine& eng, int ps_id, std::vector<int> servers, std::vector
 
 PSClient::~PSClient() {
   if (hook_ >= 0) eng_.remove_hook(hook_);
+  if (lstream_) {
+    hipSetDevice(eng_.device());
+    hipStreamSynchronize(lstream_);
+    hipStreamDestroy(lstream_);
+  }
   // gates never retired (the client went away with pushes queued): release their events
   // and their pending count, or deep parking stays disabled for the rest of the process
   std::deque<GateQueue::Gate> left;
@@ -676,15 +826,54 @@ void PSClient::gate(hipStream_t s, std::function<void()> send) {
 }
 
 // the message of shard entry k: whole-shard entries carry no piece (aux2 = 0)
+void PSClient::set_link(PsLink* l, uintptr_t rx, uintptr_t tx, int tx_es) {
+  link_ = l;
+  rx_ = reinterpret_cast<uint8_t*>(rx);
+  tx_ = reinterpret_cast<uint8_t*>(tx);
+  tx_es_ = tx_es;
+  if (l && l->device() && !lstream_) {
+    hipp(hipSetDevice(eng_.device()), "hipSetDevice");
+    int lo = 0, hi = 0;
+    hipp(hipDeviceGetStreamPriorityRange(&lo, &hi), "priority range");
+    hipp(hipStreamCreateWithPriority(&lstream_, hipStreamNonBlocking, hi), "client link stream");
+  }
+}
+
+int PSClient::link_recvs(int k, int tag, int64_t flags) const {
+  if (!link_ || servers_[size_t(k)] == eng_.rank()) return 0;
+  return (tag == kTagHeader || (tag == kTagGrad && (flags & kPsWithPull))) ? 1 : 0;
+}
+
+void PSClient::local_done() {
+  pending_.fetch_sub(1, std::memory_order_seq_cst);
+  reply_seq_.fetch_add(1, std::memory_order_seq_cst);
+  futex_wake_all(&reply_seq_, false);
+}
+
 void PSClient::send_entry(int k, int tag, int64_t flags) {
-  const bool whole = std::count(servers_.begin(), servers_.end(), servers_[size_t(k)]) == 1;
-  eng_.send_am(servers_[size_t(k)], ps_am_id(ps_id_, tag), nullptr, 0, flags, whole ? 0 : offs_[size_t(k)],
-               whole ? 0 : lens_[size_t(k)]);
+  const int srv = servers_[size_t(k)];
+  const bool whole = std::count(servers_.begin(), servers_.end(), srv) == 1;
+  eng_.send_am(srv, ps_am_id(ps_id_, tag), nullptr, 0, flags, whole ? 0 : offs_[size_t(k)], whole ? 0 : lens_[size_t(k)]);
+  if (!link_ || srv == eng_.rank()) return;
+  // datapath 3: the entry's data right behind its control message, in call order (link.h)
+  const int64_t o = offs_[size_t(k)], n = lens_[size_t(k)];
+  if (tag == kTagGrad) {
+    link_->send(srv, false, tx_ + o * tx_es_, n * tx_es_, lstream_);
+  } else if (tag == kTagParam) {
+    if (flags & kPsFromRx) link_->send(srv, false, rx_ + o * 4, n * 4, lstream_);
+    else link_->send(srv, false, tx_ + o * tx_es_, n * tx_es_, lstream_);
+  }
+  if (link_recvs(k, tag, flags)) {
+    link_->recv(srv, false, rx_ + o * 4, n * 4, lstream_);
+    link_->then(srv, false, lstream_, [this] { local_done(); });  // the shard has landed in rx
+  }
 }
 
 void PSClient::send_grad(hipStream_t s, bool with_pull) {
   const int64_t n = int64_t(servers_.size());
-  pending_.fetch_add(with_pull ? 2 * n : n);
+  int64_t extra = 0;
+  for (int k = 0; k < int(n); ++k) extra += link_recvs(k, kTagGrad, with_pull ? kPsWithPull : 0);
+  pending_.fetch_add((with_pull ? 2 * n : n) + extra);
   gate(s, [this, with_pull, n] {
     for (int k = 0; k < int(n); ++k) send_entry(k, kTagGrad, with_pull ? kPsWithPull : 0);
   });
@@ -692,13 +881,15 @@ void PSClient::send_grad(hipStream_t s, bool with_pull) {
 
 void PSClient::send_grad_to(hipStream_t s, int k, bool with_pull) {
   if (k < 0 || k >= int(servers_.size())) throw std::out_of_range("PSClient::send_grad_to: bad shard");
-  pending_.fetch_add(with_pull ? 2 : 1);
+  pending_.fetch_add((with_pull ? 2 : 1) + link_recvs(k, kTagGrad, with_pull ? kPsWithPull : 0));
   gate(s, [this, k, with_pull] { send_entry(k, kTagGrad, with_pull ? kPsWithPull : 0); });
 }
 
 void PSClient::recv_param(hipStream_t s) {
   const int n = int(servers_.size());
-  pending_.fetch_add(n);
+  int64_t extra = 0;
+  for (int k = 0; k < n; ++k) extra += link_recvs(k, kTagHeader, 0);
+  pending_.fetch_add(n + extra);
   // ordered behind any gated push of this client
   gate(s, [this, n] {
     for (int k = 0; k < n; ++k) send_entry(k, kTagHeader, 0);

@@ -39,6 +39,7 @@
 #include <vector>
 
 #include "engine.h"
+#include "link.h"
 #include "window.h"
 
 namespace mpit {
@@ -106,6 +107,8 @@ class PSServer {
   }
   void set_lr(float lr);
   void sync();  // wait for all queued server work
+  // datapath 3: the instance's two-sided data plane (csrc/core/link.h); set before start()
+  void set_link(PsLink* l) { link_ = l; }
 
  private:
   void on_msg(const Msg& m);
@@ -138,6 +141,12 @@ class PSServer {
   std::shared_ptr<FlushGate> fg_;
   int hook_ = -1;
   void copy_out(int c, Sub sb);
+  // datapath 3: the shard's data with remote client c as RCCL / host messages (link.h)
+  PsLink* link_ = nullptr;
+  bool messaged(int ci, int c) const { return datapath_ == 3 && ci >= 0 && c != eng_.rank(); }
+  void grad_msg(int c, int ci, bool pull, bool defer_pull, Sub sb);
+  void pull_msg(int c, int ci, Sub sb);
+  void param_msg(int c, int ci, bool from_rx, Sub sb, std::function<void()> after = nullptr);
   void reply(int c, int tag);
   void finish(std::function<void()> then);
   void release_deferred();
@@ -212,8 +221,11 @@ class PSClient {
   void send_param(hipStream_t s, bool from_rx = false);
   void stop();
   // until every outstanding reply arrived (GIL released); raises after MPIT_PS_TIMEOUT_S
-  // (default 300 s, 0 = never) with the number of replies still missing
+  // (default 0 = never) with the number of replies still missing
   void wait();
+  // datapath 3: shard data as messages over `l` (link.h) from / into this client's own
+  // buffers: rx (fp32 parameters, pulls land here), tx (push window, tx_es bytes / element)
+  void set_link(PsLink* l, uintptr_t rx, uintptr_t tx, int tx_es);
   bool test() const { return pending_.load() == 0; }
   int64_t pending() const { return pending_.load(); }
   int64_t replies() const { return replies_.load(); }
@@ -223,6 +235,14 @@ class PSClient {
   void gate(hipStream_t s, std::function<void()> send);
   void send_entry(int k, int tag, int64_t flags);
   void on_reply(const Msg& m);
+  void local_done();
+  // the entry's pull lands through the link (a completion of our own to wait for)
+  int link_recvs(int k, int tag, int64_t flags) const;
+  PsLink* link_ = nullptr;
+  uint8_t* rx_ = nullptr;
+  uint8_t* tx_ = nullptr;
+  int tx_es_ = 4;
+  hipStream_t lstream_ = nullptr;  // device: the client's own link stream
   Engine& eng_;
   std::shared_ptr<GateQueue> gq_;
   int hook_ = -1;

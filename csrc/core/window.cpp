@@ -103,7 +103,7 @@ std::string Window::blob() const {
   return std::string(reinterpret_cast<const char*>(&b), sizeof(b));
 }
 
-void Window::connect(const std::vector<std::string>& blobs, const std::vector<int>& world_ranks) {
+void Window::connect(const std::vector<std::string>& blobs, const std::vector<int>& world_ranks, bool map_remote) {
   remote_.assign(blobs.size(), Remote{});
   held_.assign(blobs.size(), 0);
   for (size_t m = 0; m < blobs.size(); ++m) {
@@ -127,7 +127,7 @@ void Window::connect(const std::vector<std::string>& blobs, const std::vector<in
     r.ctl = static_cast<WinCtl*>(r.map);
     if (!r.device) {
       r.ptr = static_cast<uint8_t*>(r.map) + kCtl;
-    } else if (b.bytes > 0 && eng_.device() >= 0) {
+    } else if (b.bytes > 0 && eng_.device() >= 0 && map_remote) {
       try {
         r.ptr = static_cast<uint8_t*>(eng_.open_ipc(b.world_rank, b.handle)) + b.offset;
       } catch (const std::exception& e) {

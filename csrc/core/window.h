@@ -39,7 +39,9 @@ class Window {
 
   // this rank's exposure blob (exchange it among the members, then connect())
   std::string blob() const;
-  void connect(const std::vector<std::string>& blobs, const std::vector<int>& world_ranks);
+  // map_remote=false: leave other ranks' device windows unmapped (PS datapath 3 moves the
+  // shard data as messages and never touches a peer allocation)
+  void connect(const std::vector<std::string>& blobs, const std::vector<int>& world_ranks, bool map_remote = true);
   void unlink_names();  // after every member connected
 
   uintptr_t local_ptr() const { return reinterpret_cast<uintptr_t>(local_); }

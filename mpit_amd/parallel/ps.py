@@ -112,11 +112,15 @@ class ServerOpt:
 
 # ------------------------------------------------------------------ shared group state
 
+class PSMapError(RuntimeError):
+    """A member could not map another member's device window (raised on every member)."""
+
+
 class _Group:
     """Windows shared by all members (servers ∪ clients) of one PS instance."""
 
     def __init__(self, ps_id: int, servers: Sequence[int], clients: Sequence[int], plong: int,
-                 rx: Optional[torch.Tensor], tx: Optional[torch.Tensor], grad_dtype=torch.float32):
+                 rx: Optional[torch.Tensor], tx: Optional[torch.Tensor], grad_dtype=torch.float32, datapath: int = 2):
         st = _rt.state()
         self.ps_id = ps_id
         self.servers, self.clients = list(servers), list(clients)
@@ -140,9 +144,27 @@ class _Group:
             else:
                 w = native().Window(eng, (1 << 28) + 4 * ps_id + k, 0, 0, st.device is not None)
             self.wins.append(w)
+        # datapath 3 moves the shards as two-sided messages (csrc/core/link.h): no rank maps
+        # another's device window
+        self.datapath = datapath
+        err = None
         for w in self.wins:
             blobs = self.comm.allgather_obj(bytes(w.blob()))
-            w.connect(blobs, self.members)
+            try:
+                w.connect(blobs, self.members, datapath != 3)
+            except RuntimeError as e:  # a peer mapping failed (the message names the pair)
+                err = str(e)
+        # agree before going on: every member raises the same error, none waits in a barrier
+        # for a member that gave up (bench.py then retries on datapath 3)
+        errs = [e for e in self.comm.allgather_obj(err) if e]
+        if errs:
+            raise PSMapError("; ".join(errs))
+        self.link = None
+        if datapath == 3:
+            self.link = native().PsLink(eng, ps_id, self.servers, self.clients, self.device)
+            mine = [(st.rank, c, bytes(i)) for c, i in self.link.make_ids()]
+            ids = [x for part in self.comm.allgather_obj(mine) for x in part]
+            self.link.connect(ids)
         self.comm.Barrier()
         for w in self.wins:
             w.unlink_names()
@@ -170,7 +192,8 @@ class PServer:
     """pServer(conf):start() — asyncsgd/pserver.lua:12-168, BiCNN/pserver.lua.
 
     conf: rank, sranks, cranks, plong, opt (ServerOpt | BiCNN opt dict), ps_id (0),
-    datapath (0 fused remote kernel | 1 SDMA copies), staleness (-1 off),
+    datapath (0 fused remote kernel | 1 SDMA copies | 2 per-client link streams (default) |
+    3 two-sided messages: RCCL send / recv between GPUs, csrc/core/link.h), staleness (-1 off),
     grad_dtype (float32 | bfloat16)."""
 
     def __init__(self, conf, state=None):
@@ -207,6 +230,8 @@ class PServer:
             dev.type == "cuda", self.p.data_ptr(), [t.data_ptr() for t in self.opt_state],
             inbox.data_ptr() if inbox is not None else 0, self.opt.native(), self.datapath, self.staleness,
             self.grad_dtype == torch.bfloat16, self.cranks[0])
+        if grp.link is not None:
+            self.native.set_link(grp.link)
         self.native.start()
         grp.server = self
 
@@ -224,7 +249,7 @@ class PServer:
             else:
                 _pending_servers[self.ps_id] = self  # launched by pClient.start
         else:
-            grp = _Group(self.ps_id, self.sranks, self.cranks, self.plong, None, None, self.grad_dtype)
+            grp = _Group(self.ps_id, self.sranks, self.cranks, self.plong, None, None, self.grad_dtype, self.datapath)
             _groups[self.ps_id] = grp
             self._launch(grp)
         if block:
@@ -281,6 +306,7 @@ class PClient:
         self.plong = int(_conf_get(conf, "plong", 0))
         self.ps_id = int(_conf_get(conf, "ps_id", 0))
         self.grad_dtype = _conf_get(conf, "grad_dtype", torch.float32)
+        self.datapath = int(_conf_get(conf, "datapath", 2))
         self.state = state or {}
         # K > 1 splits every server's shard into K entries, each pushed / pulled as its own
         # shard (bench.py --emulate-shards: the N=K shard traffic of one worker on one GPU)
@@ -320,7 +346,7 @@ class PClient:
         if p.dtype != torch.float32:
             raise TypeError("pClient parameters must be float32")
         p, g = p.reshape(-1), g.reshape(-1)
-        grp = _Group(self.ps_id, self.sranks, self.cranks, self.plong, p, g, self.grad_dtype)
+        grp = _Group(self.ps_id, self.sranks, self.cranks, self.plong, p, g, self.grad_dtype, self.datapath)
         _groups[self.ps_id] = grp
         grp.client = self
         if self.ps_id in _pending_servers:
@@ -329,6 +355,8 @@ class PClient:
         self._user_p, self._user_g = self.rx, self.tx
         self.native = native().PSClient(_rt.engine(), self.ps_id, [e[0] for e in self.entries],
                                         [e[1] for e in self.entries], [e[2] for e in self.entries])
+        if grp.link is not None:  # datapath 3: the shards' data from / into these very buffers
+            self.native.set_link(grp.link, self.rx.data_ptr(), self.tx.data_ptr(), self.tx.element_size())
         self.native.start()
         self.on = True
         # the first client initialises every shard with its parameters

@@ -50,7 +50,7 @@ class TrainConfig:
     l2wd: float = 0.0
     amp: bool = True  # bf16 autocast on GPU
     channels_last: bool = True
-    datapath: int = 2  # 0 fused remote kernel, 1 serial SDMA, 2 per-client link streams
+    datapath: int = 2  # 0 fused remote kernel, 1 serial SDMA, 2 per-client link streams, 3 RCCL send/recv
     staleness: int = -1  # bounded staleness (SSP) for the PS; -1 = fully asynchronous
     wire_dtype: str = "fp32"  # "bf16": EASGD elastic differences / all-reduce buckets cross xGMI in bf16
     server_rule: Optional[ServerOpt] = None

@@ -13,7 +13,8 @@ from mpit_amd.parallel.ps import PClient, PServer, ServerOpt
 mp.Init()
 W = mp.COMM_WORLD()
 r = W.Get_rank()
-conf = dict(rank=r, sranks=[0], cranks=[1, 2], plong=64, opt=ServerOpt("sum"), staleness=0)
+conf = dict(rank=r, sranks=[0], cranks=[1, 2], plong=64, opt=ServerOpt("sum"), staleness=0,
+            datapath=int(os.environ.get("T_DATAPATH", "2")))
 if r == 0:
     s = PServer(conf)
     s.start(block=True)

@@ -28,3 +28,21 @@ def test_bench_three_ranks_cpu():
     assert sec["dedicated"]["parallelism"] == "async-ps-dedicated-1srv-2wrk" and sec["dedicated"]["ps_check"]["ok"]
     assert sec["ps_pingpong"]["clients"] == 2 and sec["ps_pingpong"]["aggregate_GBps_bidir"] > 0
     assert sec["allreduce"]["correct"] and sec["allreduce"]["MiB"] == 40.0
+
+
+def test_bench_preflight_falls_back_to_datapath3_cpu():
+    """A broken one-sided (worker, server) path (injected: server 1's pulls to worker 2 arrive
+    corrupted) is caught by the pre-timing check; the job switches to the two-sided data plane
+    (datapath 3) and runs, reporting why."""
+    e = dict(os.environ, MPIT_CPU_ONLY="1", HSA_ENABLE_IPC_MODE_LEGACY="0", MPIT_PS_FAULT="badpull",
+             MPIT_PS_FAULT_RANK="1", MPIT_PS_FAULT_CLIENT="2")
+    e["PYTHONPATH"] = ROOT + os.pathsep + e.get("PYTHONPATH", "")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.join(ROOT, "bench.py"), "--gpus", "3",
+           "--model", "cnn7", "--batch", "8", "--steps", "2", "--warmup", "1", "--no-secondary"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=e, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert out["config"]["datapath"] == 3 and out["ps_check"]["ok"], out
+    fb = out["preflight"]["fallback"]
+    assert fb["from_datapath"] == 2 and "[2, 1]" in fb["reason"], fb

@@ -538,3 +538,90 @@ def test_wgrad_split_once_bitwise_equal_per_tile_split(tmp_path):
         res.append(torch.load(f, weights_only=True))
     for i, (u, v) in enumerate(zip(*res)):
         assert torch.equal(u.view(torch.int32), v.view(torch.int32)), (i, _rel(u, v))
+
+
+# ---- fp16x3 on hostile operands (verdict r03 #8): heavy tails and a 2^20 outlier row, judged
+# per output row against fp64 (a Frobenius norm over the whole output hides per-row loss)
+
+def _row_rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return (a - b).norm(dim=1) / (b.norm(dim=1) + 1e-300)
+
+
+def _hostile(dist, shape, seed, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    if dist == "student_t2":  # nu = 2: infinite variance, |x| up to ~1e3 x the median
+        z = torch.randn(shape, generator=g)
+        chi2 = torch.randn(shape, generator=g) ** 2 + torch.randn(shape, generator=g) ** 2
+        t = z / torch.sqrt(chi2 / 2)
+    else:  # gaussian with one row 2^20 above the rest
+        t = torch.randn(shape, generator=g)
+        t[shape[0] // 3] *= 2.0 ** 20
+    return (t * scale).cuda()
+
+
+# per-row slack: the fp16x3 split drops the l*l term (2^-22 relative per product) and the
+# operand's power-of-two scale is per tensor, so a row far below the tensor's bound keeps
+# 22 bits only while it stays within 2^27 of it
+_ROW_FLOOR = 2.0 ** -21
+
+
+@gpu
+@pytest.mark.parametrize("dist", ["student_t2", "outlier_row"])
+@pytest.mark.parametrize("M,N,K", [(1000, 192, 128), (4096, 256, 512), (12544, 512, 2048)])
+def test_gemm_nt_f16x3_hostile_rows(dist, M, N, K):
+    a = _hostile(dist, (M, K), M + K)
+    b = _hostile("student_t2", (N, K), N + K, 0.05)
+    ref = a.double().cpu() @ b.double().cpu().t()
+    c = C.gemm_nt(a, b, f16x3=True)
+    lib = a @ b.t()
+    ours, theirs = _row_rel(c, ref), _row_rel(lib, ref)
+    worst = int(torch.argmax(ours / (theirs + _ROW_FLOOR)))
+    print(f"{dist} {M}x{N}x{K}: max row err ours {ours.max():.3e} lib {theirs.max():.3e}; "
+          f"worst row {worst}: {ours[worst]:.3e} vs {theirs[worst]:.3e}")
+    assert torch.isfinite(c).all()
+    assert (ours <= 2.0 * theirs + _ROW_FLOOR).all(), (worst, ours[worst].item(), theirs[worst].item())
+
+
+@gpu
+@pytest.mark.parametrize("dist", ["student_t2", "outlier_row"])
+@pytest.mark.parametrize("M,N,K", [(5000, 192, 320), (12544, 512, 256)])
+def test_gemm_tn_f16x3_hostile_rows(dist, M, N, K):
+    """The backward-weight shape: dW[N, K] = dY^T X with heavy-tailed gradients and an outlier
+    activation column (a 2^20 row of X^T)."""
+    y = _hostile("student_t2", (M, N), M + N, 1e-6)
+    x = _hostile(dist, (K, M), K + M).t().contiguous()
+    ref = y.double().cpu().t() @ x.double().cpu()
+    out = C.gemm_tn(y, x, f16x3=True)
+    lib = y.t() @ x
+    ours, theirs = _row_rel(out, ref), _row_rel(lib, ref)
+    worst = int(torch.argmax(ours / (theirs + _ROW_FLOOR)))
+    print(f"{dist} tn {M}x{N}x{K}: max row err ours {ours.max():.3e} lib {theirs.max():.3e}")
+    assert torch.isfinite(out).all()
+    assert (ours <= 2.0 * theirs + _ROW_FLOOR).all(), (worst, ours[worst].item(), theirs[worst].item())
+
+
+@gpu
+def test_conv_f16x3_hostile_input_rows():
+    """A 3x3 convolution through the fp32 weight plan (fp16x3 planes) on a heavy-tailed input
+    with one outlier image: per output channel-row within 2x of MIOpen fp32 against fp64."""
+    torch.manual_seed(9)
+    mod = C.ConvNHWC(128, 128, 3, stride=1, padding=1).cuda().to(memory_format=torch.channels_last)
+    plan = C.WeightCastPlan(mod, torch.float32)
+    x = _hostile("student_t2", (4, 128, 14, 14), 77)
+    x[1] *= 2.0 ** 20
+    x = _cl(x)
+    plan.run()
+    y = mod(x)
+    plan.invalidate()
+    w = mod.weight.detach()
+    ref = F.conv2d(x.double().cpu(), w.double().cpu(), padding=1)
+    lib = F.conv2d(x, w, padding=1)
+
+    def rows(t):  # one row per (image, output channel)
+        return t.permute(0, 1, 2, 3).reshape(t.shape[0] * t.shape[1], -1)
+
+    ours, theirs = _row_rel(rows(y), rows(ref)), _row_rel(rows(lib), rows(ref))
+    worst = int(torch.argmax(ours / (theirs + _ROW_FLOOR)))
+    print(f"conv hostile: max row err ours {ours.max():.3e} lib {theirs.max():.3e}")
+    assert (ours <= 2.0 * theirs + _ROW_FLOOR).all(), (worst, ours[worst].item(), theirs[worst].item())

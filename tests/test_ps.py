@@ -95,3 +95,33 @@ def test_batched_server_updates_bitwise_gpu():
         res.append((int(re.search(r"bits=(-?\d+)", r).group(1)), eval(re.search(r"stats=(\{.*\})", r).group(1))))
     assert res[0][0] == res[1][0], res
     assert res[1][1].get("batches", 0) == 0 and res[0][1].get("batches", 0) >= 1, res
+
+
+# ---- datapath 3: shard data as two-sided messages (csrc/core/link.h); on CPU ranks the
+# engine's tagged host messages stand in for RCCL (same op order per (client, server) pair)
+
+@pytest.mark.parametrize("n", [3, 8])
+def test_datapath3_colocated_exact_sums(n):
+    """n co-located ranks (8 = the N=8 node layout): pushes with pulls and plain pulls
+    interleaved, deadlock-free; every worker's final pull equals the closed form, as with
+    the one-sided datapath 0."""
+    out = run_ranks("ps_link.py", n, {"MPIT_CPU_ONLY": "1", "T_CASE": "sum"}, timeout=300)
+    assert out.count("equal={3: True, 0: True}") == n, out
+
+
+def test_datapath3_trainer_bitwise_equals_datapath0():
+    """1 worker + 2 dedicated servers: Downpour through the message data plane gives exactly
+    the parameters of the one-sided data plane, and the servers' shards agree (verify_ps)."""
+    out = run_ranks("ps_link.py", 3, {"MPIT_CPU_ONLY": "1", "T_CASE": "train", "T_SERVERS": "2"}, timeout=300)
+    assert "same=True" in out and out.count("ok={3: True, 0: True}") == 3, out
+
+
+def test_datapath3_one_server_seven_workers():
+    """BASELINE config 2's layout (1 pserver + 7 workers) on the message data plane."""
+    out = run_ranks("ps_link.py", 8, {"MPIT_CPU_ONLY": "1", "T_CASE": "train", "T_SERVERS": "1"}, timeout=300)
+    assert out.count("ok={3: True, 0: True}") == 8, out
+
+
+def test_datapath3_bounded_staleness():
+    out = run_ranks("ssp_check.py", 3, {"MPIT_CPU_ONLY": "1", "T_DATAPATH": "3"})
+    assert "SSP_OK" in out, out

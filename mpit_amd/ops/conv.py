@@ -49,6 +49,11 @@ def _stream(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
+# MPIT_DEBUG_SIDE_DELAY=cycles (diagnostics only): a spin kernel ahead of every weight-gradient
+# GEMM on the side stream, so a consumer that misses the join reads an unwritten gradient
+_SIDE_DELAY = int(os.environ.get("MPIT_DEBUG_SIDE_DELAY", "0"))
+
+
 class WgradStream:
     """Weight-gradient GEMMs on a second HIP stream.
 
@@ -89,6 +94,9 @@ class WgradStream:
             return None
         st = cls.side(dev)
         st.wait_stream(torch.cuda.current_stream(dev))
+        if _SIDE_DELAY:  # race diagnostics: every weight gradient lands late
+            with torch.cuda.stream(st):
+                torch.cuda._sleep(_SIDE_DELAY)
         cls._pending.add(dev.index)
         return st
 

@@ -34,6 +34,10 @@ from ..utils import trace as _trace
 # MPIT_PUSH_ON_SIDE=1: gather + push gate on the side stream instead of joining it. Measured
 # at N=1 (one shard, fired at the end of the backward): 11.1k vs 11.65k img/s, so off.
 _PUSH_ON_SIDE = os.environ.get("MPIT_PUSH_ON_SIDE", "0") == "1"
+# MPIT_DEBUG_GATE_DELAY=cycles (diagnostics only): a spin kernel on the compute stream right
+# after each shard's gate, so the shard's pull lands before the rest of the backward runs and
+# any later reader of its parameters sees the pulled values
+_GATE_DELAY = int(os.environ.get("MPIT_DEBUG_GATE_DELAY", "0"))
 
 
 class ShardPusher:
@@ -121,6 +125,8 @@ class ShardPusher:
         for i in self.members[k]:
             self.params[i].grad = None  # the caching allocator orders reuse on the stream
         self.pc.async_send_grad_shard(k, pull=True)
+        if _GATE_DELAY and self.pc.tx.is_cuda:  # race diagnostics: the pull lands before the rest
+            torch.cuda._sleep(_GATE_DELAY)     # of this backward runs
         self.fired[k] = True
 
     def abort(self):

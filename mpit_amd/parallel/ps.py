@@ -34,6 +34,13 @@ from ..comm import Comm
 from ..utils import trace as _trace
 from ..window import host_view
 
+# MPIT_DEBUG_SYNC_GATE=1 (diagnostics only): a device synchronize ahead of every gated PS
+# operation, taking the GPU-event gate out of the picture
+_SYNC_GATE = __import__("os").environ.get("MPIT_DEBUG_SYNC_GATE", "0") == "1"
+# MPIT_DEBUG_NO_SHARD_SYNC=1 (diagnostics only): the round-3 behaviour, shard fills not ordered
+# before the server stream (tests/test_ps_gpu.py shows it fails then)
+_NO_SHARD_SYNC = __import__("os").environ.get("MPIT_DEBUG_NO_SHARD_SYNC", "0") == "1"
+
 TAGS = dict(recv_init=1, recv_grad=2, send_param=3, recv_param=4, recv_header=5, recv_stop=6,
             recv_param_tail=7, recv_grad_tail=8)
 tag_ps_recv_init = 1
@@ -159,6 +166,10 @@ class _Group:
         errs = [e for e in self.comm.allgather_obj(err) if e]
         if errs:
             raise PSMapError("; ".join(errs))
+        if self.device and me_client:
+            # the windows' contents as queued so far on our stream (rx / tx fills) are complete
+            # before any server touches them from its own, unordered streams
+            torch.cuda.current_stream(rx.device).synchronize()
         self.link = None
         if datapath == 3:
             self.link = native().PsLink(eng, ps_id, self.servers, self.clients, self.device)
@@ -225,6 +236,13 @@ class PServer:
         self.opt_state = [torch.zeros(self.size, dtype=torch.float32, device=dev) for _ in range(self.opt.nstate)]
         inbox = torch.empty(self.size, dtype=self.grad_dtype, device=dev) if (self.datapath == 1 and dev.type == "cuda") else None
         self._inbox = inbox
+        if dev.type == "cuda" and not _NO_SHARD_SYNC:
+            # the zero fills above are queued on the current (PyTorch) stream, but the server
+            # updates these buffers from its own non-blocking stream (csrc/core/ps.cpp stream_),
+            # which is not ordered after it: without this the fill of a recycled block could land
+            # AFTER the first client's initial parameter push and zero part of the shard (seen as
+            # the fp32 overlap test's 1.0 divergence in round 3: tests/test_ps_gpu.py)
+            torch.cuda.current_stream(dev).synchronize()
         self.native = native().PSServer(
             st.engine, self.ps_id, grp.wins[0], grp.wins[1], grp.members, self.cranks, self.offset, self.size,
             dev.type == "cuda", self.p.data_ptr(), [t.data_ptr() for t in self.opt_state],
@@ -328,6 +346,8 @@ class PClient:
 
     def _stream(self) -> int:
         if self.rx is not None and self.rx.is_cuda:
+            if _SYNC_GATE:  # race diagnostics: everything queued so far is done before the gate
+                torch.cuda.synchronize(self.rx.device)
             return torch.cuda.current_stream(self.rx.device).cuda_stream
         return 0
 

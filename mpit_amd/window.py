@@ -68,6 +68,11 @@ class Win:
         w = native().Window(eng, int(win_id), local, int(nbytes), bool(device))
         blobs = comm.allgather_obj(bytes(w.blob()))
         w.connect(blobs, comm.world_ranks)
+        if device:
+            # window creation is collective: what this rank queued into the exposed memory (the
+            # Allocate zero fill, the caller's writes) completes before any peer may access it
+            # from its own streams, which are not ordered after ours
+            torch.cuda.current_stream().synchronize()
         comm.Barrier()
         w.unlink_names()
         if device:

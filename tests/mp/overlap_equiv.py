@@ -36,7 +36,28 @@ for amp in (False, True):
         ps_id += 1
         if tr.is_worker:
             assert ("pusher" in tr.opt_config) == overlap
-        timed_steps(tr, steps, 0)
+        if os.environ.get("T_DEBUG"):
+            # per step: loss, bit-sum of the pushed window (scaled gradients) and of the pulled
+            # parameters, to find the first step / quantity where the arms part
+            # (snapshots queued on the stream, no host sync inside the loop: the timing stays
+            # the test's)
+            snaps = []
+            w_init = tr.flat.flat.clone() if tr.is_worker else None
+            for k in range(steps if tr.is_worker else 0):
+                loss = tr.step()
+                snaps.append((loss.clone(), tr.pc.tx.clone(), tr.flat.flat.clone()))
+            tr.sync()
+            bs = lambda t: int(t.detach().reshape(-1).view(torch.int32).to(torch.int64).sum().item())
+            prev = w_init
+            for k, (loss, txs, ws) in enumerate(snaps):
+                # one worker, server rule p += g: the pulled w must be exactly prev + pushed tx
+                exact = bool(torch.equal(ws, prev + txs)) if arm != "defer" else None
+                print(f"STEP {('bf16' if amp else 'fp32')} {arm} {k} loss={float(loss):.9g} tx={bs(txs)} "
+                      f"w={bs(ws)} txmax={float(txs.abs().max()):.4g} w0={bs(w_init)} pull_exact={exact}", flush=True)
+                prev = ws
+            tr.barrier()
+        else:
+            timed_steps(tr, steps, 0)
         chk = tr.verify_ps()
         assert chk["ok"], chk
         if tr.is_worker:

@@ -1348,7 +1348,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y
   f32x16 lacc[F32 ? TM : 1][F32 ? TN : 1];
   [[maybe_unused]] int ey = 0, ex = 0;
   [[maybe_unused]] float sy = 1.f, sy11 = 2048.f, sx = 1.f, sx11 = 2048.f;
-  if constexpr (F32 && FM == 11) {
+  if constexpr (F32 && (FM == 11 || FM == 12)) {
     ey = fp16_exp(red.amax_y);
     ex = fp16_exp(red.amax_x);
     sy = exp2i(ey);
@@ -1441,6 +1441,83 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y
             lacc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], lacc[i][j], 0, 0, 0);
           }
       }
+    } else if constexpr (F32 && FM == 12) {
+      // fp16x3, split ONCE per element (FM 11 splits every element in each of the two waves
+      // that read it, after 8 ds_read_b32 column reads per fragment): every thread takes its
+      // share of this stage's fp32 rows (row-contiguous float4), the block barriers, and the
+      // fp16 h / l planes of Y and X are written over the same ring slot in the bf16 kernel's
+      // 16-bit image layout (swizzled 256-B rows); after a second barrier the fragments are
+      // read exactly as the bf16 path reads them (ds_read_b64_tr_b16, two per fragment and
+      // plane) — no per-use split, no column reads. Same planes as FM 11 (split2h's
+      // arithmetic), so the same products; only the k order inside an MFMA differs.
+      constexpr int NY4 = kRows * TBN / 4, NF4 = kRows * (TBN + TBK) / 4 / 256;
+      constexpr int CY16 = TBN / 8, CX16 = TBK / 8;  // 16-B chunks per row of the 16-bit images
+      static_assert(kRows * (TBN + TBK) % 1024 == 0, "the stage splits evenly over 256 threads");
+      float4 v4[NF4];
+      const float4* src4 = reinterpret_cast<const float4*>(Ys);
+#pragma unroll
+      for (int u = 0; u < NF4; ++u) v4[u] = src4[t + 256 * u];
+      __syncthreads();  // every thread holds its fp32 values: the slot takes the planes
+      uint16_t* YH = reinterpret_cast<uint16_t*>(Ys);
+      uint16_t* YL = YH + kRows * TBN;
+      uint16_t* XH = YL + kRows * TBN;
+      uint16_t* XL = XH + kRows * TBK;
+#pragma unroll
+      for (int u = 0; u < NF4; ++u) {
+        const int e = t + 256 * u;
+        const bool isy = e < NY4;  // (uniform per wave: NY4 is a multiple of 64)
+        const int e2 = isy ? e : e - NY4;
+        const int cpr = (isy ? TBN : TBK) / 4;  // float4 per row
+        const int row = e2 / cpr, c4 = e2 - row * cpr;
+        const float sc = isy ? sy : sx, sc11 = isy ? sy11 : sx11;
+        const float4 x = v4[u];
+        const f32x2 x01 = {x.x, x.y}, x23 = {x.z, x.w};
+        const f16x2 h01 = __builtin_convertvector(x01 * sc, f16x2), h23 = __builtin_convertvector(x23 * sc, f16x2);
+        const f32x2 r01 = x01 * sc11 - __builtin_convertvector(h01, f32x2) * 2048.f;
+        const f32x2 r23 = x23 * sc11 - __builtin_convertvector(h23, f32x2) * 2048.f;
+        const f16x2 l01 = __builtin_convertvector(r01, f16x2), l23 = __builtin_convertvector(r23, f16x2);
+        uint2 hw, lw;
+        hw.x = __builtin_bit_cast(uint32_t, h01);
+        hw.y = __builtin_bit_cast(uint32_t, h23);
+        lw.x = __builtin_bit_cast(uint32_t, l01);
+        lw.y = __builtin_bit_cast(uint32_t, l23);
+        const int o = isy ? row * TBN + tswz<uint16_t, CY16>(row, c4 >> 1) * 8 + (c4 & 1) * 4
+                          : row * TBK + tswz<uint16_t, CX16>(row, c4 >> 1) * 8 + (c4 & 1) * 4;
+        *reinterpret_cast<uint2*>((isy ? YH : XH) + o) = hw;
+        *reinterpret_cast<uint2*>((isy ? YL : XL) + o) = lw;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int kk = 0; kk < kRows / 16; ++kk) {
+        const int rr = 16 * kk + 8 * h + q;  // row of this lane in the first 4-row block
+        f16x8 ah[TM], al[TM], bh[TN], bl[TN];
+        auto frag = [&](const uint16_t* img, int ld, int ch, auto cy) -> f16x8 {
+          constexpr int CPR = decltype(cy)::value;
+          const s16x4 lo = ds_tr16(img + rr * ld + tswz<uint16_t, CPR>(rr, ch) * 8 + cbyte);
+          const s16x4 hi = ds_tr16(img + (rr + 4) * ld + tswz<uint16_t, CPR>(rr + 4, ch) * 8 + cbyte);
+          return __builtin_bit_cast(f16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        };
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int ch = (wn * WN + i * 32) / 8 + cbase;
+          ah[i] = frag(YH, TBN, ch, std::integral_constant<int, CY16>{});
+          al[i] = frag(YL, TBN, ch, std::integral_constant<int, CY16>{});
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int ch = (wk * WK + j * 32) / 8 + cbase;
+          bh[j] = frag(XH, TBK, ch, std::integral_constant<int, CX16>{});
+          bl[j] = frag(XL, TBK, ch, std::integral_constant<int, CX16>{});
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+            lacc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], lacc[i][j], 0, 0, 0);
+            lacc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], lacc[i][j], 0, 0, 0);
+          }
+      }
     } else if constexpr (F32) {
       // v_mfma_f32_32x32x2_f32: lane (fr, fh) supplies Y[row][n0' + fr] and X[row][k0' + fr]
       // of row 2s + fh in step s (32 consecutive floats per half-wave: ds_read_b32, no
@@ -1501,7 +1578,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] += lacc[i][j];
-  } else if constexpr (F32 && FM == 11) {
+  } else if constexpr (F32 && (FM == 11 || FM == 12)) {
     const float iy = exp2i(-ey), ix = exp2i(-ex);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -2503,7 +2580,13 @@ static void launch_tn_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
   TnRed red{};
   // fp32 with both operand bounds: fp16x3 (FM 11), else bf16x6 (FM 1)
   if ((amax_y != 0) != (amax_x != 0)) throw std::invalid_argument("gemm_tn: fp16x3 needs both operand bounds");
-  const int tfm = !F32 || f32_mode() != 1 ? 0 : (amax_y ? 11 : 1);
+  // fp16x3 wgrad: FM 12 (split once per element into fp16 planes in LDS, transposed fragment
+  // reads) unless MPIT_TN_F16S=0 (FM 11: split per use after column reads)
+  static const bool f16s = [] {
+    const char* e = std::getenv("MPIT_TN_F16S");
+    return !(e && std::string(e) == "0");
+  }();
+  const int tfm = !F32 || f32_mode() != 1 ? 0 : (amax_y ? (f16s ? 12 : 11) : 1);
   red.amax_y = reinterpret_cast<const float*>(amax_y);
   red.amax_x = reinterpret_cast<const float*>(amax_x);
   const int ngr = ns > kReduceGroup ? int(tn_groups(ns)) : 1;
@@ -2557,14 +2640,22 @@ static void launch_tn_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
     size_t shm = size_t(ST) * kRows * (tbn + tbk) * sizeof(T);                                                   \
     if (tn_cap1()) {                                                                                               \
       shm = std::max(shm, kTnCapShm);                                                                              \
-      if (geo && F32 && tfm == 11) MPIT_TN_OPT_IN(A, B, ST, true, F32 ? 11 : 0);                                   \
+      if (geo && F32 && tfm == 12) MPIT_TN_OPT_IN(A, B, ST, true, F32 ? 12 : 0);                                   \
+      else if (F32 && tfm == 12) MPIT_TN_OPT_IN(A, B, ST, false, F32 ? 12 : 0);                                    \
+      else if (geo && F32 && tfm == 11) MPIT_TN_OPT_IN(A, B, ST, true, F32 ? 11 : 0);                              \
       else if (F32 && tfm == 11) MPIT_TN_OPT_IN(A, B, ST, false, F32 ? 11 : 0);                                    \
       else if (geo && F32 && f32_mode() == 1) MPIT_TN_OPT_IN(A, B, ST, true, F32 ? 1 : 0);                         \
       else if (F32 && f32_mode() == 1) MPIT_TN_OPT_IN(A, B, ST, false, F32 ? 1 : 0);                               \
       else if (geo) MPIT_TN_OPT_IN(A, B, ST, true, 0);                                                             \
       else MPIT_TN_OPT_IN(A, B, ST, false, 0);                                                                     \
     }                                                                                                              \
-    if (geo && F32 && tfm == 11)                                                                                   \
+    if (geo && F32 && tfm == 12)                                                                                   \
+      hipLaunchKernelGGL((gemm_tn_kernel<T, A, B, ST, true, F32 ? 12 : 0>), grid, dim3(256), shm, s, y, ldy, x,    \
+                         ldx, part, M, N, K, rps, ntk, ntiles, g, red);                                            \
+    else if (F32 && tfm == 12)                                                                                     \
+      hipLaunchKernelGGL((gemm_tn_kernel<T, A, B, ST, false, F32 ? 12 : 0>), grid, dim3(256), shm, s, y, ldy, x,   \
+                         ldx, part, M, N, K, rps, ntk, ntiles, g, red);                                            \
+    else if (geo && F32 && tfm == 11)                                                                              \
       hipLaunchKernelGGL((gemm_tn_kernel<T, A, B, ST, true, F32 ? 11 : 0>), grid, dim3(256), shm, s, y, ldy, x,    \
                          ldx, part, M, N, K, rps, ntk, ntiles, g, red);                                            \
     else if (F32 && tfm == 11)                                                                                     \

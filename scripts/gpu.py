@@ -12,10 +12,11 @@ Steps:
   tier                  pytest -m gpu (whole GPU tier)                  -> pytest_gpu.log
   pytest:<args>         pytest <args> (e.g. pytest:tests/test_overlap.py) -> pytest_<n>.log
   bench                 bench.py defaults (fp32 headline + bf16 secondary) -> bench.json
-  bench:<args>          bench.py <args> (comma separated)               -> bench_<n>.json
+  bench:<args>[:K=V;K=V] bench.py <args> (comma separated), extra env    -> bench_<n>.json
   prof:<name>:<args>    rocprofv3 --kernel-trace of bench.py <args> + stream table -> streams_<name>.md
+  gemmcalls:<name>:<args> per-call GEMM shapes + times of one steady step     -> gemm_calls_<name>.md
   mp:<script>:<n>[:K=V;K=V] tests/mp/<script> on n ranks with extra env   -> mp_<script>_<n>.log
-  py:<file>[:args]      python3 <file> <args> (benchmarks/ probes)      -> py_<n>.log
+  py:<file>[:args[:K=V;K=V]] python3 <file> <args> with extra env (benchmarks/ probes) -> py_<n>.log
 """
 from __future__ import annotations
 
@@ -82,8 +83,10 @@ def main(argv) -> int:
             rc = _run(out, f"pytest_{i}.log", pyt + rest.split(","), 900)
             print(_tail(os.path.join(out, f"pytest_{i}.log"), 2))
         elif kind == "bench":
-            args = rest.split(",") if rest else []
-            rc = _run(out, f"bench_{i}.err", [PY, "-u", "bench.py"] + args, 600, stdout_file=f"bench_{i}.json")
+            parts = rest.split(":")
+            args = parts[0].split(",") if parts[0] else []
+            env = dict(kv.split("=", 1) for kv in parts[1].split(";")) if len(parts) > 1 and parts[1] else {}
+            rc = _run(out, f"bench_{i}.err", [PY, "-u", "bench.py"] + args, 600, stdout_file=f"bench_{i}.json", env=env)
             print(_tail(os.path.join(out, f"bench_{i}.json"), 1)[:600])
         elif kind == "prof":
             name, _, args = rest.partition(":")
@@ -99,6 +102,19 @@ def main(argv) -> int:
                         p = os.path.join(root, fn)
                         if fn.endswith("kernel_trace.csv") and os.path.getsize(p) > 40 << 20:
                             os.remove(p)
+        elif kind == "gemmcalls":  # per-call GEMM table (shapes from MPIT_GEMM_LOG, times from the trace)
+            name, _, args = rest.partition(":")
+            d = os.path.join(out, f"gc_{name}")
+            rc = _run(out, f"gc_{name}.log", ["rocprofv3", "--kernel-trace", "-d", d, "-o", "t",
+                                             "--output-format", "csv", "--", PY, "bench.py"]
+                      + (args.split(",") if args else []), 600, env={"MPIT_GEMM_LOG": "1"})
+            if rc == 0:
+                rc = _run(out, f"gc_{name}_table.log", [PY, "scripts/gemm_calls.py", os.path.join(out, f"gc_{name}.log"),
+                                                       d, os.path.join(out, f"gemm_calls_{name}.md"), name], 300)
+                for root, _, files in os.walk(d):
+                    for fn in files:
+                        if fn.endswith("kernel_trace.csv") and os.path.getsize(os.path.join(root, fn)) > 40 << 20:
+                            os.remove(os.path.join(root, fn))
         elif kind == "mp":
             parts = rest.split(":")
             script, n = parts[0], parts[1]
@@ -110,8 +126,10 @@ def main(argv) -> int:
                       500, env=env)
             print(_tail(os.path.join(out, f"mp_{script}_{n}_{i}.log"), 6))
         elif kind == "py":
-            f, _, args = rest.partition(":")
-            rc = _run(out, f"py_{i}.log", [PY, "-u", f] + (args.split(",") if args else []), 600)
+            parts = rest.split(":")
+            f, args = parts[0], parts[1] if len(parts) > 1 else ""
+            env = dict(kv.split("=", 1) for kv in parts[2].split(";")) if len(parts) > 2 and parts[2] else {}
+            rc = _run(out, f"py_{i}.log", [PY, "-u", f] + (args.split(",") if args else []), 600, env=env)
             print(_tail(os.path.join(out, f"py_{i}.log"), 8))
         else:
             print(f"[gpu.py] unknown step {step!r}")

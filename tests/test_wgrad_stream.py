@@ -1,5 +1,5 @@
 """Weight gradients on the side stream (ops/conv.py WgradStream) equal the single-stream
-ones bit for bit (the trainer path is exercised by bench.py / scripts/gpu_configs.sh)."""
+ones bit for bit (the trainer path is exercised by bench.py and the GPU tier)."""
 import pytest
 import torch
 

@@ -218,7 +218,7 @@ def main(argv=None) -> int:
     par = _par(a, tr, nworkers)
     secondary = {}
     t_sec = time.perf_counter()
-    sec_steps, sec_warm = max(3, min(a.steps, 20)), 4
+    sec_steps, sec_warm = max(3, min(a.steps, 20)), max(4, a.warmup)
     if not a.no_secondary and tr.on_gpu:
         # the other precision on the same replicas / PS (bf16 autocast when the headline is fp32)
         tr.set_amp(not amp)

@@ -13,6 +13,7 @@ Steps:
   pytest:<args>         pytest <args> (e.g. pytest:tests/test_overlap.py) -> pytest_<n>.log
   bench                 bench.py defaults (fp32 headline + bf16 secondary) -> bench.json
   bench:<args>[:K=V;K=V] bench.py <args> (comma separated), extra env    -> bench_<n>.json
+  dbench:<n>:<args>     bench.py on n ranks sharing the box's GPU (rehearsal) -> dbench_<n>.json
   prof:<name>:<args>    rocprofv3 --kernel-trace of bench.py <args> + stream table -> streams_<name>.md
   gemmcalls:<name>:<args> per-call GEMM shapes + times of one steady step     -> gemm_calls_<name>.md
   mp:<script>:<n>[:K=V;K=V] tests/mp/<script> on n ranks with extra env   -> mp_<script>_<n>.log
@@ -88,6 +89,14 @@ def main(argv) -> int:
             env = dict(kv.split("=", 1) for kv in parts[1].split(";")) if len(parts) > 1 and parts[1] else {}
             rc = _run(out, f"bench_{i}.err", [PY, "-u", "bench.py"] + args, 600, stdout_file=f"bench_{i}.json", env=env)
             print(_tail(os.path.join(out, f"bench_{i}.json"), 1)[:600])
+        elif kind == "dbench":  # bench.py on n ranks of the box's one GPU (a rehearsal, not a scaling run)
+            parts = rest.split(":")
+            n, args = parts[0], parts[1].split(",") if len(parts) > 1 and parts[1] else []
+            port = str(29500 + (os.getpid() + i) % 2000)
+            rc = _run(out, f"dbench_{i}.err", [PY, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+                                             "--master-addr=127.0.0.1", f"--master-port={port}", "bench.py",
+                                             "--gpus", n] + args, 600, stdout_file=f"dbench_{i}.json")
+            print(_tail(os.path.join(out, f"dbench_{i}.json"), 1)[:400])
         elif kind == "prof":
             name, _, args = rest.partition(":")
             d = os.path.join(out, f"prof_{name}")

@@ -179,7 +179,7 @@ def main(argv=None) -> int:
     try:
         tr = _make(a, mp_train, amp, a.topology, a.servers, 0)
     except PSMapError as e:  # a peer window could not be mapped (every rank raised it)
-        if a.datapath == 3:
+        if a.datapath == 3 or mp.runtime.state().shared_devices:
             raise
         fallback = {"from_datapath": a.datapath, "reason": f"window mapping: {e}"}
         a.datapath = 3
@@ -192,7 +192,7 @@ def main(argv=None) -> int:
         # the job to the two-sided RCCL data plane (datapath 3, csrc/core/link.h) and checks
         # again; a pair still broken ends the run here, named, before any timing.
         preflight = tr.preflight()
-        if not preflight["ok"] and a.datapath != 3:
+        if not preflight["ok"] and a.datapath != 3 and not mp.runtime.state().shared_devices:
             fallback = {"from_datapath": a.datapath, "reason": f"pre-flight: no peer access {preflight['no_peer']}, "
                                                                  f"pulled shard bits differ {preflight['mismatches']}"}
             tr.stop()

@@ -171,6 +171,9 @@ class _Group:
             # before any server touches them from its own, unordered streams
             torch.cuda.current_stream(rx.device).synchronize()
         self.link = None
+        if datapath == 3 and self.device and st.shared_devices:
+            # RCCL refuses two ranks of one communicator on one GPU ("Duplicate GPU")
+            raise ValueError("PS datapath 3 (RCCL send/recv) needs one GPU per rank; these ranks share a GPU")
         if datapath == 3:
             self.link = native().PsLink(eng, ps_id, self.servers, self.clients, self.device)
             mine = [(st.rank, c, bytes(i)) for c, i in self.link.make_ids()]

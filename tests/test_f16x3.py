@@ -180,3 +180,36 @@ def test_stem_f16x3_vs_fp64():
 
     assert rel(y, yr) <= 2 * rel(yl, yr) + 1e-9
     assert rel(conv.weight.grad, gr) <= 2 * rel(gl, gr) + 1e-9
+
+
+@gpu
+def test_folded_finalize_on_many_streams():
+    """The BN finalize fold takes its ticket sets per (device, stream): a process that runs the
+    fold from more than the static table's 8 streams (one priority stream per Trainer, test
+    sessions) gets a zeroed allocation per extra stream instead of an exception, with the same
+    bits on every stream (round-3 verdict: an 8-stream process-lifetime cap)."""
+    from mpit_amd.ops.bn import COUNTERS, BatchNormAct2d
+
+    torch.manual_seed(7)
+    bn = BatchNormAct2d(128).cuda()
+    conv = C.Conv1x1(128, 256).cuda().to(memory_format=torch.channels_last)
+    x0 = _cl(torch.randn(2, 128, 14, 14, device="cuda"))
+    g = None
+    outs = []
+    for k in range(12):
+        st = torch.cuda.Stream()
+        st.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(st):
+            x = x0.clone().requires_grad_(True)
+            n0 = COUNTERS["bwd_folded"]
+            z = conv(bn(x))
+            if g is None:
+                g = torch.randn_like(z)
+            bn.zero_grad(set_to_none=True)
+            z.backward(g)
+            outs.append((x.grad.clone(), bn.weight.grad.clone()))
+        torch.cuda.current_stream().wait_stream(st)
+        torch.cuda.synchronize()
+        assert COUNTERS["bwd_folded"] == n0 + 1
+    for dx, dgam in outs[1:]:
+        assert torch.equal(dx, outs[0][0]) and torch.equal(dgam, outs[0][1])

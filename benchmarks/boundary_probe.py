@@ -1,0 +1,72 @@
+"""Probe: host time at the Downpour step boundary (N=1). The trace shows the GPU idle between
+the server's apply kernel and the next step's weight cast; this times, on the host, the chain
+in between: the PS reply wake-up (pc.wait return), the end of step(), the start of the next
+step() and the cast launch (wrappers around PClient.wait and WeightCastPlan.run).
+
+    python benchmarks/boundary_probe.py [bf16|fp32] [steps]
+"""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+
+def main():
+    dt = sys.argv[1] if len(sys.argv) > 1 else "bf16"
+    steps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+    import mpit_amd as mp
+    from mpit_amd.train import TrainConfig, Trainer
+
+    mp.Init()
+    tr = Trainer(TrainConfig(model="resnet50", batch=256, amp=dt == "bf16"))
+    marks = []
+    pc = tr.pc
+    wait0 = pc.wait
+
+    def wait():
+        t0 = time.perf_counter()
+        wait0()
+        marks.append(("wait_in", t0))
+        marks.append(("wait_out", time.perf_counter()))
+    pc.wait = wait
+    run0 = tr.wcast.run
+
+    def run():
+        marks.append(("cast_call", time.perf_counter()))
+        run0()
+        marks.append(("cast_done", time.perf_counter()))
+    tr.wcast.run = run
+    for _ in range(5):
+        tr.step()
+    torch.cuda.synchronize()
+    marks.clear()
+    for _ in range(steps):
+        marks.append(("step_call", time.perf_counter()))
+        tr.step()
+        marks.append(("step_ret", time.perf_counter()))
+    torch.cuda.synchronize()
+    # per boundary: wait_out -> step_ret -> step_call -> cast_call -> cast_done
+    seq = [n for n, _ in marks]
+    t = [x for _, x in marks]
+    out = {"wait_blocked_us": [], "wait_out_to_step_ret_us": [], "step_ret_to_next_cast_us": [], "cast_launch_us": []}
+    for i, n in enumerate(seq):
+        if n == "wait_out":
+            out["wait_blocked_us"].append((t[i] - t[i - 1]) * 1e6)
+            j = seq.index("step_ret", i)
+            out["wait_out_to_step_ret_us"].append((t[j] - t[i]) * 1e6)
+            if "cast_call" in seq[j:]:
+                k = seq.index("cast_call", j)
+                out["step_ret_to_next_cast_us"].append((t[k] - t[j]) * 1e6)
+        if n == "cast_call":
+            out["cast_launch_us"].append((t[i + 1] - t[i]) * 1e6)
+    summ = {k: round(sorted(v)[len(v) // 2], 1) for k, v in out.items() if v}
+    print(json.dumps({"dtype": dt, "median_us": summ}), flush=True)
+    tr.stop()
+    mp.Finalize()
+
+
+if __name__ == "__main__":
+    main()

@@ -10,10 +10,11 @@
 // The ReLU mask is one bit per element (1/16 of a bf16 tensor), so the backward never
 // re-reads the forward output y.
 // Layout: the activation is a row-major [M = N*H*W, C] matrix. A thread owns VEC = 8
-// consecutive channels (16 B bf16, 32 B fp32; the ReLU mask is one byte per 8 channels in
-// both, the layout the GEMM epilogues read) and walks rows; since every block size
-// and grid stride is a multiple of G = C/VEC, a thread keeps the same channel group for
-// its whole life, so per-channel coefficients stay in registers.
+// channels (16 B bf16, 32 B fp32; the ReLU mask is one byte per 8 channels in both, the
+// layout the GEMM epilogues read) and walks rows; since every block size and grid stride
+// is a multiple of G = C/VEC, a thread keeps the same channels for its whole life, so
+// per-channel coefficients stay in registers. The fp32 apply passes split a thread's 8
+// elements into two coalesced float4 halves (Slot below).
 // Statistics use shifted sums (shift = row 0 of each channel) accumulated in fp32 per
 // thread, combined per block in LDS, then across blocks in fp64 by the finalize kernel:
 // deterministic (no atomics) and free of the E[x^2]-E[x]^2 cancellation for |mean|>>std.
@@ -24,6 +25,7 @@
 #include <stdexcept>
 #include <cstdlib>
 #include <string>
+#include <type_traits>
 
 #include "ew.h"
 #include "kernels.h"
@@ -75,6 +77,177 @@ struct Vec<float> {
 
 // block size: the largest multiple of G that is <= 256 (G = channel groups per row)
 inline int block_for(int G) { return G >= 256 ? G : (256 / G) * G; }
+
+// ---------------------------------------------------------------- apply-pass lane layout
+// Where the 8 elements of an apply-pass thread live. A thread owns vector slot i (global
+// thread index, then + grid stride): bf16 — one 16-byte vector at element 8i, lanes
+// contiguous. fp32 with SPLIT — two float4 at 4l and 256 + 4l of its wave's 512-float chunk
+// (l = lane): each load instruction then reads 1 KiB contiguous across the wave, where one
+// 32-byte vector per lane (the unsplit fp32 layout) leaves every cache line an instruction
+// touches half used and needs a second instruction to the same lines. Element v = 4h + j is
+// at off[h] + j; its ReLU-mask bit is bit sh[h] + j of byte mb[h] (the mask format is the
+// same in both layouts: one byte per 8 consecutive elements). SPLIT needs 256-thread blocks
+// and C | 2048, so that the grid stride (a multiple of 2048 elements) keeps every lane on the
+// same channels for its life (split_ok).
+template <bool SPLIT, bool CHK = false>
+struct Slot {
+  int64_t off[2], mb[2];
+  int sh[2];
+  int64_t lim;  // elements in the tensor (CHK)
+  __device__ __forceinline__ Slot(int64_t i, int64_t nvec) : lim(nvec * 8) {
+    if constexpr (SPLIT) {
+      const int64_t w = i >> 6;
+      const int l = int(i & 63);
+      off[0] = w * 512 + 4 * l;
+      off[1] = off[0] + 256;
+      mb[0] = w * 64 + (l >> 1);
+      mb[1] = mb[0] + 32;
+      sh[0] = sh[1] = 4 * (l & 1);
+    } else {
+      off[0] = i * 8;
+      off[1] = off[0] + 4;
+      mb[0] = mb[1] = i;
+      sh[0] = 0;
+      sh[1] = 4;
+    }
+  }
+  // half h holds data: only the last, partial wave chunk of a SPLIT pass checks (CHK)
+  __device__ __forceinline__ bool valid(int h) const { return !(SPLIT && CHK) || off[h] < lim; }
+  // channel of element v (constant over the thread's life); off[h] is a multiple of 4 and C
+  // of 8, so the 4 elements of a half never wrap: 2 divisions per thread, not 8
+  __device__ __forceinline__ void chans(int C, int (&c)[8]) const {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int b = int(off[h] % C);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) c[4 * h + j] = b + j;
+    }
+  }
+};
+
+// MPIT_BN_SPLIT=0 keeps the unsplit fp32 layout (A/B knob)
+inline bool split_ok(bool f32, int C, int blk) {
+  static const bool on = [] {
+    const char* e = std::getenv("MPIT_BN_SPLIT");
+    return !(e && e[0] == '0');
+  }();
+  return on && f32 && blk == 256 && 2048 % C == 0;
+}
+
+// Walk over the thread's slots. U == 0: grid stride, body(Slot) for i, i + stride, ... while
+// live. U > 0: one pass, exactly the U slots i + k * stride (k < U) with stride = the whole
+// grid — no loop, so no wave waits for its own previous stores before its next loads
+// (vmcnt counts both). SPLIT walks whole waves (the mask store's lane swap needs every
+// lane): full chunks without checks (no branches between the loads), a partial chunk with
+// per-half checks.
+template <bool SPLIT, int U, class F>
+__device__ __forceinline__ void for_slots(int64_t i, int64_t stride, int64_t nvec, F&& body) {
+  if constexpr (U > 0) {
+#pragma unroll
+    for (int k = 0; k < U; ++k, i += stride) {
+      if constexpr (SPLIT) {
+        if ((i | 63) < nvec) body(Slot<true, false>(i, nvec));
+        else if ((i & ~int64_t(63)) < nvec) body(Slot<true, true>(i, nvec));
+      } else {
+        if (i < nvec) body(Slot<false>(i, nvec));
+      }
+    }
+  } else if constexpr (SPLIT) {
+    for (; (i | 63) < nvec; i += stride) body(Slot<true, false>(i, nvec));
+    if ((i & ~int64_t(63)) < nvec) body(Slot<true, true>(i, nvec));
+  } else {
+    for (; i < nvec; i += stride) body(Slot<false>(i, nvec));
+  }
+}
+
+// Slots per thread of the apply passes: fp32 1, bf16 2 — measured per ResNet-50 shape against
+// the grid-stride loop over <= 4096 blocks (0) and 4 (profiles/bn_apply_passes_r04.md);
+// MPIT_BN_APPLY_U overrides (0, 1, 2).
+inline int apply_u(bool f32) {
+  static const int u = [] {
+    const char* e = std::getenv("MPIT_BN_APPLY_U");
+    return e ? std::atoi(e) : -1;
+  }();
+  return u >= 0 ? u : (f32 ? 1 : 2);
+}
+
+// launch a kernel instantiated for (SPLIT, U): l(bool_constant, int_constant)
+template <bool F32, class L>
+void with_mode(bool split, int u, L&& l) {
+  auto go = [&](auto sp) {
+    switch (u) {
+      case 1: l(sp, std::integral_constant<int, 1>{}); break;
+      case 2: l(sp, std::integral_constant<int, 2>{}); break;
+      default: l(sp, std::integral_constant<int, 0>{});
+    }
+  };
+  if constexpr (F32) {
+    if (split) return go(std::true_type{});
+  }
+  go(std::false_type{});
+}
+
+// grid of an apply pass with u slots per thread (u == 0: grid stride)
+inline int apply_grid_u(int64_t nvec, int block, int u) {
+  if (u <= 0) return int(std::max<int64_t>(1, std::min<int64_t>((nvec + block - 1) / block, 4096)));
+  return int(std::max<int64_t>(1, (nvec + int64_t(block) * u - 1) / (int64_t(block) * u)));
+}
+
+template <typename T, class S>
+__device__ __forceinline__ void load8(const T* __restrict__ p, const S& s, float (&v)[8]) {
+  if constexpr (sizeof(T) == 4) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (s.valid(h)) r = *reinterpret_cast<const float4*>(p + s.off[h]);
+      v[4 * h] = r.x; v[4 * h + 1] = r.y; v[4 * h + 2] = r.z; v[4 * h + 3] = r.w;
+    }
+  } else {
+    Vec<T>::load(p + s.off[0], v);
+  }
+}
+
+template <typename T, class S>
+__device__ __forceinline__ void store8(T* __restrict__ p, const S& s, const float (&v)[8]) {
+  if constexpr (sizeof(T) == 4) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (s.valid(h))
+        *reinterpret_cast<float4*>(p + s.off[h]) = make_float4(v[4 * h], v[4 * h + 1], v[4 * h + 2], v[4 * h + 3]);
+  } else {
+    Vec<T>::store(p + s.off[0], v);
+  }
+}
+
+// the thread's 8 mask bits (bit v = element v)
+template <bool SPLIT, bool CHK>
+__device__ __forceinline__ uint32_t mask_bits(const uint8_t* __restrict__ m, const Slot<SPLIT, CHK>& s) {
+  if constexpr (SPLIT) {
+    uint32_t b = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (s.valid(h)) b |= ((uint32_t(m[s.mb[h]]) >> s.sh[h]) & 15u) << (4 * h);
+    return b;
+  } else {
+    return m[s.mb[0]];
+  }
+}
+
+// store the thread's 8 mask bits; SPLIT: lanes 2k and 2k+1 share a byte — every lane of the
+// wave must call this (the nibbles meet through a lane swap)
+template <bool SPLIT, bool CHK>
+__device__ __forceinline__ void mask_store(uint8_t* __restrict__ m, const Slot<SPLIT, CHK>& s, uint32_t bits) {
+  if constexpr (SPLIT) {
+    const uint32_t other = uint32_t(__shfl_xor(int(bits), 1));
+    if (s.sh[0] == 0) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        if (s.valid(h)) m[s.mb[h]] = uint8_t(((bits >> (4 * h)) & 15u) | (((other >> (4 * h)) & 15u) << 4));
+    }
+  } else {
+    m[s.mb[0]] = uint8_t(bits);
+  }
+}
 
 // ---------------------------------------------------------------- output bound (fp16x3)
 // An apply kernel that produces the next convolution's fp32 GEMM operand also writes max|out|
@@ -407,26 +580,29 @@ void launch_tiles_finalize(hipStream_t s, const float* part, int64_t nt, int C, 
 // ---------------------------------------------------------------- forward: apply
 // MASK: also store the ReLU mask, one byte per vector (bit v = element v of the vector is
 // positive), so the backward never re-reads y (1/16 of its bytes for bf16, 1/32 for fp32).
-template <typename T, bool RES, bool RELU, bool MASK>
+template <typename T, bool RES, bool RELU, bool MASK, bool SPLIT, int U>
 __global__ __launch_bounds__(1024) void bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res,
                                                         T* __restrict__ y, const float* __restrict__ coef, int64_t nvec,
                                                         int C, uint8_t* __restrict__ mask, AmaxOut am) {
   constexpr int V = Vec<T>::N;
-  const int G = C / V;
   int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   const int64_t stride = int64_t(gridDim.x) * blockDim.x;  // multiple of G
-  const int g = int(i % G);
   float sc[V], sh[V];
+  {
+    int ch[8];
+    Slot<SPLIT>(i, nvec).chans(C, ch);
 #pragma unroll
-  for (int v = 0; v < V; ++v) {
-    sc[v] = coef[g * V + v];
-    sh[v] = coef[C + g * V + v];
+    for (int v = 0; v < V; ++v) {
+      const int c = ch[v];
+      sc[v] = coef[c];
+      sh[v] = coef[C + c];
+    }
   }
   float mx = 0.f;
-  for (; i < nvec; i += stride) {
+  for_slots<SPLIT, U>(i, stride, nvec, [&](const auto& s) {
     float a[V], rr[V];
-    Vec<T>::load(x + i * V, a);
-    if constexpr (RES) Vec<T>::load(res + i * V, rr);
+    load8<T>(x, s, a);
+    if constexpr (RES) load8<T>(res, s, rr);
     uint32_t bits = 0;
 #pragma unroll
     for (int v = 0; v < V; ++v) {
@@ -434,15 +610,15 @@ __global__ __launch_bounds__(1024) void bn_apply_kernel(const T* __restrict__ x,
       if constexpr (RES) t += rr[v];
       if constexpr (RELU) t = fmaxf(t, 0.f);
       a[v] = t;
-      mx = fmaxf(mx, fabsf(t));
+      if (s.valid(v >> 2)) mx = fmaxf(mx, fabsf(t));
     }
-    Vec<T>::store(y + i * V, a);
+    store8<T>(y, s, a);
     if constexpr (MASK) {  // (rounding to bf16 never flips the sign of a normal number)
 #pragma unroll
       for (int v = 0; v < V; ++v) bits |= uint32_t(a[v] > 0.f) << v;
-      mask[i] = uint8_t(bits);
+      mask_store(mask, s, bits);
     }
-  }
+  });
   if (am.amax) amax_finish(mx, am);
 }
 
@@ -543,124 +719,135 @@ __device__ __forceinline__ void fin_bwd_channel(int c, double a, double b, int C
   coef[2 * C + c] = -A * mdz - Cc * mean[c];
 }
 
-template <typename T, bool RELU, bool RESGRAD>
+template <typename T, bool RELU, bool RESGRAD, bool SPLIT, int U>
 __global__ __launch_bounds__(1024) void bn_bwd_apply_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ mask,
                                                             const T* __restrict__ x, const float* __restrict__ coef,
                                                             T* __restrict__ dx, T* __restrict__ dres, int64_t nvec,
                                                             int C, AmaxOut am) {
   constexpr int V = Vec<T>::N;
-  const int G = C / V;
   int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   const int64_t stride = int64_t(gridDim.x) * blockDim.x;
-  const int g = int(i % G);
   float A[V], Cc[V], B[V];
+  {
+    int ch[8];
+    Slot<SPLIT>(i, nvec).chans(C, ch);
 #pragma unroll
-  for (int v = 0; v < V; ++v) {
-    A[v] = coef[g * V + v];
-    Cc[v] = coef[C + g * V + v];
-    B[v] = coef[2 * C + g * V + v];
+    for (int v = 0; v < V; ++v) {
+      const int c = ch[v];
+      A[v] = coef[c];
+      Cc[v] = coef[C + c];
+      B[v] = coef[2 * C + c];
+    }
   }
   float mx = 0.f;
-  for (; i < nvec; i += stride) {
+  for_slots<SPLIT, U>(i, stride, nvec, [&](const auto& s) {
     float d[V], xx[V];
-    Vec<T>::load(dy + i * V, d);
-    Vec<T>::load(x + i * V, xx);
+    load8<T>(dy, s, d);
+    load8<T>(x, s, xx);
     uint32_t mb = 0xffu;
-    if constexpr (RELU) mb = mask[i];
+    if constexpr (RELU) mb = mask_bits(mask, s);
 #pragma unroll
     for (int v = 0; v < V; ++v) {
       float dz = d[v];
       if constexpr (RELU) dz = (mb >> v) & 1u ? dz : 0.f;
       d[v] = dz;
       xx[v] = fmaf(A[v], dz, fmaf(Cc[v], xx[v], B[v]));
-      mx = fmaxf(mx, fabsf(xx[v]));
+      if (s.valid(v >> 2)) mx = fmaxf(mx, fabsf(xx[v]));
     }
-    Vec<T>::store(dx + i * V, xx);
-    if constexpr (RESGRAD) Vec<T>::store(dres + i * V, d);
-  }
+    store8<T>(dx, s, xx);
+    if constexpr (RESGRAD) store8<T>(dres, s, d);
+  });
   if (am.amax) amax_finish(mx, am);
 }
 
 // ---------------------------------------------------------------- BN pair (ResNet downsample)
 // y = relu(x1*sc1 + sh1 + x2*sc2 + sh2): a block's last BN plus its downsample shortcut's BN
 // (no ReLU on the shortcut), one pass over (x1, x2) instead of materialising bn2(x2).
-template <typename T>
+template <typename T, bool SPLIT, int U>
 __global__ __launch_bounds__(1024) void bn_pair_apply_kernel(const T* __restrict__ x1,
                                                              const T* __restrict__ x2,
                                                              T* __restrict__ y, const float* __restrict__ coef1,
                                                              const float* __restrict__ coef2, int64_t nvec, int C,
                                                              uint8_t* __restrict__ mask, AmaxOut am) {
   constexpr int V = 8;
-  const int G = C / V;
   int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   const int64_t stride = int64_t(gridDim.x) * blockDim.x;  // multiple of G
-  const int g = int(i % G);
   float a1[V], b1[V], a2[V], b2[V];
+  {
+    int ch[8];
+    Slot<SPLIT>(i, nvec).chans(C, ch);
 #pragma unroll
-  for (int v = 0; v < V; ++v) {
-    a1[v] = coef1[g * V + v];
-    b1[v] = coef1[C + g * V + v];
-    a2[v] = coef2[g * V + v];
-    b2[v] = coef2[C + g * V + v];
+    for (int v = 0; v < V; ++v) {
+      const int c = ch[v];
+      a1[v] = coef1[c];
+      b1[v] = coef1[C + c];
+      a2[v] = coef2[c];
+      b2[v] = coef2[C + c];
+    }
   }
   float mx = 0.f;
-  for (; i < nvec; i += stride) {
+  for_slots<SPLIT, U>(i, stride, nvec, [&](const auto& s) {
     float p[V], q[V];
-    Vec<T>::load(x1 + i * V, p);
-    Vec<T>::load(x2 + i * V, q);
+    load8<T>(x1, s, p);
+    load8<T>(x2, s, q);
     uint32_t bits = 0;
 #pragma unroll
     for (int v = 0; v < V; ++v) {
       const float t = fmaxf(fmaf(p[v], a1[v], b1[v]) + fmaf(q[v], a2[v], b2[v]), 0.f);
       p[v] = t;
       bits |= uint32_t(t > 0.f) << v;
-      mx = fmaxf(mx, t);
+      if (s.valid(v >> 2)) mx = fmaxf(mx, t);
     }
-    Vec<T>::store(y + i * V, p);
-    mask[i] = uint8_t(bits);
-  }
+    store8<T>(y, s, p);
+    mask_store(mask, s, bits);
+  });
   if (am.amax) amax_finish(mx, am);
 }
 
 // dz = dy * mask; dx1 = A1 dz + C1 x1 + B1, dx2 = A2 dz + C2 x2 + B2 (coef [3][C] each)
-template <typename T>
+template <typename T, bool SPLIT, int U>
 __global__ __launch_bounds__(1024) void bn_pair_bwd_apply_kernel(
     const T* __restrict__ dy, const uint8_t* __restrict__ mask, const T* __restrict__ x1,
     const float* __restrict__ coef1, T* __restrict__ dx1, const T* __restrict__ x2,
     const float* __restrict__ coef2, T* __restrict__ dx2, int64_t nvec, int C, AmaxOut am1, AmaxOut am2) {
   constexpr int V = 8;
-  const int G = C / V;
   int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   const int64_t stride = int64_t(gridDim.x) * blockDim.x;
-  const int g = int(i % G);
   float A1[V], C1[V], B1[V], A2[V], C2[V], B2[V];
+  {
+    int ch[8];
+    Slot<SPLIT>(i, nvec).chans(C, ch);
 #pragma unroll
-  for (int v = 0; v < V; ++v) {
-    A1[v] = coef1[g * V + v];
-    C1[v] = coef1[C + g * V + v];
-    B1[v] = coef1[2 * C + g * V + v];
-    A2[v] = coef2[g * V + v];
-    C2[v] = coef2[C + g * V + v];
-    B2[v] = coef2[2 * C + g * V + v];
+    for (int v = 0; v < V; ++v) {
+      const int c = ch[v];
+      A1[v] = coef1[c];
+      C1[v] = coef1[C + c];
+      B1[v] = coef1[2 * C + c];
+      A2[v] = coef2[c];
+      C2[v] = coef2[C + c];
+      B2[v] = coef2[2 * C + c];
+    }
   }
   float m1 = 0.f, m2 = 0.f;
-  for (; i < nvec; i += stride) {
+  for_slots<SPLIT, U>(i, stride, nvec, [&](const auto& s) {
     float d[V], p[V], q[V];
-    Vec<T>::load(dy + i * V, d);
-    Vec<T>::load(x1 + i * V, p);
-    Vec<T>::load(x2 + i * V, q);
-    const uint32_t mb = mask[i];
+    load8<T>(dy, s, d);
+    load8<T>(x1, s, p);
+    load8<T>(x2, s, q);
+    const uint32_t mb = mask_bits(mask, s);
 #pragma unroll
     for (int v = 0; v < V; ++v) {
       const float dz = (mb >> v) & 1u ? d[v] : 0.f;
       p[v] = fmaf(A1[v], dz, fmaf(C1[v], p[v], B1[v]));
       q[v] = fmaf(A2[v], dz, fmaf(C2[v], q[v], B2[v]));
-      m1 = fmaxf(m1, fabsf(p[v]));
-      m2 = fmaxf(m2, fabsf(q[v]));
+      if (s.valid(v >> 2)) {
+        m1 = fmaxf(m1, fabsf(p[v]));
+        m2 = fmaxf(m2, fabsf(q[v]));
+      }
     }
-    Vec<T>::store(dx1 + i * V, p);
-    Vec<T>::store(dx2 + i * V, q);
-  }
+    store8<T>(dx1, s, p);
+    store8<T>(dx2, s, q);
+  });
   if (am1.amax) amax_finish(m1, am1);
   if (am2.amax) amax_finish(m2, am2);
 }
@@ -681,10 +868,6 @@ int stat_blocks(int64_t M, int R, int64_t* rows_per_block) {
   return int(nb);
 }
 
-int apply_grid(int64_t nvec, int block) {
-  return int(std::max<int64_t>(1, std::min<int64_t>((nvec + block - 1) / block, 4096)));
-}
-
 template <typename T>
 void launch_apply(hipStream_t s, const T* x, const T* res, T* y, int64_t M, int C, const float* coef, bool relu,
                   uint8_t* mask, AmaxOut am = {}) {
@@ -692,18 +875,22 @@ void launch_apply(hipStream_t s, const T* x, const T* res, T* y, int64_t M, int 
   const int G = C / V;
   const int blk = block_for(G);
   const int64_t nvec = M * G;
-  const int grid = apply_grid(nvec, blk);
-  const dim3 g(grid), b(blk);
-  if (relu && mask) {
-    if (res) hipLaunchKernelGGL((bn_apply_kernel<T, true, true, true>), g, b, 0, s, x, res, y, coef, nvec, C, mask, am);
-    else hipLaunchKernelGGL((bn_apply_kernel<T, false, true, true>), g, b, 0, s, x, res, y, coef, nvec, C, mask, am);
-  } else if (relu) {
-    if (res) hipLaunchKernelGGL((bn_apply_kernel<T, true, true, false>), g, b, 0, s, x, res, y, coef, nvec, C, mask, am);
-    else hipLaunchKernelGGL((bn_apply_kernel<T, false, true, false>), g, b, 0, s, x, res, y, coef, nvec, C, mask, am);
-  } else {
-    if (res) hipLaunchKernelGGL((bn_apply_kernel<T, true, false, false>), g, b, 0, s, x, res, y, coef, nvec, C, mask, am);
-    else hipLaunchKernelGGL((bn_apply_kernel<T, false, false, false>), g, b, 0, s, x, res, y, coef, nvec, C, mask, am);
-  }
+  const int u = apply_u(sizeof(T) == 4);
+  const dim3 g(apply_grid_u(nvec, blk, u)), b(blk);
+  with_mode<sizeof(T) == 4>(split_ok(sizeof(T) == 4, C, blk), u, [&](auto sp, auto uu) {
+    constexpr bool SP = decltype(sp)::value;
+    constexpr int U = decltype(uu)::value;
+    if (relu && mask) {
+      if (res) hipLaunchKernelGGL((bn_apply_kernel<T, true, true, true, SP, U>), g, b, 0, s, x, res, y, coef, nvec, C, mask, am);
+      else hipLaunchKernelGGL((bn_apply_kernel<T, false, true, true, SP, U>), g, b, 0, s, x, res, y, coef, nvec, C, mask, am);
+    } else if (relu) {
+      if (res) hipLaunchKernelGGL((bn_apply_kernel<T, true, true, false, SP, U>), g, b, 0, s, x, res, y, coef, nvec, C, mask, am);
+      else hipLaunchKernelGGL((bn_apply_kernel<T, false, true, false, SP, U>), g, b, 0, s, x, res, y, coef, nvec, C, mask, am);
+    } else {
+      if (res) hipLaunchKernelGGL((bn_apply_kernel<T, true, false, false, SP, U>), g, b, 0, s, x, res, y, coef, nvec, C, mask, am);
+      else hipLaunchKernelGGL((bn_apply_kernel<T, false, false, false, SP, U>), g, b, 0, s, x, res, y, coef, nvec, C, mask, am);
+    }
+  });
 }
 
 template <typename T>
@@ -792,18 +979,23 @@ void bwd_impl(hipStream_t s, const T* dy, const uint8_t* mask, const T* x, T* dx
     if (amax) hip_check(hipMemsetAsync(reinterpret_cast<void*>(amax), 0, kBoundFloats * sizeof(float), s), "amax zero");
   }
   const int64_t nvec = M * G;
-  const dim3 g(apply_grid(nvec, blk)), b(blk);
+  const int u = apply_u(sizeof(T) == 4);
+  const dim3 g(apply_grid_u(nvec, blk, u)), b(blk);
   if (!dx) {  // coefficients only (ws[0, 3C)), dgamma / dbeta
     hip_check(hipGetLastError(), "bn_act backward launch");
     return;
   }
-  if (relu) {
-    if (dres) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, true>), g, b, 0, s, dy, mask, x, coef, dx, dres, nvec, C, am);
-    else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, false>), g, b, 0, s, dy, mask, x, coef, dx, dres, nvec, C, am);
-  } else {
-    if (dres) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false, true>), g, b, 0, s, dy, mask, x, coef, dx, dres, nvec, C, am);
-    else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false, false>), g, b, 0, s, dy, mask, x, coef, dx, dres, nvec, C, am);
-  }
+  with_mode<sizeof(T) == 4>(split_ok(sizeof(T) == 4, C, blk), u, [&](auto sp, auto uu) {
+    constexpr bool SP = decltype(sp)::value;
+    constexpr int U = decltype(uu)::value;
+    if (relu) {
+      if (dres) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, true, SP, U>), g, b, 0, s, dy, mask, x, coef, dx, dres, nvec, C, am);
+      else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, false, SP, U>), g, b, 0, s, dy, mask, x, coef, dx, dres, nvec, C, am);
+    } else {
+      if (dres) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false, true, SP, U>), g, b, 0, s, dy, mask, x, coef, dx, dres, nvec, C, am);
+      else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false, false, SP, U>), g, b, 0, s, dy, mask, x, coef, dx, dres, nvec, C, am);
+    }
+  });
   hip_check(hipGetLastError(), "bn_act backward launch");
 }
 
@@ -868,10 +1060,13 @@ static void pair_apply_t(hipStream_t s, uintptr_t x1, uintptr_t coef1, uintptr_t
                          int64_t M, int C, uintptr_t mask, uintptr_t amax, uintptr_t scratch) {
   const int G = C / 8, blk = block_for(G);
   const int64_t nvec = M * G;
-  hipLaunchKernelGGL(bn_pair_apply_kernel<T>, dim3(apply_grid(nvec, blk)), dim3(blk), 0, s,
+  const int u = apply_u(sizeof(T) == 4);
+  with_mode<sizeof(T) == 4>(split_ok(sizeof(T) == 4, C, blk), u, [&](auto sp, auto uu) {
+  hipLaunchKernelGGL((bn_pair_apply_kernel<T, decltype(sp)::value, decltype(uu)::value>), dim3(apply_grid_u(nvec, blk, u)), dim3(blk), 0, s,
                      reinterpret_cast<const T*>(x1), reinterpret_cast<const T*>(x2), reinterpret_cast<T*>(y),
                      reinterpret_cast<const float*>(coef1), reinterpret_cast<const float*>(coef2), nvec, C,
                      reinterpret_cast<uint8_t*>(mask), AmaxOut{reinterpret_cast<float*>(amax)});
+  });
 }
 
 template <typename T>
@@ -880,12 +1075,14 @@ static void pair_bwd_t(hipStream_t s, uintptr_t dy, uintptr_t mask, uintptr_t x1
                        uintptr_t scratch) {
   const int G = C / 8, blk = block_for(G);
   const int64_t nvec = M * G;
-
-  hipLaunchKernelGGL(bn_pair_bwd_apply_kernel<T>, dim3(apply_grid(nvec, blk)), dim3(blk), 0, s,
+  const int u = apply_u(sizeof(T) == 4);
+  with_mode<sizeof(T) == 4>(split_ok(sizeof(T) == 4, C, blk), u, [&](auto sp, auto uu) {
+  hipLaunchKernelGGL((bn_pair_bwd_apply_kernel<T, decltype(sp)::value, decltype(uu)::value>), dim3(apply_grid_u(nvec, blk, u)), dim3(blk), 0, s,
                      reinterpret_cast<const T*>(dy), reinterpret_cast<const uint8_t*>(mask),
                      reinterpret_cast<const T*>(x1), reinterpret_cast<const float*>(coef1), reinterpret_cast<T*>(dx1),
                      reinterpret_cast<const T*>(x2), reinterpret_cast<const float*>(coef2), reinterpret_cast<T*>(dx2),
                      nvec, C, AmaxOut{reinterpret_cast<float*>(amax1)}, AmaxOut{reinterpret_cast<float*>(amax2)});
+  });
 }
 
 void bn_pair_apply(int dev, hipStream_t s, uintptr_t x1, uintptr_t coef1, uintptr_t x2, uintptr_t coef2, uintptr_t y,

@@ -31,11 +31,26 @@ def test_cpu_path_matches_plain_modules():
 @pytest.mark.parametrize("res", [False, True])
 @pytest.mark.parametrize("relu", [True, False])
 def test_bn_act_fwd_bwd(dtype, C, res, relu):
+    _check(dtype, C, res, relu, (8, 7, 9))
+
+
+@gpu
+@pytest.mark.parametrize("C", [8, 24, 64, 512])
+@pytest.mark.parametrize("shape", [(3, 5, 7), (1, 1, 3)])
+def test_bn_act_fp32_lane_layouts(C, shape):
+    """fp32 apply passes read each wave's 512-element chunk as two coalesced float4 halves
+    (C | 2048) or one 32-byte vector per lane (other C): tails that end inside a wave's chunk,
+    channel counts on both sides of the rule, the ReLU mask bytes two lanes share."""
+    _check(torch.float32, C, True, True, shape)
+    _check(torch.float32, C, False, True, shape)
+
+
+def _check(dtype, C, res, relu, shape):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     torch.manual_seed(C + res * 7 + relu)
     dev = torch.device("cuda")
-    N, H, W = 8, 7, 9
+    N, H, W = shape
     x32 = (torch.randn(N, C, H, W, device=dev) * 2 + 0.7).contiguous(memory_format=torch.channels_last)
     r32 = torch.randn(N, C, H, W, device=dev).contiguous(memory_format=torch.channels_last) if res else None
     x = x32.to(dtype).contiguous(memory_format=torch.channels_last).requires_grad_(True)

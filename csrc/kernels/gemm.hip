@@ -78,7 +78,7 @@ struct V8;
 template <>
 struct V8<uint16_t> {
   uint4 r;
-  __device__ __forceinline__ void load(const uint16_t* p) { r = *reinterpret_cast<const uint4*>(p); }
+  __device__ __forceinline__ void load(const uint16_t* p, int = 4) { r = *reinterpret_cast<const uint4*>(p); }
   __device__ __forceinline__ void zero() { r = make_uint4(0, 0, 0, 0); }
   __device__ __forceinline__ float get(int e) const {
     const uint32_t w = e < 2 ? r.x : e < 4 ? r.y : e < 6 ? r.z : r.w;
@@ -88,9 +88,9 @@ struct V8<uint16_t> {
 template <>
 struct V8<float> {
   float4 a, b;
-  __device__ __forceinline__ void load(const float* p) {
-    a = reinterpret_cast<const float4*>(p)[0];
-    b = reinterpret_cast<const float4*>(p)[1];
+  __device__ __forceinline__ void load(const float* p, int h = 4) {  // elements 4..7 at p + h
+    a = *reinterpret_cast<const float4*>(p);
+    b = *reinterpret_cast<const float4*>(p + h);
   }
   __device__ __forceinline__ void zero() { a = b = make_float4(0.f, 0.f, 0.f, 0.f); }
   __device__ __forceinline__ float get(int e) const {
@@ -99,7 +99,7 @@ struct V8<float> {
     return k == 0 ? q.x : k == 1 ? q.y : k == 2 ? q.z : q.w;
   }
 };
-__device__ __forceinline__ void store8(uint16_t* p, const float (&v)[8]) {
+__device__ __forceinline__ void store8(uint16_t* p, const float (&v)[8], int = 4) {
   uint4 r;
   r.x = uint32_t(f2bf(v[0])) | (uint32_t(f2bf(v[1])) << 16);
   r.y = uint32_t(f2bf(v[2])) | (uint32_t(f2bf(v[3])) << 16);
@@ -107,9 +107,9 @@ __device__ __forceinline__ void store8(uint16_t* p, const float (&v)[8]) {
   r.w = uint32_t(f2bf(v[6])) | (uint32_t(f2bf(v[7])) << 16);
   *reinterpret_cast<uint4*>(p) = r;
 }
-__device__ __forceinline__ void store8(float* p, const float (&v)[8]) {
-  reinterpret_cast<float4*>(p)[0] = make_float4(v[0], v[1], v[2], v[3]);
-  reinterpret_cast<float4*>(p)[1] = make_float4(v[4], v[5], v[6], v[7]);
+__device__ __forceinline__ void store8(float* p, const float (&v)[8], int h = 4) {  // elements 4..7 at p + h
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(p + h) = make_float4(v[4], v[5], v[6], v[7]);
 }
 // value as stored in T (the epilogue's statistics see exactly what is written)
 template <typename T>
@@ -960,7 +960,19 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
   constexpr int HALVES = BM / 128, RPH = RPP / HALVES;  // row-threads per 128-row half
   const int ch = t % CPR, rg = t / CPR;
   const int rr = (rg / RPH) * 128 + rg % RPH;  // first row of this thread; rows rr + p*RPH
-  const int nc = n0 + ch * 8;  // first global column of this thread
+  // fp32: the thread's 8 channels are two float4 halves HOFF = BN/2 apart (columns 4ch.. and
+  // BN/2 + 4ch..), so each access instruction of a wave covers 256-B row segments instead of
+  // 32-B lane strides that leave every cache line it touches half used; bf16: 8 consecutive
+  // channels, one 16-B chunk
+  constexpr int HOFF = F32 ? BN / 2 : 4;
+  const int cl0 = F32 ? ch * 4 : ch * 8;  // tile column of element 0; element e at ecol(e)
+  auto ecol = [&](int e) { return cl0 + (e < 4 ? e : HOFF + e - 4); };
+  const int nc = n0 + cl0;  // first global column of this thread
+  // the 8 mask bits of the thread's elements at offset o (one mask byte per 8 channels)
+  auto mbits = [](const uint8_t* mk, int64_t o) -> uint32_t {
+    if constexpr (HOFF == 4) return mk[o >> 3];
+    else return ((uint32_t(mk[o >> 3]) >> (o & 7)) & 15u) | (((uint32_t(mk[(o + HOFF) >> 3]) >> ((o + HOFF) & 7)) & 15u) << 4);
+  };
   float s1[8], s2[8], sf[8], mu[8];
   int nv = 0;
 #pragma unroll
@@ -971,13 +983,13 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
   for (int e = 0; e < 8; ++e) s3[e] = mu2[e] = 0.f;
   if constexpr (BNRED) {
     const float4 a0 = *reinterpret_cast<const float4*>(ep.mean + nc);
-    const float4 a1 = *reinterpret_cast<const float4*>(ep.mean + nc + 4);
+    const float4 a1 = *reinterpret_cast<const float4*>(ep.mean + nc + HOFF);
     mu[0] = a0.x; mu[1] = a0.y; mu[2] = a0.z; mu[3] = a0.w;
     mu[4] = a1.x; mu[5] = a1.y; mu[6] = a1.z; mu[7] = a1.w;
   }
   if constexpr (DUAL) {
     const float4 a0 = *reinterpret_cast<const float4*>(ep.mean2 + nc);
-    const float4 a1 = *reinterpret_cast<const float4*>(ep.mean2 + nc + 4);
+    const float4 a1 = *reinterpret_cast<const float4*>(ep.mean2 + nc + HOFF);
     mu2[0] = a0.x; mu2[1] = a0.y; mu2[2] = a0.z; mu2[3] = a0.w;
     mu2[4] = a1.x; mu2[5] = a1.y; mu2[6] = a1.z; mu2[7] = a1.w;
   }
@@ -1008,17 +1020,17 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
     const bool ok = m < M;
     const int64_t o = orow[q] * ldc + nc;
     if (Cin != nullptr) {
-      if (ok) cv[q].load(Cin + o);
+      if (ok) cv[q].load(Cin + o, HOFF);
       else cv[q].zero();
-      cmb[q] = Cmask ? (ok ? uint32_t(Cmask[o >> 3]) : 0u) : 0xffu;
+      cmb[q] = Cmask ? (ok ? mbits(Cmask, o) : 0u) : 0xffu;
     }
     if constexpr (BNRED) {
-      if (ok) xq[q].load(epx + o);
+      if (ok) xq[q].load(epx + o, HOFF);
       else xq[q].zero();
-      xmb[q] = ok ? (ep.mask ? uint32_t(ep.mask[o >> 3]) : 0xffu) : 0u;
+      xmb[q] = ok ? (ep.mask ? mbits(ep.mask, o) : 0xffu) : 0u;
     }
     if constexpr (DUAL) {
-      if (ok) xq2[q].load(epx2 + o);
+      if (ok) xq2[q].load(epx2 + o, HOFF);
       else xq2[q].zero();
     }
   }
@@ -1029,13 +1041,13 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
     const int64_t o = orow[q] * ldc + nc;
     float v[8];
     if constexpr (F32) {
-      const float4 h0 = *reinterpret_cast<const float4*>(tl + tsw(rl, ch * 8));
-      const float4 h1 = *reinterpret_cast<const float4*>(tl + tsw(rl, ch * 8 + 4));
+      const float4 h0 = *reinterpret_cast<const float4*>(tl + tsw(rl, cl0));
+      const float4 h1 = *reinterpret_cast<const float4*>(tl + tsw(rl, cl0 + HOFF));
       v[0] = h0.x; v[1] = h0.y; v[2] = h0.z; v[3] = h0.w;
       v[4] = h1.x; v[5] = h1.y; v[6] = h1.z; v[7] = h1.w;
     } else {
       V8<uint16_t> hv;
-      hv.load(tl + tsw(rl, ch * 8));
+      hv.load(tl + tsw(rl, cl0));
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = hv.get(e);
     }
@@ -1046,16 +1058,16 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = rnd<T>(v[e] + ((mb >> e) & 1u ? cv[q].get(e) : 0.f));
     }
-    store8(C + o, v);
+    store8(C + o, v, HOFF);
     if constexpr (CONV) {
       if (geo.ozero) {  // class (0,0) of a stride-2 conv whose other parities have no taps
         const int64_t pix = orow[q] % (int64_t(geo.OH) * geo.OW);
         const int oh = int(pix / geo.OW), ow = int(pix % geo.OW);
         const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        if (ow + 1 < geo.OW) store8(C + o + ldc, z);
+        if (ow + 1 < geo.OW) store8(C + o + ldc, z, HOFF);
         if (oh + 1 < geo.OH) {
-          store8(C + o + int64_t(geo.OW) * ldc, z);
-          if (ow + 1 < geo.OW) store8(C + o + int64_t(geo.OW + 1) * ldc, z);
+          store8(C + o + int64_t(geo.OW) * ldc, z, HOFF);
+          if (ow + 1 < geo.OW) store8(C + o + int64_t(geo.OW + 1) * ldc, z, HOFF);
         }
       }
     }
@@ -1090,16 +1102,16 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float d = nv ? s1[e] / n : 0.f;
-        red[(rg * 3 + 0) * BN + ch * 8 + e] = n;
-        red[(rg * 3 + 1) * BN + ch * 8 + e] = nv ? sf[e] + d : 0.f;
-        red[(rg * 3 + 2) * BN + ch * 8 + e] = nv ? fmaxf(s2[e] - s1[e] * d, 0.f) : 0.f;
+        red[(rg * 3 + 0) * BN + ecol(e)] = n;
+        red[(rg * 3 + 1) * BN + ecol(e)] = nv ? sf[e] + d : 0.f;
+        red[(rg * 3 + 2) * BN + ecol(e)] = nv ? fmaxf(s2[e] - s1[e] * d, 0.f) : 0.f;
       }
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        red[(rg * 3 + 0) * BN + ch * 8 + e] = s1[e];
-        red[(rg * 3 + 1) * BN + ch * 8 + e] = s2[e];
-        if constexpr (DUAL) red[(rg * 3 + 2) * BN + ch * 8 + e] = s3[e];
+        red[(rg * 3 + 0) * BN + ecol(e)] = s1[e];
+        red[(rg * 3 + 1) * BN + ecol(e)] = s2[e];
+        if constexpr (DUAL) red[(rg * 3 + 2) * BN + ecol(e)] = s3[e];
       }
     }
     __syncthreads();

@@ -1,7 +1,8 @@
 """Probe: host time at the Downpour step boundary (N=1). The trace shows the GPU idle between
 the server's apply kernel and the next step's weight cast; this times, on the host, the chain
 in between: the PS reply wake-up (pc.wait return), the end of step(), the start of the next
-step() and the cast launch (wrappers around PClient.wait and WeightCastPlan.run).
+step(), the cast launch (wrappers around PClient.wait and WeightCastPlan.run) and the
+stem's forward pieces up to its first GEMM.
 
     python benchmarks/boundary_probe.py [bf16|fp32] [steps]
 """
@@ -39,6 +40,27 @@ def main():
         run0()
         marks.append(("cast_done", time.perf_counter()))
     tr.wcast.run = run
+    from mpit_amd.ops import conv as C
+
+    fwd0, get0, swp0 = C._StemConvFn.forward, C._StemPackBuf.get.__func__, C.stem_weight_planes
+
+    def fwd(ctx, *a, **k):
+        marks.append(("stem_fwd", time.perf_counter()))
+        r = fwd0(ctx, *a, **k)
+        marks.append(("stem_fwd_done", time.perf_counter()))
+        return r
+
+    def get(cls, *a, **k):
+        r = get0(cls, *a, **k)
+        marks.append(("stem_pack_done", time.perf_counter()))
+        return r
+
+    def swp(*a, **k):
+        marks.append(("stem_planes", time.perf_counter()))
+        return swp0(*a, **k)
+    C._StemConvFn.forward = staticmethod(fwd)
+    C._StemPackBuf.get = classmethod(get)
+    C.stem_weight_planes = swp
     for _ in range(5):
         tr.step()
     torch.cuda.synchronize()
@@ -62,6 +84,12 @@ def main():
                 out["step_ret_to_next_cast_us"].append((t[k] - t[j]) * 1e6)
         if n == "cast_call":
             out["cast_launch_us"].append((t[i + 1] - t[i]) * 1e6)
+            for a, b in (("cast_done", "stem_fwd"), ("stem_fwd", "stem_pack_done"), ("stem_pack_done", "stem_planes"),
+                         ("stem_planes", "stem_fwd_done")):
+                if a in seq[i:] and b in seq[i:]:
+                    ia = seq.index(a, i)
+                    ib = seq.index(b, ia)
+                    out.setdefault(f"{a}->{b}_us", []).append((t[ib] - t[ia]) * 1e6)
     summ = {k: round(sorted(v)[len(v) // 2], 1) for k, v in out.items() if v}
     print(json.dumps({"dtype": dt, "median_us": summ}), flush=True)
     tr.stop()

@@ -8,6 +8,7 @@
 #include "core/ps.h"
 #include "core/window.h"
 #include "kernels/kernels.h"
+#include "kernels/stem_pack.h"
 
 namespace py = pybind11;
 using namespace mpit;
@@ -256,6 +257,13 @@ PYBIND11_MODULE(_mpit, m) {
       py::arg("dev"), py::arg("stream"), py::arg("Nb"), py::arg("Hp"), py::arg("Wp"), py::arg("Co"), py::arg("Ho"),
       py::arg("Wo"), py::arg("stride"), py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stats"),
       py::arg("f32") = false, py::arg("bps") = 0, py::arg("amax_a") = 0, py::arg("amax_b") = 0);
+  m.def(
+      "stem_weight_planes",
+      [](int dev, uintptr_t s, uintptr_t w, int Co, int C, int R, int Sk, uintptr_t planes, uintptr_t bound) {
+        stem_weight_planes(dev, S(s), w, Co, C, R, Sk, planes, bound);
+      },
+      py::arg("dev"), py::arg("stream"), py::arg("w"), py::arg("Co"), py::arg("C"), py::arg("R"), py::arg("S"),
+      py::arg("planes"), py::arg("bound"));
   m.def("conv_stem_wgrad_ws_floats", &conv_stem_wgrad_ws_floats);
   m.def(
       "conv_stem_wgrad",

@@ -1041,6 +1041,34 @@ def _stem_pack_weight(weight: torch.Tensor, dt=torch.bfloat16) -> torch.Tensor:
     return wp
 
 
+_STEM_PBUF = {}
+# MPIT_STEM_NATIVE_PLANES=0: the stem's fp16x3 weight planes from PyTorch ops (A/B knob)
+_STEM_NATIVE_PLANES = os.environ.get("MPIT_STEM_NATIVE_PLANES", "1") != "0"
+
+
+def stem_weight_planes(weight: torch.Tensor):
+    """The stem weight's zero-extended [Co, 8, 8, 4] image as fp16x3 planes ([2, Co, 8, 8, 4] fp16:
+    ``f16_planes`` of the image under the bound max |w|) and that slotted bound, from ONE native
+    launch (csrc/kernels/stem_pack.hip). Kept per (device, stream, shape) like the bf16 image
+    (``_stem_pack_weight``): only this step's forward GEMM, queued on the same stream before the
+    next rewrite, reads them."""
+    co, c, r, s = weight.shape
+    w = weight.detach()
+    if not w.is_contiguous(memory_format=torch.channels_last):
+        w = w.contiguous(memory_format=torch.channels_last)
+    key = (weight.device, co, c, r, s, _stream(weight))
+    buf = _STEM_PBUF.get(key) if _StemPackBuf.enabled else None
+    if buf is None:
+        buf = (torch.empty((2, co, 8, 8, 4), dtype=torch.float16, device=weight.device),
+               torch.empty(BOUND_FLOATS, dtype=torch.float32, device=weight.device))
+        if _StemPackBuf.enabled:
+            _STEM_PBUF[key] = buf
+    planes, bound = buf
+    native().stem_weight_planes(weight.device.index, _stream(weight), w.data_ptr(), co, c, r, s, planes.data_ptr(),
+                                bound.data_ptr())
+    return planes, bound
+
+
 class _StemConvFn(torch.autograd.Function):
     """7x7 (<= 8x8), <= 4-channel strided stem convolution as an 8-row implicit GEMM on the
     MFMA kernels (csrc/kernels/gemm.hip ``conv_stem_*``): each kernel row is one 32-element
@@ -1056,22 +1084,27 @@ class _StemConvFn(torch.autograd.Function):
         ho, wo = (h + 2 * pad - r) // stride + 1, (w + 2 * pad - s) // stride + 1
         hp, wp = max(h + 2 * pad, (ho - 1) * stride + 8), max(w + 2 * pad, (wo - 1) * stride + 8)
         xp, ent = _StemPackBuf.get(x, pad, hp, wp, dt)
-        wb = _stem_pack_weight(weight, dt)
+        f16s = f32 and _F32_SPLIT == "f16x3"
+        wb = None if f16s and _STEM_NATIVE_PLANES else _stem_pack_weight(weight, dt)
         y = torch.empty((nb, co, ho, wo), dtype=dt, device=x.device, memory_format=torch.channels_last)
         st = None
         if hold is not None:
             st, nt = _tile_stats(co, nb * ho * wo, x.device)
             hold.append((st, nt))
         kw, ctx.xbound = {}, None
-        if f32 and _F32_SPLIT == "f16x3":
+        if f16s:
             # fp16x3: the image's bound (the padded copy only adds zeros) and the packed weight as
             # two fp16 planes; the row-tap GEMM then runs 32-deep tiles, one kernel row each
             ctx.xbound = amax_of(x)  # kept on the input while it is unchanged (a reused batch)
             if ctx.xbound is None:
                 ctx.xbound = bound_of_value(torch.linalg.vector_norm(x, float("inf")))
                 set_amax(x, ctx.xbound)
-            wb = f16_planes(wb.reshape(co, -1), bound_of_value(torch.linalg.vector_norm(weight.detach(), float("inf"))))
-            kw = dict(bps=wb[0].numel(), amax_a=ctx.xbound.data_ptr(), amax_b=wb._mpit_wamax.data_ptr())
+            if _STEM_NATIVE_PLANES:
+                wb, wam = stem_weight_planes(weight)
+            else:  # the PyTorch-op planes (A/B)
+                wam = bound_of_value(torch.linalg.vector_norm(weight.detach(), float("inf")))
+                wb = f16_planes(wb.reshape(co, -1), wam)
+            kw = dict(bps=wb[0].numel(), amax_a=ctx.xbound.data_ptr(), amax_b=wam.data_ptr())
         native().conv_stem_fwd(x.device.index, _stream(x), nb, hp, wp, co, ho, wo, stride, xp.data_ptr(),
                                wb.data_ptr(), y.data_ptr(), st.data_ptr() if st is not None else 0, f32=f32, **kw)
         ctx.save_for_backward(xp)

@@ -87,3 +87,29 @@ def test_stem_pack_buffer_reuse(dt):
     a, b = steps(False), steps(True)
     for i, (u, v) in enumerate(zip(a, b)):
         assert torch.equal(u, v), i
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["randn", "zero", "nchw", "tiny"])
+def test_stem_weight_planes_match_torch(case):
+    """The one-launch fp16x3 planes of the stem's zero-extended weight image (stem_pack.hip)
+    are bitwise the PyTorch-op planes (f16_planes of the packed image under max |w|), bound too."""
+    from mpit_amd.ops import conv as C
+
+    torch.manual_seed(11)
+    w = torch.randn(64, 3, 7, 7, device="cuda") * 0.05
+    if case == "zero":
+        w.zero_()
+    elif case == "tiny":
+        w = w * 2.0 ** -40
+    w[5, 1, 3, 2] = -0.9 if case != "zero" else 0.0
+    if case != "nchw":
+        w = w.contiguous(memory_format=torch.channels_last)
+    p, b = C.stem_weight_planes(w)
+    wp = torch.zeros(64, 8, 8, 4, device="cuda")
+    wp[:, :7, :7, :3] = w.permute(0, 2, 3, 1)
+    bref = C.bound_of_value(torch.linalg.vector_norm(w, float("inf")))
+    ref = C.f16_planes(wp.reshape(64, -1), bref)
+    torch.cuda.synchronize()
+    assert torch.equal(b, bref)
+    assert torch.equal(p.view(2, 64, -1).view(torch.int16), ref.view(2, 64, -1).view(torch.int16))

@@ -58,13 +58,29 @@ def main():
     def swp(*a, **k):
         marks.append(("stem_planes", time.perf_counter()))
         return swp0(*a, **k)
+    ts0, am0 = C._tile_stats, C.amax_of
+
+    def ts(*a, **k):
+        marks.append(("tile_stats", time.perf_counter()))
+        r = ts0(*a, **k)
+        marks.append(("tile_stats_done", time.perf_counter()))
+        return r
+
+    def am(*a, **k):
+        marks.append(("amax_of", time.perf_counter()))
+        return am0(*a, **k)
+    C._tile_stats, C.amax_of = ts, am
     C._StemConvFn.forward = staticmethod(fwd)
     C._StemPackBuf.get = classmethod(get)
     C.stem_weight_planes = swp
     for _ in range(5):
         tr.step()
     torch.cuda.synchronize()
+    from mpit_amd.train import gc_settle
+
+    gc_settle()  # as bench.py's timed region
     marks.clear()
+    ms0 = torch.cuda.memory_stats()
     for _ in range(steps):
         marks.append(("step_call", time.perf_counter()))
         tr.step()
@@ -85,13 +101,19 @@ def main():
         if n == "cast_call":
             out["cast_launch_us"].append((t[i + 1] - t[i]) * 1e6)
             for a, b in (("cast_done", "stem_fwd"), ("stem_fwd", "stem_pack_done"), ("stem_pack_done", "stem_planes"),
-                         ("stem_planes", "stem_fwd_done")):
+                         ("stem_pack_done", "tile_stats"), ("tile_stats", "tile_stats_done"),
+                         ("tile_stats_done", "amax_of"), ("amax_of", "stem_planes"), ("stem_planes", "stem_fwd_done")):
                 if a in seq[i:] and b in seq[i:]:
                     ia = seq.index(a, i)
                     ib = seq.index(b, ia)
                     out.setdefault(f"{a}->{b}_us", []).append((t[ib] - t[ia]) * 1e6)
     summ = {k: round(sorted(v)[len(v) // 2], 1) for k, v in out.items() if v}
-    print(json.dumps({"dtype": dt, "median_us": summ}), flush=True)
+    ms1 = torch.cuda.memory_stats()
+    alloc = {k: ms1.get(k, 0) - ms0.get(k, 0) for k in ("num_device_alloc", "num_device_free", "num_alloc_retries",
+                                                         "num_sync_all_streams")}
+    print(json.dumps({"dtype": dt, "median_us": summ, "allocator_deltas_over_steps": alloc, "steps": steps,
+                      "alloc_conf": os.environ.get("PYTORCH_HIP_ALLOC_CONF") or os.environ.get("PYTORCH_CUDA_ALLOC_CONF")}),
+          flush=True)
     tr.stop()
     mp.Finalize()
 

@@ -47,6 +47,8 @@ def _feeds_bn(*convs):
 # measurements), MPIT_MFMA_CONV3=0 only the 3x3s.
 MFMA_CONV = os.environ.get("MPIT_MFMA_CONV", "1") != "0"
 MFMA_CONV3 = MFMA_CONV and os.environ.get("MPIT_MFMA_CONV3", "1") != "0"
+# MPIT_FC_FP32=0: the classifier follows autocast (bf16) instead of running in fp32
+_FC_FP32 = os.environ.get("MPIT_FC_FP32", "1") != "0"
 
 
 def conv3x3(i, o, stride=1):
@@ -185,6 +187,12 @@ class ResNet(nn.Module):
             x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(self.avgpool(x), 1)
+        if _FC_FP32 and x.is_cuda and torch.is_autocast_enabled("cuda"):
+            # the classifier in fp32 under bf16 autocast: more accurate logits, and the bf16
+            # library GEMM's backward call left a ~100 us host gap at the start of the
+            # backward (profiles/boundary_r04/README.md); MPIT_FC_FP32=0 keeps it in bf16
+            with torch.autocast("cuda", enabled=False):
+                return self.fc(x.float())
         return self.fc(x)
 
 

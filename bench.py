@@ -209,6 +209,7 @@ def main(argv=None) -> int:
         if fallback is not None:
             preflight["fallback"] = fallback
     secs, loss = mp_train.timed_steps(tr, a.steps, a.warmup)
+    peak_gib = round(torch.cuda.max_memory_allocated(tr.device) / 2 ** 30, 2) if tr.on_gpu else None
     nworkers = len(tr.cranks)
     shape = INPUT_SHAPES.get(a.model, (3, 224, 224))
     value = a.steps * a.batch * nworkers / secs
@@ -272,7 +273,7 @@ def main(argv=None) -> int:
                        "datapath": a.datapath},
             "fp32_gemm": _fp32_gemm() if not (tr.on_gpu and amp) else None,
             "world": st.world, "shared_devices": st.shared_devices, "devices": devices, "rccl": rccl,
-            "ps_check": check, "preflight": preflight,
+            "ps_check": check, "preflight": preflight, "peak_mem_gib": peak_gib,
             **({"emulate_shards": a.emulate_shards} if a.emulate_shards > 1 else {}),
             "secondary": secondary,
             "secondary_s": round(time.perf_counter() - t_sec, 2),

@@ -65,13 +65,16 @@ class WgradStream:
     the compute stream at :meth:`join`, which every consumer of the weight gradients calls
     first (the trainer after ``backward()``, the shard pusher before a gather). Only
     enabled by a trainer whose gradients are stolen (no autograd kernel reads them before
-    that join); tensors the side stream touches are ``record_stream``-ed so the caching
-    allocator does not recycle them early. MPIT_WGRAD_STREAM=0 disables it.
+    that join); tensors the side stream touches are held until that join (``_used_on``) so
+    the caching allocator does not recycle them early. MPIT_WGRAD_STREAM=0 disables it.
     """
 
     enabled = False
     _side = {}
     _pending = set()
+    # tensors the side stream uses, per device, released at join (see _used_on)
+    hold = os.environ.get("MPIT_SIDE_HOLD", "1") != "0"
+    _held = {}
     # MPIT_WGRAD_AFTER=1: the side stream starts a convolution's weight gradient after its
     # input-gradient GEMM (so it overlaps the memory-bound BN backward that follows instead
     # of sharing the CUs with that compute-bound GEMM); default: before it
@@ -136,8 +139,14 @@ class WgradStream:
     @classmethod
     def join(cls):
         """Order the current stream after every weight gradient issued so far."""
-        for idx in list(cls._pending):
-            torch.cuda.current_stream(idx).wait_stream(cls._side[idx])
+        for idx in set(cls._pending) | {i for i, _ in cls._held}:
+            cur = torch.cuda.current_stream(idx)
+            cur.wait_stream(cls._side[idx])
+            # this stream now runs behind every side-stream use of the tensors held for it: their
+            # blocks may go back to the allocator, which hands them out on this stream only. A
+            # join on another stream (a gradient hook runs on its AccumulateGrad node's stream)
+            # releases nothing of the compute stream's.
+            cls._held.pop((idx, cur.cuda_stream), None)
         cls._pending.clear()
 
 
@@ -560,7 +569,7 @@ class _Conv1x1Fn(torch.autograd.Function):
             m.gemm_tn(dev, side.cuda_stream if side is not None else s, M, co, ci, dy.data_ptr(), co, x.data_ptr(),
                       ci, dw.data_ptr(), ws.data_ptr() if ws is not None else 0, 0.0, f32=f32,
                       **_wgrad_kw(dy, ctx.xamax, f32, side, keep))
-            _used_on(side, dy, x, dw, ws)
+            _used_on(side, dy, x, ws, out=dw)
         return dx, dw, None, None, None, None, None
 
 
@@ -629,11 +638,28 @@ def conv_weights(weight: torch.Tensor, dgrad: bool, dtype=torch.bfloat16):
     return wb, wt
 
 
-def _used_on(side, *ts):
-    if side is not None:
-        for t in ts:
-            if t is not None:
-                t.record_stream(side)
+def _used_on(side, *ts, out=None):
+    """Keep tensors the side stream reads or writes from being recycled before it is done:
+    held until the next :meth:`WgradStream.join` (default), or ``record_stream`` (MPIT_SIDE_HOLD=0).
+    record_stream leaves one event per tensor that the caching allocator queries on its next
+    allocation once the GPU has passed it — ~200 queries per ResNet-50 step, paid by the first
+    allocation of the next step (~0.3 ms of host time while the GPU idles at the step start,
+    profiles/boundary_r04/README.md). Holding needs no event: after the join every later use of
+    the freed blocks on the compute stream is ordered behind the side stream.
+    ``out``: the weight gradient the side stream writes. Never held: autograd steals a gradient
+    only while nothing else references it, and would otherwise copy it on a stream that is not
+    ordered after the side stream; it lives until the gather that follows the join anyway."""
+    if side is None:
+        return
+    if WgradStream.hold:
+        # keyed by the stream the tensors belong to (the compute stream issuing this backward):
+        # only a join ON that stream may release them
+        key = (side.device.index, torch.cuda.current_stream(side.device).cuda_stream)
+        WgradStream._held.setdefault(key, []).extend(t for t in ts if t is not None)
+        return
+    for t in ts + (out,):
+        if t is not None:
+            t.record_stream(side)
 
 
 def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None):
@@ -688,7 +714,7 @@ def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None):
         m.conv_wgrad(dev, side.cuda_stream if side is not None else st, nb, h, w, c, co, r, s, stride, pad,
                      dz.data_ptr(), x.data_ptr(), dw.data_ptr(), ws.data_ptr() if ws is not None else 0, 0.0, f32=f32,
                      **_wgrad_kw(dz, getattr(ctx, "xamax", None), f32, side, keep))
-        _used_on(side, dz, x, dw, ws)
+        _used_on(side, dz, x, ws, out=dw)
     return dx, dw
 
 

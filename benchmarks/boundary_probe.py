@@ -70,6 +70,40 @@ def main():
         marks.append(("amax_of", time.perf_counter()))
         return am0(*a, **k)
     C._tile_stats, C.amax_of = ts, am
+    import mpit_amd.train as T
+    from mpit_amd.optim import distributed as D
+
+    step0, dp0 = tr._step, D.downpour
+
+    def step_in():
+        marks.append(("_step", time.perf_counter()))
+        return step0()
+    tr._step = step_in
+
+    def dp(*a, **k):
+        marks.append(("downpour", time.perf_counter()))
+        return dp0(*a, **k)
+    D.downpour = dp
+    T.dopt.downpour = dp
+    armcpu = []
+    pusher = tr.opt_config.get("pusher") if getattr(tr, "opt_config", None) else None
+    if pusher is not None:
+        arm0 = pusher.arm
+
+        def arm(*a, **k):
+            c0 = time.thread_time()
+            marks.append(("arm", time.perf_counter()))
+            r = arm0(*a, **k)
+            marks.append(("arm_done", time.perf_counter()))
+            armcpu.append((time.thread_time() - c0) * 1e6)
+            return r
+        pusher.arm = arm
+    fe0 = tr._feval
+
+    def fe(w):
+        marks.append(("feval", time.perf_counter()))
+        return fe0(w)
+    tr._feval = fe
     C._StemConvFn.forward = staticmethod(fwd)
     C._StemPackBuf.get = classmethod(get)
     C.stem_weight_planes = swp
@@ -79,6 +113,16 @@ def main():
     from mpit_amd.train import gc_settle
 
     gc_settle()  # as bench.py's timed region
+    import gc
+
+    gcs, gct = [], {}
+
+    def gcb(phase, info):
+        if phase == "start":
+            gct["t"] = time.perf_counter()
+        else:
+            gcs.append((info.get("generation"), (time.perf_counter() - gct.get("t", time.perf_counter())) * 1e6))
+    gc.callbacks.append(gcb)
     marks.clear()
     ms0 = torch.cuda.memory_stats()
     for _ in range(steps):
@@ -98,6 +142,13 @@ def main():
             if "cast_call" in seq[j:]:
                 k = seq.index("cast_call", j)
                 out["step_ret_to_next_cast_us"].append((t[k] - t[j]) * 1e6)
+        if n == "step_call":
+            for a, b in (("step_call", "_step"), ("_step", "downpour"), ("downpour", "arm"), ("arm", "arm_done"),
+                         ("arm_done", "feval"), ("feval", "cast_call")):
+                if a in seq[i:] and b in seq[i:]:
+                    ia = seq.index(a, i)
+                    ib = seq.index(b, ia)
+                    out.setdefault(f"{a}->{b}_us", []).append((t[ib] - t[ia]) * 1e6)
         if n == "cast_call":
             out["cast_launch_us"].append((t[i + 1] - t[i]) * 1e6)
             for a, b in (("cast_done", "stem_fwd"), ("stem_fwd", "stem_pack_done"), ("stem_pack_done", "stem_planes"),
@@ -111,6 +162,17 @@ def main():
     ms1 = torch.cuda.memory_stats()
     alloc = {k: ms1.get(k, 0) - ms0.get(k, 0) for k in ("num_device_alloc", "num_device_free", "num_alloc_retries",
                                                          "num_sync_all_streams")}
+    gc.callbacks.remove(gcb)
+    gcsum = {}
+    for g, us in gcs:
+        c = gcsum.setdefault(f"gen{g}", [0, 0.0])
+        c[0] += 1
+        c[1] += us
+    if armcpu:
+        print(json.dumps({"arm_thread_cpu_us_median": round(sorted(armcpu)[len(armcpu) // 2], 1),
+                          "arm_thread_cpu_us_max": round(max(armcpu), 1)}), flush=True)
+    print(json.dumps({"gc_per_step": {k: [round(v[0] / steps, 2), round(v[1] / steps, 1)] for k, v in gcsum.items()}}),
+          flush=True)
     print(json.dumps({"dtype": dt, "median_us": summ, "allocator_deltas_over_steps": alloc, "steps": steps,
                       "alloc_conf": os.environ.get("PYTORCH_HIP_ALLOC_CONF") or os.environ.get("PYTORCH_CUDA_ALLOC_CONF")}),
           flush=True)

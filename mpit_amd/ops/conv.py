@@ -75,6 +75,7 @@ class WgradStream:
     # tensors the side stream uses, per device, released at join (see _used_on)
     hold = os.environ.get("MPIT_SIDE_HOLD", "1") != "0"
     _held = {}
+    _ev = {}
     # MPIT_WGRAD_AFTER=1: the side stream starts a convolution's weight gradient after its
     # input-gradient GEMM (so it overlaps the memory-bound BN backward that follows instead
     # of sharing the CUs with that compute-bound GEMM); default: before it
@@ -96,7 +97,13 @@ class WgradStream:
         if not cls.enabled:
             return None
         st = cls.side(dev)
-        st.wait_stream(torch.cuda.current_stream(dev))
+        # one reused event per device (Stream.wait_stream creates a new HIP event per call: ~53
+        # per ResNet-50 step); re-recording is safe, the wait below was queued with this record
+        ev = cls._ev.get(dev.index)
+        if ev is None:
+            ev = cls._ev[dev.index] = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+        st.wait_event(ev)
         if _SIDE_DELAY:  # race diagnostics: every weight gradient lands late
             with torch.cuda.stream(st):
                 torch.cuda._sleep(_SIDE_DELAY)

@@ -23,6 +23,7 @@ control records. Servers may be co-located with workers on every GPU (the defaul
 """
 from __future__ import annotations
 
+import gc
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence
 
@@ -40,6 +41,8 @@ _SYNC_GATE = __import__("os").environ.get("MPIT_DEBUG_SYNC_GATE", "0") == "1"
 # MPIT_DEBUG_NO_SHARD_SYNC=1 (diagnostics only): the round-3 behaviour, shard fills not ordered
 # before the server stream (tests/test_ps_gpu.py shows it fails then)
 _NO_SHARD_SYNC = __import__("os").environ.get("MPIT_DEBUG_NO_SHARD_SYNC", "0") == "1"
+# MPIT_GC_AT_WAIT=0: leave Python's young-generation collections where they fall (see PClient.wait)
+_GC_AT_WAIT = __import__("os").environ.get("MPIT_GC_AT_WAIT", "1") != "0"
 
 TAGS = dict(recv_init=1, recv_grad=2, send_param=3, recv_param=4, recv_header=5, recv_stop=6,
             recv_param_tail=7, recv_grad_tail=8)
@@ -436,6 +439,12 @@ class PClient:
         return self.native.pending()
 
     def wait(self):
+        if _GC_AT_WAIT and self.native.pending() and gc.isenabled():
+            # the young generation's collection (~50 us, about once per training step) runs
+            # here, where the host would block anyway, instead of wherever the allocation count
+            # next crosses the threshold — which was the start of the next step, while the
+            # GPU waits for its first kernels (profiles/boundary_r04/README.md)
+            gc.collect(0)
         with _trace.range("ps_wait"):
             self.native.wait()
         if self._pull_pending:

@@ -77,6 +77,7 @@ class Trainer:
         # then only take the CUs the critical path leaves free, instead of delaying its small
         # kernels (BN finalize, apply) behind big split-K GEMMs. MPIT_HP_STREAM=0: off.
         self.hp_stream = None
+        self._hp_ev = None  # reused step-boundary events (step)
         if self.on_gpu and os.environ.get("MPIT_HP_STREAM", "1") != "0" and not st.shared_devices:
             lo, hi = torch.cuda.Stream.priority_range()
             self.hp_stream = torch.cuda.Stream(self.device, priority=min(lo, hi))
@@ -254,11 +255,17 @@ class Trainer:
             if self.hp_stream is None:
                 return self._step()
             cur = torch.cuda.current_stream(self.device)
+            if self._hp_ev is None:
+                # two reused events: Stream.wait_stream creates (and later destroys) a new HIP
+                # event per call, tens of us of host time at the step boundary while the GPU idles
+                self._hp_ev = (torch.cuda.Event(), torch.cuda.Event())
             with _trace.range("hp_wait"):
-                self.hp_stream.wait_stream(cur)
+                self._hp_ev[0].record(cur)
+                self.hp_stream.wait_event(self._hp_ev[0])
             with torch.cuda.stream(self.hp_stream):
                 fx = self._step()
-            cur.wait_stream(self.hp_stream)
+            self._hp_ev[1].record(self.hp_stream)
+            cur.wait_event(self._hp_ev[1])
             return fx
 
     def _step(self):

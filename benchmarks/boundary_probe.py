@@ -27,15 +27,24 @@ def main():
     pc = tr.pc
     wait0 = pc.wait
 
+    import resource
+
+    flt = []
+
+    def _minflt():
+        return resource.getrusage(getattr(resource, "RUSAGE_THREAD", resource.RUSAGE_SELF)).ru_minflt
+
     def wait():
         t0 = time.perf_counter()
         wait0()
         marks.append(("wait_in", t0))
         marks.append(("wait_out", time.perf_counter()))
+        flt.append(["w", _minflt()])
     pc.wait = wait
     run0 = tr.wcast.run
 
     def run():
+        flt.append(["c", _minflt()])
         marks.append(("cast_call", time.perf_counter()))
         run0()
         marks.append(("cast_done", time.perf_counter()))
@@ -90,13 +99,21 @@ def main():
     if pusher is not None:
         arm0 = pusher.arm
 
-        def arm(*a, **k):
-            c0 = time.thread_time()
+        def arm(a_, aux=None, b=0.0):
+            c = [time.thread_time()]
             marks.append(("arm", time.perf_counter()))
-            r = arm0(*a, **k)
+            pusher.a, pusher.aux, pusher.b = a_, aux, b
+            c.append(time.thread_time())
+            for kk, mm in enumerate(pusher.members):
+                pusher.left[kk] = len(mm)
+                pusher.fired[kk] = False
+            c.append(time.thread_time())
+            pusher.gathered[:] = pusher._nots
+            c.append(time.thread_time())
+            c.append(time.thread_time())
+            pusher.armed = True
             marks.append(("arm_done", time.perf_counter()))
-            armcpu.append((time.thread_time() - c0) * 1e6)
-            return r
+            armcpu.append([(c[j + 1] - c[j]) * 1e6 for j in range(len(c) - 1)])
         pusher.arm = arm
     fe0 = tr._feval
 
@@ -123,6 +140,8 @@ def main():
         else:
             gcs.append((info.get("generation"), (time.perf_counter() - gct.get("t", time.perf_counter())) * 1e6))
     gc.callbacks.append(gcb)
+    if os.environ.get("PROBE_GC_OFF") == "1":
+        gc.disable()
     marks.clear()
     ms0 = torch.cuda.memory_stats()
     for _ in range(steps):
@@ -168,9 +187,13 @@ def main():
         c = gcsum.setdefault(f"gen{g}", [0, 0.0])
         c[0] += 1
         c[1] += us
+    d = [b[1] - a[1] for a, b in zip(flt, flt[1:]) if a[0] == "w" and b[0] == "c"]
+    if d:
+        print(json.dumps({"minor_faults_wait_out_to_cast_median": sorted(d)[len(d) // 2], "max": max(d)}), flush=True)
     if armcpu:
-        print(json.dumps({"arm_thread_cpu_us_median": round(sorted(armcpu)[len(armcpu) // 2], 1),
-                          "arm_thread_cpu_us_max": round(max(armcpu), 1)}), flush=True)
+        cols = list(zip(*armcpu))
+        print(json.dumps({"arm_line_cpu_us_median": [round(sorted(c)[len(c) // 2], 1) for c in cols],
+                          "arm_line_cpu_us_max": [round(max(c), 1) for c in cols]}), flush=True)
     print(json.dumps({"gc_per_step": {k: [round(v[0] / steps, 2), round(v[1] / steps, 1)] for k, v in gcsum.items()}}),
           flush=True)
     print(json.dumps({"dtype": dt, "median_us": summ, "allocator_deltas_over_steps": alloc, "steps": steps,

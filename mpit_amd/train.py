@@ -150,6 +150,15 @@ class Trainer:
 
             plan = WeightCastPlan(self.model, torch.bfloat16 if cfg.amp else torch.float32)
             self.wcast = plan if plan.njobs else None
+        # Downpour su = 1 with pushed gradients and a waited pull: the weights change only by
+        # the pulls, which have landed when step() returns, so the next step's weight casts
+        # are queued right then (the GPU runs them while the host does the step boundary's
+        # bookkeeping) instead of at the next forward. Anything else that writes the weights
+        # between steps calls invalidate_precast() (load_checkpoint, set_amp). MPIT_PRECAST=0: off.
+        self._precast_ok = (self.wcast is not None and self.push_steal
+                            and not self.opt_config.get("defer_wait", False)
+                            and os.environ.get("MPIT_PRECAST", "1") != "0") if self.on_gpu else False
+        self._precast = False
         self.steps = 0
 
     # ------------------------------------------------------------------ setup
@@ -221,9 +230,10 @@ class Trainer:
         self._retire_deferred()  # the previous step's pulls land in w before anything reads it
         if not getattr(self, "steal", False):
             self.flat.zero_grad()
-        if self.wcast is not None:  # the weights as they are now, for this forward/backward only
+        if self.wcast is not None and not self._precast:  # the weights as they are now, for this step only
             with _trace.range("wcast"):
                 self.wcast.run()
+        self._precast = False
         try:
             with _trace.range("fwd"):
                 if self.on_gpu and self.cfg.amp:
@@ -253,7 +263,9 @@ class Trainer:
         """One training step of this worker; returns the loss tensor (not synced)."""
         with _trace.range("step"):
             if self.hp_stream is None:
-                return self._step()
+                fx = self._step()
+                self._precast_next()
+                return fx
             cur = torch.cuda.current_stream(self.device)
             if self._hp_ev is None:
                 # two reused events: Stream.wait_stream creates (and later destroys) a new HIP
@@ -264,9 +276,23 @@ class Trainer:
                 self.hp_stream.wait_event(self._hp_ev[0])
             with torch.cuda.stream(self.hp_stream):
                 fx = self._step()
+                self._precast_next()
             self._hp_ev[1].record(self.hp_stream)
             cur.wait_event(self._hp_ev[1])
             return fx
+
+    def _precast_next(self):
+        """Queue the next step's weight casts now (see __init__, ``_precast_ok``)."""
+        if self._precast_ok and self.wcast is not None:
+            with _trace.range("wcast"):
+                self.wcast.run()
+            self._precast = True
+
+    def invalidate_precast(self):
+        """The weights were written outside a step: the next step casts them anew."""
+        if self._precast and self.wcast is not None:
+            self.wcast.invalidate()
+        self._precast = False
 
     def _step(self):
         c = self.cfg
@@ -322,6 +348,7 @@ class Trainer:
 
         self.sync()
         self.barrier()
+        self.invalidate_precast()  # the flat weights are about to be replaced
         path = path or checkpoint.latest(directory, self.rank)
         if path is None:
             raise FileNotFoundError(f"no checkpoint of rank {self.rank} in {directory}")
@@ -348,6 +375,7 @@ class Trainer:
         the per-step weight plan follow the new dtype."""
         if amp == self.cfg.amp:
             return
+        self.invalidate_precast()
         self.cfg.amp = amp
         if self.on_gpu:
             self.x = self.x.to(torch.bfloat16 if amp else torch.float32)
@@ -386,6 +414,7 @@ class Trainer:
         if self.ps_server is not None:
             self.ps_server.native.sync()
             mine["server"] = bits(self.ps_server.p)
+        self.invalidate_precast()  # the pull above rewrote the weights
         allv = W.allgather_obj(mine)
         srv = {v["rank"]: v["server"] for v in allv if v["server"] is not None}
         bad = []

@@ -83,6 +83,8 @@ class WgradStream:
 
     @classmethod
     def enable(cls, on: bool = True):
+        if cls.enabled and not on and torch.cuda.is_available():
+            cls.join()  # release what is held for the current stream(s) before switching off
         cls.enabled = bool(on) and os.environ.get("MPIT_WGRAD_STREAM", "1") != "0"
 
     @staticmethod
@@ -645,6 +647,9 @@ def conv_weights(weight: torch.Tensor, dgrad: bool, dtype=torch.bfloat16):
     return wb, wt
 
 
+_HOLD_MAX = 4096  # tensors held for one stream before _used_on joins by itself
+
+
 def _used_on(side, *ts, out=None):
     """Keep tensors the side stream reads or writes from being recycled before it is done:
     held until the next :meth:`WgradStream.join` (default), or ``record_stream`` (MPIT_SIDE_HOLD=0).
@@ -662,7 +667,10 @@ def _used_on(side, *ts, out=None):
         # keyed by the stream the tensors belong to (the compute stream issuing this backward):
         # only a join ON that stream may release them
         key = (side.device.index, torch.cuda.current_stream(side.device).cuda_stream)
-        WgradStream._held.setdefault(key, []).extend(t for t in ts if t is not None)
+        held = WgradStream._held.setdefault(key, [])
+        held.extend(t for t in ts if t is not None)
+        if len(held) > _HOLD_MAX:  # a caller that never joins: bound the memory, keep it correct
+            WgradStream.join()
         return
     for t in ts + (out,):
         if t is not None:

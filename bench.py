@@ -30,6 +30,10 @@ The last pulls of a step are waited for at the end of that step (the reference's
 push, pull, wait: asyncsgd/optim-downpour.lua:50-53); ``--defer-ps-wait`` retires them at
 the next step's first read of the weights instead (measured slower, off by default).
 
+``peak_mem_gib``: the device memory peak of the headline run (torch.cuda.max_memory_allocated).
+The next step's weight casts are queued as soon as a step's pulls have landed (the weights
+change only by the pulls; mpit_amd/train.py precast): that is part of each timed step.
+
 Also reported, outside the timed region (``--no-secondary`` skips them):
 * ``ps_check``: after the run every worker pulls every shard again and the exact bit-sums
   of each shard must agree between all workers and the owning server (exit status 3 if

@@ -2120,7 +2120,7 @@ int64_t gemm_nt_fold_lvl_floats(int N) { return int64_t(kFoldMaxGroups) * 2 * N;
 // Block tile of gemm_nt: 0 = 128 x (128 | 64), 1 = 256 x 128, 2 = 256 x 256;
 // MPIT_GEMM_TILE=128|256x128|256 selects one (A/B runs, large plain GEMMs). fp32 runs the
 // 128-row tiles only (its MFMA is 16x slower per FLOP: LDS-bound tile shapes do not matter).
-static int nt_tile_config(int N, int K, bool conv, int cin_conv, bool f32) {
+static int nt_tile_config(int64_t M, int N, int K, bool conv, int cin_conv, bool f32) {
   static const int forced = [] {
     const char* e = std::getenv("MPIT_GEMM_TILE");
     if (!e) return -1;
@@ -2136,12 +2136,16 @@ static int nt_tile_config(int N, int K, bool conv, int cin_conv, bool f32) {
     }();
     return f32_forced == 1 && N % 128 == 0 ? 1 : 0;
   }
-  int cfg = forced >= 0 ? forced : 0;
   // Measured (profiles/gemm_big_tile_ab_r01.jsonl, gemm_bk64_128tile_ab_r01.jsonl): 256x256
   // (BK 64) beats 128x128 on large square GEMMs (8192^3: 944 vs 611 TFLOP/s) and 256x128 on
-  // 50176x256x2304 (+18 %), yet inside the models both lose end to end (ResNet-50 -1.6 %,
-  // VGG-16 -2.7 %, AlexNet -2.7 %: one or two blocks per CU leave the epilogue and the
-  // other streams nothing to overlap with), so the automatic choice stays 128x128.
+  // 50176x256x2304 (+18 %), yet inside the models all-256 tiles lose end to end (round 1:
+  // ResNet-50 -1.6 %, VGG-16 -2.7 %; round 4: ResNet-50 bf16 -3 %): one or two blocks per CU
+  // leave the epilogue and the other streams nothing to overlap with. Round 4: 256x128 only
+  // where K is deep (>= 1024) AND the grid still has >= 4 blocks per CU — VGG-16's 112/56-
+  // pixel 3x3 convolutions and their backward-data, no ResNet-50 shape — VGG-16 bf16 EASGD
+  // +3.5 % (4,944 vs 4,774 / 4,824 img/s with every GEMM on 256x128, gpurun_out/r04vgg).
+  int cfg = forced >= 0 ? forced
+                        : (K >= 1024 && N % 128 == 0 && ((M + 255) / 256) * int64_t(N / 128) >= 1024 ? 1 : 0);
   if (cfg == 2 && (N % 256 || K % 64 || (conv && cin_conv % 64))) cfg = N % 128 ? 0 : 1;
   if (cfg == 1 && N % 128) cfg = 0;
   return cfg;
@@ -2402,7 +2406,7 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
     if (geo) MPIT_NT_LAUNCH2(BM, BN, ST, true);                                                           \
     else MPIT_NT_LAUNCH2(BM, BN, ST, false);                                                              \
   } while (0)
-  const int tcfg = fm == 4 || fm >= 9 ? 0 : nt_tile_config(N, K, geo != nullptr, geo ? geo->C : 0, F32);
+  const int tcfg = fm == 4 || fm >= 9 ? 0 : nt_tile_config(M, N, K, geo != nullptr, geo ? geo->C : 0, F32);
   if constexpr (F32) {
     if (tcfg == 1) {
       MPIT_NT_LAUNCH(256, 128, 3);

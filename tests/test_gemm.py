@@ -40,7 +40,8 @@ def _rel(a, b):
 
 @gpu
 @pytest.mark.parametrize("M,N,K", [(128, 64, 64), (256, 128, 64), (1000, 192, 128), (4096, 256, 512),
-                                   (333, 64, 1024), (12544, 2048, 512), (50176, 256, 1024)])
+                                   (333, 64, 1024), (12544, 2048, 512), (50176, 256, 1024),
+                                   (262144, 128, 1024), (262000, 256, 2048)])  # (auto 256x128 tiles)
 def test_gemm_nt(M, N, K):
     torch.manual_seed(M + N + K)
     a, b = _bf(M, K), _bf(N, K, scale=0.05)
@@ -51,7 +52,7 @@ def test_gemm_nt(M, N, K):
 
 
 @gpu
-@pytest.mark.parametrize("M,N,K", [(256, 64, 64), (1000, 128, 192), (4096, 256, 256)])
+@pytest.mark.parametrize("M,N,K", [(256, 64, 64), (1000, 128, 192), (4096, 256, 256), (262100, 128, 1024)])
 def test_gemm_nt_stats(M, N, K):
     torch.manual_seed(1)
     a, b = _bf(M, K), _bf(N, K, scale=0.05)
@@ -165,7 +166,8 @@ def test_park_grad_slot_protocol():
 @gpu
 @pytest.mark.parametrize("n,ci,co,hw,k,relu", [(2, 64, 192, 13, 5, True), (3, 192, 384, 13, 3, True),
                                                (16, 64, 64, 56, 3, True),
-                                               (2, 128, 64, 9, 3, False)])
+                                               (2, 128, 64, 9, 3, False),
+                                               (16, 128, 128, 128, 3, True)])  # (auto 256x128 tiles)
 def test_conv_act_bias_relu(n, ci, co, hw, k, relu):
     """conv + bias + ReLU with the bias / ReLU in the GEMM epilogue and the one-pass
     ReLU/bias backward, against fp32 PyTorch; ReLU mask flips of near-zero outputs under

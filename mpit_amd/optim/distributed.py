@@ -80,6 +80,7 @@ def downpour(opfunc, w, config, state=None):
             pusher.abort()  # no pushes of half-computed shards
             raise
         pusher.finish()
+        pusher.reset()  # the next step's counters, while the pulls are still in flight
         if config.get("defer_wait"):
             # the caller retires the pulls right before its next read of w (mpit_amd/train.py
             # Trainer._feval / sync): the host's step bookkeeping then overlaps the servers'

@@ -62,6 +62,7 @@ class ShardPusher:
         self.gathered = [False] * len(self.params)
         self.fired = [False] * self.nshards
         self._nots = [False] * len(self.params)
+        self._reset = False
         self.armed = False
         self.handles = [p.register_post_accumulate_grad_hook(self._hook) for p in self.params]
 
@@ -73,11 +74,20 @@ class ShardPusher:
     def arm(self, a: float, aux=None, b: float = 0.0):
         """Before the backward: gradients will be pushed as ``a*g + b*aux``."""
         self.a, self.aux, self.b = a, aux, b
+        if not self._reset:
+            self.reset()
+        self._reset = False
+        self.armed = True
+
+    def reset(self):
+        """The per-step counters back to a fresh step. The optimizer calls it once the step's
+        last shard has fired and before it blocks on the PS (optim/distributed.py downpour),
+        so this host work overlaps the wait instead of following it."""
         for k, m in enumerate(self.members):
             self.left[k] = len(m)
             self.fired[k] = False
         self.gathered[:] = self._nots
-        self.armed = True
+        self._reset = True
 
     def _hook(self, p):
         if not self.armed:

@@ -150,6 +150,8 @@ def main(argv=None) -> int:
                     help="K > 1: split the (single) server's shard into K shards, each pushed from inside the "
                          "backward and served through the remote-client pipeline (link stream, inbox / outbox) — "
                          "one GPU carrying the per-worker shard traffic of an N=K job (diagnostic, not the headline)")
+    ap.add_argument("--no-rccl-fallback", action="store_true",
+                    help="fail (exit 3) when the pre-flight check fails instead of switching to datapath 3")
     ap.add_argument("--defer-ps-wait", action="store_true",
                     help="retire a step's last pulls at the next step's first weight read instead of at the "
                          "end of the step (profiles/defer_ps_wait_ab_r03.md: slower; off by default)")
@@ -183,9 +185,10 @@ def main(argv=None) -> int:
     try:
         tr = _make(a, mp_train, amp, a.topology, a.servers, 0)
     except PSMapError as e:  # a peer window could not be mapped (every rank raised it)
-        if a.datapath == 3 or mp.runtime.state().shared_devices:
+        if a.datapath == 3 or mp.runtime.state().shared_devices or a.no_rccl_fallback:
             raise
-        fallback = {"from_datapath": a.datapath, "reason": f"window mapping: {e}"}
+        fallback = {"from_datapath": a.datapath, "reason": f"window mapping: {e}",
+                    "unverified": "datapath 3's RCCL device path is exercised here for the first time"}
         a.datapath = 3
         tr = _make(a, mp_train, amp, a.topology, a.servers, 2)
     preflight = None
@@ -196,9 +199,15 @@ def main(argv=None) -> int:
         # the job to the two-sided RCCL data plane (datapath 3, csrc/core/link.h) and checks
         # again; a pair still broken ends the run here, named, before any timing.
         preflight = tr.preflight()
-        if not preflight["ok"] and a.datapath != 3 and not mp.runtime.state().shared_devices:
+        if (not preflight["ok"] and a.datapath != 3 and not mp.runtime.state().shared_devices
+                and not a.no_rccl_fallback):
+            # datapath 3 is deadlock-free by construction (csrc/core/link.h) and its clients
+            # wait at most MPIT_PS_TIMEOUT_S (300 s default there) before failing with a named
+            # error; its RCCL device path had not run on distinct GPUs before such a job, so
+            # the JSON says so
             fallback = {"from_datapath": a.datapath, "reason": f"pre-flight: no peer access {preflight['no_peer']}, "
-                                                                 f"pulled shard bits differ {preflight['mismatches']}"}
+                                                                 f"pulled shard bits differ {preflight['mismatches']}",
+                        "unverified": "datapath 3's RCCL device path is exercised here for the first time"}
             tr.stop()
             a.datapath = 3
             tr = _make(a, mp_train, amp, a.topology, a.servers, 2)

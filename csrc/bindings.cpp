@@ -439,20 +439,19 @@ PYBIND11_MODULE(_mpit, m) {
       .def("set_link", &PSClient::set_link, py::keep_alive<1, 2>());
 
   py::class_<PsLink>(m, "PsLink")
-      .def(py::init<Engine&, int, std::vector<int>, std::vector<int>, bool>(), py::keep_alive<1, 2>())
+      .def(py::init<Engine&, int, std::vector<int>, bool>(), py::keep_alive<1, 2>())
       .def_property_readonly("device", &PsLink::device)
-      .def("make_ids",
-           [](PsLink& l) {
-             py::list out;
-             for (auto& [c, id] : l.make_ids()) out.append(py::make_tuple(c, py::bytes(id)));
-             return out;
-           })
+      .def_property_readonly("legacy", &PsLink::legacy)
+      .def_property_readonly("sequencer", &PsLink::sequencer)
+      .def("make_id", [](PsLink& l) { return py::bytes(l.make_id()); })
       .def("connect",
-           [](PsLink& l, std::vector<std::tuple<int, int, py::bytes>> ids) {
-             std::vector<std::tuple<int, int, std::string>> v;
-             for (auto& [s, c, b] : ids) v.emplace_back(s, c, std::string(b));
+           [](PsLink& l, py::bytes id) {
+             std::string v(id);
              py::gil_scoped_release r;
              l.connect(v);
            })
-      .def("stats", [](PsLink& l) { return py::dict(py::arg("bytes_sent") = l.bytes_sent(), py::arg("bytes_recv") = l.bytes_recv()); });
+      .def("stats", [](PsLink& l) {
+        return py::dict(py::arg("bytes_sent") = l.bytes_sent(), py::arg("bytes_recv") = l.bytes_recv(),
+                        py::arg("ordered") = l.ordered(), py::arg("groups") = l.groups());
+      });
 }

@@ -1,8 +1,10 @@
 #include "link.h"
 
 #include <dlfcn.h>
+#include <unistd.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
@@ -60,139 +62,296 @@ void hipl(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string("mpit link HIP error in ") + what + ": " + hipGetErrorString(e));
 }
 
+bool env_on(const char* n) {
+  const char* e = std::getenv(n);
+  return e && std::atoi(e) != 0;
+}
+
+// the sequencer's notice of one transfer (AM payload, <= 64 bytes)
+struct Notice {
+  int64_t xid;    // the server's id of the transfer
+  int64_t coff;   // client buffer byte offset
+  int64_t bytes;
+  int32_t server, client;
+  int32_t to_client, window;
+};
+static_assert(sizeof(Notice) <= 64, "notice must fit an active message");
+
 }  // namespace
 
-PsLink::PsLink(Engine& eng, int ps_id, std::vector<int> servers, std::vector<int> clients, bool device)
-    : eng_(eng),
-      ps_id_(ps_id),
-      servers_(std::move(servers)),
-      clients_(std::move(clients)),
-      device_(device),
-      ctx_((1 << 26) + ps_id) {
+PsLink::PsLink(Engine& eng, int ps_id, std::vector<int> members, bool device)
+    : eng_(eng), ps_id_(ps_id), members_(std::move(members)), device_(device), ctx_((1 << 26) + ps_id) {
+  if (members_.empty()) throw std::invalid_argument("mpit: PS link without members");
   if (device_ && eng_.device() < 0) throw std::invalid_argument("mpit: device PS link on a rank without a device");
-  if (!device_) hook_ = eng_.add_hook([this] { return poll(); });
+  legacy_ = !device_ && env_on("MPIT_LINK_LEGACY");
+  rdv_ = !device_ && env_on("MPIT_LINK_RDV");
+  if (const char* e = std::getenv("MPIT_LINK_JITTER_US")) jitter_us_ = std::max(0, std::atoi(e));
+  rng_.seed(uint32_t(eng_.rank() * 7919 + ps_id * 104729 + (std::getenv("MPIT_LINK_SEED") ? std::atoi(std::getenv("MPIT_LINK_SEED")) : 0)));
+  if (device_) {
+    hipl(hipSetDevice(eng_.device()), "hipSetDevice");
+    int lo = 0, hi = 0;
+    hipl(hipDeviceGetStreamPriorityRange(&lo, &hi), "priority range");
+    hipl(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi), "link stream");
+  }
+  eng_.register_am(am_req(), [this](const Msg& m) { on_req(m); });
+  eng_.register_am(am_post(), [this](const Msg& m) { on_post(m); });
+  eng_.register_am(am_cts(), [this](const Msg& m) {
+    std::lock_guard<std::mutex> g(mu_);
+    ++cts_got_[m.src];
+  });
+  hook_ = eng_.add_hook([this] { return poll(); });
 }
 
 PsLink::~PsLink() {
   if (hook_ >= 0) eng_.remove_hook(hook_);
-  if (!comms_.empty()) {
+  for (int id : {am_req(), am_post(), am_cts()}) eng_.register_am(id, [](const Msg&) {});
+  if (device_) {
     hipSetDevice(eng_.device());
-    for (auto& kv : comms_) rccl().comm_destroy(static_cast<ncclComm_t>(kv.second));
+    if (stream_) hipStreamSynchronize(stream_);
+    if (comm_) rccl().comm_destroy(static_cast<ncclComm_t>(comm_));
+    if (stream_) hipStreamDestroy(stream_);
   }
 }
 
-std::vector<std::pair<int, std::string>> PsLink::make_ids() {
-  std::vector<std::pair<int, std::string>> out;
-  if (!device_) return out;
-  const int me = eng_.rank();
-  if (std::find(servers_.begin(), servers_.end(), me) == servers_.end()) return out;
-  for (int c : clients_) {
-    if (c == me) continue;  // the co-located worker is served by the local fused kernel
-    ncclUniqueId id;
-    nccl_check(rccl().get_unique_id(&id), "ncclGetUniqueId");
-    out.emplace_back(c, std::string(id.internal, sizeof(id.internal)));
-  }
-  return out;
+int PsLink::index_of(int world_rank) const {
+  for (size_t i = 0; i < members_.size(); ++i)
+    if (members_[i] == world_rank) return int(i);
+  throw std::invalid_argument("mpit: rank " + std::to_string(world_rank) + " is not a member of PS " + std::to_string(ps_id_));
 }
 
-void PsLink::connect(const std::vector<std::tuple<int, int, std::string>>& ids) {
+std::string PsLink::make_id() {
+  if (!device_ || eng_.rank() != sequencer()) return {};
+  ncclUniqueId id;
+  nccl_check(rccl().get_unique_id(&id), "ncclGetUniqueId");
+  return std::string(id.internal, sizeof(id.internal));
+}
+
+void PsLink::connect(const std::string& blob) {
   if (!device_) return;
-  const int me = eng_.rank();
-  std::vector<std::tuple<int, int, ncclUniqueId>> mine;
-  for (const auto& [s, c, blob] : ids) {
-    if (s != me && c != me) continue;
-    if (blob.size() != NCCL_UNIQUE_ID_BYTES) throw std::invalid_argument("mpit: bad RCCL unique id");
-    ncclUniqueId id;
-    std::memcpy(id.internal, blob.data(), sizeof(id.internal));
-    mine.emplace_back(s, c, id);
-  }
+  if (blob.size() != NCCL_UNIQUE_ID_BYTES) throw std::invalid_argument("mpit: bad RCCL unique id");
+  ncclUniqueId id;
+  std::memcpy(id.internal, blob.data(), sizeof(id.internal));
   hipl(hipSetDevice(eng_.device()), "hipSetDevice");
-  // every communicator of this rank in one group: a rank in several pairs must not block in
-  // one pair's initialisation while its partner in another pair waits for it
-  nccl_check(rccl().group_start(), "ncclGroupStart");
-  std::vector<std::pair<std::pair<int, int>, ncclComm_t>> made(mine.size());
-  for (size_t i = 0; i < mine.size(); ++i) {
-    auto& [s, c, id] = mine[i];
-    made[i].first = {s, c};
-    nccl_check(rccl().comm_init_rank(&made[i].second, 2, id, s == me ? 0 : 1), "ncclCommInitRank");
+  ncclComm_t c = nullptr;
+  nccl_check(rccl().comm_init_rank(&c, int(members_.size()), id, index_of(eng_.rank())), "ncclCommInitRank");
+  comm_ = c;
+}
+
+void PsLink::jitter() {
+  if (jitter_us_ <= 0) return;
+  std::uniform_int_distribution<int> d(0, jitter_us_);
+  const int us = d(rng_);
+  if (us > jitter_us_ / 2) ::usleep(useconds_t(us));
+}
+
+// ------------------------------------------------------------------------------ ordering
+
+void PsLink::order(int client, bool to_client, int window, int64_t coff, int64_t bytes, std::function<void()> at_server) {
+  if (legacy_) {  // pre-sequencer layout (test only): the server queues its side at once
+    at_server();
+    return;
   }
-  nccl_check(rccl().group_end(), "ncclGroupEnd");
-  for (auto& [key, comm] : made) comms_[key] = comm;
+  Notice n{};
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    n.xid = next_xid_++;
+    at_server_[n.xid] = std::move(at_server);
+  }
+  n.coff = coff;
+  n.bytes = bytes;
+  n.server = eng_.rank();
+  n.client = client;
+  n.to_client = to_client ? 1 : 0;
+  n.window = window;
+  jitter();
+  eng_.send_am(sequencer(), am_req(), &n, sizeof(n));
 }
 
-void* PsLink::comm_of(int peer, bool as_server) const {
-  const int me = eng_.rank();
-  auto it = comms_.find(as_server ? std::make_pair(me, peer) : std::make_pair(peer, me));
-  if (it == comms_.end())
-    throw std::runtime_error("mpit: no RCCL link between rank " + std::to_string(me) + " and rank " +
-                             std::to_string(peer) + " (ps " + std::to_string(ps_id_) + ")");
-  return it->second;
+void PsLink::set_client(ClientFn at_client) {
+  std::lock_guard<std::mutex> g(mu_);
+  at_client_ = std::move(at_client);
 }
 
-void PsLink::send(int peer, bool as_server, const void* buf, int64_t bytes, hipStream_t s) {
+// sequencer: the arrival order of requests here IS the global order; the notices go out to
+// both endpoints in it (one FIFO control ring from here to each rank)
+void PsLink::on_req(const Msg& m) {
+  if (eng_.rank() != sequencer()) throw std::runtime_error("mpit: PS link request at a rank that is not the sequencer");
+  Notice n;
+  std::memcpy(&n, m.data, sizeof(n));
+  ++ordered_;
+  eng_.send_am(n.server, am_post(), &n, sizeof(n), 0);
+  if (n.client != n.server) eng_.send_am(n.client, am_post(), &n, sizeof(n), 1);
+}
+
+void PsLink::on_post(const Msg& m) {
+  Notice n;
+  std::memcpy(&n, m.data, sizeof(n));
+  jitter();
+  const bool as_client = m.aux0 == 1;
+  if (!as_client) {
+    std::function<void()> f;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      auto it = at_server_.find(n.xid);
+      if (it == at_server_.end()) throw std::runtime_error("mpit: PS link notice for an unknown transfer");
+      f = std::move(it->second);
+      at_server_.erase(it);
+    }
+    f();
+  } else {
+    ClientFn c;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      c = at_client_;
+    }
+    if (!c) throw std::runtime_error("mpit: PS link notice for a client that has no link buffers");
+    c(n.server, n.to_client != 0, n.window, n.coff, n.bytes);
+  }
+}
+
+// ------------------------------------------------------------------------------ data ops
+
+void PsLink::send(int peer, const void* buf, int64_t bytes, hipEvent_t after) {
   if (bytes <= 0) return;
   bytes_sent_ += bytes;
   if (device_) {
-    nccl_check(rccl().send(buf, size_t(bytes), ncclUint8, as_server ? 1 : 0, static_cast<ncclComm_t>(comm_of(peer, as_server)), s),
-               "ncclSend");
+    if (after) {
+      flush_group();
+      hipl(hipStreamWaitEvent(stream_, after, 0), "link waits local work");
+    }
+    batch_.push_back({true, peer, const_cast<void*>(buf), bytes});
     return;
   }
-  const int64_t id = eng_.isend(buf, bytes, false, peer, tag_of(as_server), ctx_, false);
+  Op o{kSend};
+  o.peer = peer;
+  o.sbuf = buf;
+  o.bytes = bytes;
   std::lock_guard<std::mutex> g(mu_);
-  q_[{peer, as_server}].push_back(Item{id, nullptr});
+  q_.push_back(std::move(o));
 }
 
-void PsLink::recv(int peer, bool as_server, void* buf, int64_t bytes, hipStream_t s) {
+void PsLink::recv(int peer, void* buf, int64_t bytes, hipEvent_t after) {
   if (bytes <= 0) return;
   bytes_recv_ += bytes;
   if (device_) {
-    nccl_check(rccl().recv(buf, size_t(bytes), ncclUint8, as_server ? 1 : 0, static_cast<ncclComm_t>(comm_of(peer, as_server)), s),
-               "ncclRecv");
+    if (after) {
+      flush_group();
+      hipl(hipStreamWaitEvent(stream_, after, 0), "link waits local work");
+    }
+    batch_.push_back({false, peer, buf, bytes});
     return;
   }
-  const int64_t id = eng_.irecv(buf, bytes, false, peer, tag_of(!as_server), ctx_);
+  Op o{kRecv};
+  o.peer = peer;
+  o.rbuf = buf;
+  o.bytes = bytes;
   std::lock_guard<std::mutex> g(mu_);
-  q_[{peer, as_server}].push_back(Item{id, nullptr});
+  q_.push_back(std::move(o));
 }
 
-void PsLink::then(int peer, bool as_server, hipStream_t s, std::function<void()> f) {
+void PsLink::then(std::function<void()> f) {
   if (device_) {
+    if (!batch_.empty()) {
+      batch_then_.push_back(std::move(f));  // after the group the pending ops go out in
+      return;
+    }
     hipEvent_t ev = eng_.get_event();
-    Engine::record_event(ev, s);
+    Engine::record_event(ev, stream_);
     eng_.track_copy(ev, std::move(f));
     return;
   }
+  call(std::move(f));
+}
+
+void PsLink::call(std::function<void()> f) {
+  if (device_) {
+    f();
+    return;
+  }
+  Op o{kCall};
+  o.f = std::move(f);
   {
     std::lock_guard<std::mutex> g(mu_);
-    q_[{peer, as_server}].push_back(Item{-1, std::move(f)});
+    q_.push_back(std::move(o));
   }
   eng_.kick();
 }
 
+void PsLink::record(hipEvent_t e) {
+  if (!device_) return;
+  flush_group();
+  hipl(hipEventRecord(e, stream_), "link record");
+}
+
+void PsLink::flush_group() {
+  if (!device_ || batch_.empty()) return;
+  hipl(hipSetDevice(eng_.device()), "hipSetDevice");
+  auto* c = static_cast<ncclComm_t>(comm_);
+  if (!c) throw std::runtime_error("mpit: PS link used before connect()");
+  nccl_check(rccl().group_start(), "ncclGroupStart");
+  for (const auto& o : batch_) {
+    const int pr = index_of(o.peer);
+    if (o.send) nccl_check(rccl().send(o.buf, size_t(o.bytes), ncclUint8, pr, c, stream_), "ncclSend");
+    else nccl_check(rccl().recv(o.buf, size_t(o.bytes), ncclUint8, pr, c, stream_), "ncclRecv");
+  }
+  nccl_check(rccl().group_end(), "ncclGroupEnd");
+  ++groups_;
+  batch_.clear();
+  std::vector<std::function<void()>> fs;
+  fs.swap(batch_then_);
+  if (!fs.empty()) {
+    hipEvent_t ev = eng_.get_event();
+    Engine::record_event(ev, stream_);
+    eng_.track_copy(ev, [fs] {
+      for (auto& f : fs) f();
+    });
+  }
+}
+
+// host: the FIFO as a stream. The head op starts when everything before it is done.
 bool PsLink::poll() {
+  if (device_) {
+    const bool did = !batch_.empty();
+    flush_group();
+    return did;
+  }
   bool did = false;
   for (;;) {
     std::function<void()> run;
     {
       std::lock_guard<std::mutex> g(mu_);
-      for (auto& kv : q_) {
-        auto& q = kv.second;
-        while (!q.empty() && q.front().req >= 0) {
-          Status st;
-          if (!eng_.test(q.front().req, &st)) break;
-          if (st.error) throw std::runtime_error("mpit: PS link transfer failed");
-          q.pop_front();
-          did = true;
+      if (q_.empty()) break;
+      Op& o = q_.front();
+      if (o.kind == kCall) {
+        run = std::move(o.f);
+        q_.pop_front();
+      } else if (o.kind == kSend) {
+        if (o.req < 0) {
+          // rendezvous: a send runs only against a receive at the head of the peer's FIFO
+          if (rdv_ && cts_got_[o.peer] <= cts_used_[o.peer]) break;
+          if (rdv_) ++cts_used_[o.peer];
+          o.req = eng_.isend(o.sbuf, o.bytes, false, o.peer, 1, ctx_, false);
         }
-        if (!q.empty() && q.front().req < 0) {
-          run = std::move(q.front().f);
-          q.pop_front();
-          break;
+        Status st;
+        if (!eng_.test(o.req, &st)) break;
+        if (st.error) throw std::runtime_error("mpit: PS link send failed");
+        q_.pop_front();
+        did = true;
+        continue;
+      } else {
+        if (o.req < 0) {
+          o.req = eng_.irecv(o.rbuf, o.bytes, false, o.peer, 1, ctx_);
+          if (rdv_) eng_.send_am(o.peer, am_cts(), nullptr, 0);
         }
+        Status st;
+        if (!eng_.test(o.req, &st)) break;
+        if (st.error) throw std::runtime_error("mpit: PS link receive failed");
+        q_.pop_front();
+        did = true;
+        continue;
       }
     }
-    if (!run) break;
-    run();  // may queue more transfers / continuations (lock released)
+    run();  // local work / continuation (may queue more ops; lock released)
     did = true;
   }
   return did;

@@ -73,19 +73,24 @@ PSServer::PSServer(Engine& eng, int ps_id, Window& rx, Window& tx, std::vector<i
     hipp(hipDeviceGetStreamPriorityRange(&lo, &hi), "priority range");
     hipp(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi), "server stream");
     if (datapath_ == 2 || datapath_ == 3) {
-      // link streams: at most 2 by default (MPIT_PS_LINK_STREAMS=k overrides), shared
-      // round-robin by the clients. A co-located N=8 process already holds the compute,
-      // priority, side, server, engine and RCCL streams; one link stream per client would
-      // put 7 more on the 4 hardware queues a process gets (GPU_MAX_HW_QUEUES), and queue
-      // oversubscription is what collapsed the 8-rank rehearsal
-      // (profiles/collapse_8rank_1gpu_r03.md). The per-client events keep every client's
-      // inbox / update / outbox order whatever stream it shares.
       const size_t nc = clients_.size();
-      size_t nl = std::min<size_t>(nc, 2);
-      if (const char* e = std::getenv("MPIT_PS_LINK_STREAMS"))
-        if (std::atoi(e) > 0) nl = std::min(nc, size_t(std::atoi(e)));
-      cstream_.resize(std::max<size_t>(nl, 1));
-      for (auto& cs : cstream_) hipp(hipStreamCreateWithPriority(&cs, hipStreamNonBlocking, hi), "link stream");
+      if (datapath_ == 2) {
+        // link streams. A server co-located with a worker shares its process with the
+        // compute, priority, side, server and engine streams; one link stream per client
+        // would put 7 more on the 4 hardware queues a process gets (GPU_MAX_HW_QUEUES), and
+        // queue oversubscription is what collapsed the 8-rank rehearsal
+        // (profiles/collapse_8rank_1gpu_r03.md): there at most 2, shared round-robin. A
+        // dedicated server (no compute of its own) keeps one per client, so one client's
+        // transfers never queue behind another's. MPIT_PS_LINK_STREAMS=k overrides. The
+        // per-client events keep every client's inbox / update / outbox order whatever
+        // stream it shares. (Datapath 3 moves its data on the PS link's one stream.)
+        const bool colocated = client_index(eng_.rank()) >= 0;
+        size_t nl = colocated ? std::min<size_t>(nc, 2) : nc;
+        if (const char* e = std::getenv("MPIT_PS_LINK_STREAMS"))
+          if (std::atoi(e) > 0) nl = std::min(nc, size_t(std::atoi(e)));
+        cstream_.resize(std::max<size_t>(nl, 1));
+        for (auto& cs : cstream_) hipp(hipStreamCreateWithPriority(&cs, hipStreamNonBlocking, hi), "link stream");
+      }
       ev_in_.resize(nc);
       ev_up_.resize(nc);
       ev_out_.resize(nc);
@@ -279,8 +284,9 @@ void PSServer::on_msg(const Msg& m) {
           for (auto& x : later) on_msg(x);
         }
       };
-      if (init_piece && !device_ && messaged(client_index(m.src), m.src)) {
-        // host link: the shard holds the initial parameters only once their message landed
+      if (init_piece && messaged(client_index(m.src), m.src)) {
+        // datapath 3: the shard holds the initial parameters only once their transfer's turn
+        // came (host: once the message landed; device: once the copy is queued on stream_)
         TraceRange tr("ps_server_param");
         maybe_fault(3);
         param_msg(m.src, client_index(m.src), (m.aux0 & kPsFromRx) != 0, sb, init_done);
@@ -569,10 +575,11 @@ void PSServer::do_grad(int c, bool pull, Sub sb) {
 }
 
 // ---- datapath 3: the shard's data as two-sided messages with a remote client (link.h) -----
-// Device: the same staging and stream choreography as the link-stream path of datapath 2,
-// with the peer copies replaced by RCCL recv / send on the client's link stream. Host (no
-// GPU): per-message buffers, each step a continuation once the previous one's transfer is
-// done (PsLink::then), in arrival order per client.
+// Every transfer is put in the instance's global order first (PsLink::order); this server's
+// side is queued when its turn comes. Device: the link stream carries the RCCL ops, the
+// update / snapshot kernels stay on stream_ (one stream per shard: every update of the shard
+// serialised), events order the two. Host (no GPU): per-transfer buffers, the link's FIFO runs
+// the receive, the update as a queued call, then the send — in the same order.
 
 void PSServer::grad_msg(int c, int ci, bool pull, bool defer_pull, Sub sb) {
   const int64_t es = grad_bf16_ ? 2 : 4;
@@ -586,40 +593,50 @@ void PSServer::grad_msg(int c, int ci, bool pull, bool defer_pull, Sub sb) {
       ++stats_.deferred;
     }
   }
+  const int64_t goff = (off_ + sb.o) * es, roff = (off_ + sb.o) * 4;
   if (device_) {
-    hipp(hipSetDevice(eng_.device()), "hipSetDevice");
     const size_t k = size_t(ci);
-    hipStream_t cs = link(ci);
     uint8_t* in = stage_ + k * size_t(len_) * 8 + size_t(sb.o * es);
     uint8_t* out = stage_ + k * size_t(len_) * 8 + size_t(len_) * 4 + size_t(sb.o) * 4;
-    link_->recv(c, true, in, sb.n * es, cs);
-    hipp(hipEventRecord(ev_in_[k], cs), "record inbox full");
-    hipp(hipStreamWaitEvent(stream_, ev_in_[k], 0), "update waits inbox");
-    if (push_back) hipp(hipStreamWaitEvent(stream_, ev_out_[k], 0), "update waits outbox free");
-    apply_rule(in, push_back ? out : nullptr, sb, ci);
-    hipp(hipEventRecord(ev_up_[k], stream_), "record update");
-    hipp(hipStreamWaitEvent(cs, ev_up_[k], 0), "link waits update");
-    if (push_back) {
-      link_->send(c, true, out, sb.n * 4, cs);
-      hipp(hipEventRecord(ev_out_[k], cs), "record outbox sent");
-    }
-    link_->then(c, true, cs, [this, c, push_back] {
-      reply(c, kTagGradTail);
-      if (push_back) reply(c, kTagSendParam);
+    link_->order(c, false, 1, goff, sb.n * es, [this, c, ci, k, in, out, sb, es, push_back] {
+      hipp(hipSetDevice(eng_.device()), "hipSetDevice");
+      link_->recv(c, in, sb.n * es, ev_up_[k]);  // the inbox is free once the last update read it
+      link_->record(ev_in_[k]);
+      hipp(hipStreamWaitEvent(stream_, ev_in_[k], 0), "update waits inbox");
+      if (push_back) hipp(hipStreamWaitEvent(stream_, ev_out_[k], 0), "update waits outbox free");
+      apply_rule(in, push_back ? out : nullptr, sb, ci);
+      hipp(hipEventRecord(ev_up_[k], stream_), "record update");
+      if (!push_back) finish_on(stream_, [this, c] { reply(c, kTagGradTail); });
     });
+    if (push_back)
+      link_->order(c, true, 0, roff, sb.n * 4, [this, c, k, out, sb] {
+        link_->send(c, out, sb.n * 4, ev_up_[k]);
+        link_->record(ev_out_[k]);
+        link_->then([this, c] {
+          reply(c, kTagGradTail);
+          reply(c, kTagSendParam);
+        });
+      });
   } else {
     auto in = std::make_shared<std::vector<uint8_t>>(size_t(sb.n * es));
-    link_->recv(c, true, in->data(), sb.n * es, nullptr);
-    link_->then(c, true, nullptr, [this, c, ci, sb, in, push_back] {
-      auto out = push_back ? std::make_shared<std::vector<uint8_t>>(size_t(sb.n) * 4) : nullptr;
-      apply_rule(in->data(), out ? out->data() : nullptr, sb, ci);
-      if (out) link_->send(c, true, out->data(), sb.n * 4, nullptr);
-      link_->then(c, true, nullptr, [this, c, out, push_back] {
-        reply(c, kTagGradTail);
-        if (push_back) reply(c, kTagSendParam);
+    auto out = push_back ? std::make_shared<std::vector<uint8_t>>(size_t(sb.n) * 4) : nullptr;
+    link_->order(c, false, 1, goff, sb.n * es, [this, c, ci, sb, es, in, out, push_back] {
+      link_->recv(c, in->data(), sb.n * es);
+      link_->call([this, c, ci, sb, in, out, push_back] {
+        apply_rule(in->data(), out ? out->data() : nullptr, sb, ci);
+        if (!push_back) reply(c, kTagGradTail);
       });
     });
+    if (push_back)
+      link_->order(c, true, 0, roff, sb.n * 4, [this, c, sb, out] {
+        link_->send(c, out->data(), sb.n * 4);
+        link_->call([this, c, out] {
+          reply(c, kTagGradTail);
+          reply(c, kTagSendParam);
+        });
+      });
   }
+  // pulls released by this push are ordered after it: their snapshots see its update
   release_deferred();
 }
 
@@ -628,29 +645,30 @@ void PSServer::pull_msg(int c, int ci, Sub sb) {
     std::lock_guard<std::mutex> g(mu_);
     ++stats_.pulls;
   }
+  const int64_t roff = (off_ + sb.o) * 4;
   if (device_) {
-    hipp(hipSetDevice(eng_.device()), "hipSetDevice");
     const size_t k = size_t(ci);
-    hipStream_t cs = link(ci);
     uint8_t* out = stage_ + k * size_t(len_) * 8 + size_t(len_) * 4 + size_t(sb.o) * 4;
-    const uint8_t* src = static_cast<const uint8_t*>(p_) + sb.o * 4;
-    // the snapshot in update order on stream_, sent on the client's link stream
-    hipp(hipStreamWaitEvent(stream_, ev_out_[k], 0), "wait outbox free");
-    ew_update(kCopy, 0, eng_.device(), stream_, sb.n, {reinterpret_cast<uintptr_t>(out), reinterpret_cast<uintptr_t>(src)},
-              0u, {1.f});
-    hipp(hipEventRecord(ev_up_[k], stream_), "record snapshot");
-    hipp(hipStreamWaitEvent(cs, ev_up_[k], 0), "link waits snapshot");
-    link_->send(c, true, out, sb.n * 4, cs);
-    hipp(hipEventRecord(ev_out_[k], cs), "record outbox sent");
-    link_->then(c, true, cs, [this, c] { reply(c, kTagSendParam); });
+    link_->order(c, true, 0, roff, sb.n * 4, [this, c, k, out, sb] {
+      hipp(hipSetDevice(eng_.device()), "hipSetDevice");
+      const uint8_t* src = static_cast<const uint8_t*>(p_) + sb.o * 4;
+      // the snapshot in update order on stream_, sent on the link stream
+      hipp(hipStreamWaitEvent(stream_, ev_out_[k], 0), "wait outbox free");
+      ew_update(kCopy, 0, eng_.device(), stream_, sb.n, {reinterpret_cast<uintptr_t>(out), reinterpret_cast<uintptr_t>(src)},
+                0u, {1.f});
+      hipp(hipEventRecord(ev_up_[k], stream_), "record snapshot");
+      link_->send(c, out, sb.n * 4, ev_up_[k]);
+      link_->record(ev_out_[k]);
+      link_->then([this, c] { reply(c, kTagSendParam); });
+    });
     return;
   }
-  // host: snapshot once every earlier message of this client has been applied
-  link_->then(c, true, nullptr, [this, c, sb] {
-    auto out = std::make_shared<std::vector<uint8_t>>(size_t(sb.n) * 4);
-    std::memcpy(out->data(), static_cast<const uint8_t*>(p_) + sb.o * 4, size_t(sb.n) * 4);
-    link_->send(c, true, out->data(), sb.n * 4, nullptr);
-    link_->then(c, true, nullptr, [this, c, out] { reply(c, kTagSendParam); });
+  auto out = std::make_shared<std::vector<uint8_t>>(size_t(sb.n) * 4);
+  link_->order(c, true, 0, roff, sb.n * 4, [this, c, sb, out] {
+    // host: the snapshot is taken when the FIFO reaches it, after every update queued before
+    link_->call([this, sb, out] { std::memcpy(out->data(), static_cast<const uint8_t*>(p_) + sb.o * 4, size_t(sb.n) * 4); });
+    link_->send(c, out->data(), sb.n * 4);
+    link_->call([this, c, out] { reply(c, kTagSendParam); });
   });
 }
 
@@ -661,30 +679,35 @@ void PSServer::param_msg(int c, int ci, bool from_rx, Sub sb, std::function<void
     std::lock_guard<std::mutex> g(mu_);
     ++stats_.param_pushes;
   }
+  const int64_t coff = (off_ + sb.o) * es;
   if (device_) {
-    hipp(hipSetDevice(eng_.device()), "hipSetDevice");
     const size_t k = size_t(ci);
-    hipStream_t cs = link(ci);
     uint8_t* in = stage_ + k * size_t(len_) * 8 + size_t(sb.o * es);
-    link_->recv(c, true, in, sb.n * es, cs);
-    hipp(hipEventRecord(ev_in_[k], cs), "record inbox full");
-    hipp(hipStreamWaitEvent(stream_, ev_in_[k], 0), "copy waits inbox");
-    ew_update(kCopy, 0, eng_.device(), stream_, sb.n,
-              {reinterpret_cast<uintptr_t>(static_cast<uint8_t*>(p_) + sb.o * 4), reinterpret_cast<uintptr_t>(in)},
-              bf ? 2u : 0u, {1.f});
-    hipp(hipEventRecord(ev_up_[k], stream_), "record copy");
-    hipp(hipStreamWaitEvent(cs, ev_up_[k], 0), "link waits copy");
-    finish([this, c] { reply(c, kTagParamTail); });
+    link_->order(c, false, from_rx ? 0 : 1, coff, sb.n * es, [this, c, k, in, sb, es, bf, after] {
+      hipp(hipSetDevice(eng_.device()), "hipSetDevice");
+      link_->recv(c, in, sb.n * es, ev_up_[k]);
+      link_->record(ev_in_[k]);
+      hipp(hipStreamWaitEvent(stream_, ev_in_[k], 0), "copy waits inbox");
+      ew_update(kCopy, 0, eng_.device(), stream_, sb.n,
+                {reinterpret_cast<uintptr_t>(static_cast<uint8_t*>(p_) + sb.o * 4), reinterpret_cast<uintptr_t>(in)},
+                bf ? 2u : 0u, {1.f});
+      hipp(hipEventRecord(ev_up_[k], stream_), "record copy");
+      finish([this, c] { reply(c, kTagParamTail); });
+      // an initialising push: the backlog (local fused updates included) queues behind the copy
+      if (after) after();
+    });
     return;
   }
   auto in = std::make_shared<std::vector<uint8_t>>(size_t(sb.n * es));
-  link_->recv(c, true, in->data(), sb.n * es, nullptr);
-  link_->then(c, true, nullptr, [this, c, sb, in, bf, after] {
-    ew_update(kCopy, 0, -1, nullptr, sb.n,
-              {reinterpret_cast<uintptr_t>(static_cast<uint8_t*>(p_) + sb.o * 4), reinterpret_cast<uintptr_t>(in->data())},
-              bf ? 2u : 0u, {1.f});
-    reply(c, kTagParamTail);
-    if (after) after();
+  link_->order(c, false, from_rx ? 0 : 1, coff, sb.n * es, [this, c, sb, es, in, bf, after] {
+    link_->recv(c, in->data(), sb.n * es);
+    link_->call([this, c, sb, in, bf, after] {
+      ew_update(kCopy, 0, -1, nullptr, sb.n,
+                {reinterpret_cast<uintptr_t>(static_cast<uint8_t*>(p_) + sb.o * 4), reinterpret_cast<uintptr_t>(in->data())},
+                bf ? 2u : 0u, {1.f});
+      reply(c, kTagParamTail);
+      if (after) after();
+    });
   });
 }
 
@@ -778,11 +801,7 @@ PSClient::PSClient(Engine& eng, int ps_id, std::vector<int> servers, std::vector
 
 PSClient::~PSClient() {
   if (hook_ >= 0) eng_.remove_hook(hook_);
-  if (lstream_) {
-    hipSetDevice(eng_.device());
-    hipStreamSynchronize(lstream_);
-    hipStreamDestroy(lstream_);
-  }
+  if (link_) link_->set_client(nullptr);
   // gates never retired (the client went away with pushes queued): release their events
   // and their pending count, or deep parking stays disabled for the rest of the process
   std::deque<GateQueue::Gate> left;
@@ -825,18 +844,22 @@ void PSClient::gate(hipStream_t s, std::function<void()> send) {
   if (!g.ev) eng_.kick();
 }
 
-// the message of shard entry k: whole-shard entries carry no piece (aux2 = 0)
 void PSClient::set_link(PsLink* l, uintptr_t rx, uintptr_t tx, int tx_es) {
   link_ = l;
   rx_ = reinterpret_cast<uint8_t*>(rx);
   tx_ = reinterpret_cast<uint8_t*>(tx);
   tx_es_ = tx_es;
-  if (l && l->device() && !lstream_) {
-    hipp(hipSetDevice(eng_.device()), "hipSetDevice");
-    int lo = 0, hi = 0;
-    hipp(hipDeviceGetStreamPriorityRange(&lo, &hi), "priority range");
-    hipp(hipStreamCreateWithPriority(&lstream_, hipStreamNonBlocking, hi), "client link stream");
-  }
+  if (!l) return;
+  // this client's side of a transfer, queued at its turn in the instance's order (link.h)
+  l->set_client([this](int server, bool to_client, int window, int64_t coff, int64_t bytes) {
+    uint8_t* base = window == 0 ? rx_ : tx_;
+    if (to_client) {
+      link_->recv(server, base + coff, bytes);
+      link_->then([this] { local_done(); });  // the shard has landed in rx
+    } else {
+      link_->send(server, base + coff, bytes);
+    }
+  });
 }
 
 int PSClient::link_recvs(int k, int tag, int64_t flags) const {
@@ -854,18 +877,19 @@ void PSClient::send_entry(int k, int tag, int64_t flags) {
   const int srv = servers_[size_t(k)];
   const bool whole = std::count(servers_.begin(), servers_.end(), srv) == 1;
   eng_.send_am(srv, ps_am_id(ps_id_, tag), nullptr, 0, flags, whole ? 0 : offs_[size_t(k)], whole ? 0 : lens_[size_t(k)]);
-  if (!link_ || srv == eng_.rank()) return;
-  // datapath 3: the entry's data right behind its control message, in call order (link.h)
+  // datapath 3: the server puts the entry's data in the instance's order (PsLink::order); the
+  // pre-sequencer layout (MPIT_LINK_LEGACY, host tests only) queued it here, in call order
+  if (!link_ || srv == eng_.rank() || !link_->legacy()) return;
   const int64_t o = offs_[size_t(k)], n = lens_[size_t(k)];
   if (tag == kTagGrad) {
-    link_->send(srv, false, tx_ + o * tx_es_, n * tx_es_, lstream_);
+    link_->send(srv, tx_ + o * tx_es_, n * tx_es_);
   } else if (tag == kTagParam) {
-    if (flags & kPsFromRx) link_->send(srv, false, rx_ + o * 4, n * 4, lstream_);
-    else link_->send(srv, false, tx_ + o * tx_es_, n * tx_es_, lstream_);
+    if (flags & kPsFromRx) link_->send(srv, rx_ + o * 4, n * 4);
+    else link_->send(srv, tx_ + o * tx_es_, n * tx_es_);
   }
   if (link_recvs(k, tag, flags)) {
-    link_->recv(srv, false, rx_ + o * 4, n * 4, lstream_);
-    link_->then(srv, false, lstream_, [this] { local_done(); });  // the shard has landed in rx
+    link_->recv(srv, rx_ + o * 4, n * 4);
+    link_->then([this] { local_done(); });
   }
 }
 
@@ -925,7 +949,7 @@ void PSClient::on_reply(const Msg&) {
 // MPIT_WAIT_SPIN_US > 0 polls (pause) for up to that long before the futex sleep, keeping
 // the core awake for the step start that follows (device clients only). Measured within
 // noise of sleeping at once (profiles/step_start_host_r02.md): default 0.
-// MPIT_PS_TIMEOUT_S (default 0 = never, opt-in): a reply missing that long means a server is
+// MPIT_PS_TIMEOUT_S (default 0 = never, opt-in; 300 s on datapath 3): a reply missing that long means a server is
 // gone or stuck — raise with what is missing instead of hanging the job (a server that
 // fails raises the job-wide abort itself, Engine::fatal; a dead server process is caught by
 // the peer check). Off by default: an SSP-deferred pull may wait on a slow straggler for
@@ -935,10 +959,13 @@ void PSClient::wait() {
     const char* e = std::getenv("MPIT_WAIT_SPIN_US");
     return e ? std::max<int64_t>(0, std::atoll(e)) : int64_t(0);
   }();
-  static const double timeout_s = [] {
+  // datapath 3 (the RCCL fallback data plane) keeps a finite default: a transfer that never
+  // completes there fails with this message instead of hanging the job
+  static const double env_timeout_s = [] {
     const char* e = std::getenv("MPIT_PS_TIMEOUT_S");
-    return e ? std::max(0.0, std::atof(e)) : 0.0;
+    return e ? std::max(0.0, std::atof(e)) : -1.0;
   }();
+  const double timeout_s = env_timeout_s >= 0 ? env_timeout_s : (link_ ? 300.0 : 0.0);
   const auto t0 = std::chrono::steady_clock::now();
   if (spin_us > 0 && eng_.device() >= 0) {  // GPU workers only (CPU ranks share few cores)
     for (uint32_t i = 0;; ++i) {

@@ -172,9 +172,10 @@ class PSServer {
   // datapath 2 (default on HBM): one "link" stream + staging pair per client, so the
   // gradient pulls and parameter pushes of different clients run concurrently over
   // their own xGMI links (SDMA copies) and only the local fused update is serialised on
-  // stream_. stage_ = [clients][inbox | outbox] of shard_len fp32 each.
-  // MPIT_PS_LINK_STREAMS=k caps the link streams (client i uses stream i % k); default one
-  // per client. The link streams carry only SDMA copies and event waits.
+  // stream_. stage_ = [clients][inbox | outbox] of shard_len fp32 each (also datapath 3's
+  // staging). MPIT_PS_LINK_STREAMS=k caps the link streams (client i uses stream i % k);
+  // default 2 on a server co-located with a worker, one per client on a dedicated server.
+  // The link streams carry only SDMA copies and event waits.
   std::vector<hipStream_t> cstream_;
   hipStream_t link(int ci) const { return cstream_[size_t(ci) % cstream_.size()]; }
   std::vector<hipEvent_t> ev_in_, ev_up_, ev_out_;
@@ -221,7 +222,7 @@ class PSClient {
   void send_param(hipStream_t s, bool from_rx = false);
   void stop();
   // until every outstanding reply arrived (GIL released); raises after MPIT_PS_TIMEOUT_S
-  // (default 0 = never) with the number of replies still missing
+  // (default 0 = never; 300 s on datapath 3) with the number of replies still missing
   void wait();
   // datapath 3: shard data as messages over `l` (link.h) from / into this client's own
   // buffers: rx (fp32 parameters, pulls land here), tx (push window, tx_es bytes / element)
@@ -242,7 +243,6 @@ class PSClient {
   uint8_t* rx_ = nullptr;
   uint8_t* tx_ = nullptr;
   int tx_es_ = 4;
-  hipStream_t lstream_ = nullptr;  // device: the client's own link stream
   Engine& eng_;
   std::shared_ptr<GateQueue> gq_;
   int hook_ = -1;

@@ -178,10 +178,11 @@ class _Group:
             # RCCL refuses two ranks of one communicator on one GPU ("Duplicate GPU")
             raise ValueError("PS datapath 3 (RCCL send/recv) needs one GPU per rank; these ranks share a GPU")
         if datapath == 3:
-            self.link = native().PsLink(eng, ps_id, self.servers, self.clients, self.device)
-            mine = [(st.rank, c, bytes(i)) for c, i in self.link.make_ids()]
-            ids = [x for part in self.comm.allgather_obj(mine) for x in part]
-            self.link.connect(ids)
+            # one communicator over the members, one link stream per rank, every transfer in
+            # the sequencer's (lowest member's) global order: csrc/core/link.h
+            self.link = native().PsLink(eng, ps_id, self.members, self.device)
+            ids = [bytes(i) for i in self.comm.allgather_obj(bytes(self.link.make_id())) if i]
+            self.link.connect(ids[0] if ids else b"")
         self.comm.Barrier()
         for w in self.wins:
             w.unlink_names()

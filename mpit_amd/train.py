@@ -445,16 +445,24 @@ class Trainer:
         dev = self.device.index if self.on_gpu else None
         devs = W.allgather_obj(dev)
         no_peer = []
-        if self.on_gpu and self.pc is not None:
+        # MPIT_PREFLIGHT_NO_PEER="w:s,...": report these (worker, server) pairs as lacking peer
+        # access (tests of the fallback on CPU ranks, which have no devices to ask)
+        fake = {tuple(int(v) for v in p.split(":")) for p in os.environ.get("MPIT_PREFLIGHT_NO_PEER", "").split(",") if p}
+        if self.pc is not None:
             for s in self.sranks:
                 d = devs[s]
-                if d is not None and d != dev and not torch.cuda.can_device_access_peer(d, dev):
+                if (self.rank, s) in fake or (self.on_gpu and d is not None and d != dev
+                                              and not torch.cuda.can_device_access_peer(d, dev)):
                     no_peer.append((self.rank, s))
         no_peer = sorted({tuple(p) for lst in W.allgather_obj(no_peer) for p in lst})
         chk = self.verify_ps() if (self.pc is not None or self.ps_server is not None) else {"ok": True, "mismatches": []}
         bad = [tuple(p) for p in chk.get("mismatches", [])]
-        return {"ok": bool(chk["ok"]) and not no_peer, "devices": devs, "no_peer": [list(p) for p in no_peer],
-                "mismatches": [list(p) for p in bad], "shards": chk.get("shards"), "workers": chk.get("workers")}
+        # datapath 3 never maps a peer's memory: pairs without peer access are reported, but
+        # only the exchanged bits decide there
+        peer_ok = not no_peer or self.cfg.datapath == 3
+        return {"ok": bool(chk["ok"]) and peer_ok, "devices": devs, "no_peer": [list(p) for p in no_peer],
+                "mismatches": [list(p) for p in bad], "shards": chk.get("shards"), "workers": chk.get("workers"),
+                "datapath": self.cfg.datapath}
 
     def retire_pushes(self):
         """Wait until every push / pull this worker issued has been acknowledged (EAMSGD

@@ -111,6 +111,19 @@ def main(argv) -> int:
                         p = os.path.join(root, fn)
                         if fn.endswith("kernel_trace.csv") and os.path.getsize(p) > 40 << 20:
                             os.remove(p)
+        elif kind == "queues":  # stream -> hardware queue table (kernel + memory-copy trace)
+            name, _, args = rest.partition(":")
+            d = os.path.join(out, f"q_{name}")
+            rc = _run(out, f"q_{name}.log", ["rocprofv3", "--kernel-trace", "--memory-copy-trace", "-d", d, "-o", "t",
+                                            "--output-format", "csv", "--", PY, "bench.py"]
+                      + (args.split(",") if args else []), 600)
+            if rc == 0:
+                rc = _run(out, f"q_{name}_table.log", [PY, "scripts/queue_table.py", d,
+                                                      os.path.join(out, f"queues_{name}.md"), name], 300)
+                for root, _, files in os.walk(d):
+                    for fn in files:
+                        if fn.endswith("_trace.csv") and os.path.getsize(os.path.join(root, fn)) > 40 << 20:
+                            os.remove(os.path.join(root, fn))
         elif kind == "gemmcalls":  # per-call GEMM table (shapes from MPIT_GEMM_LOG, times from the trace)
             name, _, args = rest.partition(":")
             d = os.path.join(out, f"gc_{name}")

@@ -1,5 +1,7 @@
 """Bounded staleness: rank 0 serves, ranks 1 and 2 are clients, staleness 0.
-Client 1 pushes twice in a row; its second pull must wait for client 2's first push."""
+Client 1 pushes with a pull; the pull must wait for client 2's first push, and the
+parameters it then receives must include that push: 0 + 1 + 1 = 2 everywhere (sum rule,
+both gradients all ones)."""
 import os
 import sys
 import time
@@ -23,11 +25,13 @@ if r == 0:
     print("RESULT SSP_OK", st, flush=True)
 else:
     pc = PClient(conf).start(torch.zeros(64), torch.ones(64))
-    W_sub = None
+    pc.tx.fill_(1.0)  # the push window (host: a view of the client's shm window)
     if r == 1:
         pc.async_send_grad(pull=True)
         pc.wait()  # clocks (1, 0): 1 - 0 > 0 -> deferred until client 2 pushes
-        t_first = time.time()
+        got = pc.rx.clone()
+        assert torch.equal(got, torch.full_like(got, 2.0)), got[:8].tolist()
+        print("RESULT SSP_PULL_OK", flush=True)
     if r == 2:
         time.sleep(0.5)
         pc.async_send_grad(pull=True)

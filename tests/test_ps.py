@@ -124,4 +124,35 @@ def test_datapath3_one_server_seven_workers():
 
 def test_datapath3_bounded_staleness():
     out = run_ranks("ssp_check.py", 3, {"MPIT_CPU_ONLY": "1", "T_DATAPATH": "3"})
-    assert "SSP_OK" in out, out
+    assert "SSP_OK" in out and "SSP_PULL_OK" in out, out
+
+
+# ---- datapath 3 under blocking rendezvous semantics (MPIT_LINK_RDV=1): one FIFO per rank, a
+# send completes only against a receive at the head of the peer's FIFO (an RCCL pair at the
+# head of a hardware queue). 200 steps of randomised control-message timing each.
+
+_RDV = {"MPIT_CPU_ONLY": "1", "MPIT_LINK_RDV": "1", "MPIT_LINK_JITTER_US": "300", "T_STEPS": "200"}
+
+
+@pytest.mark.parametrize("stale", ["-1", "0"])
+def test_datapath3_rendezvous_colocated_8(stale):
+    """8 co-located ranks (worker + shard server each), random shard order per push, random
+    timing, plain async and SSP (deferred pulls released by other clients' pushes): every
+    step completes and the final shards equal the closed form."""
+    out = run_ranks("ps_link_rdv.py", 8, dict(_RDV, T_TOPO="colocated", T_STALE=stale, MPIT_PS_TIMEOUT_S="60"),
+                    timeout=300)
+    assert out.count("RESULT RDV_OK") == 8, out
+
+
+def test_datapath3_rendezvous_one_server_seven_workers():
+    out = run_ranks("ps_link_rdv.py", 8, dict(_RDV, T_TOPO="dedicated", MPIT_PS_TIMEOUT_S="60"), timeout=300)
+    assert out.count("RESULT RDV_OK") == 8, out
+
+
+def test_datapath3_pre_sequencer_layout_deadlocks():
+    """The layout before the sequencer (each client queues its ops when it sends its control
+    message, each server when the message arrives; all on one FIFO per rank) deadlocks under
+    the same blocking semantics: the clients' finite wait reports it."""
+    out = run_ranks("ps_link_rdv.py", 8, dict(_RDV, T_TOPO="colocated", MPIT_LINK_LEGACY="1", MPIT_PS_TIMEOUT_S="6"),
+                    timeout=300)
+    assert "RESULT RDV_TIMEOUT" in out and "RESULT RDV_OK" not in out, out

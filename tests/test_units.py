@@ -202,7 +202,7 @@ def test_bounded_staleness_defers_fast_client(world):
     from mp_util import run_ranks
 
     out = run_ranks("ssp_check.py", 3, {"MPIT_CPU_ONLY": "1"})
-    assert "SSP_OK" in out, out
+    assert "SSP_OK" in out and "SSP_PULL_OK" in out, out
 
 
 def test_checkpoint_roundtrip(world, tmp_path):

@@ -43,7 +43,8 @@ import torch
 
 import mpit_amd as mp
 from mpit_amd import ops
-from mpit_amd.apps.qa_data import load_binary, load_files, pad_batch, save_binary, synthetic_qa
+from mpit_amd.apps.qa_data import (T7_VOCAB, load_binary, load_files, load_t7_vocab, pad_batch, qa_from_vocab,
+                                   save_binary, synthetic_qa)
 from mpit_amd.launch import master_freq
 from mpit_amd.models.bicnn import (BiCNN, draw_negatives, first_violations, gesd, margin_ranking_loss, parity_grad_,
                                    parity_loss)
@@ -143,6 +144,7 @@ def build_args(argv=None):
     f("preloadBinary", action="store_true")
     f("saveBinary", action="store_true", help="write the prepared-data cache and continue")
     f("binaryFile", default="binary_qadata.pt")
+    f("binaryDir", default=".", help="-preloadBinary: directory of the reference's Torch7 caches (binary_map*)")
     f("save", default="bicnn_out")
     f("synthetic", type=int, default=200, help="synthetic answers when no data files are given")
     a = ap.parse_args(argv)
@@ -247,6 +249,12 @@ class Evaluator:
 
 def load_data(a):
     if a.preloadBinary:
+        # the reference's own caches (plaunch.lua:221-228) when they are in --binaryDir: the
+        # vocabulary from its two Torch7 maps (the other six caches are not shipped,
+        # .MISSING_LARGE_BLOBS); else this package's cache file
+        if all(os.path.exists(os.path.join(a.binaryDir, f)) for f in T7_VOCAB):
+            return qa_from_vocab(load_t7_vocab(a.binaryDir), emb_dim=a.embeddingDim, conv_width=a.contConvWidth,
+                                 n_answers=a.synthetic)
         return load_binary(a.binaryFile)
     if a.trainFile != "none":
         tests = [t for t in (a.testFile1, a.testFile2) if t != "none"]

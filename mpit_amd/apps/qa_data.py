@@ -125,13 +125,61 @@ def load_binary(path: str) -> QAData:
     return d
 
 
-def synthetic_qa(n_answers: int = 200, n_train: int = 2000, n_valid: int = 200, vocab: int = 2000, pool: int = 20,
-                 emb_dim: int = 100, conv_width: int = 2, seed: int = 1, n_tests: int = 2) -> QAData:
-    """Answers are random word sequences; a question shares 3 "key" words with its answer
-    plus noise words, so GESD ranking is learnable."""
+T7_VOCAB = ("binary_mapWordStr2WordIdx", "binary_mapWordIdx2WordStr")
+
+
+def load_t7_vocab(directory: str) -> Dict[str, int]:
+    """The reference's shipped vocabulary caches (BiCNN/binary_mapWordStr2WordIdx and
+    binary_mapWordIdx2WordStr, Torch7 tables written by prepareData.lua and loaded by
+    plaunch.lua:222-223) through the plain-data Torch7 reader (mpit_amd/utils/t7.py: no
+    torch object or function is ever constructed). The two maps must be mutually inverse
+    over ids 1..n with SENTBEGIN = 1 and SENTEND = 2 (prepareData.lua:37-42); returns
+    word -> id (the reference's 1-based ids, which are this package's ids too: 0 = pad)."""
+    import os
+
+    from ..utils import t7
+
+    s2i = t7.load(os.path.join(directory, T7_VOCAB[0]))
+    i2s = t7.load(os.path.join(directory, T7_VOCAB[1]))
+    if not isinstance(s2i, dict) or not isinstance(i2s, dict):
+        raise ValueError("t7 vocabulary: the caches must hold tables")
+    n = len(s2i)
+    if len(i2s) != n or sorted(i2s) != list(range(1, n + 1)):
+        raise ValueError(f"t7 vocabulary: id map is not 1..{n}")
+    for w, i in s2i.items():
+        if i2s.get(i) != w:
+            raise ValueError(f"t7 vocabulary: maps disagree on {w!r} -> {i}")
+    if s2i.get("SENTBEGIN") != SENTBEGIN or s2i.get("SENTEND") != SENTEND:
+        raise ValueError("t7 vocabulary: SENTBEGIN / SENTEND are not ids 1 / 2")
+    return dict(sorted(s2i.items(), key=lambda kv: kv[1]))
+
+
+def qa_from_vocab(word2idx: Dict[str, int], emb_dim: int = 100, conv_width: int = 2, seed: int = 1,
+                  **synthetic) -> QAData:
+    """QA data over a given vocabulary (ids as given, 0 = pad): embeddings uniform random as
+    the reference's out-of-vocabulary words (prepareData.lua:95-97; the word-vector cache
+    binary_mapWordIdx2Vector holds torch tensors and is not shipped), questions and answers
+    drawn as in :func:`synthetic_qa` from the vocabulary's words."""
     rng = random.Random(seed)
     d = QAData(emb_dim=emb_dim, conv_width=conv_width)
-    words = [f"w{i}" for i in range(vocab)]
+    d.word2idx = {"<pad>": PAD}
+    d.word2idx.update(word2idx)
+    if sorted(d.word2idx.values()) != list(range(len(d.word2idx))):
+        raise ValueError("qa_from_vocab: ids must be 0..n")
+    d.vectors = [[rng.random() for _ in range(emb_dim)] for _ in range(len(d.word2idx) - 3)]
+    words = [w for w in d.word2idx if w not in ("<pad>", "SENTBEGIN", "SENTEND")]
+    return synthetic_qa(emb_dim=emb_dim, conv_width=conv_width, seed=seed, base=d, words=words, **synthetic)
+
+
+def synthetic_qa(n_answers: int = 200, n_train: int = 2000, n_valid: int = 200, vocab: int = 2000, pool: int = 20,
+                 emb_dim: int = 100, conv_width: int = 2, seed: int = 1, n_tests: int = 2,
+                 base: Optional[QAData] = None, words: Optional[List[str]] = None) -> QAData:
+    """Answers are random word sequences; a question shares 3 "key" words with its answer
+    plus noise words, so GESD ranking is learnable. base / words: start from a given
+    vocabulary and draw from its words (:func:`qa_from_vocab`)."""
+    rng = random.Random(seed)
+    d = base if base is not None else QAData(emb_dim=emb_dim, conv_width=conv_width)
+    words = words if words is not None else [f"w{i}" for i in range(vocab)]
     for lab in range(n_answers):
         d.answers[lab] = d.encode(rng.sample(words, rng.randint(6, 12)), rng)
     ans_words = {lab: [w for w in d.answers[lab][conv_width:-(conv_width - 1) or None]] for lab in d.answers}

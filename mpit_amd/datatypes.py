@@ -130,6 +130,29 @@ class Datatype:
         raw[self._byte_index(count, raw.device)] = packed.reshape(-1)[: count * self.Get_size()].to(raw.device)
         return buf
 
+    def runs(self, count: int) -> List[Tuple[int, int]]:
+        """The byte runs (offset, length) that `count` instances occupy, in type-map order
+        (the order of the packed stream), adjacent segments merged: what a one-sided
+        transfer moves with one copy each."""
+        out: List[Tuple[int, int]] = []
+        for i in range(int(count)):
+            base = i * self.extent
+            for d, b in self.typemap:
+                sz = _BASIC[b][0]
+                if not sz:
+                    continue
+                o = base + d
+                if out and out[-1][0] + out[-1][1] == o:
+                    out[-1] = (out[-1][0], out[-1][1] + sz)
+                else:
+                    out.append((o, sz))
+        return out
+
+    def element_dtype(self) -> Optional[torch.dtype]:
+        """The one basic torch dtype every entry of the type map has (None: mixed / none)."""
+        kinds = {b for _, b in self.typemap if _BASIC[b][0]}
+        return _BASIC[kinds.pop()][1] if len(kinds) == 1 else None
+
     def __repr__(self):
         return f"Datatype({self._name or self.envelope[0]}, size={self.Get_size()}, extent={self.extent})"
 

@@ -426,18 +426,91 @@ def Win_create(base, size=None, disp_unit=None, info=None, comm=None):
     return Win.Create(base, comm, disp_unit, info)
 
 
+def _origin_stream(origin, count, dtype):
+    """The origin buffer's `count` instances of `dtype` as one contiguous byte stream (packed
+    when the type is derived, as the two-sided path does) and its element dtype."""
+    flat = origin.contiguous().reshape(-1)
+    if dtype is None or dtype.is_contiguous_basic():
+        es = dtype.Get_size() if dtype is not None else flat.element_size()
+        n = int(count) * es
+        raw = flat.view(torch.uint8)
+        if n > raw.numel():
+            raise ValueError(f"one-sided origin: {count} elements exceed the buffer")
+        return raw[:n], flat.dtype
+    return dtype.pack(flat, count), dtype.element_dtype()
+
+
+def _target_runs(win, target_disp, target_count, target_type, nbytes):
+    """Byte runs (window offset, length) the target (disp, count, datatype) names."""
+    base = int(target_disp) * win.disp_unit
+    if target_type is None or target_type.is_contiguous_basic():
+        size = (target_type.Get_size() if target_type is not None else win.tensor.element_size()) * int(target_count)
+        runs = [(0, size)]
+    else:
+        runs = target_type.runs(target_count)
+        size = sum(n for _, n in runs)
+    if size != nbytes:  # the type signatures must carry the same bytes (MPI_ERR_TRUNCATE / _TYPE)
+        raise ValueError(f"one-sided: origin carries {nbytes} bytes, target (count {target_count}, {target_type}) {size}")
+    return [(base + o, n) for o, n in runs]
+
+
 def Put(origin, origin_count, origin_type, target_rank, target_disp, target_count, target_type, win):
-    win.Put(origin.reshape(-1)[:origin_count], target_rank, target_disp)
+    """MPI_Put (mpifuncs.c:1656): origin (count, datatype) packed, scattered over the target
+    datatype's runs in the target window (one peer copy per contiguous run)."""
+    data, _ = _origin_stream(origin, origin_count, origin_type)
+    pos = 0
+    for off, n in _target_runs(win, target_disp, target_count, target_type, data.numel()):
+        win._put_bytes(data[pos:pos + n], target_rank, off)
+        pos += n
     return SUCCESS
 
 
 def Get(origin, origin_count, origin_type, target_rank, target_disp, target_count, target_type, win):
-    win.Get(origin.reshape(-1)[:origin_count], target_rank, target_disp)
+    """MPI_Get (mpifuncs.c:1131): the target datatype's runs gathered, unpacked into the origin
+    by the origin datatype. Complete after the epoch's synchronisation (Fence / Flush /
+    Unlock), like MPI: a derived origin type is unpacked at that point."""
+    if origin_type is None or origin_type.is_contiguous_basic():
+        es = origin_type.Get_size() if origin_type is not None else origin.element_size()
+        if not origin.is_contiguous():
+            raise ValueError("Get: contiguous origin buffer needed for a basic datatype")
+        stage = origin.reshape(-1).view(torch.uint8)[:int(origin_count) * es]
+        unpack = None
+    else:
+        stage = origin_type.staging(origin, origin_count)
+        unpack = (origin_type, stage, origin, int(origin_count))
+    pos = 0
+    for off, n in _target_runs(win, target_disp, target_count, target_type, stage.numel()):
+        win._get_bytes(stage[pos:pos + n], target_rank, off)
+        pos += n
+    if unpack is not None:  # derived origin: scatter once the data has landed
+        win.Flush()
+        t, st, buf, cnt = unpack
+        t.unpack(st, buf, cnt)
     return SUCCESS
 
 
 def Accumulate(origin, origin_count, origin_type, target_rank, target_disp, target_count, target_type, op, win):
-    win.Accumulate(origin.reshape(-1)[:origin_count], target_rank, target_disp, op)
+    """MPI_Accumulate (mpifuncs.c:9): SUM / REPLACE of fp32 / bf16 elements, per contiguous
+    run of the target datatype; both type maps must hold that one element type."""
+    from .comm import REPLACE, SUM
+
+    data, edt = _origin_stream(origin, origin_count, origin_type)
+    tdt = target_type.element_dtype() if target_type is not None else win.tensor.dtype
+    if edt not in (torch.float32, torch.bfloat16) or tdt != edt:
+        raise TypeError(f"Accumulate: fp32 / bf16 elements of one type on both sides (origin {edt}, target {tdt})")
+    op = op or SUM
+    if op is SUM:
+        a, b = 1.0, 1.0
+    elif op is REPLACE:
+        a, b = 1.0, 0.0
+    else:
+        raise ValueError("Accumulate supports SUM and REPLACE")
+    vals = data.view(edt)
+    es = vals.element_size()
+    pos = 0
+    for off, n in _target_runs(win, target_disp, target_count, target_type, data.numel()):
+        win._acc_elems(vals[pos // es:(pos + n) // es], target_rank, off, a, b)
+        pos += n
     return SUCCESS
 
 

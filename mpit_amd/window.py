@@ -142,6 +142,22 @@ class Win:
         self._w.accumulate(target_rank, target_disp * self.disp_unit, o.data_ptr(), o.is_cuda, o.numel(),
                            o.dtype == torch.bfloat16, a, b, self._stream())
 
+    # byte-addressed forms (the datatype-faithful Put / Get / Accumulate of mpiT.py): one
+    # copy / accumulate per contiguous run of the target datatype
+    def _put_bytes(self, data: torch.Tensor, target_rank: int, byte_disp: int):
+        self._w.put(target_rank, int(byte_disp), data.data_ptr(), data.numel(), self._stream())
+        self._keep_all = getattr(self, "_keep_all", [])
+        self._keep_all.append(data)
+
+    def _get_bytes(self, out: torch.Tensor, target_rank: int, byte_disp: int):
+        self._w.get(out.data_ptr(), target_rank, int(byte_disp), out.numel() * out.element_size(), self._stream())
+
+    def _acc_elems(self, data: torch.Tensor, target_rank: int, byte_disp: int, a: float, b: float):
+        self._w.accumulate(target_rank, int(byte_disp), data.data_ptr(), data.is_cuda, data.numel(),
+                           data.dtype == torch.bfloat16, a, b, self._stream())
+        self._keep_all = getattr(self, "_keep_all", [])
+        self._keep_all.append(data)
+
     def Raccumulate(self, *a, **k):
         from .comm import Request
 
@@ -163,6 +179,7 @@ class Win:
     # ------------------------------------------------------------ synchronisation
     def Flush(self, rank: Optional[int] = None):
         self._w.flush(self._stream())
+        self._keep_all = []
 
     Flush_all = Flush
     Flush_local = Flush

@@ -283,6 +283,32 @@ acc.Lock(0, mp.LOCK_EXCLUSIVE)
 acc.Unlock(0)
 win.Free()
 acc.Free()
+# derived datatypes through the facade (mpifuncs.c:1656,1131,9): origin / target (count,
+# datatype) both honoured — a vector target scatters, a vector origin gathers / unpacks
+vt = mpiT.Type_commit(mpiT.Type_vector(3, 1, 2, mpiT.FLOAT))
+dw = mpiT.Win_create(torch.zeros(8, device=dev), comm=W)
+mpiT.Win_fence(0, dw)
+src = torch.tensor([r + 1.0, r + 2.0, r + 3.0], device=dev)
+assert mpiT.Put(src, 3, mpiT.FLOAT, (r + 1) % n, 1, 1, vt, dw) == mpiT.SUCCESS
+mpiT.Win_fence(0, dw)
+q = (r - 1) % n
+assert dw.tensor.tolist() == [0.0, q + 1.0, 0.0, q + 2.0, 0.0, q + 3.0, 0.0, 0.0], dw.tensor.tolist()
+got = torch.full((6,), -1.0, device=dev)
+assert mpiT.Get(got, 1, vt, (r + 1) % n, 1, 1, vt, dw) == mpiT.SUCCESS
+mpiT.Win_fence(0, dw)
+assert got.tolist() == [r + 1.0, -1.0, r + 2.0, -1.0, r + 3.0, -1.0], got.tolist()
+assert mpiT.Accumulate(torch.ones(3, device=dev), 3, mpiT.FLOAT, 0, 1, 1, vt, mpiT.SUM, dw) == mpiT.SUCCESS
+mpiT.Win_fence(0, dw)
+if r == 0:
+    q = n - 1
+    assert dw.tensor.tolist() == [0.0, q + 1.0 + n, 0.0, q + 2.0 + n, 0.0, q + 3.0 + n, 0.0, 0.0], dw.tensor.tolist()
+try:  # signatures that do not carry the same bytes are refused, not silently truncated
+    mpiT.Put(src, 2, mpiT.FLOAT, (r + 1) % n, 1, 1, vt, dw)
+    raise AssertionError("mismatched one-sided signature accepted")
+except ValueError:
+    pass
+mpiT.Win_fence(0, dw)
+mpiT.Win_free(dw)
 ok("windows")
 
 # ---- MPI-IO: ordered / shared / explicit-offset writes

@@ -104,7 +104,7 @@ def main():
                           f32=f32, **tkw)
 
             ecin = dict(red, cin=cin.data_ptr(), cmask=cmask.data_ptr())
-            t_tn = timeit(lambda: tn_call(s1.cuda_stream))
+            t_tn = timeit(lambda: tn_call(st))  # alone (timed on the current stream)
 
             def both():
                 s1.wait_stream(s0)

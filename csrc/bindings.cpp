@@ -18,6 +18,25 @@ hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 py::tuple st_tuple(const Status& s) { return py::make_tuple(s.source, s.tag, s.error, s.count, s.cancelled); }
 }  // namespace
 
+// the BN forward-finalize fold of a stats GEMM (gemm.hip stats_fold): None, or the tuple
+// (coef, gamma, beta, running_mean, running_var, save_mean, save_rstd, lvl, zero, eps, momentum)
+static void apply_sfold(BnRed& r, const py::object& f) {
+  if (f.is_none()) return;
+  auto t = f.cast<py::tuple>();
+  if (t.size() != 11) throw std::invalid_argument("bn fold: 11 fields");
+  r.scoef = t[0].cast<uintptr_t>();
+  r.sgamma = t[1].cast<uintptr_t>();
+  r.sbeta = t[2].cast<uintptr_t>();
+  r.srmean = t[3].cast<uintptr_t>();
+  r.srvar = t[4].cast<uintptr_t>();
+  r.smean = t[5].cast<uintptr_t>();
+  r.srstd = t[6].cast<uintptr_t>();
+  r.slvl = t[7].cast<uintptr_t>();
+  r.szero = t[8].cast<uintptr_t>();
+  r.seps = t[9].cast<float>();
+  r.smom = t[10].cast<float>();
+}
+
 PYBIND11_MODULE(_mpit, m) {
   m.doc() = "mpit_amd native runtime: shm control plane, IPC windows, parameter server, CDNA4 kernels";
   m.attr("ANY_SOURCE") = kAnySource;
@@ -87,14 +106,15 @@ PYBIND11_MODULE(_mpit, m) {
       "bn_act_fwd",
       [](int dev, uintptr_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C, uintptr_t gamma,
          uintptr_t beta, uintptr_t rmean, uintptr_t rvar, uintptr_t save_mean, uintptr_t save_rstd, uintptr_t ws,
-         float momentum, float eps, bool relu, uintptr_t mask, uintptr_t stats, int64_t nstat, uintptr_t amax) {
+         float momentum, float eps, bool relu, uintptr_t mask, uintptr_t stats, int64_t nstat, uintptr_t amax,
+         uintptr_t coef) {
         bn_act_fwd(dev, S(s), bf16, x, res, y, M, C, gamma, beta, rmean, rvar, save_mean, save_rstd, ws, momentum, eps,
-                   relu, mask, stats, nstat, amax);
+                   relu, mask, stats, nstat, amax, coef);
       },
       py::arg("dev"), py::arg("stream"), py::arg("bf16"), py::arg("x"), py::arg("res"), py::arg("y"), py::arg("M"),
       py::arg("C"), py::arg("gamma"), py::arg("beta"), py::arg("rmean"), py::arg("rvar"), py::arg("save_mean"),
       py::arg("save_rstd"), py::arg("ws"), py::arg("momentum"), py::arg("eps"), py::arg("relu"), py::arg("mask"),
-      py::arg("stats") = 0, py::arg("nstat") = 0, py::arg("amax") = 0);
+      py::arg("stats") = 0, py::arg("nstat") = 0, py::arg("amax") = 0, py::arg("coef") = 0);
   m.def("bn_act_apply", [](int dev, uintptr_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C,
                            uintptr_t coef, bool relu) { bn_act_apply(dev, S(s), bf16, x, res, y, M, C, coef, relu); });
   m.def(
@@ -137,11 +157,12 @@ PYBIND11_MODULE(_mpit, m) {
          uintptr_t red_mask, uintptr_t red_mean, int64_t red_row0, uintptr_t red_part2, uintptr_t red_x2,
          uintptr_t red_mean2, bool f32, uintptr_t fold_coef, uintptr_t fold_gamma, uintptr_t fold_rstd,
          uintptr_t fold_dgamma, uintptr_t fold_dbeta, uintptr_t fold_lvl, int64_t bps, uintptr_t amax_a,
-         uintptr_t amax_b, uintptr_t fold_zero) {
+         uintptr_t amax_b, uintptr_t fold_zero, py::object bn_fold) {
         BnRed r{red_part, red_x, red_mask, red_mean, red_row0, red_part2, red_x2, red_mean2};
         r.fcoef = fold_coef; r.fgamma = fold_gamma; r.frstd = fold_rstd;
         r.fdgamma = fold_dgamma; r.fdbeta = fold_dbeta; r.flvl = fold_lvl; r.fzero = fold_zero;
         r.amax_a = amax_a; r.amax_b = amax_b;
+        apply_sfold(r, bn_fold);
         gemm_nt(dev, S(s), M, N, K, A, lda, B, ldb, C, ldc, stats, cin, cmask, &r, f32, bps);
       },
       py::arg("dev"), py::arg("stream"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("A"), py::arg("lda"),
@@ -150,7 +171,8 @@ PYBIND11_MODULE(_mpit, m) {
       py::arg("red_mean") = 0, py::arg("red_row0") = 0, py::arg("red_part2") = 0, py::arg("red_x2") = 0,
       py::arg("red_mean2") = 0, py::arg("f32") = false, py::arg("fold_coef") = 0, py::arg("fold_gamma") = 0,
       py::arg("fold_rstd") = 0, py::arg("fold_dgamma") = 0, py::arg("fold_dbeta") = 0, py::arg("fold_lvl") = 0,
-      py::arg("bps") = 0, py::arg("amax_a") = 0, py::arg("amax_b") = 0, py::arg("fold_zero") = 0);
+      py::arg("bps") = 0, py::arg("amax_a") = 0, py::arg("amax_b") = 0, py::arg("fold_zero") = 0,
+      py::arg("bn_fold") = py::none());
   m.def("gemm_nt_fold_lvl_floats", &gemm_nt_fold_lvl_floats);
   m.def("bound_floats", [] { return kBoundFloats; });
   m.def("gemm_tn_supported", &gemm_tn_supported);
@@ -203,11 +225,12 @@ PYBIND11_MODULE(_mpit, m) {
          uintptr_t red_x, uintptr_t red_mask, uintptr_t red_mean, int64_t red_row0, uintptr_t red_part2,
          uintptr_t red_x2, uintptr_t red_mean2, bool f32, uintptr_t fold_coef, uintptr_t fold_gamma,
          uintptr_t fold_rstd, uintptr_t fold_dgamma, uintptr_t fold_dbeta, uintptr_t fold_lvl, int64_t bps,
-         uintptr_t amax_a, uintptr_t amax_b, uintptr_t fold_zero) {
+         uintptr_t amax_a, uintptr_t amax_b, uintptr_t fold_zero, py::object bn_fold) {
         BnRed r{red_part, red_x, red_mask, red_mean, red_row0, red_part2, red_x2, red_mean2};
         r.fcoef = fold_coef; r.fgamma = fold_gamma; r.frstd = fold_rstd;
         r.fdgamma = fold_dgamma; r.fdbeta = fold_dbeta; r.flvl = fold_lvl; r.fzero = fold_zero;
         r.amax_a = amax_a; r.amax_b = amax_b;
+        apply_sfold(r, bn_fold);
         conv_fwd(dev, S(s), Nb, H, W, C, Co, R, S_, stride, pad, x, w, y, stats, cin, bias, relu, &r, f32, bps);
       },
       py::arg("dev"), py::arg("stream"), py::arg("Nb"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("Co"),
@@ -217,7 +240,7 @@ PYBIND11_MODULE(_mpit, m) {
       py::arg("red_part2") = 0, py::arg("red_x2") = 0, py::arg("red_mean2") = 0, py::arg("f32") = false,
       py::arg("fold_coef") = 0, py::arg("fold_gamma") = 0, py::arg("fold_rstd") = 0, py::arg("fold_dgamma") = 0,
       py::arg("fold_dbeta") = 0, py::arg("fold_lvl") = 0, py::arg("bps") = 0, py::arg("amax_a") = 0,
-      py::arg("amax_b") = 0, py::arg("fold_zero") = 0);
+      py::arg("amax_b") = 0, py::arg("fold_zero") = 0, py::arg("bn_fold") = py::none());
   m.def("conv_dgrad_strided_wfloats", &conv_dgrad_strided_wfloats);
   m.def(
       "conv_dgrad_strided_weights",
@@ -251,12 +274,15 @@ PYBIND11_MODULE(_mpit, m) {
   m.def(
       "conv_stem_fwd",
       [](int dev, uintptr_t s, int Nb, int Hp, int Wp, int Co, int Ho, int Wo, int stride, uintptr_t x, uintptr_t w,
-         uintptr_t y, uintptr_t stats, bool f32, int64_t bps, uintptr_t amax_a, uintptr_t amax_b) {
-        conv_stem_fwd(dev, S(s), Nb, Hp, Wp, Co, Ho, Wo, stride, x, w, y, stats, f32, bps, amax_a, amax_b);
+         uintptr_t y, uintptr_t stats, bool f32, int64_t bps, uintptr_t amax_a, uintptr_t amax_b, py::object bn_fold) {
+        BnRed r{};
+        apply_sfold(r, bn_fold);
+        conv_stem_fwd(dev, S(s), Nb, Hp, Wp, Co, Ho, Wo, stride, x, w, y, stats, f32, bps, amax_a, amax_b, &r);
       },
       py::arg("dev"), py::arg("stream"), py::arg("Nb"), py::arg("Hp"), py::arg("Wp"), py::arg("Co"), py::arg("Ho"),
       py::arg("Wo"), py::arg("stride"), py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stats"),
-      py::arg("f32") = false, py::arg("bps") = 0, py::arg("amax_a") = 0, py::arg("amax_b") = 0);
+      py::arg("f32") = false, py::arg("bps") = 0, py::arg("amax_a") = 0, py::arg("amax_b") = 0,
+      py::arg("bn_fold") = py::none());
   m.def(
       "stem_weight_planes",
       [](int dev, uintptr_t s, uintptr_t w, int Co, int C, int R, int Sk, uintptr_t planes, uintptr_t bound) {

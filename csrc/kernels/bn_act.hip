@@ -262,13 +262,22 @@ struct AmaxOut {
   float* amax;  // null: not wanted
 };
 
+// Barriers of an LDS hand-off only: the epilogues below run after the kernel's output
+// stores, and __syncthreads()'s workgroup fence would wait for every one of them to retire
+// (vmcnt(0)) before the block can finish.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 __device__ __forceinline__ float block_max(float m, float* red /* >= 16 floats of LDS */) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
   const int w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
-  __syncthreads();
+  lds_barrier();  // an earlier block_max of this kernel is done reading red
   if ((threadIdx.x & 63) == 0) red[w] = m;
-  __syncthreads();
+  lds_barrier();
   float b = red[0];
   for (int k = 1; k < nw; ++k) b = fmaxf(b, red[k]);
   return b;  // every thread
@@ -1008,10 +1017,24 @@ int64_t bn_mask_bytes(bool bf16, int64_t M, int C) { (void)bf16; return M * (C /
 void bn_act_fwd(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C,
                 uintptr_t gamma, uintptr_t beta, uintptr_t rmean, uintptr_t rvar, uintptr_t save_mean,
                 uintptr_t save_rstd, uintptr_t ws, float momentum, float eps, bool relu, uintptr_t mask,
-                uintptr_t stats, int64_t nstat, uintptr_t amax) {
+                uintptr_t stats, int64_t nstat, uintptr_t amax, uintptr_t coef) {
   hip_check(hipSetDevice(dev), "hipSetDevice");
   auto F = [](uintptr_t p) { return reinterpret_cast<float*>(p); };
   auto* mk = reinterpret_cast<uint8_t*>(mask);
+  if (coef) {  // finalize folded into the producing GEMM (gemm.hip stats_fold): the apply pass only
+    if (!y) throw std::invalid_argument("bn_act forward: given coefficients need y");
+    if (bf16) {
+      check_shape(M, C, 8, x);
+      launch_apply<uint16_t>(s, reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(res),
+                             reinterpret_cast<uint16_t*>(y), M, C, F(coef), relu, mk, AmaxOut{F(amax)});
+    } else {
+      check_shape(M, C, 8, x);
+      launch_apply<float>(s, reinterpret_cast<const float*>(x), reinterpret_cast<const float*>(res),
+                          reinterpret_cast<float*>(y), M, C, F(coef), relu, mk, AmaxOut{F(amax)});
+    }
+    hip_check(hipGetLastError(), "bn_act forward launch");
+    return;
+  }
   if (bf16)
     fwd_impl<uint16_t>(dev, s, reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(res),
                        reinterpret_cast<uint16_t*>(y), M, C, F(gamma), F(beta), F(rmean), F(rvar), F(save_mean),

@@ -268,6 +268,18 @@ struct EpiArgs {
   // fp16x3 (FM 11): device upper bounds of |A| and |B| that set the operand scales
   const float* amax_a;
   const float* amax_b;
+  // EPI_STATS fold (scoef != null): the BN forward's finalize runs in this GEMM's last
+  // blocks (stats_fold): the statistics of the output become the BN's scale / shift
+  // [2][N], save_mean / save_rstd and running-statistics update; flvl ([groups][3][N]),
+  // ftick, fgroup and fzero as for the backward fold
+  float* scoef;
+  const float* sgamma;
+  const float* sbeta;
+  float* srmean;
+  float* srvar;
+  float* smean;
+  float* srstd;
+  float seps, smom;
 };
 
 // write-through (sc1) store: visible to a reader on any XCD without an L2 write-back
@@ -324,6 +336,16 @@ __device__ __forceinline__ void glds16_asm(const void* src, void* lds) {
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Workgroup barrier for an LDS hand-off only: this wave's LDS operations complete, then the
+// barrier. __syncthreads()'s workgroup fence also waits vmcnt(0) — every global store the
+// wave has issued must retire first — which in an epilogue that has just stored its output
+// tile stalls the whole block for a write round trip before it can reduce and exit.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 }
 
 // Map a linear block id to a tile id so that consecutive tile ids (which share the A
@@ -427,6 +449,107 @@ __device__ __forceinline__ void bnred_fold(const EpiArgs& ep, void* smem, int64_
   ep.fcoef[2 * N + c] = -A * mdz - Cc * ep.mean[c];
 }
 
+// BN forward finalize folded into the EPI_STATS GEMM (replaces the bn_tiles_finalize launch
+// of the BN forward, bn_act.hip): the partial rows hold (mean_k, M2_k) of n_k = min(128,
+// M - 128k) rows. Level 1: the last block of a group of fgroup M-tiles (ticket) merges the
+// group's rows in fp64, shifted by the group's first row mean, into (mean_g as a float pair,
+// M2_g) in flvl[g][3][N]; level 2: the last group-folder of the column tile merges the groups
+// shifted by mean_0 (the first tile's mean) and writes what the finalize wrote: scale / shift,
+// save_mean / save_rstd, the running statistics (unbiased variance, momentum), and zeroes
+// the BN output's fp16x3 bound. Deterministic (fixed orders); the hand-off is bnred_fold's.
+template <int BN, int HALVES>
+__device__ __forceinline__ void stats_fold(const EpiArgs& ep, void* smem, int64_t M, int N, int mt, int nt, int n0) {
+  constexpr int NT = 256, L = NT / BN;
+  const int t = threadIdx.x, cl = t % BN, kl = t / BN;
+  const int64_t mtn = (M + HALVES * 128 - 1) / (HALVES * 128);
+  const int fg = ep.fgroup;
+  const int ngr = int((mtn + fg - 1) / fg);
+  const int grp = mt / fg;
+  const int gsz = int(min<int64_t>(fg, mtn - int64_t(grp) * fg));
+  uint32_t* tk = ep.ftick + size_t(nt) * size_t(ngr + 1);
+  uint32_t* flag = reinterpret_cast<uint32_t*>(smem);
+  double* sd = reinterpret_cast<double*>(smem) + 2;  // [3][L][BN]
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every partial store of this block issued and retired; LDS reads done
+  if (t == 0) flag[0] = atomicAdd(&tk[grp], 1u);
+  __syncthreads();
+  if (flag[0] != uint32_t(gsz - 1)) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int64_t nparts = (M + 127) / 128;
+  const int64_t r0 = int64_t(grp) * fg * HALVES, r1 = min(nparts, r0 + int64_t(gsz) * HALVES);
+  const int c = n0 + cl;
+  const double kg = ep.part[(r0 * 2) * N + c];  // the group's shift: its first row's mean
+  double a = 0, b = 0;
+  for (int64_t r = r0 + kl; r < r1; r += L) {
+    const double nk = double(min<int64_t>(128, M - r * 128));
+    const double d = double(ep.part[(r * 2) * N + c]) - kg;
+    a = fma(nk, d, a);
+    b += double(ep.part[(r * 2 + 1) * N + c]) + nk * d * d;
+  }
+  sd[kl * BN + cl] = a;
+  sd[(L + kl) * BN + cl] = b;
+  __syncthreads();
+  if (kl == 0) {
+#pragma unroll
+    for (int k = 1; k < L; ++k) {
+      a += sd[k * BN + cl];
+      b += sd[(L + k) * BN + cl];
+    }
+    const double ng = double(min<int64_t>(M, r1 * 128) - r0 * 128);
+    const double mg = kg + a / ng;
+    const float mh = float(mg);
+    st_wt(ep.flvl + (int64_t(grp) * 3) * N + c, mh);
+    st_wt(ep.flvl + (int64_t(grp) * 3 + 1) * N + c, float(mg - double(mh)));
+    st_wt(ep.flvl + (int64_t(grp) * 3 + 2) * N + c, float(fmax(b - a * a / ng, 0.0)));
+  }
+  if (t == 0) __hip_atomic_store(&tk[grp], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) flag[0] = atomicAdd(&tk[ngr], 1u);
+  __syncthreads();
+  if (flag[0] != uint32_t(ngr - 1)) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const double k0 = ep.part[c];  // tile 0's mean
+  a = b = 0;
+  for (int g = kl; g < ngr; g += L) {
+    const int64_t g0 = int64_t(g) * fg * HALVES, g1 = min(nparts, g0 + int64_t(fg) * HALVES);
+    const double ng = double(min<int64_t>(M, g1 * 128) - g0 * 128);
+    const double d = double(ep.flvl[(int64_t(g) * 3) * N + c]) + double(ep.flvl[(int64_t(g) * 3 + 1) * N + c]) - k0;
+    a = fma(ng, d, a);
+    b += double(ep.flvl[(int64_t(g) * 3 + 2) * N + c]) + ng * d * d;
+  }
+  sd[kl * BN + cl] = a;
+  sd[(L + kl) * BN + cl] = b;
+  __syncthreads();
+  if (t == 0) __hip_atomic_store(&tk[ngr], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t < kBoundSlots && nt == 0 && ep.fzero) ep.fzero[t * kBoundStride] = 0.f;
+  if (kl != 0) return;
+  a = b = 0;
+#pragma unroll
+  for (int k = 0; k < L; ++k) {  // lane order
+    a += sd[k * BN + cl];
+    b += sd[(L + k) * BN + cl];
+  }
+  // bn_act.hip fin_fwd_channel's math with the shift k0
+  const double md = a / double(M);
+  double var = b / double(M) - md * md;
+  if (var < 0) var = 0;
+  const double mean = k0 + md;
+  const float rstd = float(1.0 / sqrt(var + double(ep.seps)));
+  const float sc = (ep.sgamma ? ep.sgamma[c] : 1.f) * rstd;
+  ep.scoef[c] = sc;
+  ep.scoef[N + c] = (ep.sbeta ? ep.sbeta[c] : 0.f) - float(mean) * sc;
+  ep.smean[c] = float(mean);
+  ep.srstd[c] = rstd;
+  const float mom = ep.smom;
+  if (ep.srmean) ep.srmean[c] = (1.f - mom) * ep.srmean[c] + mom * float(mean);
+  if (ep.srvar) ep.srvar[c] = (1.f - mom) * ep.srvar[c] + mom * float(var * double(M) / double(M > 1 ? M - 1 : 1));
+}
+
 // ------------------------------------------------------------------------------ NT GEMM
 // Column-reduction epilogues (EPI), one fp32 partial row pair per 128-row M-tile written to
 // ep.part[ep.row0 + mt][2][N] (deterministic, no atomics; reduced by the consumer):
@@ -453,7 +576,7 @@ __device__ __forceinline__ void bnred_fold(const EpiArgs& ep, void* smem, int64_
 // is lane-linear per wave instruction (16 rows x 64 B); the swizzle is applied on the
 // global source address.
 template <typename T, int BM, int BN, int STAGES, int EPI, bool CONV, int FM = 0>
-__global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 3 : 2)) : (BM == 256 ? (BN == 256 ? 1 : 2) : (STAGES == 2 ? (CONV || EPI == 3 ? 4 : 5) : 2))) void gemm_nt_kernel(const T* __restrict__ A, int64_t lda,
+__global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 1) : (BN == 64 ? 3 : 2)) : (BM == 256 ? (BN == 256 ? 1 : 2) : (STAGES == 2 ? (CONV || EPI == 3 ? 4 : 5) : 2))) void gemm_nt_kernel(const T* __restrict__ A, int64_t lda,
                                                          const T* __restrict__ B, int64_t ldb,
                                                          T* C, int64_t ldc, int64_t M, int N, int K,
                                                          int ntn, EpiArgs ep, const T* Cin,
@@ -1096,7 +1219,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
   if constexpr (EPI != EPI_NONE) {
     // combine the RPP threads of each chunk through LDS: [RPP][3][BN] floats
     float* red = reinterpret_cast<float*>(smem);
-    __syncthreads();  // phase B is done reading the tile
+    lds_barrier();  // phase B is done reading the tile (its C stores stay in flight)
     if constexpr (EPI == EPI_STATS) {  // this thread's (n, mean, M2)
       const float n = float(nv);
 #pragma unroll
@@ -1114,7 +1237,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
         if constexpr (DUAL) red[(rg * 3 + 2) * BN + ecol(e)] = s3[e];
       }
     }
-    __syncthreads();
+    lds_barrier();
     for (int q = t; q < BN * HALVES; q += NT) {
       const int hf = q / BN, n = q % BN;
       const int64_t tile = int64_t(mt) * HALVES + hf;  // 128-row partial row
@@ -1130,8 +1253,13 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
           m2 += red[(k * 3 + 2) * BN + n] + d * d * (na * nb / tot);
           na = tot;
         }
-        prow[n] = mean;
-        prow[N + n] = m2;
+        if (ep.scoef != nullptr) {  // read by the folding blocks (any XCD)
+          st_wt(prow + n, mean);
+          st_wt(prow + N + n, m2);
+        } else {
+          prow[n] = mean;
+          prow[N + n] = m2;
+        }
       } else {
         float a = 0.f, b = 0.f, c3 = 0.f;
         for (int k = hf * RPH; k < (hf + 1) * RPH; ++k) {
@@ -1156,6 +1284,9 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? 1 : (BN == 64 ? 
   }
   if constexpr (EPI == EPI_BNRED) {
     if (ep.fcoef != nullptr) bnred_fold<BN, HALVES>(ep, smem, M, N, mt, nt, n0);
+  }
+  if constexpr (EPI == EPI_STATS) {
+    if (ep.scoef != nullptr) stats_fold<BN, HALVES>(ep, smem, M, N, mt, nt, n0);
   }
 }
 
@@ -1469,7 +1600,10 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y
       const float4* src4 = reinterpret_cast<const float4*>(Ys);
 #pragma unroll
       for (int u = 0; u < NF4; ++u) v4[u] = src4[t + 256 * u];
-      __syncthreads();  // every thread holds its fp32 values: the slot takes the planes
+      // every thread holds its fp32 values: the slot takes the planes. LDS-only barriers:
+      // a __syncthreads() here waits vmcnt(0), i.e. for the next stage's LDS DMA issued at
+      // the top of this step, and the ring never overlaps a load with the MFMAs
+      lds_barrier();
       uint16_t* YH = reinterpret_cast<uint16_t*>(Ys);
       uint16_t* YL = YH + kRows * TBN;
       uint16_t* XH = YL + kRows * TBN;
@@ -1498,7 +1632,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y
         *reinterpret_cast<uint2*>((isy ? YH : XH) + o) = hw;
         *reinterpret_cast<uint2*>((isy ? YL : XL) + o) = lw;
       }
-      __syncthreads();
+      lds_barrier();
 #pragma unroll
       for (int kk = 0; kk < kRows / 16; ++kk) {
         const int rr = 16 * kk + 8 * h + q;  // row of this lane in the first 4-row block
@@ -2115,7 +2249,7 @@ int64_t gemm_nt_stats_floats(int64_t M, int N) { return gemm_nt_tiles(M) * 2 * i
 
 int64_t gemm_nt_tiles(int64_t M) { return (M + 127) / 128; }
 
-int64_t gemm_nt_fold_lvl_floats(int N) { return int64_t(kFoldMaxGroups) * 2 * N; }
+int64_t gemm_nt_fold_lvl_floats(int N) { return int64_t(kFoldMaxGroups) * 3 * N; }
 
 // Block tile of gemm_nt: 0 = 128 x (128 | 64), 1 = 256 x 128, 2 = 256 x 256;
 // MPIT_GEMM_TILE=128|256x128|256 selects one (A/B runs, large plain GEMMs). fp32 runs the
@@ -2235,6 +2369,8 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
     if (epi == EPI_BNRED2 && geo) throw std::invalid_argument("gemm_nt: paired BN reduction is for 1x1 GEMMs");
     if (ep.fcoef && (epi != EPI_BNRED || ep.row0 != 0 || !ep.frstd || !ep.flvl))
       throw std::invalid_argument("gemm_nt: the BN finalize fold needs a single-launch EPI_BNRED with rstd and lvl");
+    if (ep.scoef && (epi != EPI_STATS || ep.row0 != 0 || !ep.smean || !ep.srstd || !ep.flvl))
+      throw std::invalid_argument("gemm_nt: the BN forward fold needs a single-launch EPI_STATS with mean, rstd and lvl");
     if (epi == EPI_BNRED || epi == EPI_BNRED2) {
       if (!ep.x || !ep.mean || ldc != N) throw std::invalid_argument("gemm_nt: BN reduction needs x, mean, ldc == N");
       check_ptr(reinterpret_cast<uintptr_t>(ep.x), "BN x");
@@ -2324,6 +2460,13 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
   } while (0)
 #define MPIT_NT_LAUNCH1(BM, BN, ST, EPI, CONV)                                                                       \
   do {                                                                                                             \
+    if constexpr (F32 && BM == 256 && BN == 64) { /* fp16x3 only (MPIT_F32_TILE=256x64) */                      \
+      if (fm != 11) throw std::logic_error("gemm_nt: 256 x 64 fp32 tiles are for the fp16x3 kernels");            \
+      MPIT_NT_OPT_IN(BM, BN, ST, EPI, CONV, 11);                                                                   \
+      hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, ST, EPI, CONV, 11>), dim3(unsigned(nb)), dim3(256), shm, s, a,   \
+                         lda, b, ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g, bps);                            \
+      break;                                                                                                       \
+    } else {                                                                                                       \
     if constexpr (F32 && BM == 128 && ST == 2) {                                                                 \
       if (fm == 11) {                                                                                              \
         if (shm > 65536) MPIT_NT_OPT_IN(BM, BN, ST, EPI, CONV, 11);                                                 \
@@ -2384,6 +2527,7 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
     if (shm > 65536) MPIT_NT_OPT_IN(BM, BN, ST, EPI, CONV, 0);                                                      \
     hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, ST, EPI, CONV>), dim3(unsigned(nb)), dim3(256), shm, s, a, lda, b, \
                        ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g, bps);                                           \
+    }                                                                                                              \
   } while (0)
 #define MPIT_NT_LAUNCH2(BM, BN, ST, CONV)                                                         \
   do {                                                                                              \
@@ -2398,7 +2542,7 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
     const int ntn = N / BN;                                                                                    \
     const int64_t nb = mtn * ntn;                                                                              \
     if (nb > INT32_MAX) throw std::invalid_argument("gemm_nt: too many tiles");                               \
-    if (ep.fcoef) fold_plan(ep, dev, s, mtn, ntn);                                                                 \
+    if (ep.fcoef || ep.scoef) fold_plan(ep, dev, s, mtn, ntn);                                                                 \
     /* LDS: the k-tile ring, reused by the epilogue's output tile and reduction table */                      \
     const size_t shm = std::max({size_t(ST) * (size_t(BM) * nt_bkb(BM, BN, fm) +                               \
                                                 (fm == 11 ? size_t(BN) * 128 : fm == 4 || fm >= 9 ? size_t(BN) * 192 : size_t(BN) * nt_bkb(BM, BN, fm))), \
@@ -2408,6 +2552,17 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
   } while (0)
   const int tcfg = fm == 4 || fm >= 9 ? 0 : nt_tile_config(M, N, K, geo != nullptr, geo ? geo->C : 0, F32);
   if constexpr (F32) {
+    // MPIT_F32_TILE=256x64: the fp16x3 GEMMs with N == 64 on 256 x 64 blocks (each wave 64 x 64
+    // instead of 32 x 64: twice the MFMAs per barrier and per A fragment split, 2 blocks/CU)
+    static const bool t256x64 = [] {
+      const char* e = std::getenv("MPIT_F32_TILE");
+      return e && std::string(e) == "256x64";
+    }();
+    if (fm == 11 && N == 64 && t256x64) {
+      MPIT_NT_LAUNCH(256, 64, 2);
+      hip_check(hipGetLastError(), "gemm_nt launch");
+      return;
+    }
     if (tcfg == 1) {
       MPIT_NT_LAUNCH(256, 128, 3);
       hip_check(hipGetLastError(), "gemm_nt launch");
@@ -2466,6 +2621,19 @@ static EpiArgs epi_args(uintptr_t stats, const BnRed* r, int* mode) {
   if (stats) {
     ep.part = reinterpret_cast<float*>(stats);
     *mode = EPI_STATS;
+    if (r && r->scoef) {
+      ep.scoef = reinterpret_cast<float*>(r->scoef);
+      ep.sgamma = reinterpret_cast<const float*>(r->sgamma);
+      ep.sbeta = reinterpret_cast<const float*>(r->sbeta);
+      ep.srmean = reinterpret_cast<float*>(r->srmean);
+      ep.srvar = reinterpret_cast<float*>(r->srvar);
+      ep.smean = reinterpret_cast<float*>(r->smean);
+      ep.srstd = reinterpret_cast<float*>(r->srstd);
+      ep.flvl = reinterpret_cast<float*>(r->slvl);
+      ep.fzero = reinterpret_cast<float*>(r->szero);
+      ep.seps = r->seps;
+      ep.smom = r->smom;
+    }
   } else if (r && r->part) {
     ep.part = reinterpret_cast<float*>(r->part);
     ep.x = reinterpret_cast<const void*>(r->x);
@@ -2795,11 +2963,11 @@ static ConvGeo stem_geo(int Nb, int Hp, int Wp, int Ho, int Wo, int stride) {
 
 void conv_stem_fwd(int dev, hipStream_t s, int Nb, int Hp, int Wp, int Co, int Ho, int Wo, int stride, uintptr_t x,
                    uintptr_t w, uintptr_t y, uintptr_t stats, bool f32, int64_t bps, uintptr_t amax_a,
-                   uintptr_t amax_b) {
+                   uintptr_t amax_b, const BnRed* fold) {
   if (Co % 64) throw std::invalid_argument("conv_stem_fwd: need Co % 64 == 0");
   const ConvGeo g = stem_geo(Nb, Hp, Wp, Ho, Wo, stride);
   int mode;
-  BnRed r{};
+  BnRed r = fold ? *fold : BnRed{};
   r.amax_a = amax_a;
   r.amax_b = amax_b;
   const EpiArgs ep = epi_args(stats, &r, &mode);

@@ -86,7 +86,7 @@ int64_t bn_mask_bytes(bool bf16, int64_t M, int C);
 void bn_act_fwd(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C,
                 uintptr_t gamma, uintptr_t beta, uintptr_t rmean, uintptr_t rvar, uintptr_t save_mean,
                 uintptr_t save_rstd, uintptr_t ws, float momentum, float eps, bool relu, uintptr_t mask,
-                uintptr_t stats = 0, int64_t nstat = 0, uintptr_t amax = 0);
+                uintptr_t stats = 0, int64_t nstat = 0, uintptr_t amax = 0, uintptr_t coef = 0);
 // amax (optional, fp32 [1]): max |y| over the tensor (bn_act_bwd: max |dx|), the scale bound of the
 // fp16x3 GEMMs that read it: zeroed by this call's finalize, raised by its apply pass. With
 // y / dx null (the coefficient-only calls of a bn_pair) amax is only zeroed, for the pair
@@ -148,6 +148,12 @@ struct BnRed {
   // with fcoef: an output bound the folded finalize sets to zero (the BN backward's apply pass
   // then raises it to max |dx|)
   uintptr_t fzero = 0;
+  // with the forward statistics (stats != 0): fold the BN forward's finalize into the GEMM
+  // (single launch): scale / shift [2][N], save mean / rstd [N], running mean / var (or 0)
+  // updated with momentum, from gamma / beta (or 0) and eps; lvl: gemm_nt_fold_lvl_floats(N);
+  // zero: the BN output's bound, set to zero (the BN apply pass raises it)
+  uintptr_t scoef = 0, sgamma = 0, sbeta = 0, srmean = 0, srvar = 0, smean = 0, srstd = 0, slvl = 0, szero = 0;
+  float seps = 1e-5f, smom = 0.1f;
 };
 int64_t gemm_nt_fold_lvl_floats(int N);
 bool gemm_nt_supported(int64_t M, int N, int K, bool f32 = false);
@@ -215,7 +221,7 @@ void conv_wgrad(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int
 // dw = [Co][8][8][4] fp32; stats: BN statistics of y as conv_fwd
 void conv_stem_fwd(int dev, hipStream_t s, int Nb, int Hp, int Wp, int Co, int Ho, int Wo, int stride, uintptr_t x,
                    uintptr_t w, uintptr_t y, uintptr_t stats, bool f32 = false, int64_t bps = 0, uintptr_t amax_a = 0,
-                   uintptr_t amax_b = 0);
+                   uintptr_t amax_b = 0, const BnRed* fold = nullptr);
 // (fp32 fp16x3: w as two fp16 planes of plane stride bps with bound amax_b, the image's bound amax_a;
 // the wgrad's amax_y / amax_x as gemm_tn)
 int64_t conv_stem_wgrad_ws_floats(int dev, int Nb, int Ho, int Wo, int Co);

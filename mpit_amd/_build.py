@@ -162,7 +162,10 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = False, sanitize: s
         # sanitized variant: the shared sanitizer runtime comes from LD_PRELOAD (Python is not
         # instrumented), the module only references it
         san = ["-Xarch_host", f"-fsanitize={sanitize}", "-shared-libsan"] if sanitize else []
-        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC"] + san + ["-o", target] + objs + [
+        # link to a temporary name and rename: a process (or a tree snapshot) that opens the
+        # module meanwhile sees the old or the new file, never a half-written one
+        tmp = target + ".tmp"
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC"] + san + ["-o", tmp] + objs + [
             f"-L{ROCM}/lib",
             "-lamdhip64",
             "-lrt",
@@ -175,6 +178,7 @@ def build(jobs: int = 8, force: bool = False, verbose: bool = False, sanitize: s
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, target)
     return target
 
 

@@ -19,7 +19,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.bn import BatchNormAct2d, bn_pair
-from ..ops.conv import Conv1x1, ConvNHWC, GradSlot, StemConv, park_grad
+from ..ops.conv import Conv1x1, ConvNHWC, GradSlot, StemConv, feeds_bn, park_grad
 from ..ops.pool import MaxPool2dNHWC
 
 # Fused BN(+add)(+ReLU) HIP kernels on MI355X (mpit_amd/ops/bn.py); same parameters and
@@ -31,15 +31,21 @@ def _bn(c, act):
     return BatchNormAct2d(c, act=act) if FUSED_BN else nn.BatchNorm2d(c)
 
 
-def _feeds_bn(*convs):
-    """The MFMA convolutions whose outputs feed a fused BN emit its statistics from the
-    GEMM accumulators (ops/bn.py), so the BN forward is one pass. A ``(conv, BN)``
-    downsample Sequential may be passed as is."""
-    for c in convs:
-        if isinstance(c, nn.Sequential) and len(c) == 2 and isinstance(c[1], BatchNormAct2d):
-            c = c[0]
-        if FUSED_BN and hasattr(c, "emit_stats"):
-            c.emit_stats = True
+def _feeds_bn(*pairs):
+    """The MFMA convolutions whose outputs feed a fused BN emit its statistics from the GEMM
+    accumulators and run that BN's forward finalize in their last blocks (ops/bn.py), so the
+    BN forward is one apply pass. Each argument is a ``(conv, BN)`` pair, or a ``(conv, BN)``
+    downsample Sequential as is."""
+    for p in pairs:
+        if p is None:
+            continue
+        if isinstance(p, nn.Sequential):
+            if not (len(p) == 2 and isinstance(p[1], BatchNormAct2d)):
+                continue
+            p = (p[0], p[1])
+        c, bn = p
+        if FUSED_BN and hasattr(c, "emit_stats") and isinstance(bn, BatchNormAct2d):
+            feeds_bn(c, bn)
 
 
 # 1x1 convolutions as MFMA GEMMs and 3x3 ones as MFMA implicit GEMMs (both fall back to
@@ -75,7 +81,7 @@ class BasicBlock(nn.Module):
         self.conv2 = conv3x3(planes, planes)
         self.bn2 = _bn(planes, True)
         self.downsample = downsample
-        _feeds_bn(self.conv1, self.conv2, downsample)
+        _feeds_bn((self.conv1, self.bn1), (self.conv2, self.bn2), downsample)
 
     def forward(self, x):
         idt = x if self.downsample is None else self.downsample(x)
@@ -100,7 +106,7 @@ class Bottleneck(nn.Module):
         self.bn3 = _bn(planes * 4, True)
         self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample
-        _feeds_bn(self.conv1, self.conv2, self.conv3, downsample)
+        _feeds_bn((self.conv1, self.bn1), (self.conv2, self.bn2), (self.conv3, self.bn3), downsample)
 
     def forward(self, x):
         if isinstance(self.bn1, BatchNormAct2d):
@@ -147,7 +153,7 @@ class ResNet(nn.Module):
         # 7x7 stem on the MFMA row-tap kernels (ops/conv.py StemConv), emitting bn1's statistics
         self.conv1 = StemConv(3, 64, 7, 2, 3) if MFMA_CONV else nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False)
         self.bn1 = _bn(64, True)
-        _feeds_bn(self.conv1)
+        _feeds_bn((self.conv1, self.bn1))
         self.relu = nn.ReLU(inplace=True)
         self.maxpool = MaxPool2dNHWC(3, stride=2, padding=1) if MFMA_CONV else nn.MaxPool2d(3, stride=2, padding=1)
         self.layer1 = self._make(block, 64, layers[0])

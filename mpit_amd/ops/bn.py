@@ -19,6 +19,8 @@ tensors (tests, gloo plumbing) it computes the same function with PyTorch ops.
 """
 from __future__ import annotations
 
+import os
+
 from typing import Optional
 
 import torch
@@ -40,7 +42,7 @@ def _cl(x: torch.Tensor) -> torch.Tensor:
 
 
 # how often each fused hand-over fired (tests assert the fused path ran)
-COUNTERS = {"fwd_tile_stats": 0, "bwd_linked": 0, "bwd_folded": 0}
+COUNTERS = {"fwd_tile_stats": 0, "fwd_folded": 0, "bwd_linked": 0, "bwd_folded": 0}
 
 
 class BNLink:
@@ -94,11 +96,54 @@ class BNLink:
 
 
 def tile_stats_of(x: torch.Tensor):
-    """(partials, tiles) a producing GEMM attached to ``x`` (see module docstring), or None."""
+    """(partials, tiles, fold) a producing GEMM attached to ``x`` (see module docstring), or
+    None; fold: a :class:`BNFold` when the GEMM also ran this BN's forward finalize."""
     ts = getattr(x, "_mpit_tstats", None)
     if ts is None or ts[2] != x.data_ptr():
         return None
-    return ts[0], ts[1]
+    return ts[0], ts[1], ts[3]
+
+
+# MPIT_BN_FOLD_FWD=0: the BN forward's finalize as its own launch instead of in the GEMM
+_FWD_FOLD = os.environ.get("MPIT_BN_FOLD_FWD", "1") != "0"
+
+
+class BNFold:
+    """A BN forward finalize run by the GEMM that produces the BN's input (gemm.hip
+    stats_fold): that GEMM's last blocks turn the output's statistics into the BN's scale /
+    shift (``coef``), ``mean`` / ``rstd`` and the running-statistics update, and zero the
+    BN output's fp16x3 bound (``amax``) — the BN forward is then its apply pass alone.
+    ``args``: the tuple the native GEMM calls take (bindings.cpp apply_sfold)."""
+
+    __slots__ = ("coef", "mean", "rstd", "amax", "args", "_buf")
+
+    def __init__(self, bn: "BatchNormAct2d", C: int, want_amax: bool, device):
+        m = native()
+        nl = m.gemm_nt_fold_lvl_floats(C)
+        nb = _conv.BOUND_FLOATS if want_amax else 0
+        self._buf = buf = torch.empty(4 * C + nl + nb, dtype=torch.float32, device=device)
+        self.coef, self.mean, self.rstd = buf[: 2 * C], buf[2 * C: 3 * C], buf[3 * C: 4 * C]
+        lvl = buf[4 * C: 4 * C + nl]
+        self.amax = buf[4 * C + nl:] if want_amax else None
+        w = bn.weight if bn.affine else None
+        b = bn.bias if bn.affine else None
+        self.args = (self.coef.data_ptr(), w.data_ptr() if w is not None else 0, b.data_ptr() if b is not None else 0,
+                     bn.running_mean.data_ptr(), bn.running_var.data_ptr(), self.mean.data_ptr(), self.rstd.data_ptr(),
+                     lvl.data_ptr(), self.amax.data_ptr() if want_amax else 0, float(bn.eps), float(bn.momentum))
+
+
+def bn_fold_for(bn, C: int, dt, device) -> Optional[BNFold]:
+    """The fold of ``bn``'s forward finalize into the GEMM producing its [*, C] input of dtype
+    ``dt``, when that BN's training forward can take it (fused kernels, running statistics
+    with a fixed momentum, fp32 parameters); else None (the BN finalizes itself)."""
+    if not (_FWD_FOLD and isinstance(bn, BatchNormAct2d) and bn.training and bn.track_running_stats
+            and bn.momentum is not None and bn.num_features == C and C % 8 == 0
+            and dt in (torch.bfloat16, torch.float32) and device.type == "cuda"):
+        return None
+    if bn.affine and (bn.weight.dtype != torch.float32 or not bn.weight.is_contiguous()
+                      or bn.bias.dtype != torch.float32 or not bn.bias.is_contiguous()):
+        return None
+    return BNFold(bn, C, dt == torch.float32 and _conv._F32_SPLIT == "f16x3", device)
 
 
 def _want_amax(x: torch.Tensor) -> bool:
@@ -131,8 +176,12 @@ class _BNActFn(torch.autograd.Function):
         # ReLU: one mask bit per element replaces keeping / re-reading y in the backward
         mask = torch.empty(m.bn_mask_bytes(bf16, M, C), dtype=torch.uint8, device=x.device) if relu else None
         ts = tstats if (tstats is not None and tstats[1] == m.gemm_nt_tiles(M)) else None
+        fold = ts[2] if ts is not None else None
         if ts is not None:
             COUNTERS["fwd_tile_stats"] += 1
+        if fold is not None:  # the producing GEMM ran the finalize (stats_fold): apply pass only
+            COUNTERS["fwd_folded"] += 1
+            mean, rstd = fold.mean, fold.rstd
         m.bn_act_fwd(dev, stream, bf16, x.data_ptr(),
                      residual.data_ptr() if residual is not None else 0, y.data_ptr(), M, C,
                      w.data_ptr() if w is not None else 0, b.data_ptr() if b is not None else 0,
@@ -141,7 +190,8 @@ class _BNActFn(torch.autograd.Function):
                      mean.data_ptr(), rstd.data_ptr(), ws.data_ptr(), float(momentum), float(eps), bool(relu),
                      mask.data_ptr() if mask is not None else 0,
                      stats=ts[0].data_ptr() if ts is not None else 0, nstat=ts[1] if ts is not None else 0,
-                     amax=amax.data_ptr() if amax is not None else 0)
+                     amax=amax.data_ptr() if amax is not None else 0,
+                     coef=fold.coef.data_ptr() if fold is not None else 0)
         ctx.save_for_backward(x, mask, w, mean, rstd)
         ctx.link = link
         if link is not None:
@@ -282,9 +332,12 @@ class BatchNormAct2d(nn.BatchNorm2d):
         if self.training or not self.track_running_stats:
             momentum, rm, rv = self._train_args()
             link = BNLink() if torch.is_grad_enabled() else None
-            amax = _amax_buf(x)
+            ts = tile_stats_of(x)
+            fold = ts[2] if ts is not None else None
+            # a folded finalize zeroed its own output bound (the apply pass raises it)
+            amax = fold.amax if (fold is not None and _want_amax(x)) else _amax_buf(x)
             y = _BNActFn.apply(x, self.weight, self.bias, rm, rv, residual, momentum, self.eps, self.act,
-                               res_slot, tile_stats_of(x), link, amax)
+                               res_slot, ts, link, amax)
             if link is not None:
                 y._mpit_bnlink = link
             if amax is not None:
@@ -310,6 +363,7 @@ class _BNPairFn(torch.autograd.Function):
         bf16 = x1.dtype == torch.bfloat16
         f32 = dict(dtype=torch.float32, device=x1.device)
         outs = []
+        zeroed = False
         for x, w, b, rm, rv, mom, eps, ts in ((x1, w1, b1, rm1, rv1, mom1, eps1, ts1),
                                              (x2, w2, b2, rm2, rv2, mom2, eps2, ts2)):
             mean, rstd = torch.empty(C, **f32), torch.empty(C, **f32)
@@ -319,14 +373,22 @@ class _BNPairFn(torch.autograd.Function):
             ts = ts if (ts is not None and ts[1] == m.gemm_nt_tiles(M)) else None
             if ts is not None:
                 COUNTERS["fwd_tile_stats"] += 1
-            # (the first call also zeroes the pair's output bound, raised by the pair apply)
+            fold = ts[2] if ts is not None else None
+            if fold is not None:  # finalize run by the producing GEMM: its coefficients
+                COUNTERS["fwd_folded"] += 1
+                outs.append((wf, fold.mean, fold.rstd, fold.coef))
+                continue
+            # (the first finalize also zeroes the pair's output bound, raised by the pair apply)
             m.bn_act_fwd(dev, stream, bf16, x.data_ptr(), 0, 0, M, C, wf.data_ptr() if wf is not None else 0,
                          bf.data_ptr() if bf is not None else 0, rm.data_ptr() if rm is not None else 0,
                          rv.data_ptr() if rv is not None else 0, mean.data_ptr(), rstd.data_ptr(), ws.data_ptr(),
                          float(mom), float(eps), False, 0, stats=ts[0].data_ptr() if ts is not None else 0,
                          nstat=ts[1] if ts is not None else 0,
-                         amax=amax.data_ptr() if (amax is not None and not outs) else 0)
+                         amax=amax.data_ptr() if (amax is not None and not zeroed) else 0)
+            zeroed = True
             outs.append((wf, mean, rstd, ws))
+        if amax is not None and not zeroed:  # both finalizes folded into their GEMMs
+            amax.zero_()
         y = torch.empty_like(x1, memory_format=torch.channels_last)
         mask = torch.empty(m.bn_mask_bytes(bf16, M, C), dtype=torch.uint8, device=x1.device)
         # (scratch of the output bound: bn1's workspace past its coefficients)

@@ -38,6 +38,8 @@ from __future__ import annotations
 
 import os
 
+import weakref
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -438,15 +440,56 @@ def _link_of(x: torch.Tensor, dt, pair_ok: bool = True):
     return link
 
 
-def _tile_stats(co: int, M: int, device):
+class _Hold(list):
+    """Receives (partials, tiles, fold) from a statistics GEMM. ``bn``: the BatchNormAct2d the
+    output feeds, whose forward finalize the GEMM then runs in its last blocks (ops/bn.py
+    bn_fold_for, gemm.hip stats_fold) — the BN forward is left with its apply pass."""
+
+    def __init__(self, bn=None):
+        super().__init__()
+        self.bn = bn
+
+
+# conv -> weak reference of the BN its output feeds (kept outside the modules: no submodule,
+# and a deep copy of a model does not inherit the original's BN — it finalizes separately)
+_FOLD_TARGET = weakref.WeakKeyDictionary()
+
+
+def _hold_for(conv) -> "_Hold":
+    """The statistics hold of a convolution's forward (None: no statistics wanted)."""
+    if not (conv.emit_stats and conv.training):
+        return None
+    ref = _FOLD_TARGET.get(conv)
+    return _Hold(ref() if ref is not None else None)
+
+
+def feeds_bn(conv, bn) -> None:
+    """Mark ``conv`` as producing the input of ``bn``: it emits the BN's statistics and runs
+    its forward finalize."""
+    conv.emit_stats = True
+    _FOLD_TARGET[conv] = weakref.ref(bn)
+
+
+def _tile_stats(co: int, M: int, device, hold=None, dt=None):
+    """(partials, tiles, fold): the statistics buffer of a GEMM emitting its output's BN
+    statistics, and the fold of the fed BN's finalize when that BN can take it."""
     nt = native().gemm_nt_tiles(M)
-    return torch.empty(nt * 2 * co, dtype=torch.float32, device=device), nt
+    fold = None
+    if hold is not None and getattr(hold, "bn", None) is not None:
+        from .bn import bn_fold_for
+
+        fold = bn_fold_for(hold.bn, co, dt, device)
+    return torch.empty(nt * 2 * co, dtype=torch.float32, device=device), nt, fold
+
+
+def _fold_arg(fold):
+    return fold.args if fold is not None else None
 
 
 def _attach_stats(y: torch.Tensor, hold: list) -> torch.Tensor:
     if hold:
-        part, nt = hold[0]
-        y._mpit_tstats = (part, nt, y.data_ptr())
+        part, nt, fold = hold[0]
+        y._mpit_tstats = (part, nt, y.data_ptr(), fold)
     return y
 
 
@@ -522,12 +565,14 @@ class _Conv1x1Fn(torch.autograd.Function):
         y = torch.empty((n, co, h, w), dtype=dt, device=x.device, memory_format=torch.channels_last)
         m = native()
         st = None
+        fold = None
         if hold is not None:  # batch-norm statistics of y from the accumulators
-            st, nt = _tile_stats(co, M, x.device)
-            hold.append((st, nt))
+            st, nt, fold = _tile_stats(co, M, x.device, hold, dt)
+            hold.append((st, nt, fold))
         keep = []
         m.gemm_nt(x.device.index, _stream(x), M, co, ci, x.data_ptr(), ci, wb.data_ptr(), ci, y.data_ptr(), co,
-                  st.data_ptr() if st is not None else 0, f32=f32, **_split_kw(x, wb, f32, keep))
+                  st.data_ptr() if st is not None else 0, f32=f32, bn_fold=_fold_arg(fold),
+                  **_split_kw(x, wb, f32, keep))
         ctx.save_for_backward(x, wt)
         ctx.xamax = amax_of(x) if f32 else None
         ctx.wshape = weight.shape
@@ -610,7 +655,7 @@ class Conv1x1(nn.Conv2d):
 
     def forward(self, x: torch.Tensor, slot: "GradSlot" = None) -> torch.Tensor:
         if self.fused(x):
-            hold = [] if (self.emit_stats and self.training) else None
+            hold = _hold_for(self)
             dt = mfma_dtype(x)
             y = _Conv1x1Fn.apply(x, self.weight, slot, hold, _link_of(x, dt) if torch.is_grad_enabled() else None,
                                  WeightCastPlan.cached(self, dt), dt)
@@ -779,14 +824,15 @@ class _ConvFn(torch.autograd.Function):
         if bias is not None:
             b = bias if (bias.dtype == torch.float32 and bias.is_contiguous()) else bias.float().contiguous()
         st = None
+        fold = None
         if hold is not None and not relu and b is None:  # batch-norm statistics of y
-            st, nt = _tile_stats(co, nb * ho * wo, x.device)
-            hold.append((st, nt))
+            st, nt, fold = _tile_stats(co, nb * ho * wo, x.device, hold, dt)
+            hold.append((st, nt, fold))
         keep = []
         native().conv_fwd(x.device.index, _stream(x), nb, h, w, c, co, r, s, stride, pad, x.data_ptr(), wb.data_ptr(),
                           y.data_ptr(), stats=st.data_ptr() if st is not None else 0,
                           bias=b.data_ptr() if b is not None else 0, relu=bool(relu), f32=f32,
-                          **_split_kw(x, wb, f32, keep))
+                          bn_fold=_fold_arg(fold), **_split_kw(x, wb, f32, keep))
         ctx.save_for_backward(x, wb, wt, y if relu else None)
         ctx.xamax = amax_of(x) if f32 else None
         ctx.geo = (stride, pad, bias is not None, bool(relu))
@@ -864,7 +910,7 @@ class ConvNHWC(nn.Conv2d):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.fused(x):
-            hold = [] if (self.emit_stats and self.training) else None
+            hold = _hold_for(self)
             dt = mfma_dtype(x)
             y = _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0], None, False, hold,
                               _link_of(x, dt, pair_ok=False) if torch.is_grad_enabled() else None,
@@ -1129,9 +1175,10 @@ class _StemConvFn(torch.autograd.Function):
         wb = None if f16s and _STEM_NATIVE_PLANES else _stem_pack_weight(weight, dt)
         y = torch.empty((nb, co, ho, wo), dtype=dt, device=x.device, memory_format=torch.channels_last)
         st = None
+        fold = None
         if hold is not None:
-            st, nt = _tile_stats(co, nb * ho * wo, x.device)
-            hold.append((st, nt))
+            st, nt, fold = _tile_stats(co, nb * ho * wo, x.device, hold, dt)
+            hold.append((st, nt, fold))
         kw, ctx.xbound = {}, None
         if f16s:
             # fp16x3: the image's bound (the padded copy only adds zeros) and the packed weight as
@@ -1147,7 +1194,8 @@ class _StemConvFn(torch.autograd.Function):
                 wb = f16_planes(wb.reshape(co, -1), wam)
             kw = dict(bps=wb[0].numel(), amax_a=ctx.xbound.data_ptr(), amax_b=wam.data_ptr())
         native().conv_stem_fwd(x.device.index, _stream(x), nb, hp, wp, co, ho, wo, stride, xp.data_ptr(),
-                               wb.data_ptr(), y.data_ptr(), st.data_ptr() if st is not None else 0, f32=f32, **kw)
+                               wb.data_ptr(), y.data_ptr(), st.data_ptr() if st is not None else 0, f32=f32,
+                               bn_fold=_fold_arg(fold), **kw)
         ctx.save_for_backward(xp)
         ctx.geo = (nb, hp, wp, co, ho, wo, stride, tuple(weight.shape))
         ctx.pack = ent
@@ -1202,7 +1250,7 @@ class StemConv(nn.Conv2d):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.fused(x):
-            hold = [] if (self.emit_stats and self.training) else None
+            hold = _hold_for(self)
             y = _StemConvFn.apply(x, self.weight, self.stride[0], self.padding[0], hold, mfma_dtype(x))
             return _attach_stats(y, hold)
         return super().forward(x)

@@ -10,7 +10,7 @@ the run with that step's exit code — nothing else touches the GPU after it.
 Steps:
   smoke                 __graft_entry__.smoke()                         -> smoke.log
   tier                  pytest -m gpu (whole GPU tier)                  -> pytest_gpu.log
-  pytest:<args>         pytest <args> (e.g. pytest:tests/test_overlap.py) -> pytest_<n>.log
+  pytest:<args>[:K=V;K=V] pytest <args> (e.g. pytest:tests/test_overlap.py), extra env -> pytest_<n>.log
   bench                 bench.py defaults (fp32 headline + bf16 secondary) -> bench.json
   bench:<args>[:K=V;K=V] bench.py <args> (comma separated), extra env    -> bench_<n>.json
   dbench:<n>:<args>     bench.py on n ranks sharing the box's GPU (rehearsal) -> dbench_<n>.json
@@ -81,7 +81,9 @@ def main(argv) -> int:
             rc = _run(out, "pytest_gpu.log", pyt + ["tests", "-m", "gpu"] + (rest.split(",") if rest else []), 1000)
             print(_tail(os.path.join(out, "pytest_gpu.log"), 2))
         elif kind == "pytest":
-            rc = _run(out, f"pytest_{i}.log", pyt + rest.split(","), 900)
+            parts = rest.split(":")
+            env = dict(kv.split("=", 1) for kv in parts[1].split(";")) if len(parts) > 1 and parts[1] else {}
+            rc = _run(out, f"pytest_{i}.log", pyt + parts[0].split(","), 900, env=env)
             print(_tail(os.path.join(out, f"pytest_{i}.log"), 2))
         elif kind == "bench":
             parts = rest.split(":")

@@ -33,7 +33,7 @@ def test_stem_emits_bn_stats():
     conv.emit_stats = True
     x = torch.randn(2, 3, 64, 64, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     y = conv(x)
-    part, nt, ptr = y._mpit_tstats
+    part, nt, ptr, _fold = y._mpit_tstats
     assert ptr == y.data_ptr()
     M = y.shape[0] * y.shape[2] * y.shape[3]
     sums = tile_stats_to_sums(part, M, 64).double()

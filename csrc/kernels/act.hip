@@ -76,7 +76,10 @@ __global__ __launch_bounds__(1024) void relu_bias_bwd_kernel(const T* __restrict
   if (!part) return;
 #pragma unroll
   for (int v = 0; v < 8; ++v) lds[rs * C + g * 8 + v] = acc[v];
-  __syncthreads();
+  // LDS hand-off only: a __syncthreads() fence would first wait for every dz store above
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     float s = 0.f;
     for (int k = 0; k < R; ++k) s += lds[k * C + c];

@@ -2278,8 +2278,14 @@ static int nt_tile_config(int64_t M, int N, int K, bool conv, int cin_conv, bool
   // where K is deep (>= 1024) AND the grid still has >= 4 blocks per CU — VGG-16's 112/56-
   // pixel 3x3 convolutions and their backward-data, no ResNet-50 shape — VGG-16 bf16 EASGD
   // +3.5 % (4,944 vs 4,774 / 4,824 img/s with every GEMM on 256x128, gpurun_out/r04vgg).
+  // MPIT_GEMM_DEEPK=k (A/B): 256 x 128 for every GEMM with K >= k, whatever its grid
+  static const int deepk = [] {
+    const char* e = std::getenv("MPIT_GEMM_DEEPK");
+    return e ? std::atoi(e) : 0;
+  }();
   int cfg = forced >= 0 ? forced
                         : (K >= 1024 && N % 128 == 0 && ((M + 255) / 256) * int64_t(N / 128) >= 1024 ? 1 : 0);
+  if (forced < 0 && deepk > 0 && K >= deepk && N % 128 == 0) cfg = 1;
   if (cfg == 2 && (N % 256 || K % 64 || (conv && cin_conv % 64))) cfg = N % 128 ? 0 : 1;
   if (cfg == 1 && N % 128) cfg = 0;
   return cfg;

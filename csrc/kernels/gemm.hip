@@ -1361,12 +1361,15 @@ __device__ __forceinline__ void tn_tile_sum(const float* src, int nsrc, int64_t 
   }
 }
 
-template <typename T, int TBN, int TBK, int STAGES, bool CONV, int FM = 0>
+template <typename T, int TBN, int TBK, int STAGES, bool CONV, int FM = 0, int KR = kRows>
 __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y, int64_t ldy,
                                                          const T* __restrict__ X, int64_t ldx,
                                                          float* __restrict__ part, int64_t M, int N, int K,
                                                          int64_t rows_per_split, int ntk, int ntiles, ConvGeo geo,
                                                          TnRed red) {
+  // rows per staged step (KR = 64, bf16 only, MPIT_TN_KROWS=64: half the barriers and ring
+  // turns per row for the memory-bound wgrads)
+  constexpr int kRows = KR;
   constexpr int WN = TBN / 2, WK = TBK / 2;
   constexpr int TM = WN / 32, TN = WK / 32;
   constexpr int EPC = epc<T>();
@@ -2869,10 +2872,60 @@ static void launch_tn_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
     if (stages == 2) MPIT_TN_LAUNCH1(A, B, 2); \
     else MPIT_TN_LAUNCH1(A, B, 4);         \
   } while (0)
+  // MPIT_TN_KROWS=64 (A/B, bf16): 64-row staged steps on a 2-deep ring (MPIT_TN_KR_STAGES=3:
+  // 3-deep) — the LDS of the default 4 x 32-row ring
+  static const int kr64_stages = [] {
+    const char* e = std::getenv("MPIT_TN_KROWS");
+    if (!(e && std::atoi(e) == 64)) return 0;
+    const char* st = std::getenv("MPIT_TN_KR_STAGES");
+    return st && std::atoi(st) == 3 ? 3 : 2;
+  }();
+  bool done64 = false;
+  if constexpr (!F32) {
+    if (kr64_stages && !fused) {
+#define MPIT_TN_K64(A, B, ST)                                                                                      \
+  do {                                                                                                             \
+    const size_t shm = size_t(ST) * 64 * (tbn + tbk) * sizeof(T);                                                  \
+    if (geo) {                                                                                                     \
+      if (shm > 65536) MPIT_TN_OPT_IN64(A, B, ST, true);                                                           \
+      hipLaunchKernelGGL((gemm_tn_kernel<T, A, B, ST, true, 0, 64>), grid, dim3(256), shm, s, y, ldy, x, ldx, part, \
+                         M, N, K, rps, ntk, ntiles, g, red);                                                       \
+    } else {                                                                                                       \
+      if (shm > 65536) MPIT_TN_OPT_IN64(A, B, ST, false);                                                          \
+      hipLaunchKernelGGL((gemm_tn_kernel<T, A, B, ST, false, 0, 64>), grid, dim3(256), shm, s, y, ldy, x, ldx,    \
+                         part, M, N, K, rps, ntk, ntiles, g, red);                                                 \
+    }                                                                                                              \
+  } while (0)
+#define MPIT_TN_OPT_IN64(A, B, ST, CV)                                                                             \
+  do {                                                                                                             \
+    static const bool opted = (hip_check(hipFuncSetAttribute(reinterpret_cast<const void*>(                       \
+                                                             &gemm_tn_kernel<T, A, B, ST, CV, 0, 64>),            \
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize, int(shm)),    \
+                                     "hipFuncSetAttribute"),                                                       \
+                               true);                                                                              \
+    (void)opted;                                                                                                   \
+  } while (0)
+#define MPIT_TN_K64S(A, B)                  \
+  do {                                      \
+    if (kr64_stages == 3) MPIT_TN_K64(A, B, 3); \
+    else MPIT_TN_K64(A, B, 2);              \
+  } while (0)
+      if (tbn == 128 && tbk == 128) MPIT_TN_K64S(128, 128);
+      else if (tbn == 128) MPIT_TN_K64S(128, 64);
+      else if (tbk == 128) MPIT_TN_K64S(64, 128);
+      else MPIT_TN_K64S(64, 64);
+#undef MPIT_TN_K64S
+#undef MPIT_TN_K64
+#undef MPIT_TN_OPT_IN64
+      done64 = true;
+    }
+  }
+  if (!done64) {
   if (tbn == 128 && tbk == 128) MPIT_TN_LAUNCH(128, 128);
   else if (tbn == 128) MPIT_TN_LAUNCH(128, 64);
   else if (tbk == 128) MPIT_TN_LAUNCH(64, 128);
   else MPIT_TN_LAUNCH(64, 64);
+  }
   }
 #undef MPIT_TN_LAUNCH
 #undef MPIT_TN_LAUNCH1

@@ -272,5 +272,5 @@ def test_folded_bn_forward_finalize_matches_separate_launch(dtype):
     # the activations, and those propagate into the gradients of the later layers
     for k in r_sep:
         assert torch.isfinite(r_fold[k]).all(), k
-        tol = 2e-5 if (dtype == torch.float32 or "running" in k) else 5e-2
+        tol = 2e-5 if dtype == torch.float32 else (1e-3 if "running" in k else 5e-2)
         assert _rel(r_fold[k], r_sep[k]) < tol, (k, _rel(r_fold[k], r_sep[k]))

@@ -274,15 +274,17 @@ PYBIND11_MODULE(_mpit, m) {
   m.def(
       "conv_stem_fwd",
       [](int dev, uintptr_t s, int Nb, int Hp, int Wp, int Co, int Ho, int Wo, int stride, uintptr_t x, uintptr_t w,
-         uintptr_t y, uintptr_t stats, bool f32, int64_t bps, uintptr_t amax_a, uintptr_t amax_b, py::object bn_fold) {
+         uintptr_t y, uintptr_t stats, bool f32, int64_t bps, uintptr_t amax_a, uintptr_t amax_b, py::object bn_fold,
+         int rows, uintptr_t bias, bool relu) {
         BnRed r{};
         apply_sfold(r, bn_fold);
-        conv_stem_fwd(dev, S(s), Nb, Hp, Wp, Co, Ho, Wo, stride, x, w, y, stats, f32, bps, amax_a, amax_b, &r);
+        conv_stem_fwd(dev, S(s), Nb, Hp, Wp, Co, Ho, Wo, stride, x, w, y, stats, f32, bps, amax_a, amax_b, &r, rows,
+                      bias, relu);
       },
       py::arg("dev"), py::arg("stream"), py::arg("Nb"), py::arg("Hp"), py::arg("Wp"), py::arg("Co"), py::arg("Ho"),
       py::arg("Wo"), py::arg("stride"), py::arg("x"), py::arg("w"), py::arg("y"), py::arg("stats"),
       py::arg("f32") = false, py::arg("bps") = 0, py::arg("amax_a") = 0, py::arg("amax_b") = 0,
-      py::arg("bn_fold") = py::none());
+      py::arg("bn_fold") = py::none(), py::arg("rows") = 8, py::arg("bias") = 0, py::arg("relu") = false);
   m.def(
       "stem_weight_planes",
       [](int dev, uintptr_t s, uintptr_t w, int Co, int C, int R, int Sk, uintptr_t planes, uintptr_t bound) {
@@ -290,16 +292,18 @@ PYBIND11_MODULE(_mpit, m) {
       },
       py::arg("dev"), py::arg("stream"), py::arg("w"), py::arg("Co"), py::arg("C"), py::arg("R"), py::arg("S"),
       py::arg("planes"), py::arg("bound"));
-  m.def("conv_stem_wgrad_ws_floats", &conv_stem_wgrad_ws_floats);
+  m.def("conv_stem_wgrad_ws_floats", &conv_stem_wgrad_ws_floats, py::arg("dev"), py::arg("Nb"), py::arg("Ho"),
+        py::arg("Wo"), py::arg("Co"), py::arg("rows") = 8);
+  m.def("stem_wgrad_rows", &stem_wgrad_rows);
   m.def(
       "conv_stem_wgrad",
       [](int dev, uintptr_t s, int Nb, int Hp, int Wp, int Co, int Ho, int Wo, int stride, uintptr_t dy, uintptr_t x,
-         uintptr_t dw, uintptr_t ws, bool f32, uintptr_t amax_y, uintptr_t amax_x) {
-        conv_stem_wgrad(dev, S(s), Nb, Hp, Wp, Co, Ho, Wo, stride, dy, x, dw, ws, f32, amax_y, amax_x);
+         uintptr_t dw, uintptr_t ws, bool f32, uintptr_t amax_y, uintptr_t amax_x, int rows) {
+        conv_stem_wgrad(dev, S(s), Nb, Hp, Wp, Co, Ho, Wo, stride, dy, x, dw, ws, f32, amax_y, amax_x, rows);
       },
       py::arg("dev"), py::arg("stream"), py::arg("Nb"), py::arg("Hp"), py::arg("Wp"), py::arg("Co"), py::arg("Ho"),
       py::arg("Wo"), py::arg("stride"), py::arg("dy"), py::arg("x"), py::arg("dw"), py::arg("ws"),
-      py::arg("f32") = false, py::arg("amax_y") = 0, py::arg("amax_x") = 0);
+      py::arg("f32") = false, py::arg("amax_y") = 0, py::arg("amax_x") = 0, py::arg("rows") = 8);
   m.def("conv_wgrad_ws_floats", &conv_wgrad_ws_floats);
   m.def(
       "conv_wgrad",

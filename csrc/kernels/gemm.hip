@@ -61,7 +61,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 constexpr int kBK = 32;  // k-depth of one staged bf16 tile (gemm_nt): 64-B LDS rows
-constexpr int kStemTap = 32, kStemK = 8 * kStemTap;  // row-tap stem: 8 pixels x 4 channels per row
+constexpr int kStemTap = 32;  // row-tap stem: 8 pixels x 4 channels per kernel row
 
 // Element types: uint16_t = bf16 operands on v_mfma_f32_32x32x16_bf16; float = fp32
 // operands on v_mfma_f32_32x32x2_f32 (exact fp32 products, fp32 accumulate: the
@@ -3011,41 +3011,49 @@ void conv_wgrad(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int
 }
 
 // Row-tap stem convolution: x is a zero-padded NHWC4 image [Nb][Hp][Wp][4] (bf16 / fp32), the
-// kernel has 8 rows of 8 pixels x 4 channels (K = 256; a 7x7x3 kernel zero-extended), output
-// pixel (ho, wo) reads rows ho*stride + r, pixels wo*stride .. +7 of each.
-static ConvGeo stem_geo(int Nb, int Hp, int Wp, int Ho, int Wo, int stride) {
-  if (Nb <= 0 || Ho <= 0 || Wo <= 0 || stride <= 0 || Hp < (Ho - 1) * stride + 8 || Wp < (Wo - 1) * stride + 8)
+// kernel has `rows` rows of 8 pixels x 4 channels (K = rows * 32; a 7x7x3 kernel zero-extended
+// to 8 rows, a 3x3x3 one to 3), output pixel (ho, wo) reads rows ho*stride + r, pixels
+// wo*stride .. +7 of each.
+static ConvGeo stem_geo(int Nb, int Hp, int Wp, int Ho, int Wo, int stride, int rows) {
+  if (rows < 1 || rows > 8) throw std::invalid_argument("conv_stem: 1 <= rows <= 8");
+  if (Nb <= 0 || Ho <= 0 || Wo <= 0 || stride <= 0 || Hp < (Ho - 1) * stride + rows || Wp < (Wo - 1) * stride + 8)
     throw std::invalid_argument("conv_stem: padded image too small for the output");
   if (int64_t(Nb) * Hp * Wp * 4 >= (int64_t(1) << 31)) throw std::invalid_argument("conv_stem: input too large");
   return ConvGeo{Hp, Wp, kStemTap, Ho, Wo, 1, stride, 0, 0, 1, 0, 0, Ho, Wo, 0, 4};
 }
 
+int stem_wgrad_rows(int rows) { return rows + (rows & 1); }
+
 void conv_stem_fwd(int dev, hipStream_t s, int Nb, int Hp, int Wp, int Co, int Ho, int Wo, int stride, uintptr_t x,
                    uintptr_t w, uintptr_t y, uintptr_t stats, bool f32, int64_t bps, uintptr_t amax_a,
-                   uintptr_t amax_b, const BnRed* fold) {
+                   uintptr_t amax_b, const BnRed* fold, int rows, uintptr_t bias, bool relu) {
   if (Co % 64) throw std::invalid_argument("conv_stem_fwd: need Co % 64 == 0");
-  const ConvGeo g = stem_geo(Nb, Hp, Wp, Ho, Wo, stride);
+  const ConvGeo g = stem_geo(Nb, Hp, Wp, Ho, Wo, stride, rows);
   int mode;
   BnRed r = fold ? *fold : BnRed{};
   r.amax_a = amax_a;
   r.amax_b = amax_b;
   const EpiArgs ep = epi_args(stats, &r, &mode);
-  launch_nt(dev, s, int64_t(Nb) * Ho * Wo, Co, kStemK, x, kStemTap, w, kStemK, y, Co, 0, 0, &g, ep, mode, f32, 0, false,
-            bps);
+  if (mode != EPI_NONE && (bias || relu)) throw std::invalid_argument("conv_stem_fwd: statistics and bias/ReLU are exclusive");
+  const int K = rows * kStemTap;
+  launch_nt(dev, s, int64_t(Nb) * Ho * Wo, Co, K, x, kStemTap, w, K, y, Co, 0, 0, &g, ep, mode, f32, bias, relu, bps);
 }
 
-int64_t conv_stem_wgrad_ws_floats(int dev, int Nb, int Ho, int Wo, int Co) {
+int64_t conv_stem_wgrad_ws_floats(int dev, int Nb, int Ho, int Wo, int Co, int rows) {
+  const int K = stem_wgrad_rows(rows) * kStemTap;
   int64_t rps;
   int tbn, tbk;
-  const int ns = tn_plan(dev, int64_t(Nb) * Ho * Wo, Co, kStemK, &rps, &tbn, &tbk, kStemTap);
-  return ns > 1 ? (int64_t(ns) + tn_groups(ns)) * Co * kStemK : 0;
+  const int ns = tn_plan(dev, int64_t(Nb) * Ho * Wo, Co, K, &rps, &tbn, &tbk, kStemTap);
+  return ns > 1 ? (int64_t(ns) + tn_groups(ns)) * Co * K : 0;
 }
 
 void conv_stem_wgrad(int dev, hipStream_t s, int Nb, int Hp, int Wp, int Co, int Ho, int Wo, int stride, uintptr_t dy,
-                     uintptr_t x, uintptr_t dw, uintptr_t ws, bool f32, uintptr_t amax_y, uintptr_t amax_x) {
+                     uintptr_t x, uintptr_t dw, uintptr_t ws, bool f32, uintptr_t amax_y, uintptr_t amax_x, int rows) {
   if (Co % 64) throw std::invalid_argument("conv_stem_wgrad: need Co % 64 == 0");
-  const ConvGeo g = stem_geo(Nb, Hp, Wp, Ho, Wo, stride);
-  launch_tn(dev, s, int64_t(Nb) * Ho * Wo, Co, kStemK, dy, Co, x, kStemTap, dw, ws, 0.f, &g, f32, amax_y, amax_x);
+  const int rw = stem_wgrad_rows(rows);
+  const ConvGeo g = stem_geo(Nb, Hp, Wp, Ho, Wo, stride, rw);
+  launch_tn(dev, s, int64_t(Nb) * Ho * Wo, Co, rw * kStemTap, dy, Co, x, kStemTap, dw, ws, 0.f, &g, f32, amax_y,
+            amax_x);
 }
 
 static void launch_cast(int dev, hipStream_t s, uintptr_t w, int R, int Cc, uintptr_t wb, uintptr_t wt, int taps,

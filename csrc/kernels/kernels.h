@@ -216,18 +216,23 @@ void conv_wgrad(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int
                 uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, float beta, bool f32 = false,
                 uintptr_t amax_y = 0, uintptr_t amax_x = 0);
 
-// Row-tap stem conv (7x7 / stride-2 / 3-channel ResNet stem on MFMA): x = zero-padded NHWC4
-// image [Nb][Hp][Wp][4], w = [Co][8][8][4] (bf16, zero-extended kernel), y = [Nb][Ho][Wo][Co];
-// dw = [Co][8][8][4] fp32; stats: BN statistics of y as conv_fwd
+// Row-tap stem conv (7x7 / stride-2 / 3-channel ResNet stem on MFMA; VGG's 3x3 / 3-channel
+// first layer with rows = 3): x = zero-padded NHWC4 image [Nb][Hp][Wp][4], w = [Co][rows][8][4]
+// (bf16, zero-extended kernel), y = [Nb][Ho][Wo][Co]; dw = [Co][rows_w][8][4] fp32 with rows_w =
+// rows rounded up to even (the weight-gradient GEMM's K = rows_w * 32 must be a multiple of 64;
+// the image then needs Hp >= (Ho - 1) * stride + rows_w); stats: BN statistics of y as conv_fwd;
+// bias / relu: the conv(+bias)(+ReLU) epilogue of conv_fwd
 void conv_stem_fwd(int dev, hipStream_t s, int Nb, int Hp, int Wp, int Co, int Ho, int Wo, int stride, uintptr_t x,
                    uintptr_t w, uintptr_t y, uintptr_t stats, bool f32 = false, int64_t bps = 0, uintptr_t amax_a = 0,
-                   uintptr_t amax_b = 0, const BnRed* fold = nullptr);
+                   uintptr_t amax_b = 0, const BnRed* fold = nullptr, int rows = 8, uintptr_t bias = 0,
+                   bool relu = false);
 // (fp32 fp16x3: w as two fp16 planes of plane stride bps with bound amax_b, the image's bound amax_a;
 // the wgrad's amax_y / amax_x as gemm_tn)
-int64_t conv_stem_wgrad_ws_floats(int dev, int Nb, int Ho, int Wo, int Co);
+int64_t conv_stem_wgrad_ws_floats(int dev, int Nb, int Ho, int Wo, int Co, int rows = 8);
 void conv_stem_wgrad(int dev, hipStream_t s, int Nb, int Hp, int Wp, int Co, int Ho, int Wo, int stride, uintptr_t dy,
                      uintptr_t x, uintptr_t dw, uintptr_t ws, bool f32 = false, uintptr_t amax_y = 0,
-                     uintptr_t amax_x = 0);
+                     uintptr_t amax_x = 0, int rows = 8);
+int stem_wgrad_rows(int rows);
 
 // ---- NHWC bf16 / fp32 max pooling with a uint8 argmax per output element (pool.hip) ---
 // x [N,H,W,C] -> y, idx [N,Ho,Wo,C]; dx [N,H,W,C] gathered from dy + idx (no atomics).

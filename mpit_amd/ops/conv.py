@@ -82,6 +82,17 @@ class WgradStream:
     # input-gradient GEMM (so it overlaps the memory-bound BN backward that follows instead
     # of sharing the CUs with that compute-bound GEMM); default: before it
     after = os.environ.get("MPIT_WGRAD_AFTER", "0") == "1"
+    # MPIT_WGRAD_SIDE: which weight gradients go to the side stream. all (default) | deep (RxS
+    # convolutions only: their wgrad is compute-bound) | fp32 (fp32 calls only) | deep16 (RxS
+    # convolutions, and every fp32 call). Concurrent memory-bound bf16 pairs run slower than
+    # back to back (profiles/epi_roofline_r05.md); the others stay on the compute stream.
+    policy = os.environ.get("MPIT_WGRAD_SIDE", "all")
+
+    @classmethod
+    def wants(cls, f32: bool, deep: bool) -> bool:
+        p = cls.policy
+        return (p == "all" or (p == "deep" and deep) or (p == "fp32" and f32)
+                or (p == "deep16" and (deep or f32)))
 
     @classmethod
     def enable(cls, on: bool = True):
@@ -592,7 +603,8 @@ class _Conv1x1Fn(torch.autograd.Function):
         m = native()
         dev, s = x.device.index, _stream(x)
         dx = dw = None
-        side = WgradStream.begin(x.device) if ctx.needs_input_grad[1] and not WgradStream.after else None
+        use_side = ctx.needs_input_grad[1] and WgradStream.wants(f32, False)
+        side = WgradStream.begin(x.device) if use_side and not WgradStream.after else None
         extra, emask = ctx.slot.take() if ctx.slot is not None else (None, None)
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x, memory_format=torch.channels_last)
@@ -614,7 +626,7 @@ class _Conv1x1Fn(torch.autograd.Function):
             if part is not None:
                 ctx.link.publish(part, nt, dx, part2, fb)
         if ctx.needs_input_grad[1]:
-            if WgradStream.after:
+            if WgradStream.after and use_side:
                 side = WgradStream.begin(x.device)
             dw = torch.empty(ctx.wshape, dtype=torch.float32, device=x.device)
             nws = m.gemm_tn_ws_floats(dev, M, co, ci)
@@ -732,7 +744,8 @@ def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None):
     m = native()
     dev, st = x.device.index, _stream(x)
     dx = dw = None
-    side = WgradStream.begin(x.device) if ctx.needs_input_grad[1] and not WgradStream.after else None
+    use_side = ctx.needs_input_grad[1] and WgradStream.wants(f32, r * s > 1)
+    side = WgradStream.begin(x.device) if use_side and not WgradStream.after else None
     if ctx.needs_input_grad[0]:
         if stride == 1 and wt is not None:
             # backward-data = forward conv of dz with the flipped, transposed weight
@@ -765,7 +778,7 @@ def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None):
             dx = torch.ops.aten.convolution_backward(dz, x, wv, None, [stride, stride], [pad, pad], [1, 1], False,
                                                      [0, 0], 1, [True, False, False])[0]
     if ctx.needs_input_grad[1]:
-        if WgradStream.after:
+        if WgradStream.after and use_side:
             side = WgradStream.begin(x.device)
         dw = torch.empty((co, c, r, s), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
         nws = m.conv_wgrad_ws_floats(dev, nb, h, w, c, co, r, s, stride, pad)
@@ -892,6 +905,9 @@ class ConvAct2d(nn.Conv2d):
             dt = mfma_dtype(x)
             return _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0], self.bias, self.act, None, None,
                                  WeightCastPlan.cached(self, dt), dt)
+        if stem_supported(x, self) and self.kernel_size[0] <= 4:  # VGG's 3-channel first layer
+            return _StemConvFn.apply(x, self.weight, self.stride[0], self.padding[0], None, mfma_dtype(x), self.bias,
+                                     self.act)
         y = super().forward(x)
         return F.relu(y) if self.act else y
 
@@ -1109,20 +1125,20 @@ def _stem_pack_input(x: torch.Tensor, pad: int, hp: int, wp: int, dt=torch.bfloa
 _STEM_WBUF = {}
 
 
-def _stem_pack_weight(weight: torch.Tensor, dt=torch.bfloat16) -> torch.Tensor:
-    """[Co, C<=4, R<=8, S<=8] -> [Co, 8, 8, 4] in ``dt``, zero-extended. With
+def _stem_pack_weight(weight: torch.Tensor, dt=torch.bfloat16, rows: int = 8) -> torch.Tensor:
+    """[Co, C<=4, R<=rows, S<=8] -> [Co, rows, 8, 4] in ``dt``, zero-extended. With
     ``_StemPackBuf.enabled`` the zero-extended buffer is kept per (device, stream, shape):
     it is only read by this step's forward GEMM, queued on the same stream before the next
     step's refill, so only the weight itself is copied in each step."""
     co, c, r, s = weight.shape
     wp = None
     if _StemPackBuf.enabled and weight.is_cuda:
-        key = (weight.device, dt, co, c, r, s, _stream(weight))
+        key = (weight.device, dt, co, c, r, s, rows, _stream(weight))
         wp = _STEM_WBUF.get(key)
         if wp is None:
-            wp = _STEM_WBUF[key] = torch.zeros((co, 8, 8, 4), dtype=dt, device=weight.device)
+            wp = _STEM_WBUF[key] = torch.zeros((co, rows, 8, 4), dtype=dt, device=weight.device)
     if wp is None:
-        wp = torch.zeros((co, 8, 8, 4), dtype=dt, device=weight.device)
+        wp = torch.zeros((co, rows, 8, 4), dtype=dt, device=weight.device)
     with torch.no_grad():  # a cached buffer must not carry an autograd edge to the weight
         wp[:, :r, :s, :c] = weight.permute(0, 2, 3, 1)
     return wp
@@ -1157,22 +1173,28 @@ def stem_weight_planes(weight: torch.Tensor):
 
 
 class _StemConvFn(torch.autograd.Function):
-    """7x7 (<= 8x8), <= 4-channel strided stem convolution as an 8-row implicit GEMM on the
-    MFMA kernels (csrc/kernels/gemm.hip ``conv_stem_*``): each kernel row is one 32-element
-    tap = 8 pixels x 4 channels of a zero-padded NHWC4 copy of the image, so the 3-channel
-    input needs no im2col and no per-channel gather. Forward also emits the BN statistics
-    of its output; backward computes the weight gradient only (the image needs none)."""
+    """<= 8x8, <= 4-channel convolution (the ResNet 7x7/2 stem, VGG's 3x3 first layer) as a
+    row-tap implicit GEMM on the MFMA kernels (csrc/kernels/gemm.hip ``conv_stem_*``): each
+    kernel row is one 32-element tap = 8 pixels x 4 channels of a zero-padded NHWC4 copy of
+    the image, so the 3-channel input needs no im2col and no per-channel gather; a kernel of
+    R rows is an R-tap GEMM (K = 32 R). Forward emits the BN statistics of its output, or
+    runs a bias (+ ReLU) epilogue (VGG); backward computes the weight (and bias) gradient only
+    (the image needs none)."""
 
     @staticmethod
-    def forward(ctx, x, weight, stride: int, pad: int, hold=None, dt=torch.bfloat16):
+    def forward(ctx, x, weight, stride: int, pad: int, hold=None, dt=torch.bfloat16, bias=None, relu=False):
         nb, _, h, w = x.shape
         co, _, r, s = weight.shape
         f32 = dt == torch.float32
+        m = native()
+        rows = 8 if r > 4 else r  # (the ResNet stem keeps its 8-row layout and weight planes)
+        rw = m.stem_wgrad_rows(rows)
         ho, wo = (h + 2 * pad - r) // stride + 1, (w + 2 * pad - s) // stride + 1
-        hp, wp = max(h + 2 * pad, (ho - 1) * stride + 8), max(w + 2 * pad, (wo - 1) * stride + 8)
+        hp, wp = max(h + 2 * pad, (ho - 1) * stride + rw), max(w + 2 * pad, (wo - 1) * stride + 8)
         xp, ent = _StemPackBuf.get(x, pad, hp, wp, dt)
         f16s = f32 and _F32_SPLIT == "f16x3"
-        wb = None if f16s and _STEM_NATIVE_PLANES else _stem_pack_weight(weight, dt)
+        native_planes = _STEM_NATIVE_PLANES and rows == 8
+        wb = None if f16s and native_planes else _stem_pack_weight(weight, dt, rows)
         y = torch.empty((nb, co, ho, wo), dtype=dt, device=x.device, memory_format=torch.channels_last)
         st = None
         fold = None
@@ -1187,17 +1209,23 @@ class _StemConvFn(torch.autograd.Function):
             if ctx.xbound is None:
                 ctx.xbound = bound_of_value(torch.linalg.vector_norm(x, float("inf")))
                 set_amax(x, ctx.xbound)
-            if _STEM_NATIVE_PLANES:
+            if native_planes:
                 wb, wam = stem_weight_planes(weight)
-            else:  # the PyTorch-op planes (A/B)
+            else:  # the PyTorch-op planes (A/B; the 3x3 layout)
                 wam = bound_of_value(torch.linalg.vector_norm(weight.detach(), float("inf")))
                 wb = f16_planes(wb.reshape(co, -1), wam)
             kw = dict(bps=wb[0].numel(), amax_a=ctx.xbound.data_ptr(), amax_b=wam.data_ptr())
-        native().conv_stem_fwd(x.device.index, _stream(x), nb, hp, wp, co, ho, wo, stride, xp.data_ptr(),
-                               wb.data_ptr(), y.data_ptr(), st.data_ptr() if st is not None else 0, f32=f32,
-                               bn_fold=_fold_arg(fold), **kw)
-        ctx.save_for_backward(xp)
-        ctx.geo = (nb, hp, wp, co, ho, wo, stride, tuple(weight.shape))
+        b = None
+        if bias is not None:
+            b = bias if (bias.dtype == torch.float32 and bias.is_contiguous()) else bias.float().contiguous()
+            kw["bias"] = b.data_ptr()
+        if relu:
+            kw["relu"] = True
+        m.conv_stem_fwd(x.device.index, _stream(x), nb, hp, wp, co, ho, wo, stride, xp.data_ptr(), wb.data_ptr(),
+                        y.data_ptr(), st.data_ptr() if st is not None else 0, f32=f32, bn_fold=_fold_arg(fold),
+                        rows=rows, **kw)
+        ctx.save_for_backward(xp, y if relu else None)
+        ctx.geo = (nb, hp, wp, co, ho, wo, stride, tuple(weight.shape), rows, bias is not None, bool(relu))
         ctx.pack = ent
         if ent is not None:
             ent.used(x.device)
@@ -1207,29 +1235,52 @@ class _StemConvFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        (xp,) = ctx.saved_tensors
-        nb, hp, wp, co, ho, wo, stride, wshape = ctx.geo
-        dw = None
+        xp, y = ctx.saved_tensors
+        nb, hp, wp, co, ho, wo, stride, wshape, rows, has_bias, relu = ctx.geo
+        dw = db = None
+        dt = xp.dtype
+        dy = _to(dy, dt)
+        m = native()
+        dev = xp.device.index
+        if relu:  # dz = dy * (y > 0) and the bias gradient in one pass (csrc/kernels/act.hip)
+            dz = torch.empty_like(dy, memory_format=torch.channels_last)
+            want_db = has_bias and ctx.needs_input_grad[6]
+            db = torch.empty(co, dtype=torch.float32, device=dy.device) if want_db else None
+            ws = torch.empty(m.relu_bias_bwd_ws_floats(co), dtype=torch.float32, device=dy.device) if want_db else None
+            m.relu_bias_bwd(dev, _stream(dy), nb * ho * wo, co, dy.data_ptr(), y.data_ptr(), dz.data_ptr(),
+                            db.data_ptr() if db is not None else 0, ws.data_ptr() if ws is not None else 0,
+                            f32=dt == torch.float32)
+            dy = dz
+        elif has_bias and ctx.needs_input_grad[6]:
+            db = dy.float().sum(dim=(0, 2, 3))
         if ctx.needs_input_grad[1]:
-            dt = xp.dtype
-            dy = _to(dy, dt)
-            m = native()
-            dev = xp.device.index
-            dwp = torch.empty((co, 8, 8, 4), dtype=torch.float32, device=xp.device)
-            nws = m.conv_stem_wgrad_ws_floats(dev, nb, ho, wo, co)
+            rw = m.stem_wgrad_rows(rows)
+            dwp = torch.empty((co, rw, 8, 4), dtype=torch.float32, device=xp.device)
+            nws = m.conv_stem_wgrad_ws_floats(dev, nb, ho, wo, co, rows)
             ws = torch.empty(nws, dtype=torch.float32, device=xp.device) if nws else None
             ya = amax_of(dy)
             kw = dict(amax_y=ya.data_ptr(), amax_x=ctx.xbound.data_ptr()) if (
                 ya is not None and ctx.xbound is not None) else {}
             m.conv_stem_wgrad(dev, _stream(xp), nb, hp, wp, co, ho, wo, stride, dy.data_ptr(), xp.data_ptr(),
-                              dwp.data_ptr(), ws.data_ptr() if ws is not None else 0, f32=dt == torch.float32, **kw)
+                              dwp.data_ptr(), ws.data_ptr() if ws is not None else 0, f32=dt == torch.float32,
+                              rows=rows, **kw)
             _, c, r, s = wshape
             dw = dwp[:, :r, :s, :c].permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
         if ctx.pack is not None:
             # the wgrad reading the buffer is queued: the next refill is ordered after it
             ctx.pack.used(xp.device)
             ctx.pack.busy = False
-        return None, dw, None, None, None, None
+        return None, dw, None, None, None, None, db, None
+
+
+def stem_supported(x: torch.Tensor, conv: nn.Conv2d) -> bool:
+    """The row-tap MFMA path: a CUDA bf16 / fp32 image that needs no gradient, <= 4 channels,
+    a square-strided / square-padded <= 8x8 kernel, Co % 64 == 0 (MPIT_MFMA_STEM=0: off)."""
+    co, c, r, s = conv.weight.shape
+    return (x.is_cuda and mfma_dtype(x) is not None and x.dim() == 4 and not x.requires_grad and c <= 4
+            and r <= 8 and s <= 8 and co % 64 == 0 and conv.dilation == (1, 1) and conv.groups == 1
+            and conv.stride[0] == conv.stride[1] and conv.padding[0] == conv.padding[1]
+            and os.environ.get("MPIT_MFMA_STEM", "1") != "0")
 
 
 class StemConv(nn.Conv2d):
@@ -1242,11 +1293,7 @@ class StemConv(nn.Conv2d):
         self.emit_stats = False
 
     def fused(self, x: torch.Tensor) -> bool:
-        co, c, r, s = self.weight.shape
-        return (x.is_cuda and mfma_dtype(x) is not None and x.dim() == 4 and not x.requires_grad and c <= 4
-                and r <= 8 and s <= 8 and co % 64 == 0 and self.dilation == (1, 1) and self.groups == 1
-                and self.stride[0] == self.stride[1] and self.padding[0] == self.padding[1]
-                and os.environ.get("MPIT_MFMA_STEM", "1") != "0")
+        return stem_supported(x, self)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.fused(x):

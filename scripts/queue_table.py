@@ -1,14 +1,16 @@
 """Stream -> hardware-queue table of a rocprofv3 trace (kernel dispatches, and memory copies
 when the trace has them): which HIP streams of a rank share a hardware queue.
 
-    python scripts/queue_table.py <trace dir> <out.md> [title]
+    python scripts/queue_table.py <trace dir> <out.md> [title] [steady_ms]
 
 rocprofv3 records the queue a dispatch went to (``Queue_Id``) next to the HIP stream it was
 launched on (``Stream_Id``). HIP maps streams onto at most GPU_MAX_HW_QUEUES hardware queues
 per process; streams that share a queue execute in one FIFO, so an RCCL kernel spinning at
 the head of a queue blocks every kernel queued behind it from the other streams of that
 queue. The table lists, per (stream, queue) pair, the dispatch count and the most frequent
-kernels, and per queue the streams that feed it.
+kernels, and per queue the streams that feed it. ``steady_ms`` (default 300): a second table
+restricted to the dispatches that start in the last steady_ms of the trace (the timed steps,
+without start-up and the post-run checks), with the host threads that issued them.
 """
 from __future__ import annotations
 
@@ -29,10 +31,12 @@ def _rows(d: str, suffix: str):
 def main(argv) -> int:
     d, out = argv[0], argv[1]
     title = argv[2] if len(argv) > 2 else d
+    steady_ms = float(argv[3]) if len(argv) > 3 else 300.0
     pairs = collections.Counter()
     names = collections.defaultdict(collections.Counter)
     busy = collections.Counter()
-    for r in _rows(d, "kernel_trace.csv"):
+    rows = list(_rows(d, "kernel_trace.csv"))
+    for r in rows:
         key = (r.get("Agent_Id", ""), r["Stream_Id"], r["Queue_Id"])
         pairs[key] += 1
         names[key][r["Kernel_Name"].split("(")[0][:70]] += 1
@@ -53,6 +57,19 @@ def main(argv) -> int:
         lines.append(f"| {a} | {q} | {', '.join(sorted(ss))} |")
     nq = len({q for _, _, q in pairs})
     lines += ["", f"kernel-dispatching streams: {len({(a, s) for a, s, _ in pairs})}; hardware queues used: {nq}"]
+    if rows:
+        tend = max(int(r["End_Timestamp"]) for r in rows)
+        late = [r for r in rows if tend - int(r["Start_Timestamp"]) < steady_ms * 1e6]
+        sp = collections.Counter((r["Stream_Id"], r["Queue_Id"]) for r in late)
+        thr = collections.defaultdict(set)
+        for r in late:
+            thr[(r["Stream_Id"], r["Queue_Id"])].add(r.get("Thread_Id", "?"))
+        lines += ["", f"## Last {steady_ms:.0f} ms of the trace (steady steps)", "",
+                  "| stream | queue | dispatches | host threads |", "|---|---|---|---|"]
+        for (s_, q), c in sorted(sp.items(), key=lambda kv: -kv[1]):
+            lines.append(f"| {s_} | {q} | {c} | {', '.join(sorted(thr[(s_, q)]))} |")
+        lines += ["", f"streams dispatching in the window: {len({s_ for s_, _ in sp})}; "
+                  f"hardware queues: {len({q for _, q in sp})}"]
     if copies:
         lines += ["", "| copy stream | direction | copies |", "|---|---|---|"]
         for (s, k), c in sorted(copies.items()):

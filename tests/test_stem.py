@@ -26,6 +26,38 @@ def test_stem_fwd_wgrad(nb, h, co, k, stride, pad):
     assert err < 1e-2, float(err)
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("nb,h,co", [(2, 224, 64), (3, 30, 128)])
+def test_first_layer_3x3_bias_relu(dt, nb, h, co):
+    """VGG's 3-channel 3x3 first layer (ConvAct2d) on the 3-row row-tap kernel with the bias
+    and ReLU in the epilogue: y, and the weight and bias gradients, against fp32 PyTorch."""
+    from mpit_amd._ext import native
+    from mpit_amd.ops.conv import ConvAct2d
+
+    assert native().stem_wgrad_rows(3) == 4
+    torch.manual_seed(0)
+    conv = ConvAct2d(3, co, 3, padding=1).cuda().to(memory_format=torch.channels_last)
+    with torch.no_grad():
+        conv.bias.uniform_(-0.5, 0.5)
+    x = torch.randn(nb, 3, h, h, device="cuda").to(dt).contiguous(memory_format=torch.channels_last)
+    assert not conv.fused(x)  # (3 channels: not the implicit-GEMM path) -> the row-tap path
+    y = conv(x)
+    assert y.grad_fn is not None and "Stem" in type(y.grad_fn).__name__
+    wq = conv.weight.detach().to(dt).float()
+    ref = F.relu(F.conv2d(x.float(), wq, conv.bias.detach(), padding=1))
+    assert y.shape == ref.shape and y.dtype == dt
+    tol = 2e-2 if dt == torch.bfloat16 else 1e-4
+    assert (y.float() - ref).abs().max() <= tol * ref.abs().max()
+    g = torch.randn_like(ref).to(dt)
+    y.backward(g.contiguous(memory_format=torch.channels_last))
+    gz = g.float() * (y.float() > 0)
+    wref = torch.nn.grad.conv2d_weight(x.float(), conv.weight.shape, gz, padding=1)
+    err = (conv.weight.grad - wref).abs().max() / wref.abs().max()
+    assert err < tol, float(err)
+    bref = gz.sum(dim=(0, 2, 3))
+    assert (conv.bias.grad - bref).abs().max() <= tol * bref.abs().max() + 1e-3
+
+
 def test_stem_emits_bn_stats():
     from mpit_amd.ops.conv import StemConv, tile_stats_to_sums
 

@@ -214,9 +214,21 @@ PYBIND11_MODULE(_mpit, m) {
   m.def(
       "maxpool_bwd",
       [](int dev, uintptr_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t dy, uintptr_t idx,
-         uintptr_t dx, bool f32) { maxpool_bwd(dev, S(s), N, H, W, C, K, stride, pad, dy, idx, dx, f32); },
+         uintptr_t dx, bool f32, uintptr_t ypool, uintptr_t db, uintptr_t ws) {
+        maxpool_bwd(dev, S(s), N, H, W, C, K, stride, pad, dy, idx, dx, f32, ypool, db, ws);
+      },
       py::arg("dev"), py::arg("stream"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("K"),
-      py::arg("stride"), py::arg("pad"), py::arg("dy"), py::arg("idx"), py::arg("dx"), py::arg("f32") = false);
+      py::arg("stride"), py::arg("pad"), py::arg("dy"), py::arg("idx"), py::arg("dx"), py::arg("f32") = false,
+      py::arg("ypool") = 0, py::arg("db") = 0, py::arg("ws") = 0);
+  m.def("maxpool_bwd_ws_floats", &maxpool_bwd_ws_floats);
+  m.def("col_sums_ws_floats", &col_sums_ws_floats);
+  m.def(
+      "col_sums",
+      [](int dev, uintptr_t s, uintptr_t part, int64_t nb, int64_t ld, int C, uintptr_t out, uintptr_t mid) {
+        col_sums(dev, S(s), part, nb, ld, C, out, mid);
+      },
+      py::arg("dev"), py::arg("stream"), py::arg("part"), py::arg("nb"), py::arg("ld"), py::arg("C"), py::arg("out"),
+      py::arg("mid") = 0);
   m.def("conv_supported", &conv_supported);
   m.def(
       "conv_fwd",
@@ -225,11 +237,12 @@ PYBIND11_MODULE(_mpit, m) {
          uintptr_t red_x, uintptr_t red_mask, uintptr_t red_mean, int64_t red_row0, uintptr_t red_part2,
          uintptr_t red_x2, uintptr_t red_mean2, bool f32, uintptr_t fold_coef, uintptr_t fold_gamma,
          uintptr_t fold_rstd, uintptr_t fold_dgamma, uintptr_t fold_dbeta, uintptr_t fold_lvl, int64_t bps,
-         uintptr_t amax_a, uintptr_t amax_b, uintptr_t fold_zero, py::object bn_fold) {
+         uintptr_t amax_a, uintptr_t amax_b, uintptr_t fold_zero, py::object bn_fold, bool red_relu) {
         BnRed r{red_part, red_x, red_mask, red_mean, red_row0, red_part2, red_x2, red_mean2};
         r.fcoef = fold_coef; r.fgamma = fold_gamma; r.frstd = fold_rstd;
         r.fdgamma = fold_dgamma; r.fdbeta = fold_dbeta; r.flvl = fold_lvl; r.fzero = fold_zero;
         r.amax_a = amax_a; r.amax_b = amax_b;
+        r.relu_y = red_relu ? 1 : 0;
         apply_sfold(r, bn_fold);
         conv_fwd(dev, S(s), Nb, H, W, C, Co, R, S_, stride, pad, x, w, y, stats, cin, bias, relu, &r, f32, bps);
       },
@@ -240,7 +253,7 @@ PYBIND11_MODULE(_mpit, m) {
       py::arg("red_part2") = 0, py::arg("red_x2") = 0, py::arg("red_mean2") = 0, py::arg("f32") = false,
       py::arg("fold_coef") = 0, py::arg("fold_gamma") = 0, py::arg("fold_rstd") = 0, py::arg("fold_dgamma") = 0,
       py::arg("fold_dbeta") = 0, py::arg("fold_lvl") = 0, py::arg("bps") = 0, py::arg("amax_a") = 0,
-      py::arg("amax_b") = 0, py::arg("fold_zero") = 0, py::arg("bn_fold") = py::none());
+      py::arg("amax_b") = 0, py::arg("fold_zero") = 0, py::arg("bn_fold") = py::none(), py::arg("red_relu") = false);
   m.def("conv_dgrad_strided_wfloats", &conv_dgrad_strided_wfloats);
   m.def(
       "conv_dgrad_strided_weights",

@@ -94,7 +94,7 @@ __global__ __launch_bounds__(1024) void relu_bias_bwd_kernel(const T* __restrict
 // (level 1 writes [groups][C]), the second launch combines the groups.
 constexpr int kSumCh = 64, kSumLanes = 16, kSumGroups = 16;
 __global__ __launch_bounds__(kSumCh * kSumLanes) void sum_parts_kernel(const float* __restrict__ part, int nb, int C,
-                                                                       float* __restrict__ out) {
+                                                                       float* __restrict__ out, int64_t ld) {
   __shared__ float sm[kSumLanes][kSumCh];
   const int cl = threadIdx.x % kSumCh, kl = threadIdx.x / kSumCh;
   const int c = blockIdx.x * kSumCh + cl;
@@ -102,7 +102,7 @@ __global__ __launch_bounds__(kSumCh * kSumLanes) void sum_parts_kernel(const flo
   float s = 0.f;
   if (c < C) {
 #pragma unroll 8
-    for (int k = r0 + kl; k < r1; k += kSumLanes) s += part[int64_t(k) * C + c];
+    for (int k = r0 + kl; k < r1; k += kSumLanes) s += part[int64_t(k) * ld + c];
   }
   sm[kl][cl] = s;
   __syncthreads();
@@ -138,20 +138,29 @@ void relu_bias_bwd(int dev, hipStream_t s, int64_t M, int C, uintptr_t dy, uintp
                        reinterpret_cast<const uint16_t*>(dy), reinterpret_cast<const uint16_t*>(y),
                        reinterpret_cast<uint16_t*>(dz), M, C, rpb, part);
   hip_check(hipGetLastError(), "relu_bias_bwd launch");
-  if (db) {
-    const dim3 cb((C + kSumCh - 1) / kSumCh);
-    if (nb > 4 * kSumLanes) {  // level 1 into the workspace tail, then the group combine
-      float* mid = part + int64_t(kMaxBlocks) * C;
-      hipLaunchKernelGGL(sum_parts_kernel, dim3(cb.x, kSumGroups), dim3(kSumCh * kSumLanes), 0, s, part, int(nb), C,
-                         mid);
-      hipLaunchKernelGGL(sum_parts_kernel, cb, dim3(kSumCh * kSumLanes), 0, s, mid, kSumGroups, C,
-                         reinterpret_cast<float*>(db));
-    } else {
-      hipLaunchKernelGGL(sum_parts_kernel, cb, dim3(kSumCh * kSumLanes), 0, s, part, int(nb), C,
-                         reinterpret_cast<float*>(db));
-    }
-    hip_check(hipGetLastError(), "relu_bias_bwd sum launch");
+  if (db) col_sums(s, part, nb, C, C, reinterpret_cast<float*>(db), part + int64_t(kMaxBlocks) * C);
+}
+
+int64_t col_sums_ws_floats(int C) { return int64_t(kSumGroups) * C; }
+
+void col_sums(hipStream_t s, const float* part, int64_t nb, int64_t ld, int C, float* out, float* mid) {
+  if (nb <= 0 || C <= 0 || ld < C) throw std::invalid_argument("col_sums: bad shape");
+  const dim3 cb((C + kSumCh - 1) / kSumCh);
+  if (nb > 4 * kSumLanes) {  // level 1 into mid [kSumGroups][C], then the group combine
+    if (!mid) throw std::invalid_argument("col_sums: many rows need the workspace");
+    hipLaunchKernelGGL(sum_parts_kernel, dim3(cb.x, kSumGroups), dim3(kSumCh * kSumLanes), 0, s, part, int(nb), C, mid,
+                       ld);
+    hipLaunchKernelGGL(sum_parts_kernel, cb, dim3(kSumCh * kSumLanes), 0, s, mid, kSumGroups, C, out, int64_t(C));
+  } else {
+    hipLaunchKernelGGL(sum_parts_kernel, cb, dim3(kSumCh * kSumLanes), 0, s, part, int(nb), C, out, ld);
   }
+  hip_check(hipGetLastError(), "col_sums launch");
+}
+
+void col_sums(int dev, hipStream_t s, uintptr_t part, int64_t nb, int64_t ld, int C, uintptr_t out, uintptr_t mid) {
+  hip_check(hipSetDevice(dev), "hipSetDevice");
+  col_sums(s, reinterpret_cast<const float*>(part), nb, ld, C, reinterpret_cast<float*>(out),
+           reinterpret_cast<float*>(mid));
 }
 
 }  // namespace mpit

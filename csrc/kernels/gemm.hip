@@ -242,7 +242,7 @@ struct ConvGeo {
   int pitch;
 };
 
-enum { EPI_NONE = 0, EPI_STATS = 1, EPI_BNRED = 2, EPI_BNRED2 = 3 };
+enum { EPI_NONE = 0, EPI_STATS = 1, EPI_BNRED = 2, EPI_BNRED2 = 3, EPI_RELUB = 4 };
 
 // column-reduction epilogue operands (see gemm_nt_kernel)
 struct EpiArgs {
@@ -1100,7 +1100,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
   int nv = 0;
 #pragma unroll
   for (int e = 0; e < 8; ++e) s1[e] = s2[e] = sf[e] = mu[e] = 0.f;
-  constexpr bool BNRED = EPI == EPI_BNRED || EPI == EPI_BNRED2, DUAL = EPI == EPI_BNRED2;
+  constexpr bool BNRED = EPI == EPI_BNRED || EPI == EPI_BNRED2, DUAL = EPI == EPI_BNRED2, RELUB = EPI == EPI_RELUB;
   float s3[8], mu2[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) s3[e] = mu2[e] = 0.f;
@@ -1152,6 +1152,10 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
       else xq[q].zero();
       xmb[q] = ok ? (ep.mask ? mbits(ep.mask, o) : 0xffu) : 0u;
     }
+    if constexpr (RELUB) {
+      if (ok) xq[q].load(epx + o, HOFF);
+      else xq[q].zero();
+    }
     if constexpr (DUAL) {
       if (ok) xq2[q].load(epx2 + o, HOFF);
       else xq2[q].zero();
@@ -1180,6 +1184,13 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
       const uint32_t mb = cmb[q];
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = rnd<T>(v[e] + ((mb >> e) & 1u ? cv[q].get(e) : 0.f));
+    }
+    if constexpr (RELUB) {  // dz = dy * (y > 0) of the layer below, as stored
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        v[e] = xq[q].get(e) > 0.f ? rnd<T>(v[e]) : 0.f;
+        s1[e] += v[e];
+      }
     }
     store8(C + o, v, HOFF);
     if constexpr (CONV) {
@@ -1267,7 +1278,9 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
           b += red[(k * 3 + 1) * BN + n];
           if constexpr (DUAL) c3 += red[(k * 3 + 2) * BN + n];
         }
-        if (EPI == EPI_BNRED && ep.fcoef != nullptr) {  // read by the folding block (any XCD)
+        if constexpr (RELUB) {
+          prow[n] = a;  // (the second row is unused)
+        } else if (EPI == EPI_BNRED && ep.fcoef != nullptr) {  // read by the folding block (any XCD)
           st_wt(prow + n, a);
           st_wt(prow + N + n, b);
         } else {
@@ -2380,6 +2393,11 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
       throw std::invalid_argument("gemm_nt: the BN finalize fold needs a single-launch EPI_BNRED with rstd and lvl");
     if (ep.scoef && (epi != EPI_STATS || ep.row0 != 0 || !ep.smean || !ep.srstd || !ep.flvl))
       throw std::invalid_argument("gemm_nt: the BN forward fold needs a single-launch EPI_STATS with mean, rstd and lvl");
+    if (epi == EPI_RELUB) {
+      if (!geo || geo->ostr != 1) throw std::invalid_argument("gemm_nt: the fused ReLU epilogue is for stride-1 convolutions");
+      if (!ep.x || ldc != N) throw std::invalid_argument("gemm_nt: the fused ReLU epilogue needs x and ldc == N");
+      check_ptr(reinterpret_cast<uintptr_t>(ep.x), "ReLU y");
+    }
     if (epi == EPI_BNRED || epi == EPI_BNRED2) {
       if (!ep.x || !ep.mean || ldc != N) throw std::invalid_argument("gemm_nt: BN reduction needs x, mean, ldc == N");
       check_ptr(reinterpret_cast<uintptr_t>(ep.x), "BN x");
@@ -2543,6 +2561,7 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
     if (epi == EPI_STATS) MPIT_NT_LAUNCH1(BM, BN, ST, EPI_STATS, CONV);                        \
     else if (epi == EPI_BNRED) MPIT_NT_LAUNCH1(BM, BN, ST, EPI_BNRED, CONV);                   \
     else if (epi == EPI_BNRED2 && !CONV) MPIT_NT_LAUNCH1(BM, BN, ST, EPI_BNRED2, false);       \
+    else if (epi == EPI_RELUB && CONV) MPIT_NT_LAUNCH1(BM, BN, ST, EPI_RELUB, true);           \
     else MPIT_NT_LAUNCH1(BM, BN, ST, EPI_NONE, CONV);                                          \
   } while (0)
 #define MPIT_NT_LAUNCH(BM, BN, ST)                                                                             \
@@ -2643,6 +2662,12 @@ static EpiArgs epi_args(uintptr_t stats, const BnRed* r, int* mode) {
       ep.seps = r->seps;
       ep.smom = r->smom;
     }
+  } else if (r && r->part && r->relu_y) {
+    if (r->mask || r->mean || r->part2 || r->fcoef) throw std::invalid_argument("gemm_nt: relu_y excludes a BN reduction");
+    ep.part = reinterpret_cast<float*>(r->part);
+    ep.x = reinterpret_cast<const void*>(r->x);
+    ep.row0 = r->row0;
+    *mode = EPI_RELUB;
   } else if (r && r->part) {
     ep.part = reinterpret_cast<float*>(r->part);
     ep.x = reinterpret_cast<const void*>(r->x);
@@ -2697,7 +2722,9 @@ static bool tn_cap1() {
 
 static int tn_plan(int dev, int64_t M, int N, int K, int64_t* rows_per_split, int* tbn, int* tbk, int cin = 0) {
   *tbn = N % 128 == 0 ? 128 : 64;
-  *tbk = (cin ? cin : K) % 128 == 0 ? 128 : 64;  // conv: a column tile never straddles two taps
+  // conv: a column tile never straddles two taps — except the row-tap stem (cin = kStemTap),
+  // whose lanes locate their tap per 16-B chunk: there 128-wide tiles read dY half as often
+  *tbk = (cin && cin != kStemTap ? cin : K) % 128 == 0 ? 128 : 64;
   const int64_t ntiles = int64_t(N / *tbn) * (K / *tbk);
   const int per_cu = tn_cap1() ? 1 : 2 * (128 / *tbn) * (128 / *tbk);
   // MPIT_TN_SPLIT_MUL=k: k times the splits (shorter blocks that free their CU sooner for

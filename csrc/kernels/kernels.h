@@ -154,6 +154,10 @@ struct BnRed {
   // zero: the BN output's bound, set to zero (the BN apply pass raises it)
   uintptr_t scoef = 0, sgamma = 0, sbeta = 0, srmean = 0, srvar = 0, smean = 0, srstd = 0, slvl = 0, szero = 0;
   float seps = 1e-5f, smom = 0.1f;
+  // relu_y: instead of a BN reduction, the epilogue applies the ReLU of the conv(+bias)(+ReLU)
+  // layer whose output x is this GEMM's input-gradient target: C = A.B^T * (x > 0) is that
+  // layer's dz, and part[tile][0][N] its per-tile column sums (its bias gradient, col_sums)
+  int relu_y = 0;
 };
 int64_t gemm_nt_fold_lvl_floats(int N);
 bool gemm_nt_supported(int64_t M, int N, int K, bool f32 = false);
@@ -208,6 +212,11 @@ void conv_dgrad_strided(int dev, hipStream_t s, int Nb, int H, int W, int C, int
                         uintptr_t dy, uintptr_t wcls, uintptr_t dx, const BnRed* red = nullptr, bool f32 = false,
                         int64_t bps = 0);
 int64_t relu_bias_bwd_ws_floats(int C);
+// out[c] = sum over rows k < nb of part[k * ld + c] (fp32, fixed order: deterministic); mid:
+// col_sums_ws_floats(C) floats of workspace (needed when nb > 64)
+int64_t col_sums_ws_floats(int C);
+void col_sums(hipStream_t s, const float* part, int64_t nb, int64_t ld, int C, float* out, float* mid);
+void col_sums(int dev, hipStream_t s, uintptr_t part, int64_t nb, int64_t ld, int C, uintptr_t out, uintptr_t mid);
 void relu_bias_bwd(int dev, hipStream_t s, int64_t M, int C, uintptr_t dy, uintptr_t y, uintptr_t dz, uintptr_t db,
                    uintptr_t ws, bool f32 = false);
 // dw [Co,R,S,C] (fp32) = beta*dw + dY^T . im2col(x)   (C % 64 == 0, Co % 64 == 0)
@@ -238,7 +247,12 @@ int stem_wgrad_rows(int rows);
 // x [N,H,W,C] -> y, idx [N,Ho,Wo,C]; dx [N,H,W,C] gathered from dy + idx (no atomics).
 void maxpool_fwd(int dev, hipStream_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t x,
                  uintptr_t y, uintptr_t idx, bool f32 = false);
+// ypool (optional): the pool's output, when its input is a ReLU'd conv(+bias) output: dx is
+// then that conv's dz = dx * (y > 0), and db (optional, fp32 [C]) its bias gradient; ws:
+// maxpool_bwd_ws_floats(C) floats. Needs 256 % (C / 8) == 0.
 void maxpool_bwd(int dev, hipStream_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t dy,
-                 uintptr_t idx, uintptr_t dx, bool f32 = false);
+                 uintptr_t idx, uintptr_t dx, bool f32 = false, uintptr_t ypool = 0, uintptr_t db = 0,
+                 uintptr_t ws = 0);
+int64_t maxpool_bwd_ws_floats(int C);
 
 }  // namespace mpit

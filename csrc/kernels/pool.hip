@@ -95,12 +95,20 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const T* __restrict__ 
   }
 }
 
-template <typename T, typename I>
+// RB (a ReLU'd conv(+bias) below the pool, VGG / AlexNet): the gradient that reaches the
+// pool's input is dz = dx * (y > 0) with y the pool's input; at a window's argmax y equals the
+// pooled value, so the mask is ypool > 0, read per window. Each thread also accumulates the
+// channel sums of what it writes (the conv's bias gradient): the grid-stride step is a
+// multiple of C / 8 (host-checked), so a thread's 8 channels never change; per block the
+// sums go through LDS into part[block][C].
+template <typename T, typename I, bool RB>
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ dy,
                                                           const uint8_t* __restrict__ idx, T* __restrict__ dx,
-                                                          PoolGeo g) {
+                                                          PoolGeo g, const T* __restrict__ ypool,
+                                                          float* __restrict__ part) {
   const I cv = I(g.C / 8);
   const I total = I(g.N) * I(g.H) * I(g.W) * cv;
+  float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (I t = I(blockIdx.x) * blockDim.x + threadIdx.x; t < total; t += I(gridDim.x) * blockDim.x) {
     const int c8 = int(t % cv);
     const I pix = t / cv;
@@ -122,15 +130,50 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ 
         const uint2 a = *reinterpret_cast<const uint2*>(idx + o);
         float gv[8];
         ld8(dy + o, gv);
+        float yv[8];
+        if constexpr (RB) ld8(ypool + o, yv);
         const uint8_t k = uint8_t(i * g.K + j);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const uint8_t ae = uint8_t(((e < 4 ? a.x : a.y) >> (8 * (e & 3))) & 0xff);
-          if (ae == k) acc[e] += gv[e];
+          bool take = ae == k;
+          if constexpr (RB) take = take && yv[e] > 0.f;
+          if (take) acc[e] += gv[e];
         }
       }
     }
-    st8(dx + int64_t(pix) * g.C + c8 * 8, acc);
+    if constexpr (RB) {
+      float q[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) q[e] = acc[e];
+      st8(dx + int64_t(pix) * g.C + c8 * 8, q);
+      if constexpr (sizeof(T) == 2) {  // the bias gradient of the values as stored
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bsum[e] += bf2f(f2bf(acc[e]));
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bsum[e] += acc[e];
+      }
+    } else {
+      st8(dx + int64_t(pix) * g.C + c8 * 8, acc);
+    }
+  }
+  if constexpr (RB) {
+    __shared__ float red[256 * 8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[threadIdx.x * 8 + e] = bsum[e];
+    // LDS hand-off only: a __syncthreads() fence would first wait for every dx store above
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int cvi = g.C / 8;
+    for (int c = threadIdx.x; c < g.C; c += blockDim.x) {
+      const int c8 = c / 8, e = c % 8;
+      float sum = 0.f;
+      // the threads whose channel group is c8: tid % cv == c8 (cv divides 256)
+      for (int tid = c8; tid < 256; tid += cvi) sum += red[tid * 8 + e];
+      part[int64_t(blockIdx.x) * g.C + c] = sum;
+    }
   }
 }
 
@@ -161,19 +204,35 @@ void maxpool_fwd_t(int dev, hipStream_t s, int N, int H, int W, int C, int K, in
   hip_check(hipGetLastError(), "maxpool_fwd launch");
 }
 
+constexpr int kPoolRbBlocks = 1024;  // partial rows of the fused bias gradient
+
 template <typename T>
 void maxpool_bwd_t(int dev, hipStream_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t dy,
-                   uintptr_t idx, uintptr_t dx) {
+                   uintptr_t idx, uintptr_t dx, uintptr_t ypool, uintptr_t db, uintptr_t ws) {
   const PoolGeo g = pool_geo(N, H, W, C, K, stride, pad);
-  if ((dy | dx) % 16 || idx % 8) throw std::invalid_argument("maxpool_bwd: misaligned buffers");
+  if ((dy | dx | ypool) % 16 || idx % 8) throw std::invalid_argument("maxpool_bwd: misaligned buffers");
+  if (db && (!ypool || !ws)) throw std::invalid_argument("maxpool_bwd: the bias gradient needs ypool and ws");
+  if (ypool && 256 % (C / 8)) throw std::invalid_argument("maxpool_bwd: the fused ReLU needs 256 % (C / 8) == 0");
   hip_check(hipSetDevice(dev), "hipSetDevice");
   const int64_t work = int64_t(N) * H * W * (C / 8);
-  const bool narrow = work + int64_t(grid_for(work)) * 256 < (int64_t(1) << 32);
-  auto* k = narrow ? maxpool_bwd_kernel<T, uint32_t> : maxpool_bwd_kernel<T, int64_t>;
-  hipLaunchKernelGGL(k, dim3(grid_for(work)), dim3(256), 0, s, reinterpret_cast<const T*>(dy),
-                     reinterpret_cast<const uint8_t*>(idx), reinterpret_cast<T*>(dx), g);
+  const unsigned grid = ypool ? unsigned(std::min<int64_t>((work + 255) / 256, kPoolRbBlocks)) : grid_for(work);
+  const bool narrow = work + int64_t(grid) * 256 < (int64_t(1) << 32);
+  const auto* y = reinterpret_cast<const T*>(ypool);
+  float* part = reinterpret_cast<float*>(ws);
+  if (ypool) {
+    auto* k = narrow ? maxpool_bwd_kernel<T, uint32_t, true> : maxpool_bwd_kernel<T, int64_t, true>;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, s, reinterpret_cast<const T*>(dy),
+                       reinterpret_cast<const uint8_t*>(idx), reinterpret_cast<T*>(dx), g, y, part);
+  } else {
+    auto* k = narrow ? maxpool_bwd_kernel<T, uint32_t, false> : maxpool_bwd_kernel<T, int64_t, false>;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, s, reinterpret_cast<const T*>(dy),
+                       reinterpret_cast<const uint8_t*>(idx), reinterpret_cast<T*>(dx), g, y, part);
+  }
   hip_check(hipGetLastError(), "maxpool_bwd launch");
+  if (db) col_sums(s, part, grid, C, C, reinterpret_cast<float*>(db), part + int64_t(kPoolRbBlocks) * C);
 }
+
+int64_t maxpool_bwd_ws_floats(int C) { return int64_t(kPoolRbBlocks) * C + col_sums_ws_floats(C); }
 
 void maxpool_fwd(int dev, hipStream_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t x,
                  uintptr_t y, uintptr_t idx, bool f32) {
@@ -182,9 +241,9 @@ void maxpool_fwd(int dev, hipStream_t s, int N, int H, int W, int C, int K, int 
 }
 
 void maxpool_bwd(int dev, hipStream_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t dy,
-                 uintptr_t idx, uintptr_t dx, bool f32) {
-  if (f32) maxpool_bwd_t<float>(dev, s, N, H, W, C, K, stride, pad, dy, idx, dx);
-  else maxpool_bwd_t<uint16_t>(dev, s, N, H, W, C, K, stride, pad, dy, idx, dx);
+                 uintptr_t idx, uintptr_t dx, bool f32, uintptr_t ypool, uintptr_t db, uintptr_t ws) {
+  if (f32) maxpool_bwd_t<float>(dev, s, N, H, W, C, K, stride, pad, dy, idx, dx, ypool, db, ws);
+  else maxpool_bwd_t<uint16_t>(dev, s, N, H, W, C, K, stride, pad, dy, idx, dx, ypool, db, ws);
 }
 
 }  // namespace mpit

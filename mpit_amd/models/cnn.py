@@ -13,6 +13,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.conv import ConvAct2d
+from ..ops.linear import LinearAct
 from ..ops.pool import MaxPool2dNHWC
 from . import register
 
@@ -65,9 +66,11 @@ class AlexNet(nn.Module):
             ConvAct2d(256, 256, 3, padding=1), MaxPool2dNHWC(3, 2),
         )
         self.avgpool = nn.AdaptiveAvgPool2d((6, 6))
+        # Linear + ReLU pairs as LinearAct (ops/linear.py; the Identity keeps the reference's
+        # layer indices, so state_dict keys are those of the nn.Linear / nn.ReLU layout)
         self.classifier = nn.Sequential(
-            nn.Dropout(dropout), nn.Linear(256 * 36, 4096), nn.ReLU(inplace=True),
-            nn.Dropout(dropout), nn.Linear(4096, 4096), nn.ReLU(inplace=True), nn.Linear(4096, num_classes),
+            nn.Dropout(dropout), LinearAct(256 * 36, 4096), nn.Identity(),
+            nn.Dropout(dropout), LinearAct(4096, 4096), nn.Identity(), nn.Linear(4096, num_classes),
         )
 
     def forward(self, x):
@@ -79,7 +82,9 @@ _VGG16 = [64, 64, "M", 128, 128, "M", 256, 256, 256, "M", 512, 512, 512, "M", 51
 
 class VGG(nn.Module):
     """Without batch norm every conv(+bias)+ReLU is one :class:`ConvAct2d` (bias and ReLU in
-    the MFMA GEMM epilogue on MI355X) and the pools are NHWC max-pool kernels."""
+    the MFMA GEMM epilogue on MI355X; the 3-channel first layer on the row-tap kernel), the
+    pools are NHWC max-pool kernels, and the classifier's Linear + ReLU pairs are
+    :class:`LinearAct` (bf16 steps)."""
 
     def __init__(self, cfg=_VGG16, num_classes: int = 1000, dropout: float = 0.5, batch_norm: bool = False):
         super().__init__()
@@ -96,8 +101,8 @@ class VGG(nn.Module):
         self.features = nn.Sequential(*layers)
         self.avgpool = nn.AdaptiveAvgPool2d((7, 7))
         self.classifier = nn.Sequential(
-            nn.Linear(512 * 49, 4096), nn.ReLU(inplace=True), nn.Dropout(dropout),
-            nn.Linear(4096, 4096), nn.ReLU(inplace=True), nn.Dropout(dropout), nn.Linear(4096, num_classes),
+            LinearAct(512 * 49, 4096), nn.Identity(), nn.Dropout(dropout),
+            LinearAct(4096, 4096), nn.Identity(), nn.Dropout(dropout), nn.Linear(4096, num_classes),
         )
 
     def forward(self, x):

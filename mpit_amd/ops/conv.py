@@ -564,6 +564,69 @@ def park_grad(x: torch.Tensor, slot: GradSlot) -> torch.Tensor:
     return v
 
 
+class ReluLink:
+    """Hands the ReLU (+ bias) backward of a conv(+bias)+ReLU layer (VGG, AlexNet) to the
+    kernel that produces its output gradient, so the separate pass over (dy, y) of
+    ``relu_bias_bwd`` disappears:
+
+    * a stride-1 convolution consuming the output computes its input gradient with the
+      ``red_relu`` GEMM epilogue (csrc/kernels/gemm.hip ``EPI_RELUB``): C = dY.W * (y > 0) is
+      the layer's dz, and the per-tile column sums its bias gradient (``col_sums``);
+    * a max pool consuming it masks with its pooled output (csrc/kernels/pool.hip: at a
+      window's argmax y is the pooled value) and sums the bias gradient as it writes.
+
+    The producer attaches the link to its output (``y._mpit_relu``); a consumer that finds it
+    on its input ``give``s (dz, db); the layer's backward ``take``s them when the gradient it
+    receives IS that dz (same storage) and otherwise runs the ReLU backward itself — a
+    gradient autograd summed from several consumers is a new tensor and takes that path, which
+    stays exact (dz is already masked, and masking is idempotent). MPIT_RELU_FUSE=0 disables."""
+
+    enabled = os.environ.get("MPIT_RELU_FUSE", "1") != "0"
+    hits = 0  # backwards that took a handed dz (tests)
+    __slots__ = ("dz", "db", "has_bias", "__weakref__")
+
+    def __init__(self, has_bias: bool):
+        self.dz = self.db = None
+        self.has_bias = bool(has_bias)
+
+    @staticmethod
+    def of(x: torch.Tensor):
+        link = getattr(x, "_mpit_relu", None) if ReluLink.enabled else None
+        return link
+
+    def give(self, dz: torch.Tensor, db):
+        self.dz, self.db = dz, db
+
+    def take(self, dy: torch.Tensor):
+        """(True, db) when ``dy`` is the handed dz, else (False, None)."""
+        dz, db = self.dz, self.db
+        self.dz = self.db = None
+        if dz is not None and dy.data_ptr() == dz.data_ptr() and dy.shape == dz.shape and dy.dtype == dz.dtype:
+            ReluLink.hits += 1
+            return True, db
+        return False, None
+
+
+def relu_dgrad_args(y: torch.Tensor, c: int, M: int, keep: list) -> dict:
+    """conv_fwd kwargs of the ``red_relu`` epilogue: the masking layer's output ``y`` (NHWC,
+    laid out like the input gradient) and per-tile column partials of dz."""
+    nt = native().gemm_nt_tiles(M)
+    part = torch.empty(nt * 2 * c, dtype=torch.float32, device=y.device)
+    keep.append((part, nt))
+    return dict(red_part=part.data_ptr(), red_x=y.data_ptr(), red_relu=True)
+
+
+def relu_bias_from_parts(up: "ReluLink", dz: torch.Tensor, keep: list, c: int, stream: int):
+    part, nt = keep[-1]
+    db = None
+    if up.has_bias:
+        m = native()
+        db = torch.empty(c, dtype=torch.float32, device=dz.device)
+        mid = torch.empty(m.col_sums_ws_floats(c), dtype=torch.float32, device=dz.device)
+        m.col_sums(dz.device.index, stream, part.data_ptr(), nt, 2 * c, c, db.data_ptr(), mid.data_ptr())
+    up.give(dz, db)
+
+
 class _Conv1x1Fn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, slot=None, hold=None, link=None, wcast=None, dt=torch.bfloat16):
@@ -734,9 +797,10 @@ def _used_on(side, *ts, out=None):
             t.record_stream(side)
 
 
-def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None):
+def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None, up=None):
     """(dx, dw) of an NHWC implicit-GEMM conv from the gradient ``dz`` of its output; with a
-    BNLink the backward-data GEMM also produces the producing BN's backward reduction."""
+    BNLink the backward-data GEMM also produces the producing BN's backward reduction, with a
+    ReluLink (``up``) the producing conv's ReLU / bias backward."""
     nb, c, h, w = x.shape
     f32 = x.dtype == torch.float32
     co, r, s, _ = wb.shape[-4:]  # (pre-split planes carry a leading dim of 3)
@@ -751,14 +815,19 @@ def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None):
             # backward-data = forward conv of dz with the flipped, transposed weight
             dx = torch.empty_like(x, memory_format=torch.channels_last)
             kw, part, nt = {}, None, 0
+            rkeep = []
             if link is not None:
                 nt = m.gemm_nt_tiles(nb * h * w)
                 kw, part, _, fb = _red_args(link, c, nt, x.device, fold=True)
+            elif up is not None and x.is_contiguous(memory_format=torch.channels_last):
+                kw = relu_dgrad_args(x, c, nb * h * w, rkeep)
             keep = []
             m.conv_fwd(dev, st, nb, ho, wo, co, c, r, s, 1, r - 1 - pad, dz.data_ptr(), wt.data_ptr(),
                        dx.data_ptr(), f32=f32, **_split_kw(dz, wt, f32, keep), **kw)
             if part is not None:
                 link.publish(part, nt, dx, None, fb)
+            elif rkeep:
+                relu_bias_from_parts(up, dx, rkeep, c, st)
         elif wt is not None:
             # strided: stride^2 parity classes, each a stride-1 implicit GEMM over dz whose
             # epilogue writes its pixels of dx (wt = the packed class weights)
@@ -819,7 +888,8 @@ class _ConvFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, stride: int, pad: int, bias=None, relu: bool = False, hold=None, link=None,
-                wcast=None, dt=torch.bfloat16):
+                wcast=None, dt=torch.bfloat16, rlink=None):
+        up = ReluLink.of(x)  # x is a ReLU'd conv output: its ReLU / bias backward rides on our dgrad
         x = _to(x, dt)
         f32 = dt == torch.float32
         nb, c, h, w = x.shape
@@ -850,6 +920,8 @@ class _ConvFn(torch.autograd.Function):
         ctx.xamax = amax_of(x) if f32 else None
         ctx.geo = (stride, pad, bias is not None, bool(relu))
         ctx.link = link
+        ctx.up = up if (up is not None and need_dx and stride == 1 and link is None) else None
+        ctx.rlink = rlink
         return y
 
     @staticmethod
@@ -859,7 +931,12 @@ class _ConvFn(torch.autograd.Function):
         dt = x.dtype
         dy = _to(dy, dt)
         db = None
-        if relu:
+        fused, fdb = ctx.rlink.take(dy) if ctx.rlink is not None else (False, None)
+        if fused:  # the consumer's kernel already applied the ReLU (and summed the bias gradient)
+            dz = dy
+            if has_bias and ctx.needs_input_grad[4]:
+                db = fdb
+        elif relu:
             nb_, co, ho, wo = dy.shape
             M = nb_ * ho * wo
             dz = torch.empty_like(dy, memory_format=torch.channels_last)
@@ -874,8 +951,8 @@ class _ConvFn(torch.autograd.Function):
             dz = dy
             if has_bias and ctx.needs_input_grad[4]:
                 db = dy.float().sum(dim=(0, 2, 3))
-        dx, dw = _conv_backward(ctx, x, wb, wt, dz, stride, pad, ctx.link)
-        return dx, dw, None, None, db, None, None, None, None, None
+        dx, dw = _conv_backward(ctx, x, wb, wt, dz, stride, pad, ctx.link, ctx.up)
+        return dx, dw, None, None, db, None, None, None, None, None, None
 
 
 def conv_supported(x: torch.Tensor, weight: torch.Tensor) -> bool:
@@ -901,15 +978,20 @@ class ConvAct2d(nn.Conv2d):
         return conv_supported(x, self.weight)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        rl = ReluLink(self.bias is not None) if (self.act and ReluLink.enabled and torch.is_grad_enabled()) else None
         if self.fused(x):
             dt = mfma_dtype(x)
-            return _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0], self.bias, self.act, None, None,
-                                 WeightCastPlan.cached(self, dt), dt)
-        if stem_supported(x, self) and self.kernel_size[0] <= 4:  # VGG's 3-channel first layer
-            return _StemConvFn.apply(x, self.weight, self.stride[0], self.padding[0], None, mfma_dtype(x), self.bias,
-                                     self.act)
-        y = super().forward(x)
-        return F.relu(y) if self.act else y
+            y = _ConvFn.apply(x, self.weight, self.stride[0], self.padding[0], self.bias, self.act, None, None,
+                              WeightCastPlan.cached(self, dt), dt, rl)
+        elif stem_supported(x, self) and self.kernel_size[0] <= 4:  # VGG's 3-channel first layer
+            y = _StemConvFn.apply(x, self.weight, self.stride[0], self.padding[0], None, mfma_dtype(x), self.bias,
+                                  self.act, rl)
+        else:
+            y = super().forward(x)
+            return F.relu(y) if self.act else y
+        if rl is not None:
+            y._mpit_relu = rl
+        return y
 
 
 class ConvNHWC(nn.Conv2d):
@@ -967,6 +1049,15 @@ class WeightCastPlan:
         self.amax = None
         for mod in self.model.modules():
             kind = None
+            if getattr(mod, "_mpit_linear", False):  # ops/linear.py LinearAct: wt[K, N] only, bf16 steps
+                w = mod.weight
+                if f32 or not w.is_cuda or w.dtype != torch.float32 or not w.is_contiguous():
+                    continue
+                co, c = w.shape
+                wt = torch.empty((c, co), dtype=torch.bfloat16, device=w.device)
+                specs.append([4096, w.data_ptr(), 0, wt.data_ptr(), co, c, 1, 1, 1, 0, 0])
+                self.mods.append((mod, w.data_ptr(), (None, wt)))
+                continue
             if isinstance(mod, Conv1x1) and mod.stride == (1, 1):
                 kind = 0
             elif isinstance(mod, (ConvNHWC, ConvAct2d)):
@@ -1182,7 +1273,8 @@ class _StemConvFn(torch.autograd.Function):
     (the image needs none)."""
 
     @staticmethod
-    def forward(ctx, x, weight, stride: int, pad: int, hold=None, dt=torch.bfloat16, bias=None, relu=False):
+    def forward(ctx, x, weight, stride: int, pad: int, hold=None, dt=torch.bfloat16, bias=None, relu=False,
+                rlink=None):
         nb, _, h, w = x.shape
         co, _, r, s = weight.shape
         f32 = dt == torch.float32
@@ -1226,6 +1318,7 @@ class _StemConvFn(torch.autograd.Function):
                         rows=rows, **kw)
         ctx.save_for_backward(xp, y if relu else None)
         ctx.geo = (nb, hp, wp, co, ho, wo, stride, tuple(weight.shape), rows, bias is not None, bool(relu))
+        ctx.rlink = rlink
         ctx.pack = ent
         if ent is not None:
             ent.used(x.device)
@@ -1242,7 +1335,10 @@ class _StemConvFn(torch.autograd.Function):
         dy = _to(dy, dt)
         m = native()
         dev = xp.device.index
-        if relu:  # dz = dy * (y > 0) and the bias gradient in one pass (csrc/kernels/act.hip)
+        fused, fdb = ctx.rlink.take(dy) if ctx.rlink is not None else (False, None)
+        if fused:  # the consumer's kernel applied the ReLU and summed the bias gradient
+            db = fdb if (has_bias and ctx.needs_input_grad[6]) else None
+        elif relu:  # dz = dy * (y > 0) and the bias gradient in one pass (csrc/kernels/act.hip)
             dz = torch.empty_like(dy, memory_format=torch.channels_last)
             want_db = has_bias and ctx.needs_input_grad[6]
             db = torch.empty(co, dtype=torch.float32, device=dy.device) if want_db else None
@@ -1270,7 +1366,7 @@ class _StemConvFn(torch.autograd.Function):
             # the wgrad reading the buffer is queued: the next refill is ordered after it
             ctx.pack.used(xp.device)
             ctx.pack.busy = False
-        return None, dw, None, None, None, None, db, None
+        return None, dw, None, None, None, None, db, None, None
 
 
 def stem_supported(x: torch.Tensor, conv: nn.Conv2d) -> bool:

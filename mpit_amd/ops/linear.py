@@ -1,0 +1,135 @@
+"""Fully connected layers (+ bias, + ReLU) of the VGG / AlexNet classifiers on the MFMA GEMM
+kernels, bf16 steps (the reference's nn.Linear + nn.ReLU pairs: asyncsgd/models, the
+Torch7 ``nn.Linear``).
+
+Under autocast a plain ``nn.Linear`` costs, per step, a bf16 cast of its fp32 weight in the
+forward, a hipBLASLt GEMM picked for a 64-row batch, and a bf16 -> fp32 cast of the weight
+gradient in the backward. For VGG-16's first classifier layer (25088 x 4096, 411 MB of fp32
+weight) the two casts alone move 1.2 GB per step. Here:
+
+* the weight is cast ONCE per step by the model's :class:`ops.conv.WeightCastPlan` launch,
+  as its transpose ``wt[K, N]`` only: every GEMM below reads that one operand;
+* forward ``y = x W^T`` runs as the split-K weight-gradient kernel ``gemm_tn`` over the
+  K = in_features rows of ``wt`` and ``x^T``, a grid of (N / 128) x splits blocks instead of a
+  64-row GEMM's N / 128 (which leaves most of the 256 CUs idle); bias + ReLU on its small
+  [N, batch] fp32 output;
+* backward: ``dz = dy * (y > 0)`` and the bias gradient in one pass (``relu_bias_bwd``),
+  ``dx = dz W`` as ``gemm_nt`` against ``wt``, and the weight gradient ``dz^T x`` as
+  ``gemm_tn`` written in fp32 straight into the gradient (no cast).
+
+Falls back to ``F.linear`` (+ ``F.relu``) off the bf16 MFMA path (CPU, fp32 steps) or when
+the shapes do not tile (in / out features % 64, batch % 64). MPIT_LINEAR_FUSE=0: always the
+fallback."""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .._ext import native
+from .conv import WeightCastPlan, mfma_dtype
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _wt_of(mod, weight: torch.Tensor) -> torch.Tensor:
+    """wt[K, N] bf16 of this step: the cast plan's, else cast here (one launch)."""
+    c = WeightCastPlan.cached(mod, torch.bfloat16)
+    if c is not None:
+        return c[1]
+    n, k = weight.shape
+    wt = torch.empty((k, n), dtype=torch.bfloat16, device=weight.device)
+    w = weight.detach()
+    if not w.is_contiguous():
+        w = w.contiguous()
+    native().cast_transpose(w.device.index, _stream(w), w.data_ptr(), n, k, 0, wt.data_ptr(), f32=False)
+    return wt
+
+
+class _LinearActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, act: bool, wt):
+        m = native()
+        dev = x.device.index
+        st = _stream(x)
+        xb = x.to(torch.bfloat16)
+        M, K = xb.shape
+        N = weight.shape[0]
+        xt = xb.t().contiguous()  # [K, M]: the reduction runs over the rows of wt and x^T
+        yt = torch.empty((N, M), dtype=torch.float32, device=x.device)
+        nws = m.gemm_tn_ws_floats(dev, K, N, M)
+        ws = torch.empty(nws, dtype=torch.float32, device=x.device) if nws else None
+        m.gemm_tn(dev, st, K, N, M, wt.data_ptr(), N, xt.data_ptr(), M, yt.data_ptr(),
+                  ws.data_ptr() if ws is not None else 0, 0.0, f32=False)
+        y = yt.t().contiguous()  # [M, N] row-major (1 MB at VGG's shapes)
+        if bias is not None:
+            y.add_(bias)
+        if act:
+            y.relu_()
+        y = y.to(torch.bfloat16)
+        ctx.save_for_backward(xb, wt, y if act else None)
+        ctx.flags = (act, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xb, wt, y = ctx.saved_tensors
+        act, has_bias = ctx.flags
+        m = native()
+        dev = xb.device.index
+        st = _stream(xb)
+        M, K = xb.shape
+        N = wt.shape[1]
+        dy = dy.to(torch.bfloat16).contiguous()
+        want_db = has_bias and ctx.needs_input_grad[2]
+        db = None
+        if act:
+            dz = torch.empty_like(dy)
+            db = torch.empty(N, dtype=torch.float32, device=dy.device) if want_db else None
+            rws = torch.empty(m.relu_bias_bwd_ws_floats(N), dtype=torch.float32, device=dy.device) if want_db else None
+            m.relu_bias_bwd(dev, st, M, N, dy.data_ptr(), y.data_ptr(), dz.data_ptr(),
+                            db.data_ptr() if db is not None else 0, rws.data_ptr() if rws is not None else 0)
+        else:
+            dz = dy
+            if want_db:
+                db = dz.float().sum(0)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:  # dx[M, K] = dz[M, N] . W[N, K] = dz . wt^T
+            dx = torch.empty((M, K), dtype=torch.bfloat16, device=dy.device)
+            m.gemm_nt(dev, st, M, K, N, dz.data_ptr(), N, wt.data_ptr(), N, dx.data_ptr(), K, 0)
+        if ctx.needs_input_grad[1]:  # dW[N, K] = dz^T . x, fp32 straight into the gradient
+            dw = torch.empty((N, K), dtype=torch.float32, device=dy.device)
+            nws = m.gemm_tn_ws_floats(dev, M, N, K)
+            ws = torch.empty(nws, dtype=torch.float32, device=dy.device) if nws else None
+            m.gemm_tn(dev, st, M, N, K, dz.data_ptr(), N, xb.data_ptr(), K, dw.data_ptr(),
+                      ws.data_ptr() if ws is not None else 0, 0.0, f32=False)
+        return dx, dw, db, None, None
+
+
+class LinearAct(nn.Linear):
+    """``act(linear(x))`` with act = ReLU or identity; the bf16 MFMA path above when it
+    applies (see module docstring), ``F.linear`` (+ ``F.relu``) otherwise."""
+
+    _mpit_linear = True  # (ops.conv.WeightCastPlan: cast with the model's convolutions)
+    enabled = os.environ.get("MPIT_LINEAR_FUSE", "1") != "0"
+
+    def __init__(self, in_features: int, out_features: int, bias: bool = True, act: bool = True):
+        super().__init__(in_features, out_features, bias=bias)
+        self.act = act
+
+    def fused(self, x: torch.Tensor) -> bool:
+        return (LinearAct.enabled and x.is_cuda and x.dim() == 2 and mfma_dtype(x) == torch.bfloat16
+                and self.in_features % 64 == 0
+                and self.out_features % 64 == 0 and x.shape[0] % 64 == 0 and self.weight.dtype == torch.float32
+                and self.weight.is_contiguous())
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.fused(x):
+            with torch.autocast("cuda", enabled=False):
+                return _LinearActFn.apply(x, self.weight, self.bias, self.act, _wt_of(self, self.weight))
+        y = F.linear(x, self.weight, self.bias)
+        return F.relu(y) if self.act else y

@@ -4,6 +4,8 @@ The forward keeps a one-byte argmax per output element; the backward gathers, fo
 input pixel, the gradients of the windows that selected it (dx written once, no atomics,
 no zero fill). :class:`MaxPool2dNHWC` is a drop-in ``nn.MaxPool2d`` that takes this path
 for bf16 / fp32 channels_last CUDA tensors with C % 8 == 0 and falls back to PyTorch otherwise.
+Below a conv(+bias)+ReLU (VGG, AlexNet: ``ops.conv.ReluLink`` on the input) the backward also
+applies that ReLU (mask = pooled output > 0) and sums the conv's bias gradient.
 """
 from __future__ import annotations
 
@@ -11,7 +13,7 @@ import torch
 import torch.nn as nn
 
 from .._ext import native
-from .conv import amax_of, set_amax
+from .conv import ReluLink, amax_of, set_amax
 
 
 def _stream(t: torch.Tensor) -> int:
@@ -21,6 +23,9 @@ def _stream(t: torch.Tensor) -> int:
 class _MaxPoolFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, k: int, stride: int, pad: int):
+        up = ReluLink.of(x)
+        if up is not None and 256 % (x.shape[1] // 8):
+            up = None
         if not x.is_contiguous(memory_format=torch.channels_last):
             x = x.contiguous(memory_format=torch.channels_last)
         n, c, h, w = x.shape
@@ -30,21 +35,30 @@ class _MaxPoolFn(torch.autograd.Function):
         native().maxpool_fwd(x.device.index, _stream(x), n, h, w, c, k, stride, pad, x.data_ptr(), y.data_ptr(),
                              idx.data_ptr(), f32=x.dtype == torch.float32)
         ctx.dt = x.dtype
-        ctx.save_for_backward(idx)
+        ctx.up = up
+        ctx.save_for_backward(idx, y if up is not None else None)
         ctx.geo = (n, c, h, w, k, stride, pad)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        (idx,) = ctx.saved_tensors
+        idx, yp = ctx.saved_tensors
         n, c, h, w, k, stride, pad = ctx.geo
         if dy.dtype != ctx.dt:
             dy = dy.to(ctx.dt)
         if not dy.is_contiguous(memory_format=torch.channels_last):
             dy = dy.contiguous(memory_format=torch.channels_last)
         dx = torch.empty((n, c, h, w), dtype=ctx.dt, device=dy.device, memory_format=torch.channels_last)
-        native().maxpool_bwd(dy.device.index, _stream(dy), n, h, w, c, k, stride, pad, dy.data_ptr(), idx.data_ptr(),
-                             dx.data_ptr(), f32=ctx.dt == torch.float32)
+        m = native()
+        kw, db, up = {}, None, ctx.up
+        if up is not None:  # dx is the conv's dz (ReLU applied), db its bias gradient
+            ws = torch.empty(m.maxpool_bwd_ws_floats(c), dtype=torch.float32, device=dy.device)
+            db = torch.empty(c, dtype=torch.float32, device=dy.device) if up.has_bias else None
+            kw = dict(ypool=yp.data_ptr(), db=db.data_ptr() if db is not None else 0, ws=ws.data_ptr())
+        m.maxpool_bwd(dy.device.index, _stream(dy), n, h, w, c, k, stride, pad, dy.data_ptr(), idx.data_ptr(),
+                      dx.data_ptr(), f32=ctx.dt == torch.float32, **kw)
+        if up is not None:
+            up.give(dx, db)
         return dx, None, None, None
 
 

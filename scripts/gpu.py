@@ -14,7 +14,7 @@ Steps:
   bench                 bench.py defaults (fp32 headline + bf16 secondary) -> bench.json
   bench:<args>[:K=V;K=V] bench.py <args> (comma separated), extra env    -> bench_<n>.json
   dbench:<n>:<args>     bench.py on n ranks sharing the box's GPU (rehearsal) -> dbench_<n>.json
-  prof:<name>:<args>    rocprofv3 --kernel-trace of bench.py <args> + stream table -> streams_<name>.md
+  prof:<name>:<args>[:K=V;K=V] rocprofv3 --kernel-trace of bench.py <args> (extra env) + stream table -> streams_<name>.md
   gemmcalls:<name>:<args> per-call GEMM shapes + times of one steady step     -> gemm_calls_<name>.md
   mp:<script>:<n>[:K=V;K=V] tests/mp/<script> on n ranks with extra env   -> mp_<script>_<n>.log
   py:<file>[:args[:K=V;K=V]] python3 <file> <args> with extra env (benchmarks/ probes) -> py_<n>.log
@@ -71,7 +71,9 @@ def main(argv) -> int:
         return 2
     out = os.path.join(ROOT, "gpurun_out", argv[0])
     os.makedirs(out, exist_ok=True)
-    pyt = [PY, "-u", "-m", "pytest", "-x", "-v", "--timeout", "120", "--timeout-method", "thread"]
+    # --tb=short: a failure's report never formats the (large, on-GPU) tensor arguments of the
+    # frames it crossed, which can take longer than the time limit
+    pyt = [PY, "-u", "-m", "pytest", "-x", "-v", "--tb=short", "--timeout", "120", "--timeout-method", "thread"]
     for i, step in enumerate(argv[1:]):
         kind, _, rest = step.partition(":")
         if kind == "smoke":
@@ -101,10 +103,12 @@ def main(argv) -> int:
             print(_tail(os.path.join(out, f"dbench_{i}.json"), 1)[:400])
         elif kind == "prof":
             name, _, args = rest.partition(":")
+            args, _, envs = args.partition(":")
+            env = dict(kv.split("=", 1) for kv in envs.split(";")) if envs else {}
             d = os.path.join(out, f"prof_{name}")
             rc = _run(out, f"prof_{name}.log", ["rocprofv3", "--kernel-trace", "--stats", "-d", d, "-o", "t",
                                                "--output-format", "csv", "--", PY, "bench.py"]
-                      + (args.split(",") if args else []), 600)
+                      + (args.split(",") if args else []), 600, env=env)
             if rc == 0:
                 rc = _run(out, f"streams_{name}.log", [PY, "scripts/stream_summary.py", d,
                                                        os.path.join(out, f"streams_{name}.md"), "cast_batch_kernel", "3"], 300)

@@ -1,0 +1,48 @@
+"""LinearAct (ops/linear.py): the classifier's Linear(+ReLU) on the MFMA kernels in bf16
+steps, against fp32 PyTorch on the same bf16-rounded operands; CPU fallback == F.linear."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+
+def test_linear_act_cpu_fallback():
+    from mpit_amd.ops.linear import LinearAct
+
+    torch.manual_seed(0)
+    lin = LinearAct(128, 64)
+    x = torch.randn(8, 128)
+    assert not lin.fused(x)
+    assert torch.equal(lin(x), F.relu(F.linear(x, lin.weight, lin.bias)))
+    lin.act = False
+    assert torch.equal(lin(x), F.linear(x, lin.weight, lin.bias))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("act", [True, False])
+@pytest.mark.parametrize("M,K,N", [(64, 25088, 4096), (128, 1024, 512), (64, 4096, 4096)])
+def test_linear_act_bf16(act, M, K, N):
+    from mpit_amd.ops.linear import LinearAct
+
+    torch.manual_seed(0)
+    lin = LinearAct(K, N, act=act).cuda()
+    with torch.no_grad():
+        lin.bias.uniform_(-0.1, 0.1)
+    x = torch.randn(M, K, device="cuda").requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        assert lin.fused(x)
+        y = lin(x)
+    assert y.dtype == torch.bfloat16 and y.shape == (M, N)
+    xq = x.detach().to(torch.bfloat16).float().requires_grad_(True)
+    wq = lin.weight.detach().to(torch.bfloat16).float().requires_grad_(True)
+    bq = lin.bias.detach().clone().requires_grad_(True)
+    ref = F.linear(xq, wq, bq)
+    if act:
+        ref = F.relu(ref)
+    scale = ref.abs().max().item()
+    assert (y.float() - ref).abs().max().item() <= 1e-2 * scale
+    g = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    y.backward(g)
+    ref.backward(g.float() * ((y.float() > 0).float() if act else 1.0))  # the same mask as the layer's
+    for a, r, name in ((x.grad, xq.grad, "x"), (lin.weight.grad, wq.grad, "w"), (lin.bias.grad, bq.grad, "b")):
+        assert a.dtype == torch.float32 and a.shape == r.shape, name
+        assert (a - r).abs().max().item() <= 2e-2 * r.abs().max().item() + 1e-4, name

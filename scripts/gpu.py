@@ -11,6 +11,7 @@ Steps:
   smoke                 __graft_entry__.smoke()                         -> smoke.log
   tier                  pytest -m gpu (whole GPU tier)                  -> pytest_gpu.log
   pytest:<args>[:K=V;K=V] pytest <args> (e.g. pytest:tests/test_overlap.py), extra env -> pytest_<n>.log
+  pytestall:<args>[:K=V] the same without -x (a diagnosis run: every test reports)
   bench                 bench.py defaults (fp32 headline + bf16 secondary) -> bench.json
   bench:<args>[:K=V;K=V] bench.py <args> (comma separated), extra env    -> bench_<n>.json
   dbench:<n>:<args>     bench.py on n ranks sharing the box's GPU (rehearsal) -> dbench_<n>.json
@@ -82,10 +83,11 @@ def main(argv) -> int:
         elif kind == "tier":
             rc = _run(out, "pytest_gpu.log", pyt + ["tests", "-m", "gpu"] + (rest.split(",") if rest else []), 1000)
             print(_tail(os.path.join(out, "pytest_gpu.log"), 2))
-        elif kind == "pytest":
+        elif kind in ("pytest", "pytestall"):  # pytestall: no -x (every test reports)
             parts = rest.split(":")
             env = dict(kv.split("=", 1) for kv in parts[1].split(";")) if len(parts) > 1 and parts[1] else {}
-            rc = _run(out, f"pytest_{i}.log", pyt + parts[0].split(","), 900, env=env)
+            base = pyt if kind == "pytest" else [a for a in pyt if a != "-x"]
+            rc = _run(out, f"pytest_{i}.log", base + parts[0].split(","), 900, env=env)
             print(_tail(os.path.join(out, f"pytest_{i}.log"), 2))
         elif kind == "bench":
             parts = rest.split(":")

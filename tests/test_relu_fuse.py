@@ -75,10 +75,20 @@ def test_vgg_block_fused_relu_backward(dt):
     xr = x.float().requires_grad_(False)
     yr = _ref_forward(list(ref), xr)
     yr.backward(g.float())
-    tol = 3e-2 if dt == torch.bfloat16 else 2e-3
+    # bf16: the 4-layer chain against an fp32 forward differs by 5-17 % of max (r05h): bf16
+    # rounding makes near-ties in the 2x2 pools pick other argmax pixels and flips ReLU masks
+    # near 0, so the gradient lands on other pixels. Each layer alone is held to the fp32
+    # reference in test_conv_act / test_stem; the claim here is fused == unfused, and a sanity
+    # bound against fp32.
+    tol = 0.25 if dt == torch.bfloat16 else 2e-3
+    report, bad = [], []
     for (name, p), a, b in zip(ref.named_parameters(), grads[True], grads[False]):
         r = p.grad
         scale = r.abs().max().item() + 1e-6
-        assert (a - r).abs().max().item() <= tol * scale, (name, (a - r).abs().max().item(), scale)
+        ea, eb, eab = ((a - r).abs().max().item() / scale, (b - r).abs().max().item() / scale,
+                       (a - b).abs().max().item() / scale)
+        report.append(f"{name}: fused {ea:.2e} unfused {eb:.2e} fused-unfused {eab:.2e}")
         # fused vs unfused: the same math on the same kernels (the bias sums differ in order only)
-        assert (a - b).abs().max().item() <= (1e-2 if dt == torch.bfloat16 else 1e-4) * scale, name
+        if ea > tol or eab > (1e-2 if dt == torch.bfloat16 else 1e-4):
+            bad.append(name)
+    assert not bad, "; ".join(report)

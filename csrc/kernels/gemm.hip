@@ -2063,6 +2063,34 @@ __device__ __forceinline__ void cast_tile(const float* __restrict__ w, int R, in
   }
 }
 
+// A large 1-tap weight's bf16 transpose only (the classifier layers, ops/linear.py): one
+// 64 x 64 tile per block, float4 row reads and 8-byte packed bf16 writes, so every wave
+// instruction covers 256-B input / 128-B output row segments (the 32 x 32 scalar tile above
+// moves VGG-16's 411 MB fc1 weight at ~1.2 TB/s). Host-checked: R, Cc % 64 == 0, w 16-B aligned.
+__device__ __forceinline__ void cast_tile64_t(const float* __restrict__ w, int R, int Cc, uint16_t* __restrict__ wt,
+                                              int cx, int ry) {
+  __shared__ float tile[64][65];
+  const int c0 = cx * 64, r0 = ry * 64;
+  const int t = threadIdx.x, cc = (t & 15) * 4, rr = t >> 4;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int r = rr + 16 * p;
+    const float4 v = *reinterpret_cast<const float4*>(w + int64_t(r0 + r) * Cc + c0 + cc);
+    tile[r][cc] = v.x;
+    tile[r][cc + 1] = v.y;
+    tile[r][cc + 2] = v.z;
+    tile[r][cc + 3] = v.w;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int c = rr + 16 * p;
+    const uint32_t lo = uint32_t(f2bf(tile[cc][c])) | (uint32_t(f2bf(tile[cc + 1][c])) << 16);
+    const uint32_t hi = uint32_t(f2bf(tile[cc + 2][c])) | (uint32_t(f2bf(tile[cc + 3][c])) << 16);
+    *reinterpret_cast<uint2*>(wt + int64_t(c0 + c) * R + r0 + cc) = make_uint2(lo, hi);
+  }
+}
+
 // The bf16x6 operand split of one fp32 value: h = bf16(v), m = bf16(v - h), l = bf16(v - h - m)
 // (round to nearest; for normal numbers v == h + m + l exactly) — split3's arithmetic.
 __device__ __forceinline__ void split1(float v, uint16_t& h, uint16_t& m, uint16_t& l) {
@@ -2147,6 +2175,7 @@ struct CastJob {
   void* wb;
   void* wt;
   int R, Cc, T, tcx, tcy;  // tiles along Cc and R
+  int big;                 // cast_tile64_t (64 x 64 tiles: a large 1-tap bf16 transpose only)
   int f32;                 // outputs: 0 bf16, 1 fp32 (no plain copy), 2 pre-split planes
   int f16;                 // (f32 == 2) planes are fp16 h, l of the weight scaled by amax's 2^e
   const float* amax;       // (f16) device upper bound of |w| over the plan
@@ -2208,7 +2237,9 @@ __global__ __launch_bounds__(256) void cast_batch_kernel(const CastJob* __restri
   const int64_t local = int64_t(blockIdx.x) - J.block0;
   const int per_tap = J.tcx * J.tcy;
   const int tap = int(local / per_tap), rem = int(local % per_tap);
-  if (J.f32 == 2) {
+  if (J.big) {
+    cast_tile64_t(J.w, J.R, J.Cc, static_cast<uint16_t*>(J.wt), rem % J.tcx, rem / J.tcx);
+  } else if (J.f32 == 2) {
     float sc = 1.f, sc11 = 2048.f;
     if (J.f16) {
       const int e = fp16_exp(J.amax);
@@ -3184,6 +3215,7 @@ int64_t cast_jobs_build(uintptr_t host_table, const std::vector<std::array<int64
     //        | 512: wb as three pre-split bf16 planes (else none: the forward reads the master)
     //        | 1024: wt as three pre-split bf16 planes (else fp32)
     //        | 2048: the planes are fp16x3's two fp16 planes, scaled by the bound at q[10]
+    //        | 4096: a classifier weight: its bf16 transpose only (64 x 64 tiles when they fit)
     const int kind = int(q[0] & 0xff), Co = int(q[4]), C = int(q[5]), R = int(q[6]), S = int(q[7]);
     const int stride = int(q[8]), pad = int(q[9]);
     CastJob J{};
@@ -3213,8 +3245,10 @@ int64_t cast_jobs_build(uintptr_t host_table, const std::vector<std::array<int64
       }
       if (kind == 2) J.wt = nullptr;
     }
-    J.tcx = (C + 31) / 32;
-    J.tcy = (Co + 31) / 32;
+    J.big = ((q[0] >> 12) & 1) && J.f32 == 0 && kind == 0 && J.T == 1 && C % 64 == 0 && Co % 64 == 0 && !J.wb &&
+            J.wt && q[1] % 16 == 0 && q[3] % 8 == 0;
+    J.tcx = J.big ? C / 64 : (C + 31) / 32;
+    J.tcy = J.big ? Co / 64 : (Co + 31) / 32;
     J.block0 = blocks;
     blocks += int64_t(J.tcx) * J.tcy * J.T;
     jobs[k] = J;

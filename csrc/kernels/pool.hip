@@ -9,6 +9,7 @@
 // max_pool_backward walks the same windows but at ~6x the time (rocprof, profiles/).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -177,6 +178,81 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const T* __restrict__ 
   }
 }
 
+// Backward of a pool whose windows partition the input (K == stride, pad == 0: VGG's 2x2 / 2):
+// one thread per OUTPUT window x 8 channels reads the window's argmax, gradient (and pooled
+// value, RB) once and writes all K x K input pixels of the window (zeros off the argmax) —
+// the input-pixel gather above reads each window K^2 times. Input rows / columns past the last
+// full window (H % K) get zeros. RB as above: mask ypool > 0, channel sums of what is stored.
+template <typename T, typename I, bool RB>
+__global__ __launch_bounds__(256) void maxpool_bwd_part_kernel(const T* __restrict__ dy,
+                                                               const uint8_t* __restrict__ idx, T* __restrict__ dx,
+                                                               PoolGeo g, const T* __restrict__ ypool,
+                                                               float* __restrict__ part) {
+  const I cv = I(g.C / 8);
+  const I total = I(g.N) * I(g.Ho) * I(g.Wo) * cv;
+  float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (I t = I(blockIdx.x) * blockDim.x + threadIdx.x; t < total; t += I(gridDim.x) * blockDim.x) {
+    const int c8 = int(t % cv);
+    const I pix = t / cv;
+    const int wo = int(pix % I(g.Wo));
+    const I r = pix / I(g.Wo);
+    const int ho = int(r % I(g.Ho));
+    const int64_t n = int64_t(r / I(g.Ho));
+    const int64_t o = int64_t(pix) * g.C + c8 * 8;
+    const uint2 a = *reinterpret_cast<const uint2*>(idx + o);
+    float gv[8];
+    ld8(dy + o, gv);
+    if constexpr (RB) {
+      float yv[8];
+      ld8(ypool + o, yv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        if (!(yv[e] > 0.f)) gv[e] = 0.f;
+        if constexpr (sizeof(T) == 2) bsum[e] += bf2f(f2bf(gv[e]));
+        else bsum[e] += gv[e];
+      }
+    }
+    for (int i = 0; i < g.K; ++i) {
+      const int h = ho * g.K + i;
+      for (int j = 0; j < g.K; ++j) {
+        const int w = wo * g.K + j;
+        const uint8_t k = uint8_t(i * g.K + j);
+        float q[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint8_t ae = uint8_t(((e < 4 ? a.x : a.y) >> (8 * (e & 3))) & 0xff);
+          q[e] = ae == k ? gv[e] : 0.f;
+        }
+        st8(dx + ((n * g.H + h) * g.W + w) * g.C + c8 * 8, q);
+      }
+    }
+    // the rows / columns no window covers (H or W not a multiple of K) get zeros
+    const float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (wo == g.Wo - 1)
+      for (int i = 0; i < g.K; ++i)
+        for (int w = g.Wo * g.K; w < g.W; ++w) st8(dx + ((n * g.H + ho * g.K + i) * g.W + w) * g.C + c8 * 8, z);
+    if (ho == g.Ho - 1)
+      for (int h = g.Ho * g.K; h < g.H; ++h)
+        for (int w = wo * g.K; w < (wo == g.Wo - 1 ? g.W : wo * g.K + g.K); ++w)
+          st8(dx + ((n * g.H + h) * g.W + w) * g.C + c8 * 8, z);
+  }
+  if constexpr (RB) {
+    __shared__ float red[256 * 8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[threadIdx.x * 8 + e] = bsum[e];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int cvi = g.C / 8;
+    for (int c = threadIdx.x; c < g.C; c += blockDim.x) {
+      const int c8 = c / 8, e = c % 8;
+      float sum = 0.f;
+      for (int tid = c8; tid < 256; tid += cvi) sum += red[tid * 8 + e];
+      part[int64_t(blockIdx.x) * g.C + c] = sum;
+    }
+  }
+}
+
 PoolGeo pool_geo(int N, int H, int W, int C, int K, int stride, int pad) {
   if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 8 || K <= 0 || K > 15 || stride <= 0 || pad < 0 || 2 * pad > K)
     throw std::invalid_argument("maxpool: unsupported geometry (C % 8 == 0, K <= 15, pad <= K/2)");
@@ -204,7 +280,7 @@ void maxpool_fwd_t(int dev, hipStream_t s, int N, int H, int W, int C, int K, in
   hip_check(hipGetLastError(), "maxpool_fwd launch");
 }
 
-constexpr int kPoolRbBlocks = 1024;  // partial rows of the fused bias gradient
+constexpr int kPoolRbBlocks = 8192;  // partial rows of the fused bias gradient
 
 template <typename T>
 void maxpool_bwd_t(int dev, hipStream_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t dy,
@@ -214,12 +290,19 @@ void maxpool_bwd_t(int dev, hipStream_t s, int N, int H, int W, int C, int K, in
   if (db && (!ypool || !ws)) throw std::invalid_argument("maxpool_bwd: the bias gradient needs ypool and ws");
   if (ypool && 256 % (C / 8)) throw std::invalid_argument("maxpool_bwd: the fused ReLU needs 256 % (C / 8) == 0");
   hip_check(hipSetDevice(dev), "hipSetDevice");
-  const int64_t work = int64_t(N) * H * W * (C / 8);
-  const unsigned grid = ypool ? unsigned(std::min<int64_t>((work + 255) / 256, kPoolRbBlocks)) : grid_for(work);
-  const bool narrow = work + int64_t(grid) * 256 < (int64_t(1) << 32);
   const auto* y = reinterpret_cast<const T*>(ypool);
   float* part = reinterpret_cast<float*>(ws);
-  if (ypool) {
+  // windows that partition the input (K == stride, no padding): one thread per window
+  const bool part_win = K == stride && pad == 0 && std::getenv("MPIT_POOL_GATHER") == nullptr;
+  const int64_t work = part_win ? int64_t(N) * g.Ho * g.Wo * (C / 8) : int64_t(N) * H * W * (C / 8);
+  const unsigned grid = ypool ? unsigned(std::min<int64_t>((work + 255) / 256, kPoolRbBlocks)) : grid_for(work);
+  const bool narrow = int64_t(N) * H * W * (C / 8) + int64_t(grid) * 256 < (int64_t(1) << 32);
+  if (part_win) {
+    auto* k = ypool ? (narrow ? maxpool_bwd_part_kernel<T, uint32_t, true> : maxpool_bwd_part_kernel<T, int64_t, true>)
+                    : (narrow ? maxpool_bwd_part_kernel<T, uint32_t, false> : maxpool_bwd_part_kernel<T, int64_t, false>);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, s, reinterpret_cast<const T*>(dy),
+                       reinterpret_cast<const uint8_t*>(idx), reinterpret_cast<T*>(dx), g, y, part);
+  } else if (ypool) {
     auto* k = narrow ? maxpool_bwd_kernel<T, uint32_t, true> : maxpool_bwd_kernel<T, int64_t, true>;
     hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, s, reinterpret_cast<const T*>(dy),
                        reinterpret_cast<const uint8_t*>(idx), reinterpret_cast<T*>(dx), g, y, part);

@@ -104,8 +104,13 @@ def tile_stats_of(x: torch.Tensor):
     return ts[0], ts[1], ts[3]
 
 
-# MPIT_BN_FOLD_FWD=0: the BN forward's finalize as its own launch instead of in the GEMM
-_FWD_FOLD = os.environ.get("MPIT_BN_FOLD_FWD", "1") != "0"
+# MPIT_BN_FOLD_FWD=1: the BN forward's finalize folded into the producing GEMM's epilogue
+# (stats_fold, csrc/kernels/gemm.hip) instead of its own launch. Off by default: measured
+# slower on two boxes (r05e/r05g, fp32 5380-5433 vs 5456-5517 img/s, bf16 11.5k vs 11.7-11.8k):
+# every block of the statistics GEMMs waits for its own output stores before taking its ticket,
+# +1.23 ms of GEMM time per fp32 step against the 0.53 ms of the 53 finalize launches it saves
+# (profiles/bn_fold_fwd_ab_r05.md)
+_FWD_FOLD = os.environ.get("MPIT_BN_FOLD_FWD", "0") == "1"
 
 
 class BNFold:

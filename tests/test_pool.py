@@ -14,7 +14,10 @@ def test_maxpool_cpu_fallback():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,c,hw,k,s,p", [(4, 64, 112, 3, 2, 1), (2, 16, 15, 3, 2, 1), (3, 8, 10, 2, 2, 0),
-                                          (2, 32, 9, 3, 1, 1), (2, 24, 13, 5, 3, 2)])
+                                          (2, 32, 9, 3, 1, 1), (2, 24, 13, 5, 3, 2),
+                                          # windows partitioning the input (K == stride): the
+                                          # one-thread-per-window backward, with remainders
+                                          (2, 16, 11, 2, 2, 0), (2, 8, 10, 3, 3, 0), (2, 64, 56, 2, 2, 0)])
 def test_maxpool_fwd_bwd(n, c, hw, k, s, p):
     torch.manual_seed(hw + c)
     # distinct values per window so the argmax (and the routed gradient) is unambiguous
@@ -32,3 +35,22 @@ def test_maxpool_fwd_bwd(n, c, hw, k, s, p):
     # bf16 rounding ties can route a gradient to a different (equal-valued) input
     close = (x1.grad.float() - x2.grad).abs() <= 1e-2 * (1 + x2.grad.abs())
     assert close.float().mean().item() > 0.999
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_maxpool_partition_backward_matches_gather(dt, monkeypatch):
+    """The per-window backward (K == stride) writes exactly what the per-input-pixel gather
+    writes (MPIT_POOL_GATHER forces the gather)."""
+    torch.manual_seed(0)
+    x = torch.randn(3, 64, 23, 23, device="cuda").to(dt).contiguous(memory_format=torch.channels_last)
+    m = MaxPool2dNHWC(2, stride=2)
+    grads = []
+    for gather in (False, True):
+        if gather:
+            monkeypatch.setenv("MPIT_POOL_GATHER", "1")
+        xx = x.clone().requires_grad_(True)
+        y = m(xx)
+        y.backward(torch.ones_like(y) * torch.arange(y.numel(), device="cuda").reshape(y.shape).to(dt) / y.numel())
+        grads.append(xx.grad.clone())
+    assert torch.equal(grads[0], grads[1])

@@ -2064,30 +2064,38 @@ __device__ __forceinline__ void cast_tile(const float* __restrict__ w, int R, in
 }
 
 // A large 1-tap weight's bf16 transpose only (the classifier layers, ops/linear.py): one
-// 64 x 64 tile per block, float4 row reads and 8-byte packed bf16 writes, so every wave
-// instruction covers 256-B input / 128-B output row segments (the 32 x 32 scalar tile above
-// moves VGG-16's 411 MB fc1 weight at ~1.2 TB/s). Host-checked: R, Cc % 64 == 0, w 16-B aligned.
+// 128 (rows of w) x 64 (columns) tile per block. Eight float4 row reads in flight per thread
+// (256-B row segments), 8-byte packed bf16 writes covering 256-B output row segments. The
+// 32 x 32 scalar tile above moves VGG-16's 411 MB fc1 weight at ~1.2 TB/s, a 64 x 64 vector
+// tile with 4 reads in flight at ~1.7 TB/s (r05i). Host-checked: R % 128, Cc % 64, w 16-B aligned.
 __device__ __forceinline__ void cast_tile64_t(const float* __restrict__ w, int R, int Cc, uint16_t* __restrict__ wt,
                                               int cx, int ry) {
-  __shared__ float tile[64][65];
-  const int c0 = cx * 64, r0 = ry * 64;
-  const int t = threadIdx.x, cc = (t & 15) * 4, rr = t >> 4;
+  __shared__ float tile[128][65];
+  const int c0 = cx * 64, r0 = ry * 128;
+  const int t = threadIdx.x;
+  {
+    const int cc = (t & 15) * 4, rr = t >> 4;
+    float4 v[8];
 #pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const int r = rr + 16 * p;
-    const float4 v = *reinterpret_cast<const float4*>(w + int64_t(r0 + r) * Cc + c0 + cc);
-    tile[r][cc] = v.x;
-    tile[r][cc + 1] = v.y;
-    tile[r][cc + 2] = v.z;
-    tile[r][cc + 3] = v.w;
+    for (int p = 0; p < 8; ++p)
+      v[p] = *reinterpret_cast<const float4*>(w + int64_t(r0 + rr + 16 * p) * Cc + c0 + cc);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const int r = rr + 16 * p;
+      tile[r][cc] = v[p].x;
+      tile[r][cc + 1] = v[p].y;
+      tile[r][cc + 2] = v[p].z;
+      tile[r][cc + 3] = v[p].w;
+    }
   }
   __syncthreads();
+  const int rc = (t & 31) * 4, cr = t >> 5;
 #pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const int c = rr + 16 * p;
-    const uint32_t lo = uint32_t(f2bf(tile[cc][c])) | (uint32_t(f2bf(tile[cc + 1][c])) << 16);
-    const uint32_t hi = uint32_t(f2bf(tile[cc + 2][c])) | (uint32_t(f2bf(tile[cc + 3][c])) << 16);
-    *reinterpret_cast<uint2*>(wt + int64_t(c0 + c) * R + r0 + cc) = make_uint2(lo, hi);
+  for (int p = 0; p < 8; ++p) {
+    const int c = cr + 8 * p;
+    const uint32_t lo = uint32_t(f2bf(tile[rc][c])) | (uint32_t(f2bf(tile[rc + 1][c])) << 16);
+    const uint32_t hi = uint32_t(f2bf(tile[rc + 2][c])) | (uint32_t(f2bf(tile[rc + 3][c])) << 16);
+    *reinterpret_cast<uint2*>(wt + int64_t(c0 + c) * R + r0 + rc) = make_uint2(lo, hi);
   }
 }
 
@@ -2325,10 +2333,11 @@ static int nt_tile_config(int64_t M, int N, int K, bool conv, int cin_conv, bool
   // where K is deep (>= 1024) AND the grid still has >= 4 blocks per CU — VGG-16's 112/56-
   // pixel 3x3 convolutions and their backward-data, no ResNet-50 shape — VGG-16 bf16 EASGD
   // +3.5 % (4,944 vs 4,774 / 4,824 img/s with every GEMM on 256x128, gpurun_out/r04vgg).
-  // MPIT_GEMM_DEEPK=k (A/B): 256 x 128 for every GEMM with K >= k, whatever its grid
+  // MPIT_GEMM_DEEPK=k: 256 x 128 for every GEMM with K >= k, whatever its grid (default 2304:
+  // VGG-16 bf16 5,319 vs 5,239 img/s, r05i; ResNet-50 bf16 within noise, r05d; 0 = off)
   static const int deepk = [] {
     const char* e = std::getenv("MPIT_GEMM_DEEPK");
-    return e ? std::atoi(e) : 0;
+    return e ? std::atoi(e) : 2304;
   }();
   int cfg = forced >= 0 ? forced
                         : (K >= 1024 && N % 128 == 0 && ((M + 255) / 256) * int64_t(N / 128) >= 1024 ? 1 : 0);
@@ -3245,10 +3254,10 @@ int64_t cast_jobs_build(uintptr_t host_table, const std::vector<std::array<int64
       }
       if (kind == 2) J.wt = nullptr;
     }
-    J.big = ((q[0] >> 12) & 1) && J.f32 == 0 && kind == 0 && J.T == 1 && C % 64 == 0 && Co % 64 == 0 && !J.wb &&
+    J.big = ((q[0] >> 12) & 1) && J.f32 == 0 && kind == 0 && J.T == 1 && C % 64 == 0 && Co % 128 == 0 && !J.wb &&
             J.wt && q[1] % 16 == 0 && q[3] % 8 == 0;
     J.tcx = J.big ? C / 64 : (C + 31) / 32;
-    J.tcy = J.big ? Co / 64 : (Co + 31) / 32;
+    J.tcy = J.big ? Co / 128 : (Co + 31) / 32;
     J.block0 = blocks;
     blocks += int64_t(J.tcx) * J.tcy * J.T;
     jobs[k] = J;

@@ -45,6 +45,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .._ext import native
+from ..utils.flat import grad_out
 
 
 def _stream(t: torch.Tensor) -> int:
@@ -650,6 +651,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         ctx.save_for_backward(x, wt)
         ctx.xamax = amax_of(x) if f32 else None
         ctx.wshape = weight.shape
+        ctx.wparam = weight
         ctx.slot = slot
         ctx.link = link
         return y
@@ -691,7 +693,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             if WgradStream.after and use_side:
                 side = WgradStream.begin(x.device)
-            dw = torch.empty(ctx.wshape, dtype=torch.float32, device=x.device)
+            dw = grad_out(ctx.wparam, ctx.wshape, x.device)
             nws = m.gemm_tn_ws_floats(dev, M, co, ci)
             ws = torch.empty(nws, dtype=torch.float32, device=x.device) if nws else None
             keep = []
@@ -849,7 +851,7 @@ def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None, up=None
     if ctx.needs_input_grad[1]:
         if WgradStream.after and use_side:
             side = WgradStream.begin(x.device)
-        dw = torch.empty((co, c, r, s), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
+        dw = grad_out(getattr(ctx, "wparam", None), (co, c, r, s), x.device, torch.channels_last)
         nws = m.conv_wgrad_ws_floats(dev, nb, h, w, c, co, r, s, stride, pad)
         ws = torch.empty(nws, dtype=torch.float32, device=x.device) if nws else None
         keep = []
@@ -919,6 +921,7 @@ class _ConvFn(torch.autograd.Function):
         ctx.save_for_backward(x, wb, wt, y if relu else None)
         ctx.xamax = amax_of(x) if f32 else None
         ctx.geo = (stride, pad, bias is not None, bool(relu))
+        ctx.wparam = weight
         ctx.link = link
         ctx.up = up if (up is not None and need_dx and stride == 1 and link is None) else None
         ctx.rlink = rlink

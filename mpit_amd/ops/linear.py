@@ -29,6 +29,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .._ext import native
+from ..utils.flat import grad_out
 from .conv import WeightCastPlan, mfma_dtype
 
 
@@ -73,6 +74,7 @@ class _LinearActFn(torch.autograd.Function):
         y = y.to(torch.bfloat16)
         ctx.save_for_backward(xb, wt, y if act else None)
         ctx.flags = (act, bias is not None)
+        ctx.wparam = weight
         return y
 
     @staticmethod
@@ -102,7 +104,7 @@ class _LinearActFn(torch.autograd.Function):
             dx = torch.empty((M, K), dtype=torch.bfloat16, device=dy.device)
             m.gemm_nt(dev, st, M, K, N, dz.data_ptr(), N, wt.data_ptr(), N, dx.data_ptr(), K, 0)
         if ctx.needs_input_grad[1]:  # dW[N, K] = dz^T . x, fp32 straight into the gradient
-            dw = torch.empty((N, K), dtype=torch.float32, device=dy.device)
+            dw = grad_out(ctx.wparam, (N, K), dy.device)
             nws = m.gemm_tn_ws_floats(dev, M, N, K)
             ws = torch.empty(nws, dtype=torch.float32, device=dy.device) if nws else None
             m.gemm_tn(dev, st, M, N, K, dz.data_ptr(), N, xb.data_ptr(), K, dw.data_ptr(),

@@ -10,9 +10,15 @@ Shared (tied) parameters are stored once, as ``getParameters`` does.
 """
 from __future__ import annotations
 
+import weakref
 from typing import List, Optional
 
 import torch
+
+# id(parameter) -> (weakref to it, weakref to its stealing FlatParams, offset): see
+# FlatParams.steal_grads / grad_out (a registry, not an attribute on the Parameter, which would
+# follow it into pickles; keyed by id: tensors compare elementwise, so no WeakKeyDictionary)
+_GSLOTS = {}
 
 
 class FlatParams:
@@ -63,11 +69,25 @@ class FlatParams:
     def steal_grads(self):
         """Switch to "steal" mode: ``.grad`` is left unset so autograd hands over its
         own gradient tensors (no per-parameter ``grad += new`` kernels, no memset);
-        :meth:`stolen` then gathers them in one fused kernel (ops.gather_scale_)."""
-        for p in self.params:
+        :meth:`stolen` then gathers them in one fused kernel (ops.gather_scale_).
+
+        A backward that knows its parameter can write the gradient straight into the flat
+        gradient buffer instead (:func:`grad_out`: the MFMA convolutions' and classifier
+        layers' weight-gradient GEMMs). Autograd then steals that view as ``.grad``, and
+        :meth:`StolenGrads.materialize` skips it. VGG-16's 138 M gradients are otherwise
+        copied once more per step. MPIT_GRAD_INPLACE=0 disables it."""
+        import os
+
+        for p, off in zip(self.params, self.offsets):
             p.grad = None
+            _GSLOTS[id(p)] = (weakref.ref(p), weakref.ref(self), off)
         self._steal = True
+        self.inplace = os.environ.get("MPIT_GRAD_INPLACE", "1") != "0"
         return self
+
+    def grad_view(self, p: torch.Tensor, off: int) -> torch.Tensor:
+        """A fresh view of ``p``'s slot in the flat gradient buffer (laid out like ``p``)."""
+        return self._view(self.grad, p, off)
 
     def stolen(self) -> "StolenGrads":
         return StolenGrads(self)
@@ -97,12 +117,18 @@ class StolenGrads:
     def __init__(self, flat: FlatParams):
         self.flat = flat
 
-    def _table(self):
+    def _table(self, skip_inplace: bool = False):
         srcs, offs, ns = [], [], []
+        self.missing = []
+        gbase = self.flat.grad.data_ptr()
+        es = self.flat.grad.element_size()
         for p, off in zip(self.flat.params, self.flat.offsets):
             g = p.grad
             if g is None:
+                self.missing.append((p, off))
                 continue
+            if skip_inplace and g.data_ptr() == gbase + off * es and g.dtype == self.flat.grad.dtype:
+                continue  # written in place by its backward (grad_out)
             if not g.is_contiguous(memory_format=torch.channels_last if g.dim() == 4 and self.flat.channels_last
                                    else torch.contiguous_format):
                 g = g.contiguous(memory_format=torch.channels_last) if (g.dim() == 4 and self.flat.channels_last) \
@@ -116,19 +142,38 @@ class StolenGrads:
     def gather(self, dst: torch.Tensor, a: float = 1.0, aux: torch.Tensor = None, b: float = 0.0):
         from ..ops.fused import gather_scale_
 
-        srcs, offs, ns = self._table()
-        if len(srcs) < len(self.flat.params):
-            dst.zero_()
+        inplace = dst.data_ptr() == self.flat.grad.data_ptr() and a == 1.0 and (aux is None or b == 0.0)
+        srcs, offs, ns = self._table(skip_inplace=inplace)
+        if self.missing:
+            if inplace:  # (the in-place gradients already sit in dst: zero only the missing slots)
+                for p, off in self.missing:
+                    dst[off: off + p.numel()].zero_()
+            else:
+                dst.zero_()
             if aux is not None and b != 0.0:
                 # parameters without a gradient this step still get the weight-decay term:
                 # the reference adds l2wd*w to the whole dfdx (asyncsgd/optim-downpour.lua:24)
-                for p, off in zip(self.flat.params, self.flat.offsets):
-                    if p.grad is None:
-                        torch.mul(aux[off: off + p.numel()], b, out=dst[off: off + p.numel()])
-        gather_scale_(dst, srcs, offs, ns, a, aux, b)
+                for p, off in self.missing:
+                    torch.mul(aux[off: off + p.numel()], b, out=dst[off: off + p.numel()])
+        if srcs:
+            gather_scale_(dst, srcs, offs, ns, a, aux, b)
         for p in self.flat.params:
             p.grad = None
         return dst
 
     def materialize(self) -> torch.Tensor:
         return self.gather(self.flat.grad, 1.0)
+
+
+def grad_out(param, shape, device, memory_format=torch.contiguous_format) -> torch.Tensor:
+    """Where a backward should write ``param``'s fp32 gradient: its slot in the flat gradient
+    buffer when the parameter belongs to a stealing :class:`FlatParams` (see
+    ``steal_grads``), else a new tensor."""
+    s = _GSLOTS.get(id(param)) if param is not None else None
+    if s is not None and s[0]() is param:
+        flat = s[1]()
+        if flat is not None and getattr(flat, "inplace", False) and flat.grad.dtype == torch.float32:
+            v = flat.grad_view(param, s[2])
+            if tuple(v.shape) == tuple(shape) and v.is_contiguous(memory_format=memory_format):
+                return v
+    return torch.empty(shape, dtype=torch.float32, device=device, memory_format=memory_format)

@@ -324,3 +324,33 @@ def test_side_stream_cu_mask_spread():
         assert len(off) == reserve
         assert all(sum(1 for i in off if i % 8 == x) == reserve // 8 for x in range(8))
         assert all(sum(1 for i in off if i // 32 == b) == reserve // 8 for b in range(8))
+
+
+def test_inplace_grad_slots_skip_the_gather():
+    """utils/flat.py grad_out: a backward writing its gradient straight into the flat
+    gradient slot is not copied again by materialize(); the other gradients are gathered and
+    the slots of parameters without a gradient are zeroed."""
+    import torch.nn as nn
+
+    from mpit_amd.utils.flat import FlatParams, grad_out
+
+    torch.manual_seed(0)
+    m = nn.Sequential(nn.Linear(8, 4), nn.Linear(4, 2))
+    fp = FlatParams(m).steal_grads()
+    w0 = m[0].weight
+    g0 = grad_out(w0, w0.shape, w0.device)
+    assert g0.data_ptr() == fp.grad.data_ptr() + fp.offsets[0] * fp.grad.element_size()
+    assert grad_out(w0, (3, 3), w0.device).data_ptr() != g0.data_ptr()  # shape mismatch: a new tensor
+    fp.grad.fill_(7.0)  # stale contents every slot must lose
+    g0.fill_(3.0)
+    w0.grad = g0  # as autograd steals it
+    m[0].bias.grad = torch.full((4,), 1.0)
+    m[1].weight.grad = torch.full((2, 4), 2.0)  # m[1].bias: no gradient this step
+    out = fp.stolen().materialize()
+    assert out.data_ptr() == fp.grad.data_ptr()
+    seg = lambda i, p: out[fp.offsets[i]: fp.offsets[i] + p.numel()]  # noqa: E731
+    assert torch.equal(seg(0, w0), torch.full((32,), 3.0))
+    assert torch.equal(seg(1, m[0].bias), torch.full((4,), 1.0))
+    assert torch.equal(seg(2, m[1].weight), torch.full((8,), 2.0))
+    assert torch.equal(seg(3, m[1].bias), torch.zeros(2))
+    assert all(p.grad is None for p in m.parameters())

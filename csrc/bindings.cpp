@@ -23,7 +23,7 @@ py::tuple st_tuple(const Status& s) { return py::make_tuple(s.source, s.tag, s.e
 static void apply_sfold(BnRed& r, const py::object& f) {
   if (f.is_none()) return;
   auto t = f.cast<py::tuple>();
-  if (t.size() != 11) throw std::invalid_argument("bn fold: 11 fields");
+  if (t.size() != 11 && t.size() != 12) throw std::invalid_argument("bn fold: 11 or 12 fields");
   r.scoef = t[0].cast<uintptr_t>();
   r.sgamma = t[1].cast<uintptr_t>();
   r.sbeta = t[2].cast<uintptr_t>();
@@ -35,6 +35,7 @@ static void apply_sfold(BnRed& r, const py::object& f) {
   r.szero = t[8].cast<uintptr_t>();
   r.seps = t[9].cast<float>();
   r.smom = t[10].cast<float>();
+  if (t.size() == 12) r.ftag = t[11].cast<int>();  // tagged partials (gemm.hip stats_fold)
 }
 
 PYBIND11_MODULE(_mpit, m) {
@@ -157,11 +158,12 @@ PYBIND11_MODULE(_mpit, m) {
          uintptr_t red_mask, uintptr_t red_mean, int64_t red_row0, uintptr_t red_part2, uintptr_t red_x2,
          uintptr_t red_mean2, bool f32, uintptr_t fold_coef, uintptr_t fold_gamma, uintptr_t fold_rstd,
          uintptr_t fold_dgamma, uintptr_t fold_dbeta, uintptr_t fold_lvl, int64_t bps, uintptr_t amax_a,
-         uintptr_t amax_b, uintptr_t fold_zero, py::object bn_fold) {
+         uintptr_t amax_b, uintptr_t fold_zero, py::object bn_fold, bool fold_tag) {
         BnRed r{red_part, red_x, red_mask, red_mean, red_row0, red_part2, red_x2, red_mean2};
         r.fcoef = fold_coef; r.fgamma = fold_gamma; r.frstd = fold_rstd;
         r.fdgamma = fold_dgamma; r.fdbeta = fold_dbeta; r.flvl = fold_lvl; r.fzero = fold_zero;
         r.amax_a = amax_a; r.amax_b = amax_b;
+        r.ftag = fold_tag ? 1 : 0;
         apply_sfold(r, bn_fold);
         gemm_nt(dev, S(s), M, N, K, A, lda, B, ldb, C, ldc, stats, cin, cmask, &r, f32, bps);
       },
@@ -172,7 +174,7 @@ PYBIND11_MODULE(_mpit, m) {
       py::arg("red_mean2") = 0, py::arg("f32") = false, py::arg("fold_coef") = 0, py::arg("fold_gamma") = 0,
       py::arg("fold_rstd") = 0, py::arg("fold_dgamma") = 0, py::arg("fold_dbeta") = 0, py::arg("fold_lvl") = 0,
       py::arg("bps") = 0, py::arg("amax_a") = 0, py::arg("amax_b") = 0, py::arg("fold_zero") = 0,
-      py::arg("bn_fold") = py::none());
+      py::arg("bn_fold") = py::none(), py::arg("fold_tag") = false);
   m.def("gemm_nt_fold_lvl_floats", &gemm_nt_fold_lvl_floats);
   m.def("bound_floats", [] { return kBoundFloats; });
   m.def("gemm_tn_supported", &gemm_tn_supported);
@@ -237,12 +239,14 @@ PYBIND11_MODULE(_mpit, m) {
          uintptr_t red_x, uintptr_t red_mask, uintptr_t red_mean, int64_t red_row0, uintptr_t red_part2,
          uintptr_t red_x2, uintptr_t red_mean2, bool f32, uintptr_t fold_coef, uintptr_t fold_gamma,
          uintptr_t fold_rstd, uintptr_t fold_dgamma, uintptr_t fold_dbeta, uintptr_t fold_lvl, int64_t bps,
-         uintptr_t amax_a, uintptr_t amax_b, uintptr_t fold_zero, py::object bn_fold, bool red_relu) {
+         uintptr_t amax_a, uintptr_t amax_b, uintptr_t fold_zero, py::object bn_fold, bool red_relu,
+         bool fold_tag) {
         BnRed r{red_part, red_x, red_mask, red_mean, red_row0, red_part2, red_x2, red_mean2};
         r.fcoef = fold_coef; r.fgamma = fold_gamma; r.frstd = fold_rstd;
         r.fdgamma = fold_dgamma; r.fdbeta = fold_dbeta; r.flvl = fold_lvl; r.fzero = fold_zero;
         r.amax_a = amax_a; r.amax_b = amax_b;
         r.relu_y = red_relu ? 1 : 0;
+        r.ftag = fold_tag ? 1 : 0;
         apply_sfold(r, bn_fold);
         conv_fwd(dev, S(s), Nb, H, W, C, Co, R, S_, stride, pad, x, w, y, stats, cin, bias, relu, &r, f32, bps);
       },
@@ -253,7 +257,8 @@ PYBIND11_MODULE(_mpit, m) {
       py::arg("red_part2") = 0, py::arg("red_x2") = 0, py::arg("red_mean2") = 0, py::arg("f32") = false,
       py::arg("fold_coef") = 0, py::arg("fold_gamma") = 0, py::arg("fold_rstd") = 0, py::arg("fold_dgamma") = 0,
       py::arg("fold_dbeta") = 0, py::arg("fold_lvl") = 0, py::arg("bps") = 0, py::arg("amax_a") = 0,
-      py::arg("amax_b") = 0, py::arg("fold_zero") = 0, py::arg("bn_fold") = py::none(), py::arg("red_relu") = false);
+      py::arg("amax_b") = 0, py::arg("fold_zero") = 0, py::arg("bn_fold") = py::none(), py::arg("red_relu") = false,
+      py::arg("fold_tag") = false);
   m.def("conv_dgrad_strided_wfloats", &conv_dgrad_strided_wfloats);
   m.def(
       "conv_dgrad_strided_weights",

@@ -280,11 +280,34 @@ struct EpiArgs {
   float* smean;
   float* srstd;
   float seps, smom;
+  // tagged fold protocol (fepoch != 0, both folds): the fold ticket is taken before the
+  // block's output stores and every partial value is written as one 8-byte (value, epoch)
+  // store; the folding block spins on the epochs instead of every block draining its own
+  // output stores before its ticket (see stats_fold)
+  uint32_t fepoch;
 };
 
 // write-through (sc1) store: visible to a reader on any XCD without an L2 write-back
 __device__ __forceinline__ void st_wt(float* p, float v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// tagged partials: element i of a [rows][2][N] table of (value, epoch) pairs
+__device__ __forceinline__ void st_tag(float* part, int64_t i, float v, uint32_t epoch) {
+  __hip_atomic_store(reinterpret_cast<uint64_t*>(part) + i, (uint64_t(epoch) << 32) | __float_as_uint(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// the value once its writer's epoch is visible. The writer took its ticket before the folding
+// block took the last one and stores the pair right after its output rows, so the wait is
+// short; it is bounded (~1 s) so that a protocol error shows as wrong statistics, not a hang.
+__device__ __forceinline__ float ld_tag(const float* part, int64_t i, uint32_t epoch) {
+  const uint64_t* p = reinterpret_cast<const uint64_t*>(part) + i;
+  uint64_t v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int spin = 0; uint32_t(v >> 32) != epoch && spin < (1 << 20); ++spin) {
+    __builtin_amdgcn_s_sleep(2);
+    v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return __uint_as_float(uint32_t(v));
 }
 
 // source line for padding taps: LDS DMA of zeros (any chunk of a 256-B row, either type)
@@ -372,8 +395,17 @@ constexpr int kFoldMax = 8192;
 constexpr int kFoldMaxGroups = 128;
 __device__ uint32_t g_fold_tickets[kFoldSlots * kFoldMax];
 
+// this block's level-1 fold ticket: per (column tile, group of fgroup M-tiles)
+template <int HALVES>
+__device__ __forceinline__ uint32_t* fold_ticket(const EpiArgs& ep, int64_t M, int mt, int nt) {
+  const int64_t mtn = (M + HALVES * 128 - 1) / (HALVES * 128);
+  const int ngr = int((mtn + ep.fgroup - 1) / ep.fgroup);
+  return ep.ftick + size_t(nt) * size_t(ngr + 1) + mt / ep.fgroup;
+}
+
 template <int BN, int HALVES>
-__device__ __forceinline__ void bnred_fold(const EpiArgs& ep, void* smem, int64_t M, int N, int mt, int nt, int n0) {
+__device__ __forceinline__ void bnred_fold(const EpiArgs& ep, void* smem, int64_t M, int N, int mt, int nt, int n0,
+                                           uint32_t ftk) {
   constexpr int NT = 256, L = NT / BN;  // lanes per column
   const int t = threadIdx.x, cl = t % BN, kl = t / BN;
   const int64_t mtn = (M + HALVES * 128 - 1) / (HALVES * 128);
@@ -384,20 +416,32 @@ __device__ __forceinline__ void bnred_fold(const EpiArgs& ep, void* smem, int64_
   uint32_t* tk = ep.ftick + size_t(nt) * size_t(ngr + 1);
   uint32_t* flag = reinterpret_cast<uint32_t*>(smem);
   double* sd = reinterpret_cast<double*>(smem) + 2;  // [2][L][BN]
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();  // every partial store of this block issued and retired; LDS reads done
-  if (t == 0) flag[0] = atomicAdd(&tk[grp], 1u);
-  __syncthreads();
-  if (flag[0] != uint32_t(gsz - 1)) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  const uint32_t ep_tag = ep.fepoch;
+  if (ep_tag) {  // tagged: the ticket was taken before the output stores (ftk, block-uniform)
+    if (ftk != uint32_t(gsz - 1)) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __syncthreads();  // (LDS: phase B's reduction table is read; sd reuses it)
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // every partial store of this block issued and retired; LDS reads done
+    if (t == 0) flag[0] = atomicAdd(&tk[grp], 1u);
+    __syncthreads();
+    if (flag[0] != uint32_t(gsz - 1)) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   const int64_t nparts = (M + 127) / 128;
   const int64_t r0 = int64_t(grp) * fg * HALVES, r1 = min(nparts, r0 + int64_t(gsz) * HALVES);
   double a = 0, b = 0;
   for (int64_t r = r0 + kl; r < r1; r += L) {
-    a += double(ep.part[(r * 2) * N + n0 + cl]);
-    b += double(ep.part[(r * 2 + 1) * N + n0 + cl]);
+    if (ep_tag) {
+      a += double(ld_tag(ep.part, (r * 2) * N + n0 + cl, ep_tag));
+      b += double(ld_tag(ep.part, (r * 2 + 1) * N + n0 + cl, ep_tag));
+    } else {
+      a += double(ep.part[(r * 2) * N + n0 + cl]);
+      b += double(ep.part[(r * 2 + 1) * N + n0 + cl]);
+    }
   }
   sd[kl * BN + cl] = a;
   sd[(L + kl) * BN + cl] = b;
@@ -458,7 +502,8 @@ __device__ __forceinline__ void bnred_fold(const EpiArgs& ep, void* smem, int64_
 // save_mean / save_rstd, the running statistics (unbiased variance, momentum), and zeroes
 // the BN output's fp16x3 bound. Deterministic (fixed orders); the hand-off is bnred_fold's.
 template <int BN, int HALVES>
-__device__ __forceinline__ void stats_fold(const EpiArgs& ep, void* smem, int64_t M, int N, int mt, int nt, int n0) {
+__device__ __forceinline__ void stats_fold(const EpiArgs& ep, void* smem, int64_t M, int N, int mt, int nt, int n0,
+                                           uint32_t ftk) {
   constexpr int NT = 256, L = NT / BN;
   const int t = threadIdx.x, cl = t % BN, kl = t / BN;
   const int64_t mtn = (M + HALVES * 128 - 1) / (HALVES * 128);
@@ -469,24 +514,34 @@ __device__ __forceinline__ void stats_fold(const EpiArgs& ep, void* smem, int64_
   uint32_t* tk = ep.ftick + size_t(nt) * size_t(ngr + 1);
   uint32_t* flag = reinterpret_cast<uint32_t*>(smem);
   double* sd = reinterpret_cast<double*>(smem) + 2;  // [3][L][BN]
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();  // every partial store of this block issued and retired; LDS reads done
-  if (t == 0) flag[0] = atomicAdd(&tk[grp], 1u);
-  __syncthreads();
-  if (flag[0] != uint32_t(gsz - 1)) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  const uint32_t ep_tag = ep.fepoch;
+  if (ep_tag) {  // tagged: the ticket was taken before the output stores (ftk, block-uniform)
+    if (ftk != uint32_t(gsz - 1)) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __syncthreads();  // (LDS: phase B's reduction table is read; sd reuses it)
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // every partial store of this block issued and retired; LDS reads done
+    if (t == 0) flag[0] = atomicAdd(&tk[grp], 1u);
+    __syncthreads();
+    if (flag[0] != uint32_t(gsz - 1)) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  auto pv = [&](int64_t i) -> double {
+    return ep_tag ? double(ld_tag(ep.part, i, ep_tag)) : double(ep.part[i]);
+  };
   const int64_t nparts = (M + 127) / 128;
   const int64_t r0 = int64_t(grp) * fg * HALVES, r1 = min(nparts, r0 + int64_t(gsz) * HALVES);
   const int c = n0 + cl;
-  const double kg = ep.part[(r0 * 2) * N + c];  // the group's shift: its first row's mean
+  const double kg = pv((r0 * 2) * N + c);  // the group's shift: its first row's mean
   double a = 0, b = 0;
   for (int64_t r = r0 + kl; r < r1; r += L) {
     const double nk = double(min<int64_t>(128, M - r * 128));
-    const double d = double(ep.part[(r * 2) * N + c]) - kg;
+    const double d = pv((r * 2) * N + c) - kg;
     a = fma(nk, d, a);
-    b += double(ep.part[(r * 2 + 1) * N + c]) + nk * d * d;
+    b += pv((r * 2 + 1) * N + c) + nk * d * d;
   }
   sd[kl * BN + cl] = a;
   sd[(L + kl) * BN + cl] = b;
@@ -513,7 +568,7 @@ __device__ __forceinline__ void stats_fold(const EpiArgs& ep, void* smem, int64_
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  const double k0 = ep.part[c];  // tile 0's mean
+  const double k0 = pv(c);  // tile 0's mean
   a = b = 0;
   for (int g = kl; g < ngr; g += L) {
     const int64_t g0 = int64_t(g) * fg * HALVES, g1 = min(nparts, g0 + int64_t(fg) * HALVES);
@@ -1043,6 +1098,14 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
   // 16-B chunk index is XOR-swizzled by the row so phase A's column writes spread over banks
   constexpr int LDT = BN, CPRS = BN / EPC;
   auto tsw = [](int row, int n) { return row * LDT + (((n / EPC) ^ (row % CPRS)) * EPC) + (n % EPC); };
+  // tagged BN fold (ep.fepoch): the fold ticket is taken now, before any output store, so
+  // its return does not queue behind them (vmcnt retires in issue order)
+  [[maybe_unused]] uint32_t ftk = 0;
+  __shared__ uint32_t s_ftk;
+  if constexpr (EPI == EPI_STATS || EPI == EPI_BNRED) {
+    if (ep.fepoch && (EPI == EPI_STATS ? ep.scoef != nullptr : ep.fcoef != nullptr) && t == 0)
+      ftk = atomicAdd(fold_ticket<BM / 128>(ep, M, mt, nt), 1u);
+  }
   T* tl = smem;                // reuses the ring
   __syncthreads();             // every wave is done reading the ring
 #pragma unroll
@@ -1072,6 +1135,9 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
           *reinterpret_cast<uint2*>(tl + tsw(wm * WM + i * 32 + fr, nl)) = make_uint2(lo, hi);
         }
       }
+  if constexpr (EPI == EPI_STATS || EPI == EPI_BNRED) {
+    if (t == 0) s_ftk = ftk;  // (read by the fold after phase B's barriers)
+  }
   __syncthreads();
 
   // ---- phase B: row-major. A thread owns 8 channels (one bf16 / two fp32 16-B chunks) of a
@@ -1264,7 +1330,11 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
           m2 += red[(k * 3 + 2) * BN + n] + d * d * (na * nb / tot);
           na = tot;
         }
-        if (ep.scoef != nullptr) {  // read by the folding blocks (any XCD)
+        if (ep.scoef != nullptr && ep.fepoch) {  // (value, epoch) pairs
+          const int64_t i = (ep.row0 + tile) * 2 * int64_t(N) + n0 + n;
+          st_tag(ep.part, i, mean, ep.fepoch);
+          st_tag(ep.part, i + N, m2, ep.fepoch);
+        } else if (ep.scoef != nullptr) {  // read by the folding blocks (any XCD)
           st_wt(prow + n, mean);
           st_wt(prow + N + n, m2);
         } else {
@@ -1280,6 +1350,10 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
         }
         if constexpr (RELUB) {
           prow[n] = a;  // (the second row is unused)
+        } else if (EPI == EPI_BNRED && ep.fcoef != nullptr && ep.fepoch) {  // (value, epoch) pairs
+          const int64_t i = (ep.row0 + tile) * 2 * int64_t(N) + n0 + n;
+          st_tag(ep.part, i, a, ep.fepoch);
+          st_tag(ep.part, i + N, b, ep.fepoch);
         } else if (EPI == EPI_BNRED && ep.fcoef != nullptr) {  // read by the folding block (any XCD)
           st_wt(prow + n, a);
           st_wt(prow + N + n, b);
@@ -1296,10 +1370,10 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
     }
   }
   if constexpr (EPI == EPI_BNRED) {
-    if (ep.fcoef != nullptr) bnred_fold<BN, HALVES>(ep, smem, M, N, mt, nt, n0);
+    if (ep.fcoef != nullptr) bnred_fold<BN, HALVES>(ep, smem, M, N, mt, nt, n0, s_ftk);
   }
   if constexpr (EPI == EPI_STATS) {
-    if (ep.scoef != nullptr) stats_fold<BN, HALVES>(ep, smem, M, N, mt, nt, n0);
+    if (ep.scoef != nullptr) stats_fold<BN, HALVES>(ep, smem, M, N, mt, nt, n0, s_ftk);
   }
 }
 
@@ -2411,6 +2485,12 @@ static void fold_plan(EpiArgs& ep, int dev, hipStream_t s, int64_t mtn, int ntn)
   }
   ep.ftick = set;
   ep.fgroup = int(fg);
+  if (ep.fepoch) {  // tagged protocol requested: a fresh epoch per launch (never 0)
+    static std::atomic<uint32_t> epochs{0};
+    uint32_t e;
+    do e = epochs.fetch_add(1) + 1; while (e == 0);
+    ep.fepoch = e;
+  }
 }
 
 template <typename T>
@@ -2704,6 +2784,7 @@ static EpiArgs epi_args(uintptr_t stats, const BnRed* r, int* mode) {
       ep.fzero = reinterpret_cast<float*>(r->szero);
       ep.seps = r->seps;
       ep.smom = r->smom;
+      ep.fepoch = r->ftag ? 1u : 0u;  // (the launch assigns the epoch: fold_plan)
     }
   } else if (r && r->part && r->relu_y) {
     if (r->mask || r->mean || r->part2 || r->fcoef) throw std::invalid_argument("gemm_nt: relu_y excludes a BN reduction");
@@ -2726,6 +2807,7 @@ static EpiArgs epi_args(uintptr_t stats, const BnRed* r, int* mode) {
       ep.fdbeta = reinterpret_cast<float*>(r->fdbeta);
       ep.flvl = reinterpret_cast<float*>(r->flvl);
       ep.fzero = reinterpret_cast<float*>(r->fzero);
+      ep.fepoch = r->ftag ? 1u : 0u;
     }
     if (r->part2) {
       if (!r->x2 || !r->mean2) throw std::invalid_argument("gemm_nt: second BN reduction needs x2 and mean2");

@@ -158,6 +158,10 @@ struct BnRed {
   // layer whose output x is this GEMM's input-gradient target: C = A.B^T * (x > 0) is that
   // layer's dz, and part[tile][0][N] its per-tile column sums (its bias gradient, col_sums)
   int relu_y = 0;
+  // ftag: the fold's partials are (value, epoch) pairs (2 x the floats of part) in a buffer
+  // that held only pairs of earlier launches (zeroed once, never garbage): the tagged fold
+  // protocol of gemm.hip, in which no block waits for its own output stores
+  int ftag = 0;
 };
 int64_t gemm_nt_fold_lvl_floats(int N);
 bool gemm_nt_supported(int64_t M, int N, int K, bool f32 = false);

@@ -120,7 +120,7 @@ class BNFold:
     BN output's fp16x3 bound (``amax``) — the BN forward is then its apply pass alone.
     ``args``: the tuple the native GEMM calls take (bindings.cpp apply_sfold)."""
 
-    __slots__ = ("coef", "mean", "rstd", "amax", "args", "_buf")
+    __slots__ = ("coef", "mean", "rstd", "amax", "args", "tagged", "_buf")
 
     def __init__(self, bn: "BatchNormAct2d", C: int, want_amax: bool, device):
         m = native()
@@ -132,9 +132,12 @@ class BNFold:
         self.amax = buf[4 * C + nl:] if want_amax else None
         w = bn.weight if bn.affine else None
         b = bn.bias if bn.affine else None
+        # tagged partials (gemm.hip stats_fold; ops/conv.py tagged_part), unless MPIT_FOLD_TAG=0
+        self.tagged = _conv._FOLD_TAG
         self.args = (self.coef.data_ptr(), w.data_ptr() if w is not None else 0, b.data_ptr() if b is not None else 0,
                      bn.running_mean.data_ptr(), bn.running_var.data_ptr(), self.mean.data_ptr(), self.rstd.data_ptr(),
-                     lvl.data_ptr(), self.amax.data_ptr() if want_amax else 0, float(bn.eps), float(bn.momentum))
+                     lvl.data_ptr(), self.amax.data_ptr() if want_amax else 0, float(bn.eps), float(bn.momentum),
+                     int(self.tagged))
 
 
 def bn_fold_for(bn, C: int, dt, device) -> Optional[BNFold]:

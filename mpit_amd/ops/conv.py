@@ -414,6 +414,24 @@ def cast_transpose(w: torch.Tensor, dtype=torch.bfloat16):
 
 # MPIT_BN_FOLD=0: the BN backward's finalize as its own launch instead of in the GEMM
 _BN_FOLD = os.environ.get("MPIT_BN_FOLD", "1") != "0"
+# MPIT_FOLD_TAG=0: the folds' first protocol (every block drains its own output stores before
+# its ticket) instead of tagged (value, epoch) partials (gemm.hip stats_fold)
+_FOLD_TAG = os.environ.get("MPIT_FOLD_TAG", "1") != "0"
+# id(key tensor) -> (weakref to it, buffer): the tagged partials of one fold site, kept across
+# steps. Zeroed once, then only ever holding (value, epoch) pairs of earlier launches, so a
+# reader can never take stale memory for a fresh pair (torch.empty memory could hold anything)
+_TAG_PARTS = {}
+
+
+def tagged_part(key: torch.Tensor, site: str, nfloats: int, device) -> torch.Tensor:
+    """The persistent tagged-partials buffer of fold site (``key``, ``site``)."""
+    k = (id(key), site)
+    e = _TAG_PARTS.get(k)
+    if e is not None and e[0]() is key and e[1].numel() >= nfloats and e[1].device == device:
+        return e[1]
+    buf = torch.zeros(nfloats, dtype=torch.float32, device=device)
+    _TAG_PARTS[k] = (weakref.ref(key), buf)
+    return buf
 
 
 def _red_args(link, c: int, ntiles: int, device, fold: bool = False):
@@ -423,7 +441,11 @@ def _red_args(link, c: int, ntiles: int, device, fold: bool = False):
     BN): the GEMM's last blocks also run the BN backward's finalize and write its apply
     coefficients, dgamma and dbeta — the separate finalize launch (which in the backward
     waits for CU slots behind the side stream's GEMMs) disappears."""
-    part = torch.empty(ntiles * 2 * c, dtype=torch.float32, device=device)
+    folding = fold and _BN_FOLD and link.rstd is not None and link.x2 is None
+    if folding and _FOLD_TAG and link.w is not None:  # (value, epoch) pairs: twice the floats
+        part = tagged_part(link.w, "bwd", ntiles * 4 * c, device)
+    else:
+        part = torch.empty(ntiles * 2 * c, dtype=torch.float32, device=device)
     kw = dict(red_part=part.data_ptr(), red_x=link.x.data_ptr(),
               red_mask=link.mask.data_ptr() if link.mask is not None else 0, red_mean=link.mean.data_ptr())
     part2 = fb = None
@@ -437,7 +459,8 @@ def _red_args(link, c: int, ntiles: int, device, fold: bool = False):
         amax = buf[5 * c + nl:]  # the BN backward's output bound: zeroed by the fold, raised by its apply
         kw.update(fold_coef=coef.data_ptr(), fold_gamma=link.w.data_ptr() if link.w is not None else 0,
                   fold_rstd=link.rstd.data_ptr(), fold_dgamma=dgamma.data_ptr(), fold_dbeta=dbeta.data_ptr(),
-                  fold_lvl=lvl.data_ptr(), fold_zero=amax.data_ptr())
+                  fold_lvl=lvl.data_ptr(), fold_zero=amax.data_ptr(),
+                  fold_tag=bool(_FOLD_TAG and link.w is not None))
         fb = (coef, dgamma, dbeta, amax)
     return kw, part, part2, fb
 
@@ -491,6 +514,8 @@ def _tile_stats(co: int, M: int, device, hold=None, dt=None):
         from .bn import bn_fold_for
 
         fold = bn_fold_for(hold.bn, co, dt, device)
+    if fold is not None and fold.tagged:  # (value, epoch) pairs, read by the fold only
+        return tagged_part(hold.bn.running_mean, "fwd", nt * 4 * co, device), nt, fold
     return torch.empty(nt * 2 * co, dtype=torch.float32, device=device), nt, fold
 
 

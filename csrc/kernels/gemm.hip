@@ -395,6 +395,32 @@ constexpr int kFoldMax = 8192;
 constexpr int kFoldMaxGroups = 128;
 __device__ uint32_t g_fold_tickets[kFoldSlots * kFoldMax];
 
+// The fold's row loops read one value per row and lane; issued one dependent load at a time
+// they are latency-bound (~1 us each: a folding block held its CU slot for ~100 us, and the
+// level-2 fold is the GEMM's tail). ld_batch issues NB loads (n of them valid) before using
+// any; the callers add the values in the original row order, so the sums are bitwise the
+// one-at-a-time ones. epoch != 0: tagged pairs (ld_tag's spin only for a pair not yet there).
+template <int NB>
+__device__ __forceinline__ void ld_batch(const float* part, const int64_t (&idx)[NB], int n, float (&out)[NB],
+                                         uint32_t epoch) {
+  if (epoch) {
+    uint64_t raw[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u)
+      if (u < n)
+        raw[u] = __hip_atomic_load(reinterpret_cast<const uint64_t*>(part) + idx[u], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int u = 0; u < NB; ++u)
+      if (u < n)
+        out[u] = uint32_t(raw[u] >> 32) == epoch ? __uint_as_float(uint32_t(raw[u])) : ld_tag(part, idx[u], epoch);
+  } else {
+#pragma unroll
+    for (int u = 0; u < NB; ++u)
+      if (u < n) out[u] = part[idx[u]];
+  }
+}
+
 // this block's level-1 fold ticket: per (column tile, group of fgroup M-tiles)
 template <int HALVES>
 __device__ __forceinline__ uint32_t* fold_ticket(const EpiArgs& ep, int64_t M, int mt, int nt) {
@@ -434,14 +460,22 @@ __device__ __forceinline__ void bnred_fold(const EpiArgs& ep, void* smem, int64_
   const int64_t nparts = (M + 127) / 128;
   const int64_t r0 = int64_t(grp) * fg * HALVES, r1 = min(nparts, r0 + int64_t(gsz) * HALVES);
   double a = 0, b = 0;
-  for (int64_t r = r0 + kl; r < r1; r += L) {
-    if (ep_tag) {
-      a += double(ld_tag(ep.part, (r * 2) * N + n0 + cl, ep_tag));
-      b += double(ld_tag(ep.part, (r * 2 + 1) * N + n0 + cl, ep_tag));
-    } else {
-      a += double(ep.part[(r * 2) * N + n0 + cl]);
-      b += double(ep.part[(r * 2 + 1) * N + n0 + cl]);
+  for (int64_t rb = r0 + kl; rb < r1; rb += 8 * L) {
+    const int n = int(min<int64_t>(8, (r1 - rb + L - 1) / L));
+    int64_t ix[16];
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      ix[2 * u] = ((rb + u * L) * 2) * N + n0 + cl;
+      ix[2 * u + 1] = ix[2 * u] + N;
     }
+    ld_batch<16>(ep.part, ix, 2 * n, v, ep_tag);
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (u < n) {
+        a += double(v[2 * u]);
+        b += double(v[2 * u + 1]);
+      }
   }
   sd[kl * BN + cl] = a;
   sd[(L + kl) * BN + cl] = b;
@@ -465,9 +499,22 @@ __device__ __forceinline__ void bnred_fold(const EpiArgs& ep, void* smem, int64_
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   a = b = 0;
-  for (int g = kl; g < ngr; g += L) {
-    a += double(ep.flvl[(int64_t(g) * 2) * N + n0 + cl]);
-    b += double(ep.flvl[(int64_t(g) * 2 + 1) * N + n0 + cl]);
+  for (int gb = kl; gb < ngr; gb += 8 * L) {
+    const int n = min(8, (ngr - gb + L - 1) / L);
+    int64_t ix[16];
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      ix[2 * u] = (int64_t(gb + u * L) * 2) * N + n0 + cl;
+      ix[2 * u + 1] = ix[2 * u] + N;
+    }
+    ld_batch<16>(ep.flvl, ix, 2 * n, v, 0u);
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (u < n) {
+        a += double(v[2 * u]);
+        b += double(v[2 * u + 1]);
+      }
   }
   sd[kl * BN + cl] = a;
   sd[(L + kl) * BN + cl] = b;
@@ -537,11 +584,25 @@ __device__ __forceinline__ void stats_fold(const EpiArgs& ep, void* smem, int64_
   const int c = n0 + cl;
   const double kg = pv((r0 * 2) * N + c);  // the group's shift: its first row's mean
   double a = 0, b = 0;
-  for (int64_t r = r0 + kl; r < r1; r += L) {
-    const double nk = double(min<int64_t>(128, M - r * 128));
-    const double d = pv((r * 2) * N + c) - kg;
-    a = fma(nk, d, a);
-    b += pv((r * 2 + 1) * N + c) + nk * d * d;
+  for (int64_t rb = r0 + kl; rb < r1; rb += 8 * L) {
+    const int n = int(min<int64_t>(8, (r1 - rb + L - 1) / L));
+    int64_t ix[16];
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      ix[2 * u] = ((rb + u * L) * 2) * N + c;
+      ix[2 * u + 1] = ix[2 * u] + N;
+    }
+    ld_batch<16>(ep.part, ix, 2 * n, v, ep_tag);
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (u < n) {
+        const int64_t r = rb + u * L;
+        const double nk = double(min<int64_t>(128, M - r * 128));
+        const double d = double(v[2 * u]) - kg;
+        a = fma(nk, d, a);
+        b += double(v[2 * u + 1]) + nk * d * d;
+      }
   }
   sd[kl * BN + cl] = a;
   sd[(L + kl) * BN + cl] = b;
@@ -570,12 +631,27 @@ __device__ __forceinline__ void stats_fold(const EpiArgs& ep, void* smem, int64_
   __syncthreads();
   const double k0 = pv(c);  // tile 0's mean
   a = b = 0;
-  for (int g = kl; g < ngr; g += L) {
-    const int64_t g0 = int64_t(g) * fg * HALVES, g1 = min(nparts, g0 + int64_t(fg) * HALVES);
-    const double ng = double(min<int64_t>(M, g1 * 128) - g0 * 128);
-    const double d = double(ep.flvl[(int64_t(g) * 3) * N + c]) + double(ep.flvl[(int64_t(g) * 3 + 1) * N + c]) - k0;
-    a = fma(ng, d, a);
-    b += double(ep.flvl[(int64_t(g) * 3 + 2) * N + c]) + ng * d * d;
+  for (int gb = kl; gb < ngr; gb += 8 * L) {
+    const int n = min(8, (ngr - gb + L - 1) / L);
+    int64_t ix[24];
+    float v[24];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      ix[3 * u] = (int64_t(gb + u * L) * 3) * N + c;
+      ix[3 * u + 1] = ix[3 * u] + N;
+      ix[3 * u + 2] = ix[3 * u] + 2 * N;
+    }
+    ld_batch<24>(ep.flvl, ix, 3 * n, v, 0u);
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (u < n) {
+        const int g = gb + u * L;
+        const int64_t g0 = int64_t(g) * fg * HALVES, g1 = min(nparts, g0 + int64_t(fg) * HALVES);
+        const double ng = double(min<int64_t>(M, g1 * 128) - g0 * 128);
+        const double d = double(v[3 * u]) + double(v[3 * u + 1]) - k0;
+        a = fma(ng, d, a);
+        b += double(v[3 * u + 2]) + ng * d * d;
+      }
   }
   sd[kl * BN + cl] = a;
   sd[(L + kl) * BN + cl] = b;

@@ -1082,6 +1082,8 @@ class WeightCastPlan:
                 if f32 or not w.is_cuda or w.dtype != torch.float32 or not w.is_contiguous():
                     continue
                 co, c = w.shape
+                if co % 64:  # (a padded output layer casts its own transpose: ops/linear.py _wt_of)
+                    continue
                 wt = torch.empty((c, co), dtype=torch.bfloat16, device=w.device)
                 specs.append([4096, w.data_ptr(), 0, wt.data_ptr(), co, c, 1, 1, 1, 0, 0])
                 self.mods.append((mod, w.data_ptr(), (None, wt)))

@@ -37,12 +37,26 @@ def _stream(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
+def _np(n: int) -> int:
+    return (n + 63) // 64 * 64
+
+
 def _wt_of(mod, weight: torch.Tensor) -> torch.Tensor:
-    """wt[K, N] bf16 of this step: the cast plan's, else cast here (one launch)."""
+    """wt[K, Np] bf16 of this step (Np = out_features rounded up to 64): the cast plan's, else
+    cast here. A layer whose out_features is not a multiple of 64 (the 1000-class output
+    layers) keeps a zero-padded transpose of its own and refreshes its first N columns."""
+    n, k = weight.shape
+    if n % 64:
+        buf = getattr(mod, "_mpit_wt_pad", None)
+        if buf is None or buf.device != weight.device or buf.shape != (k, _np(n)):
+            buf = torch.zeros((k, _np(n)), dtype=torch.bfloat16, device=weight.device)
+            mod._mpit_wt_pad = buf
+        with torch.no_grad():
+            buf[:, :n].copy_(weight.detach().t())
+        return buf
     c = WeightCastPlan.cached(mod, torch.bfloat16)
     if c is not None:
         return c[1]
-    n, k = weight.shape
     wt = torch.empty((k, n), dtype=torch.bfloat16, device=weight.device)
     w = weight.detach()
     if not w.is_contiguous():
@@ -60,13 +74,14 @@ class _LinearActFn(torch.autograd.Function):
         xb = x.to(torch.bfloat16)
         M, K = xb.shape
         N = weight.shape[0]
+        Np = wt.shape[1]  # (N rounded up to 64: the padded columns of wt are zero)
         xt = xb.t().contiguous()  # [K, M]: the reduction runs over the rows of wt and x^T
-        yt = torch.empty((N, M), dtype=torch.float32, device=x.device)
-        nws = m.gemm_tn_ws_floats(dev, K, N, M)
+        yt = torch.empty((Np, M), dtype=torch.float32, device=x.device)
+        nws = m.gemm_tn_ws_floats(dev, K, Np, M)
         ws = torch.empty(nws, dtype=torch.float32, device=x.device) if nws else None
-        m.gemm_tn(dev, st, K, N, M, wt.data_ptr(), N, xt.data_ptr(), M, yt.data_ptr(),
+        m.gemm_tn(dev, st, K, Np, M, wt.data_ptr(), Np, xt.data_ptr(), M, yt.data_ptr(),
                   ws.data_ptr() if ws is not None else 0, 0.0, f32=False)
-        y = yt.t().contiguous()  # [M, N] row-major (1 MB at VGG's shapes)
+        y = yt[:N].t().contiguous()  # [M, N] row-major (1 MB at VGG's shapes)
         if bias is not None:
             y.add_(bias)
         if act:
@@ -75,6 +90,7 @@ class _LinearActFn(torch.autograd.Function):
         ctx.save_for_backward(xb, wt, y if act else None)
         ctx.flags = (act, bias is not None)
         ctx.wparam = weight
+        ctx.n = N
         return y
 
     @staticmethod
@@ -85,7 +101,7 @@ class _LinearActFn(torch.autograd.Function):
         dev = xb.device.index
         st = _stream(xb)
         M, K = xb.shape
-        N = wt.shape[1]
+        N, Np = ctx.n, wt.shape[1]
         dy = dy.to(torch.bfloat16).contiguous()
         want_db = has_bias and ctx.needs_input_grad[2]
         db = None
@@ -100,15 +116,21 @@ class _LinearActFn(torch.autograd.Function):
             if want_db:
                 db = dz.float().sum(0)
         dx = dw = None
+        if Np != N:  # zero-padded columns (their products vanish against wt's zero columns)
+            dzp = torch.zeros((M, Np), dtype=torch.bfloat16, device=dy.device)
+            dzp[:, :N].copy_(dz)
+            dz = dzp
         if ctx.needs_input_grad[0]:  # dx[M, K] = dz[M, N] . W[N, K] = dz . wt^T
             dx = torch.empty((M, K), dtype=torch.bfloat16, device=dy.device)
-            m.gemm_nt(dev, st, M, K, N, dz.data_ptr(), N, wt.data_ptr(), N, dx.data_ptr(), K, 0)
+            m.gemm_nt(dev, st, M, K, Np, dz.data_ptr(), Np, wt.data_ptr(), Np, dx.data_ptr(), K, 0)
         if ctx.needs_input_grad[1]:  # dW[N, K] = dz^T . x, fp32 straight into the gradient
-            dw = grad_out(ctx.wparam, (N, K), dy.device)
-            nws = m.gemm_tn_ws_floats(dev, M, N, K)
+            full = grad_out(ctx.wparam, (N, K), dy.device) if Np == N else torch.empty(
+                (Np, K), dtype=torch.float32, device=dy.device)
+            nws = m.gemm_tn_ws_floats(dev, M, Np, K)
             ws = torch.empty(nws, dtype=torch.float32, device=dy.device) if nws else None
-            m.gemm_tn(dev, st, M, N, K, dz.data_ptr(), N, xb.data_ptr(), K, dw.data_ptr(),
+            m.gemm_tn(dev, st, M, Np, K, dz.data_ptr(), Np, xb.data_ptr(), K, full.data_ptr(),
                       ws.data_ptr() if ws is not None else 0, 0.0, f32=False)
+            dw = full[:N]
         return dx, dw, db, None, None
 
 
@@ -119,15 +141,18 @@ class LinearAct(nn.Linear):
     _mpit_linear = True  # (ops.conv.WeightCastPlan: cast with the model's convolutions)
     enabled = os.environ.get("MPIT_LINEAR_FUSE", "1") != "0"
 
-    def __init__(self, in_features: int, out_features: int, bias: bool = True, act: bool = True):
+    def __init__(self, in_features: int, out_features: int, bias: bool = True, act: bool = True,
+                 pad_out: bool = False):
         super().__init__(in_features, out_features, bias=bias)
         self.act = act
+        # out_features not a multiple of 64 (a 1000-class output layer): run the GEMMs on N
+        # padded to 64 with zero columns (its transpose then is cast here, not by the plan)
+        self.pad_out = pad_out
 
     def fused(self, x: torch.Tensor) -> bool:
         return (LinearAct.enabled and x.is_cuda and x.dim() == 2 and mfma_dtype(x) == torch.bfloat16
-                and self.in_features % 64 == 0
-                and self.out_features % 64 == 0 and x.shape[0] % 64 == 0 and self.weight.dtype == torch.float32
-                and self.weight.is_contiguous())
+                and self.in_features % 64 == 0 and (self.out_features % 64 == 0 or self.pad_out)
+                and x.shape[0] % 64 == 0 and self.weight.dtype == torch.float32 and self.weight.is_contiguous())
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.fused(x):

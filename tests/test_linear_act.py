@@ -19,12 +19,12 @@ def test_linear_act_cpu_fallback():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("act", [True, False])
-@pytest.mark.parametrize("M,K,N", [(64, 25088, 4096), (128, 1024, 512), (64, 4096, 4096)])
+@pytest.mark.parametrize("M,K,N", [(64, 25088, 4096), (128, 1024, 512), (64, 4096, 4096), (256, 2048, 1000)])
 def test_linear_act_bf16(act, M, K, N):
     from mpit_amd.ops.linear import LinearAct
 
     torch.manual_seed(0)
-    lin = LinearAct(K, N, act=act).cuda()
+    lin = LinearAct(K, N, act=act, pad_out=N % 64 != 0).cuda()
     with torch.no_grad():
         lin.bias.uniform_(-0.1, 0.1)
     x = torch.randn(M, K, device="cuda").requires_grad_(True)

@@ -274,3 +274,51 @@ def test_folded_bn_forward_finalize_matches_separate_launch(dtype):
         assert torch.isfinite(r_fold[k]).all(), k
         tol = 2e-5 if dtype == torch.float32 else (1e-3 if "running" in k else 5e-2)
         assert _rel(r_fold[k], r_sep[k]) < tol, (k, _rel(r_fold[k], r_sep[k]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_tagged_fold_protocol_is_bitwise_the_ticket_protocol(dtype):
+    """The tagged fold protocol (ops/conv.py _FOLD_TAG: fold ticket before the output stores,
+    (value, epoch) partials in persistent buffers) against the first one (every block drains
+    its own stores, then takes its ticket): the same sums in the same order, so the outputs,
+    running statistics and every gradient are bitwise equal, for both folds at once, over
+    three steps (the persistent buffers then hold an earlier epoch's pairs)."""
+    from mpit_amd.ops import bn as bnmod
+    from mpit_amd.ops import conv as convmod
+
+    torch.manual_seed(17)
+    down = torch.nn.Sequential(conv1x1(256, 512, 2), BatchNormAct2d(512, act=False))
+    net = torch.nn.Sequential(Bottleneck(256, 128, 2, down), Bottleneck(512, 128)).cuda()
+    net = net.to(memory_format=torch.channels_last)
+    x = torch.randn(16, 256, 56, 56, device="cuda").contiguous(memory_format=torch.channels_last)
+    g = torch.randn(16, 512, 28, 28, device="cuda").contiguous(memory_format=torch.channels_last)
+    state0 = {k: v.clone() for k, v in net.state_dict().items()}
+
+    def run(tag):
+        saved = (bnmod._FWD_FOLD, convmod._BN_FOLD, convmod._FOLD_TAG)
+        bnmod._FWD_FOLD, convmod._BN_FOLD, convmod._FOLD_TAG = True, True, tag
+        try:
+            net.load_state_dict(state0)
+            outs = []
+            for _ in range(3):
+                f0, b0 = bnmod.COUNTERS["fwd_folded"], bnmod.COUNTERS["bwd_folded"]
+                xi = x.clone().to(dtype).requires_grad_(True)
+                with torch.autocast("cuda", dtype=torch.bfloat16, enabled=dtype == torch.bfloat16):
+                    y = net(xi)
+                y.backward(g.to(y.dtype))
+                torch.cuda.synchronize()
+                assert bnmod.COUNTERS["fwd_folded"] > f0 and bnmod.COUNTERS["bwd_folded"] > b0
+                out = {n: p.grad.detach().clone() for n, p in net.named_parameters()}
+                out.update({"y": y.detach().clone(), "x": xi.grad.detach().clone()})
+                out.update({k: v.clone() for k, v in net.state_dict().items() if "running" in k})
+                net.zero_grad(set_to_none=True)
+                outs.append(out)
+            return outs
+        finally:
+            bnmod._FWD_FOLD, convmod._BN_FOLD, convmod._FOLD_TAG = saved
+
+    first, tagged = run(False), run(True)
+    for step, (a, b) in enumerate(zip(first, tagged)):
+        for k in a:
+            assert torch.equal(a[k], b[k]), (step, k)

@@ -3100,11 +3100,12 @@ static void launch_tn_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
     if (stages == 2) MPIT_TN_LAUNCH1(A, B, 2); \
     else MPIT_TN_LAUNCH1(A, B, 4);         \
   } while (0)
-  // MPIT_TN_KROWS=64 (A/B, bf16): 64-row staged steps on a 2-deep ring (MPIT_TN_KR_STAGES=3:
-  // 3-deep) — the LDS of the default 4 x 32-row ring
+  // bf16: 64-row staged steps on a 2-deep ring (MPIT_TN_KR_STAGES=3: 3-deep) — the LDS of a
+  // 4 x 32-row ring, half its barriers per row. Default since r05o: VGG-16 bf16 5,557 vs 5,480
+  // img/s, ResNet-50 bf16 11,674 vs 11,596 (r05d). MPIT_TN_KROWS=32: the 4 x 32-row ring
   static const int kr64_stages = [] {
     const char* e = std::getenv("MPIT_TN_KROWS");
-    if (!(e && std::atoi(e) == 64)) return 0;
+    if (e && std::atoi(e) == 32) return 0;
     const char* st = std::getenv("MPIT_TN_KR_STAGES");
     return st && std::atoi(st) == 3 ? 3 : 2;
   }();

@@ -70,7 +70,8 @@ class AlexNet(nn.Module):
         # layer indices, so state_dict keys are those of the nn.Linear / nn.ReLU layout)
         self.classifier = nn.Sequential(
             nn.Dropout(dropout), LinearAct(256 * 36, 4096), nn.Identity(),
-            nn.Dropout(dropout), LinearAct(4096, 4096), nn.Identity(), nn.Linear(4096, num_classes),
+            nn.Dropout(dropout), LinearAct(4096, 4096), nn.Identity(),
+            LinearAct(4096, num_classes, act=False, pad_out=True),
         )
 
     def forward(self, x):
@@ -102,7 +103,8 @@ class VGG(nn.Module):
         self.avgpool = nn.AdaptiveAvgPool2d((7, 7))
         self.classifier = nn.Sequential(
             LinearAct(512 * 49, 4096), nn.Identity(), nn.Dropout(dropout),
-            LinearAct(4096, 4096), nn.Identity(), nn.Dropout(dropout), nn.Linear(4096, num_classes),
+            LinearAct(4096, 4096), nn.Identity(), nn.Dropout(dropout),
+            LinearAct(4096, num_classes, act=False, pad_out=True),
         )
 
     def forward(self, x):

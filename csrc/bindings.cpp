@@ -223,6 +223,13 @@ PYBIND11_MODULE(_mpit, m) {
       py::arg("stride"), py::arg("pad"), py::arg("dy"), py::arg("idx"), py::arg("dx"), py::arg("f32") = false,
       py::arg("ypool") = 0, py::arg("db") = 0, py::arg("ws") = 0);
   m.def("maxpool_bwd_ws_floats", &maxpool_bwd_ws_floats);
+  m.def(
+      "avgpool_bwd",
+      [](int dev, uintptr_t s, int N, int HW, int C, uintptr_t dy, uintptr_t dx, bool f32) {
+        avgpool_bwd(dev, S(s), N, HW, C, dy, dx, f32);
+      },
+      py::arg("dev"), py::arg("stream"), py::arg("N"), py::arg("HW"), py::arg("C"), py::arg("dy"), py::arg("dx"),
+      py::arg("f32") = false);
   m.def("col_sums_ws_floats", &col_sums_ws_floats);
   m.def(
       "col_sums",

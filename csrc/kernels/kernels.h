@@ -258,5 +258,7 @@ void maxpool_bwd(int dev, hipStream_t s, int N, int H, int W, int C, int K, int 
                  uintptr_t idx, uintptr_t dx, bool f32 = false, uintptr_t ypool = 0, uintptr_t db = 0,
                  uintptr_t ws = 0);
 int64_t maxpool_bwd_ws_floats(int C);
+// global average pool backward over NHWC: dx[n][p][c] = dy[n][c] / HW (bf16 / fp32)
+void avgpool_bwd(int dev, hipStream_t s, int N, int HW, int C, uintptr_t dy, uintptr_t dx, bool f32 = false);
 
 }  // namespace mpit

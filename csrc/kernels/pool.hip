@@ -253,6 +253,25 @@ __global__ __launch_bounds__(256) void maxpool_bwd_part_kernel(const T* __restri
   }
 }
 
+// Backward of a global average pool over an NHWC image: dx[n, p, c] = dy[n, c] / HW, one thread
+// per 8 channels of one pixel (16-B bf16 / 32-B fp32 writes). PyTorch's expand + copy into the
+// channels_last gradient ran at ~1 TB/s (~80-100 us per ResNet-50 step).
+template <typename T>
+__global__ __launch_bounds__(256) void avgpool_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, int64_t total,
+                                                          int HW, int C, float inv) {
+  const int64_t cv = C / 8;
+  for (int64_t t = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; t < total; t += int64_t(gridDim.x) * blockDim.x) {
+    const int c8 = int(t % cv);
+    const int64_t pix = t / cv;
+    const int64_t n = pix / HW;
+    float v[8];
+    ld8(dy + n * C + c8 * 8, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] *= inv;
+    st8(dx + pix * C + c8 * 8, v);
+  }
+}
+
 PoolGeo pool_geo(int N, int H, int W, int C, int K, int stride, int pad) {
   if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 8 || K <= 0 || K > 15 || stride <= 0 || pad < 0 || 2 * pad > K)
     throw std::invalid_argument("maxpool: unsupported geometry (C % 8 == 0, K <= 15, pad <= K/2)");
@@ -316,6 +335,21 @@ void maxpool_bwd_t(int dev, hipStream_t s, int N, int H, int W, int C, int K, in
 }
 
 int64_t maxpool_bwd_ws_floats(int C) { return int64_t(kPoolRbBlocks) * C + col_sums_ws_floats(C); }
+
+void avgpool_bwd(int dev, hipStream_t s, int N, int HW, int C, uintptr_t dy, uintptr_t dx, bool f32) {
+  if (N <= 0 || HW <= 0 || C <= 0 || C % 8) throw std::invalid_argument("avgpool_bwd: need C % 8 == 0");
+  if ((dy | dx) % 16) throw std::invalid_argument("avgpool_bwd: misaligned buffers");
+  hip_check(hipSetDevice(dev), "hipSetDevice");
+  const int64_t total = int64_t(N) * HW * (C / 8);
+  const float inv = 1.f / float(HW);
+  if (f32)
+    hipLaunchKernelGGL(avgpool_bwd_kernel<float>, dim3(grid_for(total)), dim3(256), 0, s,
+                       reinterpret_cast<const float*>(dy), reinterpret_cast<float*>(dx), total, HW, C, inv);
+  else
+    hipLaunchKernelGGL(avgpool_bwd_kernel<uint16_t>, dim3(grid_for(total)), dim3(256), 0, s,
+                       reinterpret_cast<const uint16_t*>(dy), reinterpret_cast<uint16_t*>(dx), total, HW, C, inv);
+  hip_check(hipGetLastError(), "avgpool_bwd launch");
+}
 
 void maxpool_fwd(int dev, hipStream_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t x,
                  uintptr_t y, uintptr_t idx, bool f32) {

@@ -21,7 +21,7 @@ import torch.nn as nn
 from ..ops.bn import BatchNormAct2d, bn_pair
 from ..ops.conv import Conv1x1, ConvNHWC, GradSlot, StemConv, feeds_bn, park_grad
 from ..ops.linear import LinearAct
-from ..ops.pool import MaxPool2dNHWC
+from ..ops.pool import GlobalAvgPoolNHWC, MaxPool2dNHWC
 
 # Fused BN(+add)(+ReLU) HIP kernels on MI355X (mpit_amd/ops/bn.py); same parameters and
 # state dict as nn.BatchNorm2d, and plain PyTorch math on CPU tensors.
@@ -161,7 +161,7 @@ class ResNet(nn.Module):
         self.layer2 = self._make(block, 128, layers[1], 2)
         self.layer3 = self._make(block, 256, layers[2], 2)
         self.layer4 = self._make(block, 512, layers[3], 2)
-        self.avgpool = nn.AdaptiveAvgPool2d(1)
+        self.avgpool = GlobalAvgPoolNHWC() if MFMA_CONV else nn.AdaptiveAvgPool2d(1)
         # the classifier on the MFMA kernels in bf16 steps (ops/linear.py; N padded to 64 inside
         # the GEMMs): no hipBLASLt call and no per-step weight / gradient casts. nn.Linear's
         # parameters and state_dict keys; fp32 steps run F.linear

@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from .._ext import native
 from .conv import ReluLink, amax_of, set_amax
@@ -83,4 +84,38 @@ class MaxPool2dNHWC(nn.MaxPool2d):
             if a is not None:  # every output is one of the inputs: the input's bound holds
                 set_amax(y, a)
             return y
+        return super().forward(x)
+
+
+class _GlobalAvgPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.geo = (x.shape, x.dtype)
+        return F.adaptive_avg_pool2d(x, 1)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (n, c, h, w), dt = ctx.geo
+        dy = dy.reshape(n, c).to(dt).contiguous()
+        dx = torch.empty((n, c, h, w), dtype=dt, device=dy.device, memory_format=torch.channels_last)
+        native().avgpool_bwd(dy.device.index, _stream(dy), n, h * w, c, dy.data_ptr(), dx.data_ptr(),
+                             f32=dt == torch.float32)
+        return dx
+
+
+class GlobalAvgPoolNHWC(nn.AdaptiveAvgPool2d):
+    """``nn.AdaptiveAvgPool2d(1)`` whose backward writes the channels_last input gradient in one
+    HIP pass (csrc/kernels/pool.hip ``avgpool_bwd``: dy / HW broadcast over the pixels) instead
+    of PyTorch's expand + copy (~1 TB/s; 80-100 us per ResNet-50 step). Forward unchanged."""
+
+    def __init__(self):
+        super().__init__(1)
+
+    def fused(self, x: torch.Tensor) -> bool:
+        return (x.is_cuda and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float32) and x.shape[1] % 8 == 0
+                and x.is_contiguous(memory_format=torch.channels_last) and torch.is_grad_enabled())
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if self.fused(x):
+            return _GlobalAvgPoolFn.apply(x)
         return super().forward(x)

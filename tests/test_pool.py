@@ -54,3 +54,23 @@ def test_maxpool_partition_backward_matches_gather(dt, monkeypatch):
         y.backward(torch.ones_like(y) * torch.arange(y.numel(), device="cuda").reshape(y.shape).to(dt) / y.numel())
         grads.append(xx.grad.clone())
     assert torch.equal(grads[0], grads[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float32])
+def test_global_avgpool_backward(dt):
+    """GlobalAvgPoolNHWC: PyTorch's forward, the one-pass HIP backward (dy / HW per pixel)."""
+    from mpit_amd.ops.pool import GlobalAvgPoolNHWC
+
+    torch.manual_seed(0)
+    x = torch.randn(4, 256, 7, 7, device="cuda").to(dt).contiguous(memory_format=torch.channels_last)
+    m = GlobalAvgPoolNHWC()
+    x1, x2 = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    assert m.fused(x1)
+    y1, y2 = m(x1), F.adaptive_avg_pool2d(x2, 1)
+    assert torch.equal(y1, y2)
+    g = torch.randn_like(y2)
+    y1.backward(g)
+    y2.backward(g)
+    assert x1.grad.is_contiguous(memory_format=torch.channels_last)
+    assert torch.allclose(x1.grad.float(), x2.grad.float(), rtol=1e-2 if dt == torch.bfloat16 else 1e-6, atol=1e-6)

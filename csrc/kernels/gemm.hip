@@ -351,10 +351,33 @@ __device__ __forceinline__ s16x4 ds_tr16(const uint16_t* p) {
 // which serialises the ring; issued from asm it is invisible to that tracking and the
 // kernel's own counted vmcnt waits order it. m0 carries the wave-uniform LDS base; no
 // other instruction of the kernels using this helper reads m0.
+// (s_nop 0: an SALU write of M0 needs one wait state before an LDS DMA reads it)
 __device__ __forceinline__ void glds16_asm(const void* src, void* lds) {
   const uint32_t l = __builtin_amdgcn_readfirstlane(uint32_t(reinterpret_cast<uintptr_t>((lds_void*)lds)));
-  asm volatile("s_mov_b32 m0, %0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(l), "v"(src) : "memory", "m0");
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(l), "v"(src) : "memory", "m0");
 }
+
+// The same DMA through a buffer descriptor: 16 B per lane from (descriptor base + voff) to
+// LDS byte address lds + 16 * lane. The descriptor is raw (stride 0) with num_records =
+// 2^31, so a lane offset >= 2^31 is out of range and DMAs zeros (padding taps). The base
+// and the LDS address are wave-uniform SGPR values built by SALU arithmetic.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+constexpr uint32_t kBufOob = 0x80000000u;
+__device__ __forceinline__ i32x4 buf_rsrc(uint64_t base) {
+  return i32x4{int(uint32_t(base)), int(uint32_t(base >> 32) & 0xffffu), int(kBufOob), 0x00020000};
+}
+__device__ __forceinline__ void blds16(i32x4 rsrc, uint32_t voff, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rsrc),
+               "s"(lds)
+               : "memory", "m0");
+}
+// MPIT_F11_GLOBAL_DMA (build define, A/B only): FM 11 stages through per-lane 64-bit global
+// addresses (glds16_asm) as before round 5 instead of the buffer descriptors
+#ifdef MPIT_F11_GLOBAL_DMA
+constexpr bool kF11Buf = false;
+#else
+constexpr bool kF11Buf = true;
+#endif
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -787,6 +810,40 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
       pbp[i] = Bh + int64_t(n0 + row) * ldb + c * 8;
     }
   }
+  // FM 11 staging through buffer descriptors (blds16): each lane keeps 32-bit byte offsets
+  // from block-uniform bases — A: the block's first row (plain) or first image (CONV, offsets
+  // re-made once per tap, out-of-range for padding taps); B: the block's first column row of
+  // each plane — and a tile's k offset moves the descriptor base (SALU), so issuing a tile
+  // costs no per-lane 64-bit address arithmetic, no padding branches and no readfirstlane
+  // of the LDS address. The host checks that every offset stays below 2^31.
+  constexpr bool F11B = F32 && FM == 11 && kF11Buf;
+  [[maybe_unused]] uint32_t voa[F11B ? IA : 1], vob[F11B ? IBP : 1];
+  [[maybe_unused]] uint64_t abase = 0, bbase = 0;
+  [[maybe_unused]] uint32_t lds0 = 0;
+  [[maybe_unused]] int ih0 = 0;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  if constexpr (F11B) {
+    lds0 = __builtin_amdgcn_readfirstlane(uint32_t(reinterpret_cast<uintptr_t>((lds_void*)smem)));
+    if constexpr (CONV) {
+      const int64_t img0 = m0 / (int64_t(geo.Ho) * geo.Wo);
+      ih0 = int(img0) * geo.H;
+      abase = reinterpret_cast<uint64_t>(A) + uint64_t(img0 * geo.H * geo.W) * uint64_t(pitch) * 4u;
+    } else {
+      abase = reinterpret_cast<uint64_t>(A) + uint64_t(m0) * uint64_t(lda) * 4u;
+#pragma unroll
+      for (int i = 0; i < IA; ++i) {
+        const int row = (w * IA + i) * RPI + lane / CPK, c = swzk<BKB>(row, lane % CPK);
+        const int64_t gm = min(m0 + row, M - 1);
+        voa[i] = uint32_t(((gm - m0) * lda + c * EPC) * 4);
+      }
+    }
+    bbase = reinterpret_cast<uint64_t>(B) + uint64_t(n0) * uint64_t(ldb) * 2u;
+#pragma unroll
+    for (int i = 0; i < IBP; ++i) {
+      const int row = (w * IBP + i) * 16 + lane / 4, c = swz(row, lane % 4);
+      vob[i] = uint32_t((row * ldb + c * 8) * 2);
+    }
+  }
   // fp32 tiles issue their LDS DMA from inline asm: with the builtin, hipcc cannot tell
   // that the next stage's DMA targets the other ring buffer and drains it (vmcnt(0)) before
   // the first fragment read of the current stage, so the load of stage kt + 1 never
@@ -799,6 +856,36 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
   auto issue = [&](int kt, int buf) {
     T* As = smem + buf * TILE;
     T* Bs = As + BM * BK;
+    if constexpr (F11B) {
+      // (the prologue's descriptors may come straight from a v_readfirstlane: a VALU write of
+      // an SGPR needs 5 wait states before a VMEM instruction reads it)
+      if (kt < STAGES - 1) asm volatile("s_nop 4" ::: "memory");
+      uint64_t ab;
+      if constexpr (CONV) {
+        if (kc == 0) {  // first tile of the tap (kr, ks): this lane's pixel offsets for it
+#pragma unroll
+          for (int i = 0; i < IA; ++i) {
+            const int hi = hi0[i] + kr, wi = wi0[i] + ks;
+            const bool ok = unsigned(hi) < unsigned(geo.H) && unsigned(wi) < unsigned(geo.W);
+            voa[i] = ok ? uint32_t((((img[i] - ih0) + hi) * geo.W + wi) * pitch + ca[i]) * 4u : kBufOob;
+          }
+        }
+        ab = abase + uint64_t(kc) * 4u;
+      } else {
+        ab = abase + uint64_t(kt) * uint64_t(BK * 4);
+      }
+      const i32x4 ra = buf_rsrc(ab);
+      const uint32_t la = lds0 + uint32_t((buf * TILE + wu * IA * RPI * BK) * 4);
+#pragma unroll
+      for (int i = 0; i < IA; ++i) blds16(ra, voa[i], la + uint32_t(i * RPI * BK * 4));
+      const uint32_t lb = lds0 + uint32_t((buf * TILE + BM * BK) * 4 + wu * IBP * 16 * 32 * 2);
+#pragma unroll
+      for (int p = 0; p < NPL; ++p) {
+        const i32x4 rb = buf_rsrc(bbase + (uint64_t(p) * uint64_t(bps) + uint64_t(kt) * 32u) * 2u);
+#pragma unroll
+        for (int i = 0; i < IBP; ++i) blds16(rb, vob[i], lb + uint32_t(p * BN * 32 * 2 + i * 16 * 32 * 2));
+      }
+    } else {
 #pragma unroll
     for (int i = 0; i < IA; ++i) {
       if constexpr (CONV) {
@@ -821,6 +908,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
 #pragma unroll
       for (int i = 0; i < IB; ++i)
         glds(pb[i] + kt * BK, Bs + (w * IB + i) * RPI * BK);
+    }
     }
     if constexpr (CONV) {  // tiles are issued in k order: step to the next (tap, channel) slab
       kc += BK;
@@ -2655,6 +2743,19 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
       if (!ep.amax_a) throw std::invalid_argument("gemm_nt: fp16 B planes need the A operand's amax bound");
       check_ptr(B + uintptr_t(bps) * 2, "B plane 1");
       fm = 11;
+      if (kF11Buf) {  // the buffer-descriptor staging keeps lane offsets below 2^31 bytes
+        const int64_t lim = int64_t(1) << 31;
+        int64_t aspan;
+        if (geo) {
+          const int64_t hw = int64_t(geo->Ho) * geo->Wo;
+          const int64_t imgs = std::min<int64_t>((M + hw - 1) / hw, (256 + hw - 1) / hw + 1);
+          aspan = imgs * geo->H * geo->W * int64_t(geo->pitch ? geo->pitch : geo->C) * 4;
+        } else {
+          aspan = (int64_t(256) * lda + K) * 4;
+        }
+        if (aspan >= lim || (int64_t(256) * ldb + K) * 2 >= lim)
+          throw std::invalid_argument("gemm_nt: fp16x3 operand rows (or images) span >= 2 GiB per block");
+      }
     }
   } else if (ep.amax_b) {
     throw std::invalid_argument("gemm_nt: amax_b is the scale of fp16 B planes (bps > 0)");

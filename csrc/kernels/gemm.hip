@@ -363,20 +363,37 @@ __device__ __forceinline__ void glds16_asm(const void* src, void* lds) {
 // and the LDS address are wave-uniform SGPR values built by SALU arithmetic.
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 constexpr uint32_t kBufOob = 0x80000000u;
-__device__ __forceinline__ i32x4 buf_rsrc(uint64_t base) {
-  return i32x4{int(uint32_t(base)), int(uint32_t(base >> 32) & 0xffffu), int(kBufOob), 0x00020000};
+__device__ __forceinline__ i32x4 buf_rsrc(uint64_t base, uint32_t nrec = kBufOob) {
+  return i32x4{int(uint32_t(base)), int(uint32_t(base >> 32) & 0xffffu), int(nrec), 0x00020000};
 }
 __device__ __forceinline__ void blds16(i32x4 rsrc, uint32_t voff, uint32_t lds) {
   asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rsrc),
                "s"(lds)
                : "memory", "m0");
 }
-// MPIT_F11_GLOBAL_DMA (build define, A/B only): FM 11 stages through per-lane 64-bit global
-// addresses (glds16_asm) as before round 5 instead of the buffer descriptors
-#ifdef MPIT_F11_GLOBAL_DMA
+// For descriptors the compiler cannot prove wave-uniform (gemm_tn's split / step arithmetic):
+// each word through v_readfirstlane (a no-op for SGPR values), and the 5 wait states a VALU
+// write of an SGPR needs before a VMEM instruction reads it
+__device__ __forceinline__ void blds16u(i32x4 rsrc, uint32_t voff, uint32_t lds) {
+  const i32x4 r = {__builtin_amdgcn_readfirstlane(rsrc[0]), __builtin_amdgcn_readfirstlane(rsrc[1]),
+                   __builtin_amdgcn_readfirstlane(rsrc[2]), __builtin_amdgcn_readfirstlane(rsrc[3])};
+  const uint32_t l = __builtin_amdgcn_readfirstlane(lds);
+  asm volatile("s_nop 4\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff),
+               "s"(r), "s"(l)
+               : "memory", "m0");
+}
+// MPIT_GLOBAL_DMA (build define, A/B only): gemm_nt's bf16 and fp16x3 kernels and gemm_tn
+// stage through per-lane 64-bit global addresses as before round 5 instead of the buffer
+// descriptors; MPIT_F11_GLOBAL_DMA only the fp16x3 gemm_nt ones
+#if defined(MPIT_GLOBAL_DMA) || defined(MPIT_F11_GLOBAL_DMA)
 constexpr bool kF11Buf = false;
 #else
 constexpr bool kF11Buf = true;
+#endif
+#ifdef MPIT_GLOBAL_DMA
+constexpr bool kBf16Buf = false, kTnBuf = false;
+#else
+constexpr bool kBf16Buf = true, kTnBuf = true;
 #endif
 
 template <int N>
@@ -810,14 +827,15 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
       pbp[i] = Bh + int64_t(n0 + row) * ldb + c * 8;
     }
   }
-  // FM 11 staging through buffer descriptors (blds16): each lane keeps 32-bit byte offsets
-  // from block-uniform bases — A: the block's first row (plain) or first image (CONV, offsets
-  // re-made once per tap, out-of-range for padding taps); B: the block's first column row of
-  // each plane — and a tile's k offset moves the descriptor base (SALU), so issuing a tile
-  // costs no per-lane 64-bit address arithmetic, no padding branches and no readfirstlane
-  // of the LDS address. The host checks that every offset stays below 2^31.
-  constexpr bool F11B = F32 && FM == 11 && kF11Buf;
-  [[maybe_unused]] uint32_t voa[F11B ? IA : 1], vob[F11B ? IBP : 1];
+  // bf16 and FM 11 staging through buffer descriptors (blds16): each lane keeps 32-bit byte
+  // offsets from block-uniform bases — A: the block's first row (plain) or first image (CONV,
+  // offsets re-made once per tap, out-of-range for padding taps); B: the block's first
+  // column row (of each plane) — and a tile's k offset moves the descriptor base (SALU), so
+  // issuing a tile costs no per-lane 64-bit address arithmetic, no padding branches and no
+  // readfirstlane of the LDS address. The host checks that every offset stays below 2^31.
+  constexpr bool F11B = (F32 && FM == 11 && kF11Buf) || (!F32 && FM == 0 && kBf16Buf);
+  constexpr int NVB = BSPLIT ? IBP : IB;
+  [[maybe_unused]] uint32_t voa[F11B ? IA : 1], vob[F11B ? NVB : 1];
   [[maybe_unused]] uint64_t abase = 0, bbase = 0;
   [[maybe_unused]] uint32_t lds0 = 0;
   [[maybe_unused]] int ih0 = 0;
@@ -827,21 +845,29 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
     if constexpr (CONV) {
       const int64_t img0 = m0 / (int64_t(geo.Ho) * geo.Wo);
       ih0 = int(img0) * geo.H;
-      abase = reinterpret_cast<uint64_t>(A) + uint64_t(img0 * geo.H * geo.W) * uint64_t(pitch) * 4u;
+      abase = reinterpret_cast<uint64_t>(A) + uint64_t(img0 * geo.H * geo.W) * uint64_t(pitch) * sizeof(T);
     } else {
-      abase = reinterpret_cast<uint64_t>(A) + uint64_t(m0) * uint64_t(lda) * 4u;
+      abase = reinterpret_cast<uint64_t>(A) + uint64_t(m0) * uint64_t(lda) * sizeof(T);
 #pragma unroll
       for (int i = 0; i < IA; ++i) {
         const int row = (w * IA + i) * RPI + lane / CPK, c = swzk<BKB>(row, lane % CPK);
         const int64_t gm = min(m0 + row, M - 1);
-        voa[i] = uint32_t(((gm - m0) * lda + c * EPC) * 4);
+        voa[i] = uint32_t(((gm - m0) * lda + c * EPC) * int(sizeof(T)));
       }
     }
-    bbase = reinterpret_cast<uint64_t>(B) + uint64_t(n0) * uint64_t(ldb) * 2u;
+    bbase = reinterpret_cast<uint64_t>(B) + uint64_t(n0) * uint64_t(ldb) * (BSPLIT ? 2u : sizeof(T));
+    if constexpr (BSPLIT) {
 #pragma unroll
-    for (int i = 0; i < IBP; ++i) {
-      const int row = (w * IBP + i) * 16 + lane / 4, c = swz(row, lane % 4);
-      vob[i] = uint32_t((row * ldb + c * 8) * 2);
+      for (int i = 0; i < IBP; ++i) {
+        const int row = (w * IBP + i) * 16 + lane / 4, c = swz(row, lane % 4);
+        vob[i] = uint32_t((row * ldb + c * 8) * 2);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < IB; ++i) {
+        const int row = (w * IB + i) * RPI + lane / CPK, c = swzk<BKB>(row, lane % CPK);
+        vob[i] = uint32_t((row * ldb + c * EPC) * int(sizeof(T)));
+      }
     }
   }
   // fp32 tiles issue their LDS DMA from inline asm: with the builtin, hipcc cannot tell
@@ -857,6 +883,11 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
     T* As = smem + buf * TILE;
     T* Bs = As + BM * BK;
     if constexpr (F11B) {
+      // (fp16x3: the descriptors are provably SGPR values; bf16: not always — blds16u)
+      auto bl = [](i32x4 r, uint32_t v, uint32_t l) {
+        if constexpr (F32) blds16(r, v, l);
+        else blds16u(r, v, l);
+      };
       // (the prologue's descriptors may come straight from a v_readfirstlane: a VALU write of
       // an SGPR needs 5 wait states before a VMEM instruction reads it)
       if (kt < STAGES - 1) asm volatile("s_nop 4" ::: "memory");
@@ -867,23 +898,32 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
           for (int i = 0; i < IA; ++i) {
             const int hi = hi0[i] + kr, wi = wi0[i] + ks;
             const bool ok = unsigned(hi) < unsigned(geo.H) && unsigned(wi) < unsigned(geo.W);
-            voa[i] = ok ? uint32_t((((img[i] - ih0) + hi) * geo.W + wi) * pitch + ca[i]) * 4u : kBufOob;
+            voa[i] = ok ? uint32_t((((img[i] - ih0) + hi) * geo.W + wi) * pitch + ca[i]) * uint32_t(sizeof(T))
+                        : kBufOob;
           }
         }
-        ab = abase + uint64_t(kc) * 4u;
+        ab = abase + uint64_t(kc) * sizeof(T);
       } else {
-        ab = abase + uint64_t(kt) * uint64_t(BK * 4);
+        ab = abase + uint64_t(kt) * uint64_t(BK * sizeof(T));
       }
+      constexpr int TB = int(sizeof(T));
       const i32x4 ra = buf_rsrc(ab);
-      const uint32_t la = lds0 + uint32_t((buf * TILE + wu * IA * RPI * BK) * 4);
+      const uint32_t la = lds0 + uint32_t((buf * TILE + wu * IA * RPI * BK) * TB);
 #pragma unroll
-      for (int i = 0; i < IA; ++i) blds16(ra, voa[i], la + uint32_t(i * RPI * BK * 4));
-      const uint32_t lb = lds0 + uint32_t((buf * TILE + BM * BK) * 4 + wu * IBP * 16 * 32 * 2);
+      for (int i = 0; i < IA; ++i) bl(ra, voa[i], la + uint32_t(i * RPI * BK * TB));
+      if constexpr (BSPLIT) {
+        const uint32_t lb = lds0 + uint32_t((buf * TILE + BM * BK) * TB + wu * IBP * 16 * 32 * 2);
 #pragma unroll
-      for (int p = 0; p < NPL; ++p) {
-        const i32x4 rb = buf_rsrc(bbase + (uint64_t(p) * uint64_t(bps) + uint64_t(kt) * 32u) * 2u);
+        for (int p = 0; p < NPL; ++p) {
+          const i32x4 rb = buf_rsrc(bbase + (uint64_t(p) * uint64_t(bps) + uint64_t(kt) * 32u) * 2u);
 #pragma unroll
-        for (int i = 0; i < IBP; ++i) blds16(rb, vob[i], lb + uint32_t(p * BN * 32 * 2 + i * 16 * 32 * 2));
+          for (int i = 0; i < IBP; ++i) bl(rb, vob[i], lb + uint32_t(p * BN * 32 * 2 + i * 16 * 32 * 2));
+        }
+      } else {
+        const i32x4 rb = buf_rsrc(bbase + uint64_t(kt) * uint64_t(BK * TB));
+        const uint32_t lb = lds0 + uint32_t((buf * TILE + BM * BK + wu * IB * RPI * BK) * TB);
+#pragma unroll
+        for (int i = 0; i < IB; ++i) bl(rb, vob[i], lb + uint32_t(i * RPI * BK * TB));
       }
     } else {
 #pragma unroll
@@ -1698,10 +1738,67 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y
     }
   }
   const int64_t nsteps = r1 > r0 ? (r1 - r0 + kRows - 1) / kRows : 0;
+  // Buffer-descriptor staging (blds16, as gemm_nt): 32-bit lane offsets from uniform bases —
+  // Y and plain X: the step's first row (the base moves per step in SALU; the descriptor
+  // ends at the split's last row, so rows past it read zeros instead of re-reading that
+  // row); CONV X: the split's first image, padding taps and rows past the split out of range.
+  constexpr bool TBUF = kTnBuf;
+  constexpr int TB = int(sizeof(T));
+  [[maybe_unused]] uint32_t voy[TBUF ? IY : 1], vox[TBUF ? IX : 1];
+  [[maybe_unused]] uint32_t lds0 = 0;
+  [[maybe_unused]] uint64_t xbase = 0;
+  [[maybe_unused]] int pn0 = 0;
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  if constexpr (TBUF) {
+    lds0 = __builtin_amdgcn_readfirstlane(uint32_t(reinterpret_cast<uintptr_t>((lds_void*)smem)));
+#pragma unroll
+    for (int i = 0; i < IY; ++i) voy[i] = uint32_t((ry[i] * ldy + tswz<T, CY>(ry[i], lane % CY) * EPC) * TB);
+    if constexpr (CONV) {
+      pn0 = int(r0 / (int64_t(geo.Ho) * geo.Wo));
+      xbase = reinterpret_cast<uint64_t>(X) + uint64_t(int64_t(pn0) * geo.H * geo.W) * uint64_t(pitch) * TB;
+    } else {
+#pragma unroll
+      for (int i = 0; i < IX; ++i) vox[i] = uint32_t((rx[i] * ldx + ox[i]) * TB);
+    }
+  }
   auto issue = [&](int64_t st, int buf) {
     T* Ys = smem + buf * TILE;
     T* Xs = Ys + kRows * TBN;
     const int rs = int(st) * kRows;  // first row of the step, relative to r0
+    if constexpr (TBUF) {
+      // (the prologue's descriptors may come straight from a v_readfirstlane: 5 wait states)
+      if (st < STAGES - 1) asm volatile("s_nop 4" ::: "memory");
+      const int64_t left = int64_t(nrows - rs);
+      const uint32_t ly = lds0 + uint32_t((buf * TILE + wu * IY * RY * TBN) * TB);
+      const i32x4 ry4 = buf_rsrc(reinterpret_cast<uint64_t>(Y) + uint64_t(((r0 + rs) * ldy + n0) * TB),
+                                 uint32_t(min<int64_t>(left * ldy * TB, int64_t(kBufOob))));
+#pragma unroll
+      for (int i = 0; i < IY; ++i) blds16u(ry4, voy[i], ly + uint32_t(i * RY * TBN * TB));
+      const uint32_t lx = lds0 + uint32_t((buf * TILE + kRows * TBN + wu * IX * RX * TBK) * TB);
+      if constexpr (CONV) {
+        const i32x4 rx4 = buf_rsrc(xbase);
+#pragma unroll
+        for (int i = 0; i < IX; ++i) {
+          const int hi = pho[i] * geo.stride - geo.pad + xr[i], wi = pwo[i] * geo.stride - geo.padw + xs[i];
+          const bool ok = rs + rx[i] < nrows && unsigned(hi) < unsigned(geo.H) && unsigned(wi) < unsigned(geo.W);
+          const uint32_t off = uint32_t(((((pn[i] - pn0) * geo.H + hi) * geo.W + wi) * pitch + xc[i]) * TB);
+          blds16u(rx4, ok ? off : kBufOob, lx + uint32_t(i * RX * TBK * TB));
+          pwo[i] += dw;  // next step's rows (issued strictly in order)
+          const int cw = pwo[i] >= geo.Wo;
+          pwo[i] -= cw ? geo.Wo : 0;
+          pho[i] += dh + cw;
+          const int ch = pho[i] >= geo.Ho;
+          pho[i] -= ch ? geo.Ho : 0;
+          pn[i] += dn + ch;
+        }
+      } else {
+        const i32x4 rx4 = buf_rsrc(reinterpret_cast<uint64_t>(X) + uint64_t(((r0 + rs) * ldx + k0) * TB),
+                                   uint32_t(min<int64_t>(left * ldx * TB, int64_t(kBufOob))));
+#pragma unroll
+        for (int i = 0; i < IX; ++i) blds16u(rx4, vox[i], lx + uint32_t(i * RX * TBK * TB));
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < IY; ++i) {
       glds16_asm(rs + ry[i] < nrows ? py[i] : pyl[i], Ys + (w * IY + i) * RY * TBN);
@@ -2743,22 +2840,23 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
       if (!ep.amax_a) throw std::invalid_argument("gemm_nt: fp16 B planes need the A operand's amax bound");
       check_ptr(B + uintptr_t(bps) * 2, "B plane 1");
       fm = 11;
-      if (kF11Buf) {  // the buffer-descriptor staging keeps lane offsets below 2^31 bytes
-        const int64_t lim = int64_t(1) << 31;
-        int64_t aspan;
-        if (geo) {
-          const int64_t hw = int64_t(geo->Ho) * geo->Wo;
-          const int64_t imgs = std::min<int64_t>((M + hw - 1) / hw, (256 + hw - 1) / hw + 1);
-          aspan = imgs * geo->H * geo->W * int64_t(geo->pitch ? geo->pitch : geo->C) * 4;
-        } else {
-          aspan = (int64_t(256) * lda + K) * 4;
-        }
-        if (aspan >= lim || (int64_t(256) * ldb + K) * 2 >= lim)
-          throw std::invalid_argument("gemm_nt: fp16x3 operand rows (or images) span >= 2 GiB per block");
-      }
     }
   } else if (ep.amax_b) {
     throw std::invalid_argument("gemm_nt: amax_b is the scale of fp16 B planes (bps > 0)");
+  }
+  if ((F32 && fm == 11 && kF11Buf) || (!F32 && kBf16Buf)) {
+    // the buffer-descriptor staging keeps every lane offset below 2^31 bytes of its block base
+    const int64_t lim = int64_t(1) << 31, esz = int64_t(sizeof(T));
+    int64_t aspan;
+    if (geo) {
+      const int64_t hw = int64_t(geo->Ho) * geo->Wo;
+      const int64_t imgs = std::min<int64_t>((M + hw - 1) / hw, (256 + hw - 1) / hw + 1);
+      aspan = imgs * geo->H * geo->W * int64_t(geo->pitch ? geo->pitch : geo->C) * esz;
+    } else {
+      aspan = (int64_t(256) * lda + K) * esz;
+    }
+    if (aspan >= lim || (int64_t(256) * ldb + K) * esz >= lim)
+      throw std::invalid_argument("gemm_nt: operand rows (or images) span >= 2 GiB per block");
   }
   const int nk = K / (fm >= 3 ? 32 : nt_bk_of<T>());
   // MPIT_GEMM_STAGES caps the ring depth (A/B measurements). fp32: the 64 KB epilogue tile
@@ -3082,6 +3180,12 @@ static void launch_tn_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
   if (gemm_log())
     std::fprintf(stderr, "MPIT_GEMM tn %lld %d %d conv=%d splits=%d f32=%d\n", (long long)M, N, K, geo ? 1 : 0, ns,
                  F32 ? 1 : 0);
+  if (geo && kTnBuf) {  // buffer-descriptor staging: a split's images span < 2^31 bytes
+    const int64_t hw = int64_t(geo->Ho) * geo->Wo;
+    const int64_t imgs = std::min<int64_t>((M + hw - 1) / hw, (rps + hw - 1) / hw + 1);
+    if (imgs * geo->H * geo->W * int64_t(geo->pitch ? geo->pitch : geo->C) * int64_t(sizeof(T)) >= (int64_t(1) << 31))
+      throw std::invalid_argument("gemm_tn: the images of one split span >= 2 GiB");
+  }
   const int ntk = K / tbk;
   const int ntiles = (N / tbn) * ntk;
   const bool direct = ns == 1 && beta == 0.f;

@@ -371,7 +371,7 @@ __device__ __forceinline__ void blds16(i32x4 rsrc, uint32_t voff, uint32_t lds) 
                "s"(lds)
                : "memory", "m0");
 }
-// For descriptors the compiler cannot prove wave-uniform (gemm_tn's split / step arithmetic):
+// For descriptors the compiler cannot prove wave-uniform (gemm_nt's bf16 256 x 256 tiles):
 // each word through v_readfirstlane (a no-op for SGPR values), and the 5 wait states a VALU
 // write of an SGPR needs before a VMEM instruction reads it
 __device__ __forceinline__ void blds16u(i32x4 rsrc, uint32_t voff, uint32_t lds) {
@@ -883,10 +883,11 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
     T* As = smem + buf * TILE;
     T* Bs = As + BM * BK;
     if constexpr (F11B) {
-      // (fp16x3: the descriptors are provably SGPR values; bf16: not always — blds16u)
+      // (the compiler keeps the descriptors in SGPRs except in the bf16 256 x 256 kernels,
+      // where they go through v_readfirstlane: blds16u)
       auto bl = [](i32x4 r, uint32_t v, uint32_t l) {
-        if constexpr (F32) blds16(r, v, l);
-        else blds16u(r, v, l);
+        if constexpr (!F32 && BM == 256 && BN == 256) blds16u(r, v, l);
+        else blds16(r, v, l);
       };
       // (the prologue's descriptors may come straight from a v_readfirstlane: a VALU write of
       // an SGPR needs 5 wait states before a VMEM instruction reads it)
@@ -1773,7 +1774,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y
       const i32x4 ry4 = buf_rsrc(reinterpret_cast<uint64_t>(Y) + uint64_t(((r0 + rs) * ldy + n0) * TB),
                                  uint32_t(min<int64_t>(left * ldy * TB, int64_t(kBufOob))));
 #pragma unroll
-      for (int i = 0; i < IY; ++i) blds16u(ry4, voy[i], ly + uint32_t(i * RY * TBN * TB));
+      for (int i = 0; i < IY; ++i) blds16(ry4, voy[i], ly + uint32_t(i * RY * TBN * TB));
       const uint32_t lx = lds0 + uint32_t((buf * TILE + kRows * TBN + wu * IX * RX * TBK) * TB);
       if constexpr (CONV) {
         const i32x4 rx4 = buf_rsrc(xbase);
@@ -1782,7 +1783,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y
           const int hi = pho[i] * geo.stride - geo.pad + xr[i], wi = pwo[i] * geo.stride - geo.padw + xs[i];
           const bool ok = rs + rx[i] < nrows && unsigned(hi) < unsigned(geo.H) && unsigned(wi) < unsigned(geo.W);
           const uint32_t off = uint32_t(((((pn[i] - pn0) * geo.H + hi) * geo.W + wi) * pitch + xc[i]) * TB);
-          blds16u(rx4, ok ? off : kBufOob, lx + uint32_t(i * RX * TBK * TB));
+          blds16(rx4, ok ? off : kBufOob, lx + uint32_t(i * RX * TBK * TB));
           pwo[i] += dw;  // next step's rows (issued strictly in order)
           const int cw = pwo[i] >= geo.Wo;
           pwo[i] -= cw ? geo.Wo : 0;
@@ -1795,7 +1796,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y
         const i32x4 rx4 = buf_rsrc(reinterpret_cast<uint64_t>(X) + uint64_t(((r0 + rs) * ldx + k0) * TB),
                                    uint32_t(min<int64_t>(left * ldx * TB, int64_t(kBufOob))));
 #pragma unroll
-        for (int i = 0; i < IX; ++i) blds16u(rx4, vox[i], lx + uint32_t(i * RX * TBK * TB));
+        for (int i = 0; i < IX; ++i) blds16(rx4, vox[i], lx + uint32_t(i * RX * TBK * TB));
       }
       return;
     }

@@ -58,6 +58,9 @@ _REPO = os.path.dirname(os.path.abspath(__file__))
 # algorithm choices of earlier runs (only the fc layer and fallbacks still reach MIOpen).
 os.environ.setdefault("MIOPEN_USER_DB_PATH", os.path.join(_REPO, "miopen_db"))
 os.environ.setdefault("MIOPEN_CUSTOM_CACHE_DIR", os.path.join(_REPO, "miopen_db", "kcache"))
+# a benchmark has no slow straggler to wait for: a PS reply missing for 5 minutes is a stuck
+# job, so the bench fails with the missing replies named (the library default is no limit)
+os.environ.setdefault("MPIT_PS_TIMEOUT_S", "300")
 
 
 def _par(a, tr, nworkers) -> str:
@@ -201,9 +204,9 @@ def main(argv=None) -> int:
         preflight = tr.preflight()
         if (not preflight["ok"] and a.datapath != 3 and not mp.runtime.state().shared_devices
                 and not a.no_rccl_fallback):
-            # datapath 3 is deadlock-free by construction (csrc/core/link.h) and its clients
-            # wait at most MPIT_PS_TIMEOUT_S (300 s default there) before failing with a named
-            # error; its RCCL device path had not run on distinct GPUs before such a job, so
+            # datapath 3 is deadlock-free by construction (csrc/core/link.h) and the bench's
+            # clients wait at most MPIT_PS_TIMEOUT_S (300 s, set above) before failing with a
+            # named error; its RCCL device path had not run on distinct GPUs before such a job, so
             # the JSON says so
             fallback = {"from_datapath": a.datapath, "reason": f"pre-flight: no peer access {preflight['no_peer']}, "
                                                                  f"pulled shard bits differ {preflight['mismatches']}",

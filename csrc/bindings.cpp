@@ -507,6 +507,7 @@ PYBIND11_MODULE(_mpit, m) {
            })
       .def("stats", [](PsLink& l) {
         return py::dict(py::arg("bytes_sent") = l.bytes_sent(), py::arg("bytes_recv") = l.bytes_recv(),
-                        py::arg("ordered") = l.ordered(), py::arg("groups") = l.groups());
+                        py::arg("ordered") = l.ordered(), py::arg("groups") = l.groups(),
+                        py::arg("self_mode") = PsLink::self_mode());
       });
 }

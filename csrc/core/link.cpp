@@ -183,6 +183,25 @@ void PsLink::on_req(const Msg& m) {
   if (n.client != n.server) eng_.send_am(n.client, am_post(), &n, sizeof(n), 1);
 }
 
+bool PsLink::self_mode() {
+  static const bool on = env_on("MPIT_LINK_SELF");
+  return on;
+}
+
+// self-loop: queue the client's side of the armed notice right behind the server's op (the
+// two then go out in one RCCL group: a send to self needs its receive in the same group)
+void PsLink::self_join() {
+  if (!self_armed_) return;
+  self_armed_ = false;
+  ClientFn c;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    c = at_client_;
+  }
+  if (!c) throw std::runtime_error("mpit: PS link self-loop notice without a client");
+  c(eng_.rank(), self_to_client_, self_window_, self_coff_, self_bytes_);
+}
+
 void PsLink::on_post(const Msg& m) {
   Notice n;
   std::memcpy(&n, m.data, sizeof(n));
@@ -197,7 +216,15 @@ void PsLink::on_post(const Msg& m) {
       f = std::move(it->second);
       at_server_.erase(it);
     }
+    if (n.client == n.server) {  // self-loop (the sequencer sent this rank one notice)
+      self_armed_ = true;
+      self_coff_ = n.coff;
+      self_bytes_ = n.bytes;
+      self_window_ = n.window;
+      self_to_client_ = n.to_client != 0;
+    }
     f();
+    if (self_armed_) throw std::runtime_error("mpit: PS link self-loop transfer queued no server side");
   } else {
     ClientFn c;
     {
@@ -220,14 +247,18 @@ void PsLink::send(int peer, const void* buf, int64_t bytes, hipEvent_t after) {
       hipl(hipStreamWaitEvent(stream_, after, 0), "link waits local work");
     }
     batch_.push_back({true, peer, const_cast<void*>(buf), bytes});
+    if (peer == eng_.rank()) self_join();
     return;
   }
   Op o{kSend};
   o.peer = peer;
   o.sbuf = buf;
   o.bytes = bytes;
-  std::lock_guard<std::mutex> g(mu_);
-  q_.push_back(std::move(o));
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    q_.push_back(std::move(o));
+  }
+  if (peer == eng_.rank()) self_join();
 }
 
 void PsLink::recv(int peer, void* buf, int64_t bytes, hipEvent_t after) {
@@ -239,14 +270,18 @@ void PsLink::recv(int peer, void* buf, int64_t bytes, hipEvent_t after) {
       hipl(hipStreamWaitEvent(stream_, after, 0), "link waits local work");
     }
     batch_.push_back({false, peer, buf, bytes});
+    if (peer == eng_.rank()) self_join();
     return;
   }
   Op o{kRecv};
   o.peer = peer;
   o.rbuf = buf;
   o.bytes = bytes;
-  std::lock_guard<std::mutex> g(mu_);
-  q_.push_back(std::move(o));
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    q_.push_back(std::move(o));
+  }
+  if (peer == eng_.rank()) self_join();
 }
 
 void PsLink::then(std::function<void()> f) {
@@ -308,6 +343,18 @@ void PsLink::flush_group() {
   }
 }
 
+// host self-loop: the head op is one half of a send / receive pair to this rank itself
+// (queued back to back, like the device path's one RCCL group): the other half starts too,
+// or the head would wait forever for an op queued behind it. (mu_ held)
+void PsLink::start_self_partner() {
+  if (q_.size() < 2) return;
+  Op& h = q_[0];
+  Op& o = q_[1];
+  if (h.peer != eng_.rank() || o.peer != eng_.rank() || o.req >= 0 || o.kind == kCall || o.kind == h.kind) return;
+  o.req = o.kind == kSend ? eng_.isend(o.sbuf, o.bytes, false, o.peer, 1, ctx_, false)
+                          : eng_.irecv(o.rbuf, o.bytes, false, o.peer, 1, ctx_);
+}
+
 // host: the FIFO as a stream. The head op starts when everything before it is done.
 bool PsLink::poll() {
   if (device_) {
@@ -328,12 +375,17 @@ bool PsLink::poll() {
       } else if (o.kind == kSend) {
         if (o.req < 0) {
           // rendezvous: a send runs only against a receive at the head of the peer's FIFO
-          if (rdv_ && cts_got_[o.peer] <= cts_used_[o.peer]) break;
-          if (rdv_) ++cts_used_[o.peer];
+          // (a self-loop pair is one group: no clear-to-send between its two halves)
+          const bool self = o.peer == eng_.rank();
+          if (rdv_ && !self && cts_got_[o.peer] <= cts_used_[o.peer]) break;
+          if (rdv_ && !self) ++cts_used_[o.peer];
           o.req = eng_.isend(o.sbuf, o.bytes, false, o.peer, 1, ctx_, false);
         }
         Status st;
-        if (!eng_.test(o.req, &st)) break;
+        if (!eng_.test(o.req, &st)) {
+          start_self_partner();
+          break;
+        }
         if (st.error) throw std::runtime_error("mpit: PS link send failed");
         q_.pop_front();
         did = true;
@@ -341,10 +393,13 @@ bool PsLink::poll() {
       } else {
         if (o.req < 0) {
           o.req = eng_.irecv(o.rbuf, o.bytes, false, o.peer, 1, ctx_);
-          if (rdv_) eng_.send_am(o.peer, am_cts(), nullptr, 0);
+          if (rdv_ && o.peer != eng_.rank()) eng_.send_am(o.peer, am_cts(), nullptr, 0);
         }
         Status st;
-        if (!eng_.test(o.req, &st)) break;
+        if (!eng_.test(o.req, &st)) {
+          start_self_partner();
+          break;
+        }
         if (st.error) throw std::runtime_error("mpit: PS link receive failed");
         q_.pop_front();
         did = true;

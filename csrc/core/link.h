@@ -30,6 +30,11 @@
 //  * Consecutive link ops queued in one progress sweep are issued as one ncclGroupStart/End,
 //    so a worker's receives from its K servers progress together instead of one by one.
 //
+// Self-loop (MPIT_LINK_SELF=1): the sequencer's notice of a transfer between a rank's own
+// server and client goes to that rank once (as server); when the server queues its side
+// (send or recv to itself) the client's matching side is queued right behind it, into the
+// same RCCL group, before anything flushes the batch. Same order, same events, one GPU.
+//
 // Without a GPU (the CPU test tier) the same ops run over the engine's tagged host messages
 // in ONE FIFO per rank, processed like a stream: an op starts when the ops before it are
 // done, and local work runs as a queued call. Two host modes: free (a send completes once
@@ -67,6 +72,11 @@ class PsLink {
 
   bool device() const { return device_; }
   bool legacy() const { return legacy_; }
+  // self-loop (MPIT_LINK_SELF=1, datapath 3 only): a rank's own client and server also move
+  // their shard through the link — a grouped RCCL send / recv to itself on the link stream —
+  // instead of the local fused path. This puts datapath 3's device branch (RCCL ops, link
+  // stream, event hand-offs, continuations) on ONE GPU: a 1-rank job runs it end to end.
+  static bool self_mode();
   int sequencer() const { return members_.front(); }
   // RCCL: the sequencer makes the communicator's unique id (128 bytes; others: empty); the
   // caller broadcasts it and every member calls connect() with it (collective)
@@ -119,6 +129,7 @@ class PsLink {
   void on_post(const Msg& m);  // endpoint
   void jitter();
   bool poll();                 // host FIFO (engine hook)
+  void start_self_partner();   // host self-loop pair (mu_ held)
   void flush_group();          // device: issue the batched RCCL ops
   int index_of(int world_rank) const;
 
@@ -144,6 +155,13 @@ class PsLink {
   int64_t next_xid_ = 1;
   std::map<int64_t, std::function<void()>> at_server_;  // xid -> this server's side
   ClientFn at_client_;
+  // self-loop: the notice whose server side is being queued; the client side joins the RCCL
+  // group of the server's op (a send to self and its receive must be in one ncclGroup)
+  bool self_armed_ = false;
+  int64_t self_coff_ = 0, self_bytes_ = 0;
+  int self_window_ = 0;
+  bool self_to_client_ = false;
+  void self_join();
   // host FIFO (one per rank: every op of the instance on this rank)
   std::deque<Op> q_;
   std::map<int, int64_t> cts_got_, cts_used_;  // rendezvous: clear-to-send per peer

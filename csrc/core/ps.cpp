@@ -863,7 +863,7 @@ void PSClient::set_link(PsLink* l, uintptr_t rx, uintptr_t tx, int tx_es) {
 }
 
 int PSClient::link_recvs(int k, int tag, int64_t flags) const {
-  if (!link_ || servers_[size_t(k)] == eng_.rank()) return 0;
+  if (!link_ || (servers_[size_t(k)] == eng_.rank() && !PsLink::self_mode())) return 0;
   return (tag == kTagHeader || (tag == kTagGrad && (flags & kPsWithPull))) ? 1 : 0;
 }
 
@@ -949,23 +949,21 @@ void PSClient::on_reply(const Msg&) {
 // MPIT_WAIT_SPIN_US > 0 polls (pause) for up to that long before the futex sleep, keeping
 // the core awake for the step start that follows (device clients only). Measured within
 // noise of sleeping at once (profiles/step_start_host_r02.md): default 0.
-// MPIT_PS_TIMEOUT_S (default 0 = never, opt-in; 300 s on datapath 3): a reply missing that long means a server is
-// gone or stuck — raise with what is missing instead of hanging the job (a server that
-// fails raises the job-wide abort itself, Engine::fatal; a dead server process is caught by
-// the peer check). Off by default: an SSP-deferred pull may wait on a slow straggler for
-// as long as that straggler takes, as the reference's blocking MPI calls do.
+// MPIT_PS_TIMEOUT_S (default 0 = never, opt-in on every datapath): a reply missing that long
+// means a server is gone or stuck — raise with what is missing instead of hanging the job (a
+// server that fails raises the job-wide abort itself, Engine::fatal; a dead server process is
+// caught by the peer check). Off by default: an SSP-deferred pull may wait on a slow
+// straggler (validation, checkpointing) for as long as that straggler takes, as the
+// reference's blocking MPI calls do. bench.py opts in (300 s) for its own runs.
 void PSClient::wait() {
   static const int64_t spin_us = [] {
     const char* e = std::getenv("MPIT_WAIT_SPIN_US");
     return e ? std::max<int64_t>(0, std::atoll(e)) : int64_t(0);
   }();
-  // datapath 3 (the RCCL fallback data plane) keeps a finite default: a transfer that never
-  // completes there fails with this message instead of hanging the job
-  static const double env_timeout_s = [] {
+  static const double timeout_s = [] {
     const char* e = std::getenv("MPIT_PS_TIMEOUT_S");
-    return e ? std::max(0.0, std::atof(e)) : -1.0;
+    return e ? std::max(0.0, std::atof(e)) : 0.0;
   }();
-  const double timeout_s = env_timeout_s >= 0 ? env_timeout_s : (link_ ? 300.0 : 0.0);
   const auto t0 = std::chrono::steady_clock::now();
   if (spin_us > 0 && eng_.device() >= 0) {  // GPU workers only (CPU ranks share few cores)
     for (uint32_t i = 0;; ++i) {

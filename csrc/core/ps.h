@@ -143,7 +143,11 @@ class PSServer {
   void copy_out(int c, Sub sb);
   // datapath 3: the shard's data with remote client c as RCCL / host messages (link.h)
   PsLink* link_ = nullptr;
-  bool messaged(int ci, int c) const { return datapath_ == 3 && ci >= 0 && c != eng_.rank(); }
+  // datapath 3: a remote client's data as link messages; with the link's self-loop
+  // (PsLink::self_mode) the co-located client's too
+  bool messaged(int ci, int c) const {
+    return datapath_ == 3 && ci >= 0 && (c != eng_.rank() || PsLink::self_mode());
+  }
   void grad_msg(int c, int ci, bool pull, bool defer_pull, Sub sb);
   void pull_msg(int c, int ci, Sub sb);
   void param_msg(int c, int ci, bool from_rx, Sub sb, std::function<void()> after = nullptr);
@@ -222,7 +226,7 @@ class PSClient {
   void send_param(hipStream_t s, bool from_rx = false);
   void stop();
   // until every outstanding reply arrived (GIL released); raises after MPIT_PS_TIMEOUT_S
-  // (default 0 = never; 300 s on datapath 3) with the number of replies still missing
+  // (default 0 = never, opt-in on every datapath) with the number of replies still missing
   void wait();
   // datapath 3: shard data as messages over `l` (link.h) from / into this client's own
   // buffers: rx (fp32 parameters, pulls land here), tx (push window, tx_es bytes / element)

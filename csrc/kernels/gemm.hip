@@ -1075,8 +1075,13 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
           const int r = wm * WM + i * 32 + fr;
           const float4 x0 = *reinterpret_cast<const float4*>(As + r * BK + swzk<BKB>(r, 4 * kk + 2 * fh) * 4);
           const float4 x1 = *reinterpret_cast<const float4*>(As + r * BK + swzk<BKB>(r, 4 * kk + 2 * fh + 1) * 4);
+#if defined(MPIT_ABLATE_PLANES) || defined(MPIT_ABLATE_PLANES_NT)  // timing ablation: A as if it arrived as fp16 planes (no split)
+          ah[i] = __builtin_bit_cast(f16x8, x0);
+          al[i] = __builtin_bit_cast(f16x8, x1);
+#else
           const float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
           split2h(v, sa, sa11, ah[i], al[i]);
+#endif
         }
 #pragma unroll
         for (int i = 0; i < TM; ++i)
@@ -1948,6 +1953,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y
       constexpr int NY4 = kRows * TBN / 4, NF4 = kRows * (TBN + TBK) / 4 / 256;
       constexpr int CY16 = TBN / 8, CX16 = TBK / 8;  // 16-B chunks per row of the 16-bit images
       static_assert(kRows * (TBN + TBK) % 1024 == 0, "the stage splits evenly over 256 threads");
+#if !defined(MPIT_ABLATE_PLANES) && !defined(MPIT_ABLATE_PLANES_TN)  // (timing ablation: the staged rows taken as if they were the planes)
       float4 v4[NF4];
       const float4* src4 = reinterpret_cast<const float4*>(Ys);
 #pragma unroll
@@ -1985,6 +1991,12 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y
         *reinterpret_cast<uint2*>((isy ? YL : XL) + o) = lw;
       }
       lds_barrier();
+#else
+      uint16_t* YH = reinterpret_cast<uint16_t*>(Ys);
+      uint16_t* YL = YH + kRows * TBN;
+      uint16_t* XH = YL + kRows * TBN;
+      uint16_t* XL = XH + kRows * TBK;
+#endif
 #pragma unroll
       for (int kk = 0; kk < kRows / 16; ++kk) {
         const int rr = 16 * kk + 8 * h + q;  // row of this lane in the first 4-row block

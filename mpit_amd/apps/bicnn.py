@@ -249,10 +249,17 @@ class Evaluator:
 
 def load_data(a):
     if a.preloadBinary:
-        # the reference's own caches (plaunch.lua:221-228) when they are in --binaryDir: the
-        # vocabulary from its two Torch7 maps (the other six caches are not shipped,
-        # .MISSING_LARGE_BLOBS); else this package's cache file
+        # this package's cache (-saveBinary's --binaryFile) whenever it exists; otherwise the
+        # reference's own Torch7 caches (plaunch.lua:221-228) in --binaryDir. Only the two
+        # vocabulary maps of those ship (the other six are .MISSING_LARGE_BLOBS), so that
+        # mode trains on SYNTHETIC questions / answers and random embeddings over the
+        # reference's vocabulary — said loudly, never silently
+        if os.path.exists(a.binaryFile):
+            return load_binary(a.binaryFile)
         if all(os.path.exists(os.path.join(a.binaryDir, f)) for f in T7_VOCAB):
+            print(f"bicnn: -preloadBinary: {a.binaryFile!r} not found; using the Torch7 vocabulary maps in "
+                  f"{a.binaryDir!r} with SYNTHETIC questions/answers and random embeddings (the reference's "
+                  f"dataset caches are not shipped)", file=sys.stderr, flush=True)
             return qa_from_vocab(load_t7_vocab(a.binaryDir), emb_dim=a.embeddingDim, conv_width=a.contConvWidth,
                                  n_answers=a.synthetic)
         return load_binary(a.binaryFile)

@@ -788,6 +788,13 @@ class Comm:
         if recvbuf is None:
             recvbuf = sendbuf
         src = _flat(sendbuf)
+        if self.Get_size() == 1:
+            # one rank: the reduction is the rank's own data — a stream-ordered copy (or
+            # nothing, in place), complete at once; no background thread per call
+            dst = _flat(recvbuf)
+            if dst.data_ptr() != src.data_ptr():
+                dst.copy_(src)
+            return Request(self, keep=(sendbuf, recvbuf))
         if self._use_rccl(src) and _rccl_op(op) is not None:
             import torch.distributed as dist
 

@@ -719,6 +719,8 @@ class _Conv1x1Fn(torch.autograd.Function):
             if WgradStream.after and use_side:
                 side = WgradStream.begin(x.device)
             dw = grad_out(ctx.wparam, ctx.wshape, x.device)
+            if getattr(dw, "_mpit_repeat", False):
+                side = None  # a weight used twice: autograd sums the gradients on this stream
             nws = m.gemm_tn_ws_floats(dev, M, co, ci)
             ws = torch.empty(nws, dtype=torch.float32, device=x.device) if nws else None
             keep = []
@@ -877,6 +879,8 @@ def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None, up=None
         if WgradStream.after and use_side:
             side = WgradStream.begin(x.device)
         dw = grad_out(getattr(ctx, "wparam", None), (co, c, r, s), x.device, torch.channels_last)
+        if getattr(dw, "_mpit_repeat", False):
+            side = None  # a weight used twice: autograd sums the gradients on this stream
         nws = m.conv_wgrad_ws_floats(dev, nb, h, w, c, co, r, s, stride, pad)
         ws = torch.empty(nws, dtype=torch.float32, device=x.device) if nws else None
         keep = []

@@ -18,6 +18,14 @@ non-blocking all-reduce (RCCL on its own stream) as soon as it is complete. ``fi
 waits for the outstanding buckets; the 1/N averaging is fused into the optimizer kernel
 (``gscale``).
 
+``steal=True`` (the trainer's GPU path, as the parameter-server steps run it): gradients are
+stolen (utils/flat.py ``steal_grads``). The MFMA layers' weight-gradient GEMMs write straight
+into their flat slots on the side stream (ops/conv.py WgradStream), and autograd hands over
+the other gradients as its own tensors. A complete bucket then joins the side stream, gathers
+the handed-over gradients into its slice in one launch (ops.gather_scale_), zeroes the slots
+of parameters without a gradient, and launches its all-reduce. No ``grad += new`` kernel per
+parameter, no memset of the flat gradient per step.
+
 ``wire="bf16"``: each bucket is cast into a bf16 mirror of the flat gradient and reduced in
 bf16 (half the bytes on every xGMI link), then cast back into the fp32 gradient at
 ``finish()``; the sum of the N gradients is rounded to bf16 once per ring step.
@@ -34,11 +42,13 @@ from ..utils.flat import FlatParams
 
 class BucketedAllreduce:
     def __init__(self, model: torch.nn.Module, flat: FlatParams, bucket_mb: float = 25.0, comm: Optional[Comm] = None,
-                 first_bucket_mb: float = 4.0, wire: str = "fp32"):
+                 first_bucket_mb: float = 4.0, wire: str = "fp32", steal: bool = False):
         if wire not in ("fp32", "bf16"):
             raise ValueError(f"BucketedAllreduce: wire must be fp32 or bf16, not {wire!r}")
         self.comm = comm or COMM_WORLD()
         self.flat = flat
+        self.steal = steal
+        self.members: List[List[int]] = []  # parameter indices per bucket (steal mode)
         self.wire = wire
         self.wbuf = torch.empty(flat.numel, dtype=torch.bfloat16, device=flat.grad.device) if wire == "bf16" else None
         es = flat.grad.element_size()
@@ -65,6 +75,7 @@ class BucketedAllreduce:
             b = next(k for k, (lo, hi) in enumerate(self.buckets) if lo <= off < hi)
             self.bucket_of[i] = b
             self.sizes[b] += 1
+        self.members = [[i for i in range(len(flat.params)) if self.bucket_of[i] == b] for b in range(len(self.buckets))]
         self.pending = list(self.sizes)
         self.reqs: List[Optional[Request]] = [None] * len(self.buckets)
         self._hooks = []
@@ -80,7 +91,43 @@ class BucketedAllreduce:
 
         return hook
 
+    def _gather(self, b):
+        """Steal mode: bucket b's gradients into its slice of the flat gradient."""
+        from ..ops.conv import WgradStream
+        from ..ops.fused import gather_scale_
+
+        WgradStream.join()  # in-place weight gradients may still be in flight on the side stream
+        fl = self.flat
+        gbase, es = fl.grad.data_ptr(), fl.grad.element_size()
+        srcs, offs, ns = [], [], []
+        for i in self.members[b]:
+            p, off = fl.params[i], fl.offsets[i]
+            g = p.grad
+            if g is None:  # no gradient this step: its slot holds the last step's
+                fl.grad[off:off + p.numel()].zero_()
+                continue
+            if g.data_ptr() == gbase + off * es and g.dtype == fl.grad.dtype:
+                p.grad = None  # written in place by its backward (grad_out)
+                continue
+            if g.dim() == 4 and fl.channels_last:
+                g = g.contiguous(memory_format=torch.channels_last)
+            else:
+                g = g.contiguous()
+            srcs.append(g.data_ptr())
+            offs.append(off)
+            ns.append(g.numel())
+            p.grad = g  # alive until the gather is queued
+        if srcs:
+            gather_scale_(fl.grad, srcs, offs, ns, 1.0, None, 0.0)
+        handed = fl.__dict__.get("_handed")
+        for i in self.members[b]:
+            fl.params[i].grad = None  # (the caching allocator orders any reuse on the stream)
+            if handed:  # consumed: the next backward takes its flat slot again (grad_out)
+                handed.discard(id(fl.params[i]))
+
     def _launch(self, b):
+        if self.steal:
+            self._gather(b)
         lo, hi = self.buckets[b]
         seg = self.flat.grad[lo:hi]
         if self.wbuf is not None:

@@ -140,8 +140,11 @@ class ShardPusher:
         if srcs:
             with _trace.range(f"gather_shard{k}"):
                 gather_scale_(self.pc.tx, srcs, offs, ns, self.a, self.aux, self.b)
+        handed = self.flat.__dict__.get("_handed")
         for i in self.members[k]:
             self.params[i].grad = None  # the caching allocator orders reuse on the stream
+            if handed:  # consumed: the next step's backward takes its flat slot again (grad_out)
+                handed.discard(id(self.params[i]))
         self.pc.async_send_grad_shard(k, pull=True)
         if _GATE_DELAY and self.pc.tx.is_cuda:  # race diagnostics: the pull lands before the rest
             torch.cuda._sleep(_GATE_DELAY)     # of this backward runs

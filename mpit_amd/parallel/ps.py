@@ -382,6 +382,7 @@ class PClient:
         self._user_p, self._user_g = self.rx, self.tx
         self.native = native().PSClient(_rt.engine(), self.ps_id, [e[0] for e in self.entries],
                                         [e[1] for e in self.entries], [e[2] for e in self.entries])
+        self.link = grp.link  # datapath 3's PsLink (its stats(): bytes, RCCL groups), else None
         if grp.link is not None:  # datapath 3: the shards' data from / into these very buffers
             self.native.set_link(grp.link, self.rx.data_ptr(), self.tx.data_ptr(), self.tx.element_size())
         self.native.start()

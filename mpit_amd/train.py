@@ -112,7 +112,14 @@ class Trainer:
         if cfg.optimizer == "allreduce":
             from .parallel.ddp import BucketedAllreduce
 
-            self.ddp = BucketedAllreduce(self.model, self.flat, bucket_mb=cfg.bucket_mb, wire=cfg.wire_dtype)
+            # the PS path's step machinery (gradients stolen, weight gradients on the side
+            # stream written into their flat slots, next step's weight casts queued early)
+            # unless MPIT_AR_STEAL=0; one rank has nothing to overlap: one bucket
+            self.ar_steal = self.on_gpu and os.environ.get("MPIT_AR_STEAL", "1") != "0" and \
+                cfg.extra.get("steal_grads", True)
+            bmb = cfg.bucket_mb if self.world > 1 else float(1 << 20)
+            self.ddp = BucketedAllreduce(self.model, self.flat, bucket_mb=bmb, wire=cfg.wire_dtype,
+                                         first_bucket_mb=4.0 if self.world > 1 else 0.0, steal=self.ar_steal)
         else:
             self._start_ps()
         # Downpour su=1 on the GPU: let autograd hand over its gradient tensors and gather
@@ -121,8 +128,8 @@ class Trainer:
         # the flat gradient replaces its memset plus one "grad += new" kernel per parameter.
         self.push_steal = (self.on_gpu and cfg.optimizer == "downpour" and cfg.su <= 1 and self.pc is not None
                            and cfg.extra.get("steal_grads", True))
-        self.steal = self.push_steal or (self.on_gpu and cfg.optimizer != "allreduce"
-                                         and cfg.extra.get("steal_grads", True))
+        self.steal = self.push_steal or getattr(self, "ar_steal", False) or (
+            self.on_gpu and cfg.optimizer != "allreduce" and cfg.extra.get("steal_grads", True))
         if self.steal:
             self.flat.steal_grads()
             # nothing reads a weight gradient before the join points (ops/conv.py WgradStream)
@@ -132,6 +139,10 @@ class Trainer:
             # time-slice the card (4 ranks: 8136 -> 1809 img/s)
             WgradStream.enable(self.on_gpu and (not st.shared_devices or WgradStream.forced())
                                and cfg.extra.get("wgrad_stream", True))
+        elif self.on_gpu:
+            from .ops.conv import WgradStream
+
+            WgradStream.enable(False)  # autograd accumulates the weight gradients: no side stream
         if self.push_steal:
             # push each shard during the backward as soon as its gradients are complete
             if cfg.extra.get("overlap_push", True):
@@ -155,8 +166,10 @@ class Trainer:
         # are queued right then (the GPU runs them while the host does the step boundary's
         # bookkeeping) instead of at the next forward. Anything else that writes the weights
         # between steps calls invalidate_precast() (load_checkpoint, set_amp). MPIT_PRECAST=0: off.
-        self._precast_ok = (self.wcast is not None and self.push_steal
-                            and not self.opt_config.get("defer_wait", False)
+        # (sync all-reduce: the optimizer kernel at the end of step() is the weights' last
+        # writer, so the casts queued after it see this step's update)
+        self._precast_ok = (self.wcast is not None and (self.push_steal or getattr(self, "ar_steal", False))
+                            and not getattr(self, "opt_config", {}).get("defer_wait", False)
                             and os.environ.get("MPIT_PRECAST", "1") != "0") if self.on_gpu else False
         self._precast = False
         self.steps = 0
@@ -255,6 +268,8 @@ class Trainer:
                 WgradStream.join()
         if getattr(self, "push_steal", False):
             return loss.detach(), self.flat.stolen()  # gathered straight into the push window
+        if getattr(self, "ar_steal", False):
+            return loss.detach(), self.flat.grad  # gathered per bucket by the all-reduce (ddp.finish)
         if getattr(self, "steal", False):
             return loss.detach(), self.flat.stolen().materialize()
         return loss.detach(), self.flat.grad

@@ -83,6 +83,7 @@ class FlatParams:
             _GSLOTS[id(p)] = (weakref.ref(p), weakref.ref(self), off)
         self._steal = True
         self.inplace = os.environ.get("MPIT_GRAD_INPLACE", "1") != "0"
+        self._handed = set()  # parameters whose slot grad_out handed out since the last gather
         return self
 
     def grad_view(self, p: torch.Tensor, off: int) -> torch.Tensor:
@@ -159,6 +160,7 @@ class StolenGrads:
             gather_scale_(dst, srcs, offs, ns, a, aux, b)
         for p in self.flat.params:
             p.grad = None
+        self.flat._handed = set()  # the next step's backwards may take the slots again
         return dst
 
     def materialize(self) -> torch.Tensor:
@@ -168,12 +170,27 @@ class StolenGrads:
 def grad_out(param, shape, device, memory_format=torch.contiguous_format) -> torch.Tensor:
     """Where a backward should write ``param``'s fp32 gradient: its slot in the flat gradient
     buffer when the parameter belongs to a stealing :class:`FlatParams` (see
-    ``steal_grads``), else a new tensor."""
+    ``steal_grads``), else a new tensor.
+
+    The slot is handed out once per step: a parameter used twice in one forward (a module
+    applied twice, tied weights) gets its slot for the first backward that runs and a fresh
+    tensor for every later one, which autograd then adds into the slot (g1 + g2). Handing the
+    slot out twice would let the second backward overwrite the first gradient and autograd
+    sum two aliases of one buffer (2 g2)."""
     s = _GSLOTS.get(id(param)) if param is not None else None
     if s is not None and s[0]() is param:
         flat = s[1]()
         if flat is not None and getattr(flat, "inplace", False) and flat.grad.dtype == torch.float32:
+            handed = flat.__dict__.setdefault("_handed", set())
             v = flat.grad_view(param, s[2])
-            if tuple(v.shape) == tuple(shape) and v.is_contiguous(memory_format=memory_format):
+            if (id(param) not in handed and tuple(v.shape) == tuple(shape)
+                    and v.is_contiguous(memory_format=memory_format)):
+                handed.add(id(param))
                 return v
+            if id(param) in handed:
+                # a repeated use: autograd adds this tensor into the slot on the compute
+                # stream, so its producer must not write it on the side stream (conv.py)
+                g = torch.empty(shape, dtype=torch.float32, device=device, memory_format=memory_format)
+                g._mpit_repeat = True
+                return g
     return torch.empty(shape, dtype=torch.float32, device=device, memory_format=memory_format)

@@ -177,9 +177,15 @@ class Win:
         return Request(self.comm)
 
     # ------------------------------------------------------------ synchronisation
-    def Flush(self, rank: Optional[int] = None):
+    def _flush(self):
+        # every epoch-closing synchronisation completes the origin reads of the queued copies:
+        # the origin buffers held for them (_put_bytes / _acc_elems) are released here, so a
+        # Fence- or Unlock-synchronised Put loop keeps only the current epoch's origins alive
         self._w.flush(self._stream())
         self._keep_all = []
+
+    def Flush(self, rank: Optional[int] = None):
+        self._flush()
 
     Flush_all = Flush
     Flush_local = Flush
@@ -187,14 +193,14 @@ class Win:
     Sync = Flush
 
     def Fence(self, assertion: int = 0):
-        self._w.flush(self._stream())
+        self._flush()
         self.comm.Barrier()
 
     def Lock(self, rank: int, lock_type: int = LOCK_EXCLUSIVE, assertion: int = 0):
         self._w.lock(rank, lock_type == LOCK_EXCLUSIVE)
 
     def Unlock(self, rank: int):
-        self._w.flush(self._stream())
+        self._flush()
         self._w.unlock(rank)
 
     def Lock_all(self, assertion: int = 0):
@@ -202,7 +208,7 @@ class Win:
             self._w.lock(r, False)
 
     def Unlock_all(self):
-        self._w.flush(self._stream())
+        self._flush()
         for r in range(self.comm.Get_size()):
             self._w.unlock(r)
 
@@ -219,7 +225,7 @@ class Win:
         self._epoch_targets = list(group.world_ranks)
 
     def Complete(self):
-        self._w.flush(self._stream())
+        self._flush()
         z = torch.zeros(1, dtype=torch.uint8)
         for w in self._epoch_targets:
             self.comm._csend(z, self.comm._from_world(w), 32).Wait()

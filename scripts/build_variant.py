@@ -3,7 +3,8 @@ flags): every other object is reused from build/obj; the variant lands in build/
 is loaded instead of the in-tree module with MPIT_NATIVE_SO=build/var_<name>/_mpit<ext>.
 
 Usage: python scripts/build_variant.py NAME SOURCE [--replace gemm.hip] [extra hipcc flags...]
-(SOURCE stands in for csrc/kernels/<--replace>, default gemm.hip)
+(SOURCE stands in for csrc/kernels/<--replace>, default gemm.hip; --no-base skips the in-tree
+build first, so two variants can compile at once once build/obj is current)
 """
 import os
 import subprocess
@@ -19,7 +20,10 @@ def main():
     rep = "gemm.hip"
     if flags[:1] == ["--replace"]:
         rep, flags = flags[1], flags[2:]
-    B.build()  # the in-tree objects the variant reuses
+    base = "--no-base" not in flags  # --no-base: reuse build/obj as it is (another build made it)
+    flags = [f for f in flags if f != "--no-base"]
+    if base:
+        B.build()  # the in-tree objects the variant reuses
     out = os.path.join(B.ROOT, "build", f"var_{name}")
     os.makedirs(out, exist_ok=True)
     hipcc = os.path.join(B.ROCM, "bin", "hipcc")

@@ -302,6 +302,17 @@ mpiT.Win_fence(0, dw)
 if r == 0:
     q = n - 1
     assert dw.tensor.tolist() == [0.0, q + 1.0 + n, 0.0, q + 2.0 + n, 0.0, q + 3.0 + n, 0.0, 0.0], dw.tensor.tolist()
+# 1,000 Fence-synchronised datatype-faithful Puts: each closed epoch releases its origin
+# buffers (Win._keep_all), so retained memory stays flat instead of growing per Put
+mem0 = torch.cuda.memory_allocated(dev) if dev.type == "cuda" else 0
+for _ in range(1000):
+    mpiT.Put(src * 1.0, 3, mpiT.FLOAT, (r + 1) % n, 1, 1, vt, dw)
+    mpiT.Win_fence(0, dw)
+    assert not getattr(dw, "_keep_all", []), len(dw._keep_all)
+if dev.type == "cuda":
+    assert torch.cuda.memory_allocated(dev) <= mem0 + (1 << 20), (mem0, torch.cuda.memory_allocated(dev))
+q = (r - 1) % n
+assert dw.tensor[1].item() == q + 1.0 and dw.tensor[5].item() == q + 3.0
 try:  # signatures that do not carry the same bytes are refused, not silently truncated
     mpiT.Put(src, 2, mpiT.FLOAT, (r + 1) % n, 1, 1, vt, dw)
     raise AssertionError("mismatched one-sided signature accepted")

@@ -156,3 +156,31 @@ def test_datapath3_pre_sequencer_layout_deadlocks():
     out = run_ranks("ps_link_rdv.py", 8, dict(_RDV, T_TOPO="colocated", MPIT_LINK_LEGACY="1", MPIT_PS_TIMEOUT_S="6"),
                     timeout=300)
     assert "RESULT RDV_TIMEOUT" in out and "RESULT RDV_OK" not in out, out
+
+
+def test_bucketed_allreduce_equals_one_bucket_training_two_ranks():
+    """Sync DP with many buckets (non-blocking all-reduces launched from the backward) ends
+    bit-identical to one bucket: 2 ranks, CNN-7, 4 steps (a two-term sum is order-free)."""
+    res = eval(_result(run_ranks("ddp_bucket_equiv.py", 2, {"MPIT_CPU_ONLY": "1", "T_TRAIN": "1"}, timeout=300)))
+    for rr in res:
+        assert rr["train"]["same"], rr
+        assert rr["train"]["buckets"][0] > 3 and rr["train"]["buckets"][1] == 1, rr
+        assert rr["exact"]["same"] and rr["exact"]["exact"], rr
+
+
+@pytest.mark.parametrize("n", [3, 4])
+def test_bucketed_allreduce_exact_sums(n):
+    """3-4 ranks: exactly representable gradients through tiny buckets and one bucket give
+    the exact sum bit for bit (every element reduced once, whatever the bucket layout)."""
+    res = eval(_result(run_ranks("ddp_bucket_equiv.py", n, {"MPIT_CPU_ONLY": "1"}, timeout=300)))
+    assert len(res) == n
+    for rr in res:
+        assert rr["exact"]["same"] and rr["exact"]["exact"] and rr["exact"]["buckets"][0] > 3, rr
+
+
+@pytest.mark.gpu
+def test_allreduce_steal_machinery_bitwise_on_gpu():
+    """BASELINE config 3 on the PS path's machinery (train.py ar_steal) == the plain path."""
+    res = eval(_result(run_ranks("ar_steal_equiv.py", 1, {}, timeout=400)))
+    for prec, (same, diff) in res.items():
+        assert same, (prec, diff)

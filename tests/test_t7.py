@@ -63,3 +63,21 @@ def test_t7_rejects_truncated_and_trailing():
         t7.loads(blob[:-1])
     with pytest.raises(ValueError):
         t7.loads(blob + b"\0")
+
+
+@needs_ref
+def test_bicnn_preload_binary_prefers_the_binary_file(tmp_path, capsys):
+    """-preloadBinary takes --binaryFile when it exists, even next to the Torch7 maps; the
+    vocabulary-only mode says loudly that its questions / answers are synthetic."""
+    from mpit_amd.apps import bicnn
+    from mpit_amd.apps.qa_data import save_binary, synthetic_qa
+
+    f = str(tmp_path / "qa.pt")
+    save_binary(synthetic_qa(n_answers=7, pool=5, n_train=50, n_valid=10, emb_dim=16, conv_width=2), f)
+    a = bicnn.build_args(["-preloadBinary", "-binaryDir", REF, "-binaryFile", f, "-embeddingDim", "16"])
+    assert len(bicnn.load_data(a).answers) == 7
+    assert "SYNTHETIC" not in capsys.readouterr().err
+    a = bicnn.build_args(["-preloadBinary", "-binaryDir", REF, "-binaryFile", str(tmp_path / "none.pt"),
+                          "-synthetic", "20"])
+    assert len(bicnn.load_data(a).answers) == 20
+    assert "SYNTHETIC" in capsys.readouterr().err

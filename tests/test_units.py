@@ -354,3 +354,23 @@ def test_inplace_grad_slots_skip_the_gather():
     assert torch.equal(seg(2, m[1].weight), torch.full((8,), 2.0))
     assert torch.equal(seg(3, m[1].bias), torch.zeros(2))
     assert all(p.grad is None for p in m.parameters())
+
+
+def test_grad_slot_handed_out_once_per_step():
+    """grad_out hands a parameter's flat-gradient slot to ONE backward per step: a second use
+    of the same weight in one forward gets a fresh tensor (marked for the compute stream),
+    which autograd then adds into the slot; gather() makes the slot available again."""
+    import torch.nn as nn
+
+    from mpit_amd.utils.flat import FlatParams, grad_out
+
+    m = nn.Linear(4, 4)
+    fp = FlatParams(m).steal_grads()
+    w = m.weight
+    slot = fp.grad.data_ptr() + fp.offsets[0] * fp.grad.element_size()
+    g1 = grad_out(w, w.shape, w.device)
+    g2 = grad_out(w, w.shape, w.device)
+    assert g1.data_ptr() == slot and g2.data_ptr() != slot and getattr(g2, "_mpit_repeat", False)
+    assert not getattr(g1, "_mpit_repeat", False)
+    fp.stolen().materialize()
+    assert grad_out(w, w.shape, w.device).data_ptr() == slot

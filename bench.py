@@ -88,7 +88,9 @@ def _fp32_gemm() -> str:
     """How the fp32 step's GEMMs use the matrix cores (ops/conv.py MPIT_F32_SPLIT)."""
     from mpit_amd.ops import conv
 
-    return conv._F32_SPLIT
+    # "+planes": activations and gradients that only GEMMs read are written as the two fp16
+    # planes by their producers (ops/conv.py _F32_PLANES, gemm.hip FM 13)
+    return conv._F32_SPLIT + ("+planes" if conv._F32_PLANES else "")
 
 
 def _devices(W, tr) -> list:

@@ -38,6 +38,23 @@ static void apply_sfold(BnRed& r, const py::object& f) {
   if (t.size() == 12) r.ftag = t[11].cast<int>();  // tagged partials (gemm.hip stats_fold)
 }
 
+// a PlaneSpec (kernels.h) from Python: None, or a dict of its fields (missing ones 0)
+static bool plane_spec(const py::object& o, PlaneSpec& ps) {
+  if (o.is_none()) return false;
+  const py::dict d = o.cast<py::dict>();
+  auto u = [&](const char* k) -> uintptr_t { return d.contains(k) ? d[k].cast<uintptr_t>() : 0; };
+  ps.obound = u("obound");
+  ps.xmax = u("xmax");
+  ps.xmax2 = u("xmax2");
+  ps.gmax = u("gmax");
+  ps.xep = uint32_t(u("xep"));
+  ps.xep2 = uint32_t(u("xep2"));
+  ps.gep = uint32_t(u("gep"));
+  ps.rbound = u("rbound");
+  ps.rplanes = int(u("rplanes"));
+  return true;
+}
+
 PYBIND11_MODULE(_mpit, m) {
   m.doc() = "mpit_amd native runtime: shm control plane, IPC windows, parameter server, CDNA4 kernels";
   m.attr("ANY_SOURCE") = kAnySource;
@@ -108,46 +125,58 @@ PYBIND11_MODULE(_mpit, m) {
       [](int dev, uintptr_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C, uintptr_t gamma,
          uintptr_t beta, uintptr_t rmean, uintptr_t rvar, uintptr_t save_mean, uintptr_t save_rstd, uintptr_t ws,
          float momentum, float eps, bool relu, uintptr_t mask, uintptr_t stats, int64_t nstat, uintptr_t amax,
-         uintptr_t coef) {
+         uintptr_t coef, py::object planes) {
+        PlaneSpec ps;
+        const bool pl = plane_spec(planes, ps);
         bn_act_fwd(dev, S(s), bf16, x, res, y, M, C, gamma, beta, rmean, rvar, save_mean, save_rstd, ws, momentum, eps,
-                   relu, mask, stats, nstat, amax, coef);
+                   relu, mask, stats, nstat, amax, coef, pl ? &ps : nullptr);
       },
       py::arg("dev"), py::arg("stream"), py::arg("bf16"), py::arg("x"), py::arg("res"), py::arg("y"), py::arg("M"),
       py::arg("C"), py::arg("gamma"), py::arg("beta"), py::arg("rmean"), py::arg("rvar"), py::arg("save_mean"),
       py::arg("save_rstd"), py::arg("ws"), py::arg("momentum"), py::arg("eps"), py::arg("relu"), py::arg("mask"),
-      py::arg("stats") = 0, py::arg("nstat") = 0, py::arg("amax") = 0, py::arg("coef") = 0);
+      py::arg("stats") = 0, py::arg("nstat") = 0, py::arg("amax") = 0, py::arg("coef") = 0,
+      py::arg("planes") = py::none());
   m.def("bn_act_apply", [](int dev, uintptr_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C,
                            uintptr_t coef, bool relu) { bn_act_apply(dev, S(s), bf16, x, res, y, M, C, coef, relu); });
   m.def(
       "bn_act_bwd",
       [](int dev, uintptr_t s, bool bf16, uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t dx, uintptr_t dres,
          int64_t M, int C, uintptr_t gamma, uintptr_t mean, uintptr_t rstd, uintptr_t dgamma, uintptr_t dbeta,
-         uintptr_t ws, bool relu, uintptr_t part, int64_t npart, uintptr_t coef, uintptr_t amax) {
+         uintptr_t ws, bool relu, uintptr_t part, int64_t npart, uintptr_t coef, uintptr_t amax, py::object planes) {
+        PlaneSpec ps;
+        const bool pl = plane_spec(planes, ps);
         bn_act_bwd(dev, S(s), bf16, dy, mask, x, dx, dres, M, C, gamma, mean, rstd, dgamma, dbeta, ws, relu, part, npart,
-                   coef, amax);
+                   coef, amax, pl ? &ps : nullptr);
       },
       py::arg("dev"), py::arg("stream"), py::arg("bf16"), py::arg("dy"), py::arg("mask"), py::arg("x"), py::arg("dx"),
       py::arg("dres"), py::arg("M"), py::arg("C"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
       py::arg("dgamma"), py::arg("dbeta"), py::arg("ws"), py::arg("relu"), py::arg("part") = 0, py::arg("npart") = 0,
-      py::arg("coef") = 0, py::arg("amax") = 0);
+      py::arg("coef") = 0, py::arg("amax") = 0, py::arg("planes") = py::none());
   m.def(
       "bn_pair_apply",
       [](int dev, uintptr_t s, uintptr_t x1, uintptr_t coef1, uintptr_t x2, uintptr_t coef2, uintptr_t y, int64_t M,
-         int C, uintptr_t mask, bool f32, uintptr_t amax, uintptr_t scratch) {
-        bn_pair_apply(dev, S(s), x1, coef1, x2, coef2, y, M, C, mask, f32, amax, scratch);
+         int C, uintptr_t mask, bool f32, uintptr_t amax, uintptr_t scratch, py::object planes) {
+        PlaneSpec ps;
+        const bool pl = plane_spec(planes, ps);
+        bn_pair_apply(dev, S(s), x1, coef1, x2, coef2, y, M, C, mask, f32, amax, scratch, pl ? &ps : nullptr);
       },
       py::arg("dev"), py::arg("stream"), py::arg("x1"), py::arg("coef1"), py::arg("x2"), py::arg("coef2"), py::arg("y"),
-      py::arg("M"), py::arg("C"), py::arg("mask"), py::arg("f32") = false, py::arg("amax") = 0, py::arg("scratch") = 0);
+      py::arg("M"), py::arg("C"), py::arg("mask"), py::arg("f32") = false, py::arg("amax") = 0, py::arg("scratch") = 0,
+      py::arg("planes") = py::none());
   m.def(
       "bn_pair_bwd_apply",
       [](int dev, uintptr_t s, uintptr_t dy, uintptr_t mask, uintptr_t x1, uintptr_t coef1, uintptr_t dx1, uintptr_t x2,
          uintptr_t coef2, uintptr_t dx2, int64_t M, int C, bool f32, uintptr_t amax1, uintptr_t amax2,
-         uintptr_t scratch) {
-        bn_pair_bwd_apply(dev, S(s), dy, mask, x1, coef1, dx1, x2, coef2, dx2, M, C, f32, amax1, amax2, scratch);
+         uintptr_t scratch, py::object planes1, py::object planes2) {
+        PlaneSpec p1, p2;
+        const bool a = plane_spec(planes1, p1), b = plane_spec(planes2, p2);
+        bn_pair_bwd_apply(dev, S(s), dy, mask, x1, coef1, dx1, x2, coef2, dx2, M, C, f32, amax1, amax2, scratch,
+                          a ? &p1 : nullptr, b ? &p2 : nullptr);
       },
       py::arg("dev"), py::arg("stream"), py::arg("dy"), py::arg("mask"), py::arg("x1"), py::arg("coef1"),
       py::arg("dx1"), py::arg("x2"), py::arg("coef2"), py::arg("dx2"), py::arg("M"), py::arg("C"),
-      py::arg("f32") = false, py::arg("amax1") = 0, py::arg("amax2") = 0, py::arg("scratch") = 0);
+      py::arg("f32") = false, py::arg("amax1") = 0, py::arg("amax2") = 0, py::arg("scratch") = 0,
+      py::arg("planes1") = py::none(), py::arg("planes2") = py::none());
   m.def("gemm_nt_supported", &gemm_nt_supported, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("f32") = false);
   m.def("gemm_nt_stats_floats", &gemm_nt_stats_floats);
   m.def("gemm_nt_tiles", &gemm_nt_tiles);
@@ -158,11 +187,12 @@ PYBIND11_MODULE(_mpit, m) {
          uintptr_t red_mask, uintptr_t red_mean, int64_t red_row0, uintptr_t red_part2, uintptr_t red_x2,
          uintptr_t red_mean2, bool f32, uintptr_t fold_coef, uintptr_t fold_gamma, uintptr_t fold_rstd,
          uintptr_t fold_dgamma, uintptr_t fold_dbeta, uintptr_t fold_lvl, int64_t bps, uintptr_t amax_a,
-         uintptr_t amax_b, uintptr_t fold_zero, py::object bn_fold, bool fold_tag) {
+         uintptr_t amax_b, uintptr_t fold_zero, py::object bn_fold, bool fold_tag, int64_t aps, uintptr_t omax,
+         uint32_t oepoch) {
         BnRed r{red_part, red_x, red_mask, red_mean, red_row0, red_part2, red_x2, red_mean2};
         r.fcoef = fold_coef; r.fgamma = fold_gamma; r.frstd = fold_rstd;
         r.fdgamma = fold_dgamma; r.fdbeta = fold_dbeta; r.flvl = fold_lvl; r.fzero = fold_zero;
-        r.amax_a = amax_a; r.amax_b = amax_b;
+        r.amax_a = amax_a; r.amax_b = amax_b; r.aps = aps; r.omax = omax; r.oepoch = oepoch;
         r.ftag = fold_tag ? 1 : 0;
         apply_sfold(r, bn_fold);
         gemm_nt(dev, S(s), M, N, K, A, lda, B, ldb, C, ldc, stats, cin, cmask, &r, f32, bps);
@@ -174,7 +204,8 @@ PYBIND11_MODULE(_mpit, m) {
       py::arg("red_mean2") = 0, py::arg("f32") = false, py::arg("fold_coef") = 0, py::arg("fold_gamma") = 0,
       py::arg("fold_rstd") = 0, py::arg("fold_dgamma") = 0, py::arg("fold_dbeta") = 0, py::arg("fold_lvl") = 0,
       py::arg("bps") = 0, py::arg("amax_a") = 0, py::arg("amax_b") = 0, py::arg("fold_zero") = 0,
-      py::arg("bn_fold") = py::none(), py::arg("fold_tag") = false);
+      py::arg("bn_fold") = py::none(), py::arg("fold_tag") = false, py::arg("aps") = 0, py::arg("omax") = 0,
+      py::arg("oepoch") = 0);
   m.def("gemm_nt_fold_lvl_floats", &gemm_nt_fold_lvl_floats);
   m.def("bound_floats", [] { return kBoundFloats; });
   m.def("gemm_tn_supported", &gemm_tn_supported);
@@ -184,12 +215,13 @@ PYBIND11_MODULE(_mpit, m) {
   m.def(
       "gemm_tn",
       [](int dev, uintptr_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X, int64_t ldx,
-         uintptr_t out, uintptr_t ws, float beta, bool f32, uintptr_t amax_y, uintptr_t amax_x) {
-        gemm_tn(dev, S(s), M, N, K, Y, ldy, X, ldx, out, ws, beta, f32, amax_y, amax_x);
+         uintptr_t out, uintptr_t ws, float beta, bool f32, uintptr_t amax_y, uintptr_t amax_x, int64_t yps,
+         int64_t xps) {
+        gemm_tn(dev, S(s), M, N, K, Y, ldy, X, ldx, out, ws, beta, f32, amax_y, amax_x, yps, xps);
       },
       py::arg("dev"), py::arg("stream"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("Y"), py::arg("ldy"),
       py::arg("X"), py::arg("ldx"), py::arg("out"), py::arg("ws"), py::arg("beta"), py::arg("f32") = false,
-      py::arg("amax_y") = 0, py::arg("amax_x") = 0);
+      py::arg("amax_y") = 0, py::arg("amax_x") = 0, py::arg("yps") = 0, py::arg("xps") = 0);
   m.def(
       "cast_transpose",
       [](int dev, uintptr_t s, uintptr_t w, int R, int Cc, uintptr_t wb, uintptr_t wt, int taps, bool f32) {
@@ -210,9 +242,12 @@ PYBIND11_MODULE(_mpit, m) {
   m.def(
       "maxpool_fwd",
       [](int dev, uintptr_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t x, uintptr_t y,
-         uintptr_t idx, bool f32) { maxpool_fwd(dev, S(s), N, H, W, C, K, stride, pad, x, y, idx, f32); },
+         uintptr_t idx, bool f32, uintptr_t ibound, uintptr_t obound) {
+        maxpool_fwd(dev, S(s), N, H, W, C, K, stride, pad, x, y, idx, f32, ibound, obound);
+      },
       py::arg("dev"), py::arg("stream"), py::arg("N"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("K"),
-      py::arg("stride"), py::arg("pad"), py::arg("x"), py::arg("y"), py::arg("idx"), py::arg("f32") = false);
+      py::arg("stride"), py::arg("pad"), py::arg("x"), py::arg("y"), py::arg("idx"), py::arg("f32") = false,
+      py::arg("ibound") = 0, py::arg("obound") = 0);
   m.def(
       "maxpool_bwd",
       [](int dev, uintptr_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t dy, uintptr_t idx,
@@ -247,11 +282,11 @@ PYBIND11_MODULE(_mpit, m) {
          uintptr_t red_x2, uintptr_t red_mean2, bool f32, uintptr_t fold_coef, uintptr_t fold_gamma,
          uintptr_t fold_rstd, uintptr_t fold_dgamma, uintptr_t fold_dbeta, uintptr_t fold_lvl, int64_t bps,
          uintptr_t amax_a, uintptr_t amax_b, uintptr_t fold_zero, py::object bn_fold, bool red_relu,
-         bool fold_tag) {
+         bool fold_tag, int64_t aps, uintptr_t omax, uint32_t oepoch) {
         BnRed r{red_part, red_x, red_mask, red_mean, red_row0, red_part2, red_x2, red_mean2};
         r.fcoef = fold_coef; r.fgamma = fold_gamma; r.frstd = fold_rstd;
         r.fdgamma = fold_dgamma; r.fdbeta = fold_dbeta; r.flvl = fold_lvl; r.fzero = fold_zero;
-        r.amax_a = amax_a; r.amax_b = amax_b;
+        r.amax_a = amax_a; r.amax_b = amax_b; r.aps = aps; r.omax = omax; r.oepoch = oepoch;
         r.relu_y = red_relu ? 1 : 0;
         r.ftag = fold_tag ? 1 : 0;
         apply_sfold(r, bn_fold);
@@ -265,7 +300,7 @@ PYBIND11_MODULE(_mpit, m) {
       py::arg("fold_coef") = 0, py::arg("fold_gamma") = 0, py::arg("fold_rstd") = 0, py::arg("fold_dgamma") = 0,
       py::arg("fold_dbeta") = 0, py::arg("fold_lvl") = 0, py::arg("bps") = 0, py::arg("amax_a") = 0,
       py::arg("amax_b") = 0, py::arg("fold_zero") = 0, py::arg("bn_fold") = py::none(), py::arg("red_relu") = false,
-      py::arg("fold_tag") = false);
+      py::arg("fold_tag") = false, py::arg("aps") = 0, py::arg("omax") = 0, py::arg("oepoch") = 0);
   m.def("conv_dgrad_strided_wfloats", &conv_dgrad_strided_wfloats);
   m.def(
       "conv_dgrad_strided_weights",
@@ -279,16 +314,17 @@ PYBIND11_MODULE(_mpit, m) {
       [](int dev, uintptr_t s, int Nb, int H, int W, int C, int Co, int R, int S_, int stride, int pad, uintptr_t dy,
          uintptr_t wcls, uintptr_t dx, uintptr_t red_part, uintptr_t red_x, uintptr_t red_mask, uintptr_t red_mean,
          uintptr_t red_part2, uintptr_t red_x2, uintptr_t red_mean2, bool f32, int64_t bps, uintptr_t amax_a,
-         uintptr_t amax_b) {
+         uintptr_t amax_b, int64_t aps, uintptr_t omax, uint32_t oepoch) {
         BnRed r{red_part, red_x, red_mask, red_mean, 0, red_part2, red_x2, red_mean2};
-        r.amax_a = amax_a; r.amax_b = amax_b;
+        r.amax_a = amax_a; r.amax_b = amax_b; r.aps = aps; r.omax = omax; r.oepoch = oepoch;
         conv_dgrad_strided(dev, S(s), Nb, H, W, C, Co, R, S_, stride, pad, dy, wcls, dx, &r, f32, bps);
       },
       py::arg("dev"), py::arg("stream"), py::arg("Nb"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("Co"),
       py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("dy"), py::arg("wcls"), py::arg("dx"),
       py::arg("red_part") = 0, py::arg("red_x") = 0, py::arg("red_mask") = 0, py::arg("red_mean") = 0,
       py::arg("red_part2") = 0, py::arg("red_x2") = 0, py::arg("red_mean2") = 0, py::arg("f32") = false,
-      py::arg("bps") = 0, py::arg("amax_a") = 0, py::arg("amax_b") = 0);
+      py::arg("bps") = 0, py::arg("amax_a") = 0, py::arg("amax_b") = 0, py::arg("aps") = 0, py::arg("omax") = 0,
+      py::arg("oepoch") = 0);
   m.def("relu_bias_bwd_ws_floats", &relu_bias_bwd_ws_floats);
   m.def(
       "relu_bias_bwd",
@@ -333,12 +369,14 @@ PYBIND11_MODULE(_mpit, m) {
   m.def(
       "conv_wgrad",
       [](int dev, uintptr_t s, int Nb, int H, int W, int C, int Co, int R, int S_, int stride, int pad, uintptr_t dy,
-         uintptr_t x, uintptr_t dw, uintptr_t ws, float beta, bool f32, uintptr_t amax_y, uintptr_t amax_x) {
-        conv_wgrad(dev, S(s), Nb, H, W, C, Co, R, S_, stride, pad, dy, x, dw, ws, beta, f32, amax_y, amax_x);
+         uintptr_t x, uintptr_t dw, uintptr_t ws, float beta, bool f32, uintptr_t amax_y, uintptr_t amax_x,
+         int64_t yps, int64_t xps) {
+        conv_wgrad(dev, S(s), Nb, H, W, C, Co, R, S_, stride, pad, dy, x, dw, ws, beta, f32, amax_y, amax_x, yps, xps);
       },
       py::arg("dev"), py::arg("stream"), py::arg("Nb"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("Co"),
       py::arg("R"), py::arg("S"), py::arg("stride"), py::arg("pad"), py::arg("dy"), py::arg("x"), py::arg("dw"),
-      py::arg("ws"), py::arg("beta"), py::arg("f32") = false, py::arg("amax_y") = 0, py::arg("amax_x") = 0);
+      py::arg("ws"), py::arg("beta"), py::arg("f32") = false, py::arg("amax_y") = 0, py::arg("amax_x") = 0,
+      py::arg("yps") = 0, py::arg("xps") = 0);
 
   py::class_<Engine>(m, "Engine")
       .def(py::init<const std::string&, int, int, bool, int, int64_t>(), py::arg("name"), py::arg("world"),

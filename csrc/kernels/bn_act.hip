@@ -29,6 +29,7 @@
 
 #include "ew.h"
 #include "kernels.h"
+#include "planes.h"
 
 namespace mpit {
 namespace {
@@ -260,7 +261,32 @@ __device__ __forceinline__ void mask_store(uint8_t* __restrict__ m, const Slot<S
 // |out| >= 0, so the float bits order like unsigned integers.
 struct AmaxOut {
   float* amax;  // null: not wanted
+  // fp16 planes output (kernels.h PlaneSpec, fp32 passes only): obound != null
+  float* obound = nullptr;
+  const unsigned long long* xmax = nullptr;
+  const unsigned long long* xmax2 = nullptr;
+  const unsigned long long* gmax = nullptr;
+  uint32_t xep = 0, xep2 = 0, gep = 0;
+  const float* rbound = nullptr;
+  int rplanes = 0;
 };
+
+AmaxOut amax_out(uintptr_t amax, const PlaneSpec* p) {
+  AmaxOut o{reinterpret_cast<float*>(amax)};
+  if (p) {
+    o.obound = reinterpret_cast<float*>(p->obound);
+    o.xmax = reinterpret_cast<const unsigned long long*>(p->xmax);
+    o.xmax2 = reinterpret_cast<const unsigned long long*>(p->xmax2);
+    o.gmax = reinterpret_cast<const unsigned long long*>(p->gmax);
+    o.xep = p->xep;
+    o.xep2 = p->xep2;
+    o.gep = p->gep;
+    o.rbound = reinterpret_cast<const float*>(p->rbound);
+    o.rplanes = p->rplanes;
+    if (o.obound) o.amax = nullptr;  // the planes' bound is known before the pass
+  }
+  return o;
+}
 
 // Barriers of an LDS hand-off only: the epilogues below run after the kernel's output
 // stores, and __syncthreads()'s workgroup fence would wait for every one of them to retire
@@ -288,6 +314,43 @@ __device__ __forceinline__ void amax_finish(float m, const AmaxOut& o) {
   const float b = block_max(m, red);
   if (threadIdx.x == 0)
     atomicMax(reinterpret_cast<unsigned int*>(o.amax + (blockIdx.x % kBoundSlots) * kBoundStride), __float_as_uint(b));
+}
+
+// ---------------------------------------------------------------- fp16 planes (FM 13 operands)
+// (planes.h) the slot's 8 values as planes: h at element i, l at element nel + i of the
+// 16-bit view
+template <class S>
+__device__ __forceinline__ void store_planes(float* __restrict__ y, int64_t nel, const S& s, const float (&v)[8],
+                                             PlaneScale ps) {
+  uint16_t* yh = reinterpret_cast<uint16_t*>(y);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (!s.valid(h)) continue;
+    uint32_t hw[2], lw[2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) split_pair(v[4 * h + 2 * p], v[4 * h + 2 * p + 1], ps, hw[p], lw[p]);
+    *reinterpret_cast<uint2*>(yh + s.off[h]) = make_uint2(hw[0], hw[1]);
+    *reinterpret_cast<uint2*>(yh + nel + s.off[h]) = make_uint2(lw[0], lw[1]);
+  }
+}
+// planes back to fp32 (exact, 22 significant bits)
+template <class S>
+__device__ __forceinline__ void load_planes(const float* __restrict__ r, int64_t nel, const S& s, float inv,
+                                            float (&v)[8]) {
+  const uint16_t* rh = reinterpret_cast<const uint16_t*>(r);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    uint2 a = make_uint2(0, 0), b = make_uint2(0, 0);
+    if (s.valid(h)) {
+      a = *reinterpret_cast<const uint2*>(rh + s.off[h]);
+      b = *reinterpret_cast<const uint2*>(rh + nel + s.off[h]);
+    }
+    const pf32x2 x0 = join_pair(a.x, b.x, inv), x1 = join_pair(a.y, b.y, inv);
+    v[4 * h] = x0.x;
+    v[4 * h + 1] = x0.y;
+    v[4 * h + 2] = x1.x;
+    v[4 * h + 3] = x1.y;
+  }
 }
 
 // ---------------------------------------------------------------- forward: statistics
@@ -608,10 +671,28 @@ __global__ __launch_bounds__(1024) void bn_apply_kernel(const T* __restrict__ x,
     }
   }
   float mx = 0.f;
+  // fp16 planes (fp32 passes): the output bound from the input's maximum and the coefficients,
+  // |x sc + sh (+ res)| <= max|sc| max|x| + max|sh| (+ max|res|) (the fp16x3 split tolerates
+  // values up to 4x the bound: its rounding is harmless); a block spans every channel
+  [[maybe_unused]] PlaneScale ps{1.f, 2048.f};
+  [[maybe_unused]] float rinv = 1.f;
+  const int64_t nel = nvec * 8;
+  if constexpr (sizeof(T) == 4) {
+    const float rb = RES && am.rbound ? slots_max_wave(am.rbound) : 0.f;
+    if (RES && am.rplanes) rinv = pexp2(-plane_exp(rb));
+    if (am.obound) {  // (per wave, from the coefficient arrays: no block barrier)
+      float bound = fmaf(coef_max_wave(coef, C, 0), epoch_max_wave(am.xmax, am.xep), coef_max_wave(coef, C, 1));
+      if constexpr (RES) bound += rb;
+      ps = plane_scale(bound, am.obound);
+    }
+  }
   for_slots<SPLIT, U>(i, stride, nvec, [&](const auto& s) {
     float a[V], rr[V];
     load8<T>(x, s, a);
-    if constexpr (RES) load8<T>(res, s, rr);
+    if constexpr (RES) {
+      if (sizeof(T) == 4 && am.rplanes) load_planes(reinterpret_cast<const float*>(res), nel, s, rinv, rr);
+      else load8<T>(res, s, rr);
+    }
     uint32_t bits = 0;
 #pragma unroll
     for (int v = 0; v < V; ++v) {
@@ -621,7 +702,8 @@ __global__ __launch_bounds__(1024) void bn_apply_kernel(const T* __restrict__ x,
       a[v] = t;
       if (s.valid(v >> 2)) mx = fmaxf(mx, fabsf(t));
     }
-    store8<T>(y, s, a);
+    if (sizeof(T) == 4 && am.obound) store_planes(reinterpret_cast<float*>(y), nel, s, a, ps);
+    else store8<T>(y, s, a);
     if constexpr (MASK) {  // (rounding to bf16 never flips the sign of a normal number)
 #pragma unroll
       for (int v = 0; v < V; ++v) bits |= uint32_t(a[v] > 0.f) << v;
@@ -749,6 +831,16 @@ __global__ __launch_bounds__(1024) void bn_bwd_apply_kernel(const T* __restrict_
     }
   }
   float mx = 0.f;
+  // fp16 planes: |A dz + Cc x + B| <= max|A| max|dy| + max|Cc| max|x| + max|B|
+  [[maybe_unused]] PlaneScale ps{1.f, 2048.f};
+  const int64_t nel = nvec * 8;
+  if constexpr (sizeof(T) == 4) {
+    if (am.obound) {  // (per wave, from the coefficient arrays: no block barrier)
+      const float ma = coef_max_wave(coef, C, 0), mc = coef_max_wave(coef, C, 1), mbb = coef_max_wave(coef, C, 2);
+      ps = plane_scale(fmaf(ma, epoch_max_wave(am.gmax, am.gep), fmaf(mc, epoch_max_wave(am.xmax, am.xep), mbb)),
+                       am.obound);
+    }
+  }
   for_slots<SPLIT, U>(i, stride, nvec, [&](const auto& s) {
     float d[V], xx[V];
     load8<T>(dy, s, d);
@@ -763,7 +855,8 @@ __global__ __launch_bounds__(1024) void bn_bwd_apply_kernel(const T* __restrict_
       xx[v] = fmaf(A[v], dz, fmaf(Cc[v], xx[v], B[v]));
       if (s.valid(v >> 2)) mx = fmaxf(mx, fabsf(xx[v]));
     }
-    store8<T>(dx, s, xx);
+    if (sizeof(T) == 4 && am.obound) store_planes(reinterpret_cast<float*>(dx), nel, s, xx, ps);
+    else store8<T>(dx, s, xx);
     if constexpr (RESGRAD) store8<T>(dres, s, d);
   });
   if (am.amax) amax_finish(mx, am);
@@ -795,6 +888,15 @@ __global__ __launch_bounds__(1024) void bn_pair_apply_kernel(const T* __restrict
     }
   }
   float mx = 0.f;
+  [[maybe_unused]] PlaneScale ps{1.f, 2048.f};
+  const int64_t nel = nvec * 8;
+  if constexpr (sizeof(T) == 4) {
+    if (am.obound) {  // |y| <= max|a1| max|x1| + max|b1| + max|a2| max|x2| + max|b2| (per wave)
+      ps = plane_scale(fmaf(coef_max_wave(coef1, C, 0), epoch_max_wave(am.xmax, am.xep), coef_max_wave(coef1, C, 1)) +
+                           fmaf(coef_max_wave(coef2, C, 0), epoch_max_wave(am.xmax2, am.xep2), coef_max_wave(coef2, C, 1)),
+                       am.obound);
+    }
+  }
   for_slots<SPLIT, U>(i, stride, nvec, [&](const auto& s) {
     float p[V], q[V];
     load8<T>(x1, s, p);
@@ -807,7 +909,8 @@ __global__ __launch_bounds__(1024) void bn_pair_apply_kernel(const T* __restrict
       bits |= uint32_t(t > 0.f) << v;
       if (s.valid(v >> 2)) mx = fmaxf(mx, t);
     }
-    store8<T>(y, s, p);
+    if (sizeof(T) == 4 && am.obound) store_planes(reinterpret_cast<float*>(y), nel, s, p, ps);
+    else store8<T>(y, s, p);
     mask_store(mask, s, bits);
   });
   if (am.amax) amax_finish(mx, am);
@@ -838,6 +941,19 @@ __global__ __launch_bounds__(1024) void bn_pair_bwd_apply_kernel(
     }
   }
   float m1 = 0.f, m2 = 0.f;
+  [[maybe_unused]] PlaneScale ps1{1.f, 2048.f}, ps2{1.f, 2048.f};
+  const int64_t nel = nvec * 8;
+  if constexpr (sizeof(T) == 4) {
+    // |dx_k| <= max|A_k| max|dy| + max|C_k| max|x_k| + max|B_k| (per wave, no block barrier)
+    if (am1.obound)
+      ps1 = plane_scale(fmaf(coef_max_wave(coef1, C, 0), epoch_max_wave(am1.gmax, am1.gep),
+                             fmaf(coef_max_wave(coef1, C, 1), epoch_max_wave(am1.xmax, am1.xep), coef_max_wave(coef1, C, 2))),
+                        am1.obound);
+    if (am2.obound)
+      ps2 = plane_scale(fmaf(coef_max_wave(coef2, C, 0), epoch_max_wave(am2.gmax, am2.gep),
+                             fmaf(coef_max_wave(coef2, C, 1), epoch_max_wave(am2.xmax, am2.xep), coef_max_wave(coef2, C, 2))),
+                        am2.obound);
+  }
   for_slots<SPLIT, U>(i, stride, nvec, [&](const auto& s) {
     float d[V], p[V], q[V];
     load8<T>(dy, s, d);
@@ -854,8 +970,10 @@ __global__ __launch_bounds__(1024) void bn_pair_bwd_apply_kernel(
         m2 = fmaxf(m2, fabsf(q[v]));
       }
     }
-    store8<T>(dx1, s, p);
-    store8<T>(dx2, s, q);
+    if (sizeof(T) == 4 && am1.obound) store_planes(reinterpret_cast<float*>(dx1), nel, s, p, ps1);
+    else store8<T>(dx1, s, p);
+    if (sizeof(T) == 4 && am2.obound) store_planes(reinterpret_cast<float*>(dx2), nel, s, q, ps2);
+    else store8<T>(dx2, s, q);
   });
   if (am1.amax) amax_finish(m1, am1);
   if (am2.amax) amax_finish(m2, am2);
@@ -906,11 +1024,11 @@ template <typename T>
 void fwd_impl(int dev, hipStream_t s, const T* x, const T* res, T* y, int64_t M, int C, const float* gamma,
               const float* beta, float* rmean, float* rvar, float* save_mean, float* save_rstd, float* ws,
               float momentum, float eps, bool relu, uint8_t* mask, const float* tstats, int64_t nstat,
-              uintptr_t amax) {
+              uintptr_t amax, const PlaneSpec* planes) {
   constexpr int V = Vec<T>::N;
   // amax: zeroed by the finalize below (tile statistics) or a memset, raised by the apply pass;
   // with y == nullptr (coefficients only, bn_pair) only the zeroing happens
-  const AmaxOut am{y ? reinterpret_cast<float*>(amax) : nullptr};
+  const AmaxOut am = amax_out(y ? amax : 0, planes);
   check_shape(M, C, V, reinterpret_cast<uintptr_t>(x));
   const int G = C / V;
   const int blk = block_for(G);
@@ -949,11 +1067,12 @@ void fwd_impl(int dev, hipStream_t s, const T* x, const T* res, T* y, int64_t M,
 template <typename T>
 void bwd_impl(hipStream_t s, const T* dy, const uint8_t* mask, const T* x, T* dx, T* dres, int64_t M, int C,
               const float* gamma, const float* mean, const float* rstd, float* dgamma, float* dbeta, float* ws,
-              bool relu, const float* gpart, int64_t npart, const float* coef_in, uintptr_t amax) {
+              bool relu, const float* gpart, int64_t npart, const float* coef_in, uintptr_t amax,
+              const PlaneSpec* planes) {
   constexpr int V = Vec<T>::N;
   // amax: zeroed by the finalize (or, given coefficients, by the GEMM that folded it), raised
   // by the apply pass; dx == nullptr: coefficients (and the zeroing) only
-  const AmaxOut am{dx ? reinterpret_cast<float*>(amax) : nullptr};
+  const AmaxOut am = amax_out(dx ? amax : 0, planes);
   check_shape(M, C, V, reinterpret_cast<uintptr_t>(x));
   if (relu && !mask) throw std::invalid_argument("bn_act backward: ReLU needs the forward mask");
   const int G = C / V;
@@ -1017,8 +1136,11 @@ int64_t bn_mask_bytes(bool bf16, int64_t M, int C) { (void)bf16; return M * (C /
 void bn_act_fwd(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C,
                 uintptr_t gamma, uintptr_t beta, uintptr_t rmean, uintptr_t rvar, uintptr_t save_mean,
                 uintptr_t save_rstd, uintptr_t ws, float momentum, float eps, bool relu, uintptr_t mask,
-                uintptr_t stats, int64_t nstat, uintptr_t amax, uintptr_t coef) {
+                uintptr_t stats, int64_t nstat, uintptr_t amax, uintptr_t coef, const PlaneSpec* planes) {
   hip_check(hipSetDevice(dev), "hipSetDevice");
+  if (planes && (bf16 || (planes->obound && !y) || (planes->rplanes && !(res && planes->rbound)) ||
+                 (planes->obound && res && !planes->rbound)))
+    throw std::invalid_argument("bn_act forward: fp16 planes are for fp32 passes with the bounds of their inputs");
   auto F = [](uintptr_t p) { return reinterpret_cast<float*>(p); };
   auto* mk = reinterpret_cast<uint8_t*>(mask);
   if (coef) {  // finalize folded into the producing GEMM (gemm.hip stats_fold): the apply pass only
@@ -1030,7 +1152,7 @@ void bn_act_fwd(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res, u
     } else {
       check_shape(M, C, 8, x);
       launch_apply<float>(s, reinterpret_cast<const float*>(x), reinterpret_cast<const float*>(res),
-                          reinterpret_cast<float*>(y), M, C, F(coef), relu, mk, AmaxOut{F(amax)});
+                          reinterpret_cast<float*>(y), M, C, F(coef), relu, mk, amax_out(amax, planes));
     }
     hip_check(hipGetLastError(), "bn_act forward launch");
     return;
@@ -1038,11 +1160,11 @@ void bn_act_fwd(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res, u
   if (bf16)
     fwd_impl<uint16_t>(dev, s, reinterpret_cast<const uint16_t*>(x), reinterpret_cast<const uint16_t*>(res),
                        reinterpret_cast<uint16_t*>(y), M, C, F(gamma), F(beta), F(rmean), F(rvar), F(save_mean),
-                       F(save_rstd), F(ws), momentum, eps, relu, mk, F(stats), nstat, amax);
+                       F(save_rstd), F(ws), momentum, eps, relu, mk, F(stats), nstat, amax, nullptr);
   else
     fwd_impl<float>(dev, s, reinterpret_cast<const float*>(x), reinterpret_cast<const float*>(res),
                     reinterpret_cast<float*>(y), M, C, F(gamma), F(beta), F(rmean), F(rvar), F(save_mean), F(save_rstd),
-                    F(ws), momentum, eps, relu, mk, F(stats), nstat, amax);
+                    F(ws), momentum, eps, relu, mk, F(stats), nstat, amax, planes);
 }
 
 void bn_act_apply(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C,
@@ -1063,24 +1185,26 @@ void bn_act_apply(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res,
 void bn_act_bwd(int dev, hipStream_t s, bool bf16, uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t dx,
                 uintptr_t dres, int64_t M, int C, uintptr_t gamma, uintptr_t mean, uintptr_t rstd, uintptr_t dgamma,
                 uintptr_t dbeta, uintptr_t ws, bool relu, uintptr_t part, int64_t npart, uintptr_t coef,
-                uintptr_t amax) {
+                uintptr_t amax, const PlaneSpec* planes) {
   hip_check(hipSetDevice(dev), "hipSetDevice");
+  if (planes && planes->obound && (bf16 || !dx || dres))
+    throw std::invalid_argument("bn_act backward: fp16 planes are for fp32 dx passes without a residual gradient");
   auto F = [](uintptr_t p) { return reinterpret_cast<float*>(p); };
   const auto* mk = reinterpret_cast<const uint8_t*>(mask);
   if (coef && !dx) throw std::invalid_argument("bn_act backward: given coefficients need dx");
   if (bf16)
     bwd_impl<uint16_t>(s, reinterpret_cast<const uint16_t*>(dy), mk, reinterpret_cast<const uint16_t*>(x),
                        reinterpret_cast<uint16_t*>(dx), reinterpret_cast<uint16_t*>(dres), M, C, F(gamma), F(mean),
-                       F(rstd), F(dgamma), F(dbeta), F(ws), relu, F(part), npart, F(coef), amax);
+                       F(rstd), F(dgamma), F(dbeta), F(ws), relu, F(part), npart, F(coef), amax, nullptr);
   else
     bwd_impl<float>(s, reinterpret_cast<const float*>(dy), mk, reinterpret_cast<const float*>(x),
                     reinterpret_cast<float*>(dx), reinterpret_cast<float*>(dres), M, C, F(gamma), F(mean), F(rstd),
-                    F(dgamma), F(dbeta), F(ws), relu, F(part), npart, F(coef), amax);
+                    F(dgamma), F(dbeta), F(ws), relu, F(part), npart, F(coef), amax, planes);
 }
 
 template <typename T>
 static void pair_apply_t(hipStream_t s, uintptr_t x1, uintptr_t coef1, uintptr_t x2, uintptr_t coef2, uintptr_t y,
-                         int64_t M, int C, uintptr_t mask, uintptr_t amax, uintptr_t scratch) {
+                         int64_t M, int C, uintptr_t mask, uintptr_t amax, uintptr_t scratch, const PlaneSpec* planes) {
   const int G = C / 8, blk = block_for(G);
   const int64_t nvec = M * G;
   const int u = apply_u(sizeof(T) == 4);
@@ -1088,14 +1212,14 @@ static void pair_apply_t(hipStream_t s, uintptr_t x1, uintptr_t coef1, uintptr_t
   hipLaunchKernelGGL((bn_pair_apply_kernel<T, decltype(sp)::value, decltype(uu)::value>), dim3(apply_grid_u(nvec, blk, u)), dim3(blk), 0, s,
                      reinterpret_cast<const T*>(x1), reinterpret_cast<const T*>(x2), reinterpret_cast<T*>(y),
                      reinterpret_cast<const float*>(coef1), reinterpret_cast<const float*>(coef2), nvec, C,
-                     reinterpret_cast<uint8_t*>(mask), AmaxOut{reinterpret_cast<float*>(amax)});
+                     reinterpret_cast<uint8_t*>(mask), amax_out(amax, planes));
   });
 }
 
 template <typename T>
 static void pair_bwd_t(hipStream_t s, uintptr_t dy, uintptr_t mask, uintptr_t x1, uintptr_t coef1, uintptr_t dx1,
                        uintptr_t x2, uintptr_t coef2, uintptr_t dx2, int64_t M, int C, uintptr_t amax1, uintptr_t amax2,
-                       uintptr_t scratch) {
+                       uintptr_t scratch, const PlaneSpec* p1, const PlaneSpec* p2) {
   const int G = C / 8, blk = block_for(G);
   const int64_t nvec = M * G;
   const int u = apply_u(sizeof(T) == 4);
@@ -1104,29 +1228,34 @@ static void pair_bwd_t(hipStream_t s, uintptr_t dy, uintptr_t mask, uintptr_t x1
                      reinterpret_cast<const T*>(dy), reinterpret_cast<const uint8_t*>(mask),
                      reinterpret_cast<const T*>(x1), reinterpret_cast<const float*>(coef1), reinterpret_cast<T*>(dx1),
                      reinterpret_cast<const T*>(x2), reinterpret_cast<const float*>(coef2), reinterpret_cast<T*>(dx2),
-                     nvec, C, AmaxOut{reinterpret_cast<float*>(amax1)}, AmaxOut{reinterpret_cast<float*>(amax2)});
+                     nvec, C, amax_out(amax1, p1), amax_out(amax2, p2));
   });
 }
 
 void bn_pair_apply(int dev, hipStream_t s, uintptr_t x1, uintptr_t coef1, uintptr_t x2, uintptr_t coef2, uintptr_t y,
-                   int64_t M, int C, uintptr_t mask, bool f32, uintptr_t amax, uintptr_t scratch) {
+                   int64_t M, int C, uintptr_t mask, bool f32, uintptr_t amax, uintptr_t scratch,
+                   const PlaneSpec* planes) {
   hip_check(hipSetDevice(dev), "hipSetDevice");
+  if (planes && planes->obound && !f32) throw std::invalid_argument("bn_pair_apply: fp16 planes are for fp32 passes");
   check_shape(M, C, 8, x1);
   check_shape(M, C, 8, x2);
   if (!mask) throw std::invalid_argument("bn_pair_apply: needs the ReLU mask buffer");
-  if (f32) pair_apply_t<float>(s, x1, coef1, x2, coef2, y, M, C, mask, amax, scratch);
-  else pair_apply_t<uint16_t>(s, x1, coef1, x2, coef2, y, M, C, mask, amax, scratch);
+  if (f32) pair_apply_t<float>(s, x1, coef1, x2, coef2, y, M, C, mask, amax, scratch, planes);
+  else pair_apply_t<uint16_t>(s, x1, coef1, x2, coef2, y, M, C, mask, amax, scratch, nullptr);
   hip_check(hipGetLastError(), "bn_pair_apply launch");
 }
 
 void bn_pair_bwd_apply(int dev, hipStream_t s, uintptr_t dy, uintptr_t mask, uintptr_t x1, uintptr_t coef1,
                        uintptr_t dx1, uintptr_t x2, uintptr_t coef2, uintptr_t dx2, int64_t M, int C, bool f32,
-                       uintptr_t amax1, uintptr_t amax2, uintptr_t scratch) {
+                       uintptr_t amax1, uintptr_t amax2, uintptr_t scratch, const PlaneSpec* p1,
+                       const PlaneSpec* p2) {
   hip_check(hipSetDevice(dev), "hipSetDevice");
+  if (((p1 && p1->obound) || (p2 && p2->obound)) && !f32)
+    throw std::invalid_argument("bn_pair_bwd_apply: fp16 planes are for fp32 passes");
   check_shape(M, C, 8, x1);
   check_shape(M, C, 8, x2);
-  if (f32) pair_bwd_t<float>(s, dy, mask, x1, coef1, dx1, x2, coef2, dx2, M, C, amax1, amax2, scratch);
-  else pair_bwd_t<uint16_t>(s, dy, mask, x1, coef1, dx1, x2, coef2, dx2, M, C, amax1, amax2, scratch);
+  if (f32) pair_bwd_t<float>(s, dy, mask, x1, coef1, dx1, x2, coef2, dx2, M, C, amax1, amax2, scratch, p1, p2);
+  else pair_bwd_t<uint16_t>(s, dy, mask, x1, coef1, dx1, x2, coef2, dx2, M, C, amax1, amax2, scratch, nullptr, nullptr);
   hip_check(hipGetLastError(), "bn_pair_bwd_apply launch");
 }
 

@@ -268,6 +268,15 @@ struct EpiArgs {
   // fp16x3 (FM 11): device upper bounds of |A| and |B| that set the operand scales
   const float* amax_a;
   const float* amax_b;
+  // FM 13 (fp16x3, A planes): A is two fp16 planes h, l of A * 2^ea (ea from amax_a), the
+  // l plane aps elements after the h plane — written by A's producer (the BN apply passes),
+  // so the kernel splits nothing
+  int64_t aps;
+  // max |C| of this launch (the input of the BN that writes fp16 planes from it, planes.h):
+  // one 64-bit (epoch, value bits) atomic max per block into slot blockIdx % kBoundSlots of
+  // omax; a slot of an older launch (smaller epoch) is replaced, so the buffer is never zeroed
+  unsigned long long* omax;
+  uint32_t oepoch;
   // EPI_STATS fold (scoef != null): the BN forward's finalize runs in this GEMM's last
   // blocks (stats_fold): the statistics of the output become the BN's scale / shift
   // [2][N], save_mean / save_rstd and running-statistics update; flvl ([groups][3][N]),
@@ -758,7 +767,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
   // wave grid over the tile: 2 x 2 (each wave 64 x 64 of a 128 x 128 tile), or for FM 9
   // (pre-split B) 4 x 1: each wave owns 32 rows x all 128 columns, so every A row is split in
   // registers by exactly one wave (the ready-made B planes are the shared operand)
-  constexpr int WGM = (sizeof(T) == 4 && (FM == 9 || FM == 10 || FM == 11)) ? 4 : 2, WGN = NW / WGM;
+  constexpr int WGM = (sizeof(T) == 4 && (FM == 9 || FM == 10 || FM == 11 || FM == 13)) ? 4 : 2, WGN = NW / WGM;
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 32, TN = WN / 32;
   constexpr int EPC = epc<T>();                          // elements per 16-B chunk
@@ -771,10 +780,15 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
   // 32 bf16 per row — the A operand alone is split in registers
   // FM 11 (fp32, fp16x3): B arrives as two fp16 planes (h, l) of the scaled weight, staged the
   // same way (two 64-B-row images); A is scaled and split in registers (split2h)
-  constexpr bool BSPLIT = F32 && (FM == 4 || FM == 9 || FM == 10 || FM == 11);
-  constexpr int NPL = FM == 11 ? 2 : 3;           // B planes
+  constexpr bool BSPLIT = F32 && (FM == 4 || FM == 9 || FM == 10 || FM == 11 || FM == 13);
+  constexpr int NPL = FM == 11 || FM == 13 ? 2 : 3;  // B planes
   constexpr int IBP = BSPLIT ? BN / 16 / NW : 0;  // glds per wave per B plane (16 rows x 64 B)
-  constexpr int NI = BSPLIT ? IA + NPL * IBP : IA + IB;
+  // FM 13: A arrives as two fp16 planes too (h, l of A * 2^ea; plane stride ep.aps), staged
+  // like B's (two 64-B-row images of 32 halves per row): nothing is split in the kernel
+  constexpr bool ASPLIT = F32 && FM == 13;
+  constexpr int IAP = ASPLIT ? BM / 16 / NW : 0;  // glds per wave per A plane
+  static_assert(!ASPLIT || (IAP >= 1 && kF11Buf), "FM 13 stages A planes through buffer descriptors");
+  constexpr int NI = BSPLIT ? (ASPLIT ? 2 * IAP : IA) + NPL * IBP : IA + IB;
   // elements (T) per stage: A rows, then B (fp32 rows, or NPL 16-bit plane images)
   constexpr int BTILE = BSPLIT ? NPL * BN * 32 / 2 : BN * BK;
   constexpr int TILE = BM * BK + BTILE;
@@ -794,10 +808,13 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
   // CONV: the output pixel of the row (first input pixel of its window) instead
   const T* pa[IA];
   const T* pb[IB];
-  int hi0[IA], wi0[IA], ca[IA], img[IA];
+  constexpr int NAR = ASPLIT ? IAP : IA;  // per-lane A row sources
+  int hi0[NAR], wi0[NAR], ca[NAR], img[NAR];
 #pragma unroll
-  for (int i = 0; i < IA; ++i) {
-    const int row = (w * IA + i) * RPI + lane / CPK, c = swzk<BKB>(row, lane % CPK);
+  for (int i = 0; i < NAR; ++i) {
+    // (FM 13: a plane row is 64 B = 4 chunks of 8 halves, 16 rows per wave instruction)
+    const int row = ASPLIT ? (w * IAP + i) * 16 + lane / 4 : (w * IA + i) * RPI + lane / CPK;
+    const int c = ASPLIT ? swz(row, lane % 4) : swzk<BKB>(row, lane % CPK);
     const int64_t gm = min(m0 + row, M - 1);  // clamp: tail rows compute garbage, never stored
     if constexpr (CONV) {
       const int hw = geo.Ho * geo.Wo;
@@ -806,8 +823,8 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
       hi0[i] = ho * geo.stride - geo.pad;
       wi0[i] = wo * geo.stride - geo.padw;
       img[i] = int(n) * geo.H;
-      ca[i] = c * EPC;
-    } else {
+      ca[i] = c * (ASPLIT ? 8 : EPC);
+    } else if constexpr (!ASPLIT) {
       pa[i] = A + gm * lda + c * EPC;
     }
   }
@@ -833,9 +850,10 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
   // column row (of each plane) — and a tile's k offset moves the descriptor base (SALU), so
   // issuing a tile costs no per-lane 64-bit address arithmetic, no padding branches and no
   // readfirstlane of the LDS address. The host checks that every offset stays below 2^31.
-  constexpr bool F11B = (F32 && FM == 11 && kF11Buf) || (!F32 && FM == 0 && kBf16Buf);
+  constexpr bool F11B = (F32 && (FM == 11 || FM == 13) && kF11Buf) || (!F32 && FM == 0 && kBf16Buf);
   constexpr int NVB = BSPLIT ? IBP : IB;
-  [[maybe_unused]] uint32_t voa[F11B ? IA : 1], vob[F11B ? NVB : 1];
+  [[maybe_unused]] uint32_t voa[F11B ? NAR : 1], vob[F11B ? NVB : 1];
+  constexpr int AES = ASPLIT ? 2 : int(sizeof(T));  // bytes per A element in global memory
   [[maybe_unused]] uint64_t abase = 0, bbase = 0;
   [[maybe_unused]] uint32_t lds0 = 0;
   [[maybe_unused]] int ih0 = 0;
@@ -845,14 +863,15 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
     if constexpr (CONV) {
       const int64_t img0 = m0 / (int64_t(geo.Ho) * geo.Wo);
       ih0 = int(img0) * geo.H;
-      abase = reinterpret_cast<uint64_t>(A) + uint64_t(img0 * geo.H * geo.W) * uint64_t(pitch) * sizeof(T);
+      abase = reinterpret_cast<uint64_t>(A) + uint64_t(img0 * geo.H * geo.W) * uint64_t(pitch) * uint64_t(AES);
     } else {
-      abase = reinterpret_cast<uint64_t>(A) + uint64_t(m0) * uint64_t(lda) * sizeof(T);
+      abase = reinterpret_cast<uint64_t>(A) + uint64_t(m0) * uint64_t(lda) * uint64_t(AES);
 #pragma unroll
-      for (int i = 0; i < IA; ++i) {
-        const int row = (w * IA + i) * RPI + lane / CPK, c = swzk<BKB>(row, lane % CPK);
+      for (int i = 0; i < NAR; ++i) {
+        const int row = ASPLIT ? (w * IAP + i) * 16 + lane / 4 : (w * IA + i) * RPI + lane / CPK;
+        const int c = ASPLIT ? swz(row, lane % 4) : swzk<BKB>(row, lane % CPK);
         const int64_t gm = min(m0 + row, M - 1);
-        voa[i] = uint32_t(((gm - m0) * lda + c * EPC) * int(sizeof(T)));
+        voa[i] = uint32_t(((gm - m0) * lda + c * (ASPLIT ? 8 : EPC)) * AES);
       }
     }
     bbase = reinterpret_cast<uint64_t>(B) + uint64_t(n0) * uint64_t(ldb) * (BSPLIT ? 2u : sizeof(T));
@@ -896,22 +915,32 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
       if constexpr (CONV) {
         if (kc == 0) {  // first tile of the tap (kr, ks): this lane's pixel offsets for it
 #pragma unroll
-          for (int i = 0; i < IA; ++i) {
+          for (int i = 0; i < NAR; ++i) {
             const int hi = hi0[i] + kr, wi = wi0[i] + ks;
             const bool ok = unsigned(hi) < unsigned(geo.H) && unsigned(wi) < unsigned(geo.W);
-            voa[i] = ok ? uint32_t((((img[i] - ih0) + hi) * geo.W + wi) * pitch + ca[i]) * uint32_t(sizeof(T))
+            voa[i] = ok ? uint32_t((((img[i] - ih0) + hi) * geo.W + wi) * pitch + ca[i]) * uint32_t(AES)
                         : kBufOob;
           }
         }
-        ab = abase + uint64_t(kc) * sizeof(T);
+        ab = abase + uint64_t(kc) * uint64_t(AES);
       } else {
-        ab = abase + uint64_t(kt) * uint64_t(BK * sizeof(T));
+        ab = abase + uint64_t(kt) * uint64_t(BK * AES);
       }
       constexpr int TB = int(sizeof(T));
-      const i32x4 ra = buf_rsrc(ab);
-      const uint32_t la = lds0 + uint32_t((buf * TILE + wu * IA * RPI * BK) * TB);
+      if constexpr (ASPLIT) {  // two 64-B-row plane images (h, l) of BM rows, like B's
+        const uint32_t la = lds0 + uint32_t(buf * TILE * TB + wu * IAP * 16 * 32 * 2);
 #pragma unroll
-      for (int i = 0; i < IA; ++i) bl(ra, voa[i], la + uint32_t(i * RPI * BK * TB));
+        for (int p = 0; p < 2; ++p) {
+          const i32x4 ra = buf_rsrc(ab + uint64_t(p) * uint64_t(ep.aps) * 2u);
+#pragma unroll
+          for (int i = 0; i < IAP; ++i) bl(ra, voa[i], la + uint32_t(p * BM * 32 * 2 + i * 16 * 32 * 2));
+        }
+      } else {
+        const i32x4 ra = buf_rsrc(ab);
+        const uint32_t la = lds0 + uint32_t((buf * TILE + wu * IA * RPI * BK) * TB);
+#pragma unroll
+        for (int i = 0; i < IA; ++i) bl(ra, voa[i], la + uint32_t(i * RPI * BK * TB));
+      }
       if constexpr (BSPLIT) {
         const uint32_t lb = lds0 + uint32_t((buf * TILE + BM * BK) * TB + wu * IBP * 16 * 32 * 2);
 #pragma unroll
@@ -986,7 +1015,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
   // FM 11: operand scales 2^ea (A, applied in the split) and 2^eb (B, applied by the plan)
   [[maybe_unused]] int ea = 0, eb = 0;
   [[maybe_unused]] float sa = 1.f, sa11 = 2048.f;
-  if constexpr (F32 && FM == 11) {
+  if constexpr (F32 && (FM == 11 || FM == 13)) {
     ea = fp16_exp(ep.amax_a);
     eb = fp16_exp(ep.amax_b);
     sa = exp2i(ea);
@@ -1053,6 +1082,38 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pl[sl][j], ah[i], acc[i][j], 0, 0, 0);
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ph[sl][j], al[i], acc[i][j], 0, 0, 0);
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ph[sl][j], ah[i], acc[i][j], 0, 0, 0);
+          }
+      }
+      continue;
+    } else if constexpr (F32 && FM == 13) {
+      // fp16x3 on planes: A's h, l read ready-made like B's (chunk 2kk + fh of a 64-B plane
+      // row); hh -> acc, hl + lh -> tacc — FM 11's products on the same planes, no split
+      const uint16_t* Bp = reinterpret_cast<const uint16_t*>(Bs);
+      const uint16_t* Ap = reinterpret_cast<const uint16_t*>(As);
+#pragma unroll
+      for (int kk = 0; kk < BK / 16; ++kk) {
+        f16x8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int r = wn * WN + j * 32 + fr;
+          const int o = r * 32 + swz(r, 2 * kk + fh) * 8;
+          bh[j] = *reinterpret_cast<const f16x8*>(Bp + o);
+          bl[j] = *reinterpret_cast<const f16x8*>(Bp + BN * 32 + o);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int r = wm * WM + i * 32 + fr;
+          const int o = r * 32 + swz(r, 2 * kk + fh) * 8;
+          ah[i] = *reinterpret_cast<const f16x8*>(Ap + o);
+          al[i] = *reinterpret_cast<const f16x8*>(Ap + BM * 32 + o);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bh[j], ah[i], acc[i][j], 0, 0, 0);
+            tacc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bl[j], ah[i], tacc[i][j], 0, 0, 0);
+            tacc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bh[j], al[i], tacc[i][j], 0, 0, 0);
           }
       }
       continue;
@@ -1286,7 +1347,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
     }
   }
 
-  if constexpr (F32 && FM == 11) {  // (hh + 2^-11 (hl + lh)) 2^-(ea + eb), exact scalings
+  if constexpr (F32 && (FM == 11 || FM == 13)) {  // (hh + 2^-11 (hl + lh)) 2^-(ea + eb), exact scalings
     const float ia = exp2i(-ea), ib = exp2i(-eb);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -1373,6 +1434,7 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
     else return ((uint32_t(mk[o >> 3]) >> (o & 7)) & 15u) | (((uint32_t(mk[(o + HOFF) >> 3]) >> ((o + HOFF) & 7)) & 15u) << 4);
   };
   float s1[8], s2[8], sf[8], mu[8];
+  float om = 0.f;  // max |C| over this thread's stores (ep.omax)
   int nv = 0;
 #pragma unroll
   for (int e = 0; e < 8; ++e) s1[e] = s2[e] = sf[e] = mu[e] = 0.f;
@@ -1469,6 +1531,10 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
       }
     }
     store8(C + o, v, HOFF);
+    if (ep.omax != nullptr) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) om = fmaxf(om, fabsf(v[e]));
+    }
     if constexpr (CONV) {
       if (geo.ozero) {  // class (0,0) of a stride-2 conv whose other parities have no taps
         const int64_t pix = orow[q] % (int64_t(geo.OH) * geo.OW);
@@ -1502,6 +1568,20 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
       }
     }
   }
+  }
+  if (ep.omax != nullptr) {  // the block's max |C|: one (epoch, value) atomic max
+    __shared__ float s_om[NW];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) om = fmaxf(om, __shfl_xor(om, o));
+    if (lane == 0) s_om[w] = om;
+    lds_barrier();
+    if (t == 0) {
+      float b = s_om[0];
+#pragma unroll
+      for (int k = 1; k < NW; ++k) b = fmaxf(b, s_om[k]);
+      atomicMax(ep.omax + (blockIdx.x % kBoundSlots) * (kBoundStride / 2),
+                (static_cast<unsigned long long>(ep.oepoch) << 32) | __float_as_uint(b));
+    }
   }
   if constexpr (EPI != EPI_NONE) {
     // combine the RPP threads of each chunk through LDS: [RPP][3][BN] floats
@@ -1628,6 +1708,9 @@ struct TnRed {
   int ns, groups;
   const float* amax_y;  // FM 11 (fp16x3): device bounds of |Y| and |X| (operand scales)
   const float* amax_x;
+  // FM 13 (fp16x3 on planes, 16-bit kernel): Y and X are each two fp16 planes h, l of the
+  // operand times 2^e (e from its bound), the l plane yps / xps elements after the h plane
+  int64_t yps, xps;
 };
 
 // sum rows n0..n0+TBN, cols k0..k0+TBK of nsrc [N][K] slices starting at src (slice stride
@@ -1673,10 +1756,14 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y
   constexpr int CY = TBN / EPC, CX = TBK / EPC;        // 16-B chunks per row
   constexpr int RY = 64 / CY, RX = 64 / CX;           // rows per glds wave-instruction
   constexpr int IY = kRows / RY / 4, IX = kRows / RX / 4;  // glds per wave per tile
-  constexpr int NI = IY + IX;
-  constexpr int TILE = kRows * (TBN + TBK);
+  // FM 13: 16-bit staging of TWO planes (h, l) per operand: images YH, YL, XH, XL
+  constexpr bool P13 = FM == 13;
+  constexpr int NPLT = P13 ? 2 : 1;
+  constexpr int NI = (IY + IX) * NPLT;
+  constexpr int TILE = kRows * (TBN + TBK) * NPLT;
   constexpr bool F32 = sizeof(T) == 4;
   static_assert(IY >= 1 && IX >= 1, "tile too small");
+  static_assert(!P13 || (sizeof(T) == 2 && kTnBuf), "FM 13 is the 16-bit kernel on buffer descriptors");
   extern __shared__ __attribute__((aligned(16))) uint16_t smem_raw[];
   T* smem = reinterpret_cast<T*>(smem_raw);
   const T* zline = reinterpret_cast<const T*>(g_zero_line);
@@ -1769,26 +1856,32 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y
   }
   auto issue = [&](int64_t st, int buf) {
     T* Ys = smem + buf * TILE;
-    T* Xs = Ys + kRows * TBN;
+    T* Xs = Ys + kRows * TBN * NPLT;
     const int rs = int(st) * kRows;  // first row of the step, relative to r0
     if constexpr (TBUF) {
       // (the prologue's descriptors may come straight from a v_readfirstlane: 5 wait states)
       if (st < STAGES - 1) asm volatile("s_nop 4" ::: "memory");
       const int64_t left = int64_t(nrows - rs);
       const uint32_t ly = lds0 + uint32_t((buf * TILE + wu * IY * RY * TBN) * TB);
-      const i32x4 ry4 = buf_rsrc(reinterpret_cast<uint64_t>(Y) + uint64_t(((r0 + rs) * ldy + n0) * TB),
-                                 uint32_t(min<int64_t>(left * ldy * TB, int64_t(kBufOob))));
+      const uint32_t ny = uint32_t(min<int64_t>(left * ldy * TB, int64_t(kBufOob)));
 #pragma unroll
-      for (int i = 0; i < IY; ++i) blds16(ry4, voy[i], ly + uint32_t(i * RY * TBN * TB));
-      const uint32_t lx = lds0 + uint32_t((buf * TILE + kRows * TBN + wu * IX * RX * TBK) * TB);
+      for (int pl = 0; pl < NPLT; ++pl) {  // (FM 13: the h plane, then the l plane yps later)
+        const i32x4 ry4 =
+            buf_rsrc(reinterpret_cast<uint64_t>(Y) + uint64_t(((r0 + rs) * ldy + n0 + (P13 ? pl * red.yps : 0)) * TB), ny);
+#pragma unroll
+        for (int i = 0; i < IY; ++i) blds16(ry4, voy[i], ly + uint32_t((pl * kRows * TBN + i * RY * TBN) * TB));
+      }
+      const uint32_t lx = lds0 + uint32_t((buf * TILE + kRows * TBN * NPLT + wu * IX * RX * TBK) * TB);
       if constexpr (CONV) {
-        const i32x4 rx4 = buf_rsrc(xbase);
 #pragma unroll
         for (int i = 0; i < IX; ++i) {
           const int hi = pho[i] * geo.stride - geo.pad + xr[i], wi = pwo[i] * geo.stride - geo.padw + xs[i];
           const bool ok = rs + rx[i] < nrows && unsigned(hi) < unsigned(geo.H) && unsigned(wi) < unsigned(geo.W);
           const uint32_t off = uint32_t(((((pn[i] - pn0) * geo.H + hi) * geo.W + wi) * pitch + xc[i]) * TB);
-          blds16(rx4, ok ? off : kBufOob, lx + uint32_t(i * RX * TBK * TB));
+#pragma unroll
+          for (int pl = 0; pl < NPLT; ++pl)
+            blds16(buf_rsrc(xbase + uint64_t(P13 ? pl * red.xps : 0) * TB), ok ? off : kBufOob,
+                   lx + uint32_t((pl * kRows * TBK + i * RX * TBK) * TB));
           pwo[i] += dw;  // next step's rows (issued strictly in order)
           const int cw = pwo[i] >= geo.Wo;
           pwo[i] -= cw ? geo.Wo : 0;
@@ -1798,10 +1891,14 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y
           pn[i] += dn + ch;
         }
       } else {
-        const i32x4 rx4 = buf_rsrc(reinterpret_cast<uint64_t>(X) + uint64_t(((r0 + rs) * ldx + k0) * TB),
-                                   uint32_t(min<int64_t>(left * ldx * TB, int64_t(kBufOob))));
+        const uint32_t nx = uint32_t(min<int64_t>(left * ldx * TB, int64_t(kBufOob)));
 #pragma unroll
-        for (int i = 0; i < IX; ++i) blds16(rx4, vox[i], lx + uint32_t(i * RX * TBK * TB));
+        for (int pl = 0; pl < NPLT; ++pl) {
+          const i32x4 rx4 =
+              buf_rsrc(reinterpret_cast<uint64_t>(X) + uint64_t(((r0 + rs) * ldx + k0 + (P13 ? pl * red.xps : 0)) * TB), nx);
+#pragma unroll
+          for (int i = 0; i < IX; ++i) blds16(rx4, vox[i], lx + uint32_t((pl * kRows * TBK + i * RX * TBK) * TB));
+        }
       }
       return;
     }
@@ -1844,11 +1941,12 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y
   const int h = g >> 1;
   const int cbase = 2 * (g & 1) + (p >> 1), cbyte = 4 * (p & 1);  // chunk / element offset in it
   const int fr = lane & 31, fh = lane >> 5;
-  // fp32 split products (FM = 1, 11): the small-term accumulators
-  f32x16 lacc[F32 ? TM : 1][F32 ? TN : 1];
+  // fp32 split products (FM = 1, 11, 12, 13): the small-term accumulators
+  constexpr bool LACC = F32 || P13;
+  f32x16 lacc[LACC ? TM : 1][LACC ? TN : 1];
   [[maybe_unused]] int ey = 0, ex = 0;
   [[maybe_unused]] float sy = 1.f, sy11 = 2048.f, sx = 1.f, sx11 = 2048.f;
-  if constexpr (F32 && (FM == 11 || FM == 12)) {
+  if constexpr ((F32 && (FM == 11 || FM == 12)) || P13) {
     ey = fp16_exp(red.amax_y);
     ex = fp16_exp(red.amax_x);
     sy = exp2i(ey);
@@ -1857,9 +1955,9 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y
     sx11 = exp2i(ex + 11);
   }
 #pragma unroll
-  for (int i = 0; i < (F32 ? TM : 1); ++i)
+  for (int i = 0; i < (LACC ? TM : 1); ++i)
 #pragma unroll
-    for (int j = 0; j < (F32 ? TN : 1); ++j)
+    for (int j = 0; j < (LACC ? TN : 1); ++j)
 #pragma unroll
       for (int v = 0; v < 16; ++v) lacc[i][j][v] = 0.f;
 
@@ -1875,12 +1973,12 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y
     asm volatile("" ::: "memory");
     const int buf = int(st % STAGES);
     T* Ys = smem + buf * TILE;
-    T* Xs = Ys + kRows * TBN;
+    T* Xs = Ys + kRows * TBN * NPLT;
     const int64_t valid = r1 - (r0 + st * kRows);
     if (valid < kRows) {  // last, partial step of this split (nothing else in flight)
-      for (int e = t; e < kRows * (CY + CX); e += 256) {
-        const int ey = e < kRows * CY;
-        const int row = ey ? e / CY : (e - kRows * CY) / CX;
+      constexpr int NYC = kRows * CY, NXC = kRows * CX;  // 16-B chunks of one Y / X image
+      for (int e = t; e < NPLT * (NYC + NXC); e += 256) {
+        const int row = e < NPLT * NYC ? (e % NYC) / CY : ((e - NPLT * NYC) % NXC) / CX;
         if (row >= valid) reinterpret_cast<uint4*>(Ys)[e] = make_uint4(0, 0, 0, 0);  // Xs follows Ys
       }
       __syncthreads();
@@ -2028,6 +2126,44 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y
             lacc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], lacc[i][j], 0, 0, 0);
           }
       }
+    } else if constexpr (P13) {
+      // fp16x3 on planes: the staged images are FM 12's after its split (same layout, same
+      // transposed fragment reads), DMA'd straight from the producers' planes
+      const uint16_t* YH = Ys;
+      const uint16_t* YL = YH + kRows * TBN;
+      const uint16_t* XH = Xs;
+      const uint16_t* XL = XH + kRows * TBK;
+#pragma unroll
+      for (int kk = 0; kk < kRows / 16; ++kk) {
+        const int rr = 16 * kk + 8 * h + q;  // row of this lane in the first 4-row block
+        f16x8 ah[TM], al[TM], bh[TN], bl[TN];
+        auto frag = [&](const uint16_t* img, int ld, int ch, auto cy) -> f16x8 {
+          constexpr int CPR = decltype(cy)::value;
+          const s16x4 lo = ds_tr16(img + rr * ld + tswz<uint16_t, CPR>(rr, ch) * 8 + cbyte);
+          const s16x4 hi = ds_tr16(img + (rr + 4) * ld + tswz<uint16_t, CPR>(rr + 4, ch) * 8 + cbyte);
+          return __builtin_bit_cast(f16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        };
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int ch = (wn * WN + i * 32) / 8 + cbase;
+          ah[i] = frag(YH, TBN, ch, std::integral_constant<int, CY>{});
+          al[i] = frag(YL, TBN, ch, std::integral_constant<int, CY>{});
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int ch = (wk * WK + j * 32) / 8 + cbase;
+          bh[j] = frag(XH, TBK, ch, std::integral_constant<int, CX>{});
+          bl[j] = frag(XL, TBK, ch, std::integral_constant<int, CX>{});
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+            lacc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], lacc[i][j], 0, 0, 0);
+            lacc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], lacc[i][j], 0, 0, 0);
+          }
+      }
     } else if constexpr (F32) {
       // v_mfma_f32_32x32x2_f32: lane (fr, fh) supplies Y[row][n0' + fr] and X[row][k0' + fr]
       // of row 2s + fh in step s (32 consecutive floats per half-wave: ds_read_b32, no
@@ -2088,7 +2224,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const T* __restrict__ Y
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] += lacc[i][j];
-  } else if constexpr (F32 && (FM == 11 || FM == 12)) {
+  } else if constexpr ((F32 && (FM == 11 || FM == 12)) || P13) {
     const float iy = exp2i(-ey), ix = exp2i(-ex);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -2853,13 +2989,19 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
       if (!ep.amax_a) throw std::invalid_argument("gemm_nt: fp16 B planes need the A operand's amax bound");
       check_ptr(B + uintptr_t(bps) * 2, "B plane 1");
       fm = 11;
+      if (ep.aps > 0) {  // A as fp16 planes too (FM 13)
+        if (!kF11Buf || lda % 8 || (geo && geo->pitch)) throw std::invalid_argument("gemm_nt: bad A planes");
+        check_ptr(A + uintptr_t(ep.aps) * 2, "A plane 1");
+        fm = 13;
+      }
     }
   } else if (ep.amax_b) {
     throw std::invalid_argument("gemm_nt: amax_b is the scale of fp16 B planes (bps > 0)");
   }
-  if ((F32 && fm == 11 && kF11Buf) || (!F32 && kBf16Buf)) {
+  if (ep.aps > 0 && fm != 13) throw std::invalid_argument("gemm_nt: A planes need fp16 B planes (fp16x3)");
+  if ((F32 && (fm == 11 || fm == 13) && kF11Buf) || (!F32 && kBf16Buf)) {
     // the buffer-descriptor staging keeps every lane offset below 2^31 bytes of its block base
-    const int64_t lim = int64_t(1) << 31, esz = int64_t(sizeof(T));
+    const int64_t lim = int64_t(1) << 31, esz = fm == 13 ? 2 : int64_t(sizeof(T));
     int64_t aspan;
     if (geo) {
       const int64_t hw = int64_t(geo->Ho) * geo->Wo;
@@ -2899,13 +3041,19 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
 #define MPIT_NT_LAUNCH1(BM, BN, ST, EPI, CONV)                                                                       \
   do {                                                                                                             \
     if constexpr (F32 && BM == 256 && BN == 64) { /* fp16x3 only (MPIT_F32_TILE=256x64) */                      \
-      if (fm != 11) throw std::logic_error("gemm_nt: 256 x 64 fp32 tiles are for the fp16x3 kernels");            \
+      if (fm != 11) throw std::logic_error("gemm_nt: 256 x 64 fp32 tiles are for the fp16x3 kernels (FM 11)");    \
       MPIT_NT_OPT_IN(BM, BN, ST, EPI, CONV, 11);                                                                   \
       hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, ST, EPI, CONV, 11>), dim3(unsigned(nb)), dim3(256), shm, s, a,   \
                          lda, b, ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g, bps);                            \
       break;                                                                                                       \
     } else {                                                                                                       \
     if constexpr (F32 && BM == 128 && ST == 2) {                                                                 \
+      if (fm == 13) {                                                                                              \
+        if (shm > 65536) MPIT_NT_OPT_IN(BM, BN, ST, EPI, CONV, 13);                                                 \
+        hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, ST, EPI, CONV, 13>), dim3(unsigned(nb)), dim3(256), shm, s, a, \
+                           lda, b, ldb, c, ldc, M, N, K, ntn, ep, ci, cm, bs, rl, g, bps);                          \
+        break;                                                                                                     \
+      }                                                                                                            \
       if (fm == 11) {                                                                                              \
         if (shm > 65536) MPIT_NT_OPT_IN(BM, BN, ST, EPI, CONV, 11);                                                 \
         hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, ST, EPI, CONV, 11>), dim3(unsigned(nb)), dim3(256), shm, s, a, \
@@ -2984,7 +3132,7 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
     if (ep.fcoef || ep.scoef) fold_plan(ep, dev, s, mtn, ntn);                                                                 \
     /* LDS: the k-tile ring, reused by the epilogue's output tile and reduction table */                      \
     const size_t shm = std::max({size_t(ST) * (size_t(BM) * nt_bkb(BM, BN, fm) +                               \
-                                                (fm == 11 ? size_t(BN) * 128 : fm == 4 || fm >= 9 ? size_t(BN) * 192 : size_t(BN) * nt_bkb(BM, BN, fm))), \
+                                                (fm == 11 || fm == 13 ? size_t(BN) * 128 : fm == 4 || fm >= 9 ? size_t(BN) * 192 : size_t(BN) * nt_bkb(BM, BN, fm))), \
                                  size_t(BM) * BN * sizeof(T), size_t(256) * 8 * 3 * sizeof(float)});          \
     if (geo) MPIT_NT_LAUNCH2(BM, BN, ST, true);                                                           \
     else MPIT_NT_LAUNCH2(BM, BN, ST, false);                                                              \
@@ -2997,7 +3145,7 @@ static void launch_nt_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
       const char* e = std::getenv("MPIT_F32_TILE");
       return e && std::string(e) == "256x64";
     }();
-    if (fm == 11 && N == 64 && t256x64) {
+    if (fm == 11 && N == 64 && t256x64) {  // (FM 13 runs 128-row tiles)
       MPIT_NT_LAUNCH(256, 64, 2);
       hip_check(hipGetLastError(), "gemm_nt launch");
       return;
@@ -3055,6 +3203,9 @@ static EpiArgs epi_args(uintptr_t stats, const BnRed* r, int* mode) {
   if (r) {
     ep.amax_a = reinterpret_cast<const float*>(r->amax_a);
     ep.amax_b = reinterpret_cast<const float*>(r->amax_b);
+    ep.aps = r->aps;
+    ep.omax = reinterpret_cast<unsigned long long*>(r->omax);
+    ep.oepoch = r->oepoch;
   }
   if (stats && r && r->part) throw std::invalid_argument("gemm_nt: stats and BN reduction are exclusive");
   if (stats) {
@@ -3176,7 +3327,7 @@ int64_t gemm_tn_ws_floats(int dev, int64_t M, int N, int K) {
 template <typename T>
 static void launch_tn_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X,
                         int64_t ldx, uintptr_t out, uintptr_t ws, float beta, const ConvGeo* geo, uintptr_t amax_y,
-                        uintptr_t amax_x) {
+                        uintptr_t amax_x, int64_t yps = 0, int64_t xps = 0) {
   constexpr bool F32 = sizeof(T) == 4;
   constexpr int EPC = epc<T>();
   if (!gemm_tn_supported(M, N, K))
@@ -3228,6 +3379,11 @@ static void launch_tn_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
   const int tfm = !F32 || f32_mode() != 1 ? 0 : (amax_y ? (f16s ? 12 : 11) : 1);
   red.amax_y = reinterpret_cast<const float*>(amax_y);
   red.amax_x = reinterpret_cast<const float*>(amax_x);
+  red.yps = yps;
+  red.xps = xps;
+  const bool p13 = !F32 && yps > 0;  // fp32 operands as fp16 planes (launch_tn)
+  if (p13 && (!amax_y || !amax_x || xps <= 0 || !kTnBuf || (geo && geo->pitch)))
+    throw std::invalid_argument("gemm_tn: fp16 planes need both bounds and plane strides");
   const int ngr = ns > kReduceGroup ? int(tn_groups(ns)) : 1;
   const bool fused = !direct && fused_env && int64_t(ntiles) * (ngr + 1) <= kTnMaxTickets;
   if (fused) {
@@ -3247,7 +3403,7 @@ static void launch_tn_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
     const char* e = std::getenv("MPIT_GEMM_TN_STAGES");
     return e && std::atoi(e) <= 2 ? 2 : 4;
   }();
-  const int stages = F32 ? 2 : tn_stages;
+  const int stages = F32 || p13 ? 2 : tn_stages;
   // fp32 128 x 128 tiles, MPIT_TN_F32S=1: the split-once kernel (experiment; bitwise equal,
   // slower so far: profiles/wgrad_split_once_r03.md)
   static const bool f32s = [] {
@@ -3329,7 +3485,38 @@ static void launch_tn_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
   }();
   bool done64 = false;
   if constexpr (!F32) {
-    if (kr64_stages && !fused) {
+    if (p13) {  // fp16x3 planes: 32-row steps on a 2-deep ring (FM 12's LDS)
+#define MPIT_TN_P13(A, B)                                                                                          \
+  do {                                                                                                             \
+    const size_t shm = size_t(2) * kRows * (tbn + tbk) * 2 * sizeof(T);                                             \
+    if (geo) {                                                                                                     \
+      if (shm > 65536) MPIT_TN_OPT_IN13(A, B, true);                                                               \
+      hipLaunchKernelGGL((gemm_tn_kernel<T, A, B, 2, true, 13, kRows>), grid, dim3(256), shm, s, y, ldy, x, ldx,   \
+                         part, M, N, K, rps, ntk, ntiles, g, red);                                                 \
+    } else {                                                                                                       \
+      if (shm > 65536) MPIT_TN_OPT_IN13(A, B, false);                                                              \
+      hipLaunchKernelGGL((gemm_tn_kernel<T, A, B, 2, false, 13, kRows>), grid, dim3(256), shm, s, y, ldy, x, ldx,  \
+                         part, M, N, K, rps, ntk, ntiles, g, red);                                                 \
+    }                                                                                                              \
+  } while (0)
+#define MPIT_TN_OPT_IN13(A, B, CV)                                                                                 \
+  do {                                                                                                             \
+    static const bool opted = (hip_check(hipFuncSetAttribute(reinterpret_cast<const void*>(                       \
+                                                             &gemm_tn_kernel<T, A, B, 2, CV, 13, kRows>),         \
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize, int(shm)),    \
+                                     "hipFuncSetAttribute"),                                                       \
+                               true);                                                                              \
+    (void)opted;                                                                                                   \
+  } while (0)
+      if (tbn == 128 && tbk == 128) MPIT_TN_P13(128, 128);
+      else if (tbn == 128) MPIT_TN_P13(128, 64);
+      else if (tbk == 128) MPIT_TN_P13(64, 128);
+      else MPIT_TN_P13(64, 64);
+#undef MPIT_TN_P13
+#undef MPIT_TN_OPT_IN13
+      done64 = true;
+    }
+    if (!done64 && kr64_stages && !fused) {
 #define MPIT_TN_K64(A, B, ST)                                                                                      \
   do {                                                                                                             \
     const size_t shm = size_t(ST) * 64 * (tbn + tbk) * sizeof(T);                                                  \
@@ -3399,15 +3586,23 @@ static void launch_tn_t(int dev, hipStream_t s, int64_t M, int N, int K, uintptr
 
 static void launch_tn(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X,
                       int64_t ldx, uintptr_t out, uintptr_t ws, float beta, const ConvGeo* geo, bool f32,
-                      uintptr_t amax_y = 0, uintptr_t amax_x = 0) {
+                      uintptr_t amax_y = 0, uintptr_t amax_x = 0, int64_t yps = 0, int64_t xps = 0) {
+  // fp32 operands given as fp16 planes (yps / xps > 0): the 16-bit kernel's FM 13
+  if (f32 && (yps > 0 || xps > 0)) {
+    if (yps <= 0 || xps <= 0) throw std::invalid_argument("gemm_tn: both operands must be planes (FM 13)");
+    if (f32_mode() != 1) throw std::invalid_argument("gemm_tn: fp16 planes are the fp16x3 path");
+    launch_tn_t<uint16_t>(dev, s, M, N, K, Y, ldy, X, ldx, out, ws, beta, geo, amax_y, amax_x, yps, xps);
+    return;
+  }
   if (f32) launch_tn_t<float>(dev, s, M, N, K, Y, ldy, X, ldx, out, ws, beta, geo, amax_y, amax_x);
-  else if (amax_y || amax_x) throw std::invalid_argument("gemm_tn: operand bounds are for fp32 (fp16x3) calls");
+  else if (amax_y || amax_x || yps || xps) throw std::invalid_argument("gemm_tn: operand bounds are for fp32 (fp16x3) calls");
   else launch_tn_t<uint16_t>(dev, s, M, N, K, Y, ldy, X, ldx, out, ws, beta, geo, 0, 0);
 }
 
 void gemm_tn(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X, int64_t ldx,
-             uintptr_t out, uintptr_t ws, float beta, bool f32, uintptr_t amax_y, uintptr_t amax_x) {
-  launch_tn(dev, s, M, N, K, Y, ldy, X, ldx, out, ws, beta, nullptr, f32, amax_y, amax_x);
+             uintptr_t out, uintptr_t ws, float beta, bool f32, uintptr_t amax_y, uintptr_t amax_x, int64_t yps,
+             int64_t xps) {
+  launch_tn(dev, s, M, N, K, Y, ldy, X, ldx, out, ws, beta, nullptr, f32, amax_y, amax_x, yps, xps);
 }
 
 // ------------------------------------------------------------------ convolutions
@@ -3448,13 +3643,13 @@ int64_t conv_wgrad_ws_floats(int dev, int Nb, int H, int W, int C, int Co, int R
 
 void conv_wgrad(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad,
                 uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, float beta, bool f32, uintptr_t amax_y,
-                uintptr_t amax_x) {
+                uintptr_t amax_x, int64_t yps, int64_t xps) {
   if (C % 64 || Co % 64) throw std::invalid_argument("conv_wgrad: need C % 64 == 0 and Co % 64 == 0");
   if (int64_t(Nb) * H * W * C >= (int64_t(1) << 31)) throw std::invalid_argument("conv_wgrad: input too large");
   int Ho, Wo;
   const ConvGeo g = conv_geo(H, W, C, R, S, stride, pad, &Ho, &Wo);
   const int64_t M = int64_t(Nb) * Ho * Wo;
-  launch_tn(dev, s, M, Co, R * S * C, dy, Co, x, C, dw, ws, beta, &g, f32, amax_y, amax_x);
+  launch_tn(dev, s, M, Co, R * S * C, dy, Co, x, C, dw, ws, beta, &g, f32, amax_y, amax_x, yps, xps);
 }
 
 // Row-tap stem convolution: x is a zero-padded NHWC4 image [Nb][Hp][Wp][4] (bf16 / fp32), the

@@ -79,6 +79,20 @@ void gather_scale(int dev, hipStream_t s, const std::vector<uintptr_t>& srcs, co
 // mask: ReLU bit mask written by the forward (bn_mask_bytes: one byte per 8 channels, either
 // dtype) and read by the backward. C % 8 == 0.
 int64_t bn_workspace_floats(int C);
+// fp16 planes output of an fp32 apply pass (the fp16x3 GEMMs then split nothing: gemm.hip
+// FM 13). The pass writes h, l = the two fp16 planes of out * 2^e (h at element i, l at
+// element i + numel of the 16-bit view of the output), e from a bound of |out| known BEFORE
+// the pass: the maxima of its inputs (xmax / xmax2 / gmax: epoch slots a GEMM epilogue raised,
+// gemm.hip EpiArgs::omax; rbound: the residual's bound) times its per-channel coefficients.
+// obound (kBoundFloats) receives that bound in slot 0 (the other slots 0) for the consumers.
+// rplanes: the residual arrives as planes (decoded with rbound's scale).
+struct PlaneSpec {
+  uintptr_t obound = 0;
+  uintptr_t xmax = 0, xmax2 = 0, gmax = 0;
+  uint32_t xep = 0, xep2 = 0, gep = 0;
+  uintptr_t rbound = 0;
+  int rplanes = 0;
+};
 int64_t bn_mask_bytes(bool bf16, int64_t M, int C);
 // stats / nstat (optional): the statistics of x as per-128-row-tile (mean, M2) partials
 // [nstat][2][C] emitted by the GEMM that produced x (EPI_STATS) — the statistics pass over
@@ -86,7 +100,8 @@ int64_t bn_mask_bytes(bool bf16, int64_t M, int C);
 void bn_act_fwd(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res, uintptr_t y, int64_t M, int C,
                 uintptr_t gamma, uintptr_t beta, uintptr_t rmean, uintptr_t rvar, uintptr_t save_mean,
                 uintptr_t save_rstd, uintptr_t ws, float momentum, float eps, bool relu, uintptr_t mask,
-                uintptr_t stats = 0, int64_t nstat = 0, uintptr_t amax = 0, uintptr_t coef = 0);
+                uintptr_t stats = 0, int64_t nstat = 0, uintptr_t amax = 0, uintptr_t coef = 0,
+                const PlaneSpec* planes = nullptr);
 // amax (optional, fp32 [1]): max |y| over the tensor (bn_act_bwd: max |dx|), the scale bound of the
 // fp16x3 GEMMs that read it: zeroed by this call's finalize, raised by its apply pass. With
 // y / dx null (the coefficient-only calls of a bn_pair) amax is only zeroed, for the pair
@@ -100,7 +115,7 @@ void bn_act_apply(int dev, hipStream_t s, bool bf16, uintptr_t x, uintptr_t res,
 void bn_act_bwd(int dev, hipStream_t s, bool bf16, uintptr_t dy, uintptr_t mask, uintptr_t x, uintptr_t dx,
                 uintptr_t dres, int64_t M, int C, uintptr_t gamma, uintptr_t mean, uintptr_t rstd, uintptr_t dgamma,
                 uintptr_t dbeta, uintptr_t ws, bool relu, uintptr_t part = 0, int64_t npart = 0,
-                uintptr_t coef = 0, uintptr_t amax = 0);
+                uintptr_t coef = 0, uintptr_t amax = 0, const PlaneSpec* planes = nullptr);
 // coef (optional): the apply coefficients [3][C] already computed (the finalize folded into
 // the GEMM that wrote dy, BnRed::fcoef; dgamma / dbeta written there too): apply pass only.
 
@@ -110,12 +125,14 @@ void bn_act_bwd(int dev, hipStream_t s, bool bf16, uintptr_t dy, uintptr_t mask,
 // y = relu(bn1(x1) + bn2(x2)) from the two forward coefficient sets, and the backward
 // dx1 / dx2 from the two backward sets, one pass each.
 void bn_pair_apply(int dev, hipStream_t s, uintptr_t x1, uintptr_t coef1, uintptr_t x2, uintptr_t coef2, uintptr_t y,
-                   int64_t M, int C, uintptr_t mask, bool f32 = false, uintptr_t amax = 0, uintptr_t scratch = 0);
+                   int64_t M, int C, uintptr_t mask, bool f32 = false, uintptr_t amax = 0, uintptr_t scratch = 0,
+                   const PlaneSpec* planes = nullptr);
 // amax / amax1 / amax2: raised by the pass (zeroed beforehand: the bn_act_fwd / bwd coefficient
 // calls of the pair zero them); scratch: unused (kept for the call signature)
 void bn_pair_bwd_apply(int dev, hipStream_t s, uintptr_t dy, uintptr_t mask, uintptr_t x1, uintptr_t coef1,
                        uintptr_t dx1, uintptr_t x2, uintptr_t coef2, uintptr_t dx2, int64_t M, int C, bool f32 = false,
-                       uintptr_t amax1 = 0, uintptr_t amax2 = 0, uintptr_t scratch = 0);
+                       uintptr_t amax1 = 0, uintptr_t amax2 = 0, uintptr_t scratch = 0,
+                       const PlaneSpec* planes1 = nullptr, const PlaneSpec* planes2 = nullptr);
 
 // ---- MFMA GEMMs for NHWC 1x1 convolutions (gemm.hip), fp32 accumulate -------------------
 // Operands and outputs are bf16 (v_mfma_f32_32x32x16_bf16) or, with f32 = true, fp32
@@ -162,6 +179,13 @@ struct BnRed {
   // that held only pairs of earlier launches (zeroed once, never garbage): the tagged fold
   // protocol of gemm.hip, in which no block waits for its own output stores
   int ftag = 0;
+  // aps > 0 (with amax_b): A is two fp16 planes h, l of A * 2^e (e from amax_a), the l plane
+  // aps elements after the h plane (gemm.hip FM 13: nothing split in the kernel)
+  int64_t aps = 0;
+  // omax (fp32 GEMMs): the launch's max |C| as 64-bit (epoch oepoch, value) maxima in kBoundSlots
+  // slots kBoundStride floats apart (planes.h epoch_max reads them)
+  uintptr_t omax = 0;
+  uint32_t oepoch = 0;
 };
 int64_t gemm_nt_fold_lvl_floats(int N);
 bool gemm_nt_supported(int64_t M, int N, int K, bool f32 = false);
@@ -180,7 +204,8 @@ int device_cu_count(int dev);
 uintptr_t stream_create_cu_masked(int dev, const std::vector<uint32_t>& mask);
 // amax_y / amax_x (fp32, both or neither): device bounds of |Y|, |X| -> fp16x3 split products
 void gemm_tn(int dev, hipStream_t s, int64_t M, int N, int K, uintptr_t Y, int64_t ldy, uintptr_t X, int64_t ldx,
-             uintptr_t out, uintptr_t ws, float beta, bool f32 = false, uintptr_t amax_y = 0, uintptr_t amax_x = 0);
+             uintptr_t out, uintptr_t ws, float beta, bool f32 = false, uintptr_t amax_y = 0, uintptr_t amax_x = 0, int64_t yps = 0,
+             int64_t xps = 0);
 // fp32 w[R][T][Cc] -> bf16 wb[R][T][Cc] (optional) and bf16 tap-flipped transpose
 // wt[Cc][T-1-t][R] (optional); T = 1 is the plain transpose
 void cast_transpose(int dev, hipStream_t s, uintptr_t w, int R, int Cc, uintptr_t wb, uintptr_t wt, int taps = 1,
@@ -227,7 +252,8 @@ void relu_bias_bwd(int dev, hipStream_t s, int64_t M, int C, uintptr_t dy, uintp
 int64_t conv_wgrad_ws_floats(int dev, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad);
 void conv_wgrad(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad,
                 uintptr_t dy, uintptr_t x, uintptr_t dw, uintptr_t ws, float beta, bool f32 = false,
-                uintptr_t amax_y = 0, uintptr_t amax_x = 0);
+                uintptr_t amax_y = 0, uintptr_t amax_x = 0, int64_t yps = 0,
+                int64_t xps = 0);
 
 // Row-tap stem conv (7x7 / stride-2 / 3-channel ResNet stem on MFMA; VGG's 3x3 / 3-channel
 // first layer with rows = 3): x = zero-padded NHWC4 image [Nb][Hp][Wp][4], w = [Co][rows][8][4]
@@ -249,8 +275,9 @@ int stem_wgrad_rows(int rows);
 
 // ---- NHWC bf16 / fp32 max pooling with a uint8 argmax per output element (pool.hip) ---
 // x [N,H,W,C] -> y, idx [N,Ho,Wo,C]; dx [N,H,W,C] gathered from dy + idx (no atomics).
+// obound (fp32, with ibound: x's slotted bound): y as fp16 planes (planes.h) scaled by x's bound
 void maxpool_fwd(int dev, hipStream_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t x,
-                 uintptr_t y, uintptr_t idx, bool f32 = false);
+                 uintptr_t y, uintptr_t idx, bool f32 = false, uintptr_t ibound = 0, uintptr_t obound = 0);
 // ypool (optional): the pool's output, when its input is a ReLU'd conv(+bias) output: dx is
 // then that conv's dz = dx * (y > 0), and db (optional, fp32 [C]) its bias gradient; ws:
 // maxpool_bwd_ws_floats(C) floats. Needs 256 % (C / 8) == 0.

@@ -15,6 +15,7 @@
 
 #include "ew.h"
 #include "kernels.h"
+#include "planes.h"
 
 namespace mpit {
 namespace {
@@ -51,8 +52,16 @@ __device__ __forceinline__ void st8(float* p, const float (&f)[8]) {
 // divisions are emulated and made these kernels 2.5x slower than their bytes)
 template <typename T, typename I>
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
-                                                          uint8_t* __restrict__ idx, PoolGeo g) {
+                                                          uint8_t* __restrict__ idx, PoolGeo g,
+                                                          const float* __restrict__ ibound, float* obound) {
   const I cv = I(g.C / 8);
+  // fp16 planes output (fp32, obound != null): every output is one of the inputs, so the
+  // input's bound is the output's (planes.h)
+  [[maybe_unused]] PlaneScale ps{1.f, 2048.f};
+  const int64_t nel = int64_t(g.N) * g.Ho * g.Wo * g.C;
+  if constexpr (sizeof(T) == 4) {
+    if (obound) ps = plane_scale(slots_max_wave(ibound), obound);
+  }
   const I total = I(g.N) * I(g.Ho) * I(g.Wo) * cv;
   for (I t = I(blockIdx.x) * blockDim.x + threadIdx.x; t < total; t += I(gridDim.x) * blockDim.x) {
     const int c8 = int(t % cv);
@@ -88,7 +97,16 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const T* __restrict__ 
         }
       }
     }
-    st8(y + int64_t(pix) * g.C + c8 * 8, best);
+    if (sizeof(T) == 4 && obound) {
+      uint32_t hw[4], lw[4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) split_pair(best[2 * p], best[2 * p + 1], ps, hw[p], lw[p]);
+      uint16_t* yh = reinterpret_cast<uint16_t*>(y) + int64_t(pix) * g.C + c8 * 8;
+      *reinterpret_cast<uint4*>(yh) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+      *reinterpret_cast<uint4*>(yh + nel) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+    } else {
+      st8(y + int64_t(pix) * g.C + c8 * 8, best);
+    }
     uint2 a;
     a.x = uint32_t(arg[0]) | (uint32_t(arg[1]) << 8) | (uint32_t(arg[2]) << 16) | (uint32_t(arg[3]) << 24);
     a.y = uint32_t(arg[4]) | (uint32_t(arg[5]) << 8) | (uint32_t(arg[6]) << 16) | (uint32_t(arg[7]) << 24);
@@ -286,7 +304,7 @@ unsigned grid_for(int64_t work) { return unsigned(std::min<int64_t>((work + 255)
 
 template <typename T>
 void maxpool_fwd_t(int dev, hipStream_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t x,
-                   uintptr_t y, uintptr_t idx) {
+                   uintptr_t y, uintptr_t idx, uintptr_t ibound, uintptr_t obound) {
   const PoolGeo g = pool_geo(N, H, W, C, K, stride, pad);
   if ((x | y) % 16 || idx % 8) throw std::invalid_argument("maxpool_fwd: misaligned buffers");
   hip_check(hipSetDevice(dev), "hipSetDevice");
@@ -295,7 +313,8 @@ void maxpool_fwd_t(int dev, hipStream_t s, int N, int H, int W, int C, int K, in
   const bool narrow = work + int64_t(grid_for(work)) * 256 < (int64_t(1) << 32);
   auto* k = narrow ? maxpool_fwd_kernel<T, uint32_t> : maxpool_fwd_kernel<T, int64_t>;
   hipLaunchKernelGGL(k, dim3(grid_for(work)), dim3(256), 0, s, reinterpret_cast<const T*>(x),
-                     reinterpret_cast<T*>(y), reinterpret_cast<uint8_t*>(idx), g);
+                     reinterpret_cast<T*>(y), reinterpret_cast<uint8_t*>(idx), g,
+                     reinterpret_cast<const float*>(ibound), reinterpret_cast<float*>(obound));
   hip_check(hipGetLastError(), "maxpool_fwd launch");
 }
 
@@ -352,9 +371,10 @@ void avgpool_bwd(int dev, hipStream_t s, int N, int HW, int C, uintptr_t dy, uin
 }
 
 void maxpool_fwd(int dev, hipStream_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t x,
-                 uintptr_t y, uintptr_t idx, bool f32) {
-  if (f32) maxpool_fwd_t<float>(dev, s, N, H, W, C, K, stride, pad, x, y, idx);
-  else maxpool_fwd_t<uint16_t>(dev, s, N, H, W, C, K, stride, pad, x, y, idx);
+                 uintptr_t y, uintptr_t idx, bool f32, uintptr_t ibound, uintptr_t obound) {
+  if (obound && (!f32 || !ibound)) throw std::invalid_argument("maxpool_fwd: fp16 planes need fp32 and the input's bound");
+  if (f32) maxpool_fwd_t<float>(dev, s, N, H, W, C, K, stride, pad, x, y, idx, ibound, obound);
+  else maxpool_fwd_t<uint16_t>(dev, s, N, H, W, C, K, stride, pad, x, y, idx, 0, 0);
 }
 
 void maxpool_bwd(int dev, hipStream_t s, int N, int H, int W, int C, int K, int stride, int pad, uintptr_t dy,

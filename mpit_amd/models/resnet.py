@@ -179,6 +179,32 @@ class ResNet(nn.Module):
                     nn.init.zeros_(m.bn3.weight)
                 elif isinstance(m, BasicBlock):
                     nn.init.zeros_(m.bn2.weight)
+        self._plan_planes()
+
+    def _plan_planes(self):
+        """fp32 steps: which tensors are written as fp16 planes (ops/conv.py _F32_PLANES) —
+        every activation and gradient that only GEMMs (and the residual adds, which decode them)
+        read: the stem pool's output, each block's BN outputs and its BNs' input gradients. Not
+        the stem BN's (it feeds the pool; its gradient feeds the row-tap stem wgrad), and not at
+        the end of the network: the last block's output feeds the average pool, its last BN's
+        gradient comes from that pool (no producing GEMM to know its max), so the last
+        convolution's input and gradient stay fp32 (a backward-weight GEMM takes both operands
+        as planes or neither)."""
+        if not isinstance(self.bn1, BatchNormAct2d) or not isinstance(self.maxpool, MaxPool2dNHWC):
+            return
+        self.maxpool.out_planes = True
+        blocks = [b for layer in (self.layer1, self.layer2, self.layer3, self.layer4) for b in layer]
+        for b in blocks:
+            bns = [b.bn1, b.bn2] + ([b.bn3] if isinstance(b, Bottleneck) else [])
+            if b.downsample is not None and len(b.downsample) == 2:
+                bns.append(b.downsample[1])
+            for bn in bns:
+                if isinstance(bn, BatchNormAct2d):
+                    bn.out_planes = bn.grad_planes = True
+        last = blocks[-1]
+        feed_last, out_last = (last.bn2, last.bn3) if isinstance(last, Bottleneck) else (last.bn1, last.bn2)
+        feed_last.out_planes = False
+        out_last.out_planes = out_last.grad_planes = False
 
     def _make(self, block, planes, blocks, stride=1):
         down = None

@@ -29,7 +29,7 @@ import torch.nn.functional as F
 
 from .._ext import native
 from . import conv as _conv
-from .conv import set_amax
+from .conv import amax_of, omax_buf, omax_of, planes_of, set_amax, set_planes
 
 
 def _rows(x: torch.Tensor):
@@ -42,7 +42,8 @@ def _cl(x: torch.Tensor) -> torch.Tensor:
 
 
 # how often each fused hand-over fired (tests assert the fused path ran)
-COUNTERS = {"fwd_tile_stats": 0, "fwd_folded": 0, "bwd_linked": 0, "bwd_folded": 0}
+COUNTERS = {"fwd_tile_stats": 0, "fwd_folded": 0, "bwd_linked": 0, "bwd_folded": 0, "fwd_planes": 0,
+            "bwd_planes": 0}
 
 
 class BNLink:
@@ -56,9 +57,12 @@ class BNLink:
     several consumers it falls back to its own reduction pass."""
 
     __slots__ = ("x", "mask", "mean", "part", "npart", "dy_ptr", "dy_ver", "x2", "mean2", "part2", "w", "rstd",
-                 "fold")
+                 "fold", "gbuf", "gep")
 
     def __init__(self):
+        # gbuf: the epoch slots where the consumer's backward-data GEMM leaves max |dy| (gep: its
+        # launch epoch) when this BN's backward writes fp16 planes (ops/conv.py _red_args)
+        self.gbuf, self.gep = None, 0
         self.x = self.mask = self.mean = self.part = None
         self.x2 = self.mean2 = self.part2 = None  # the shortcut BN of a bn_pair
         self.w = self.rstd = None  # BN weight (fp32) and 1/std: the consumer may fold the finalize
@@ -163,12 +167,40 @@ def _amax_buf(x: torch.Tensor):
     return torch.empty(_conv.BOUND_FLOATS, dtype=torch.float32, device=x.device) if _want_amax(x) else None
 
 
+def _fwd_planes(bn, x: torch.Tensor, residual: Optional[torch.Tensor], out: bool):
+    """(PlaneSpec dict for the native call or None, the output planes' bound or None) of an fp32
+    forward: a residual given as fp16 planes is always decoded (its bound); the output is written
+    as planes when ``out`` (the BN's consumers are GEMMs) and the input's max is known."""
+    if not (x.is_cuda and x.dtype == torch.float32):
+        return None, None
+    spec, obound = {}, None
+    if residual is not None:
+        rp = planes_of(residual)
+        if rp is not None:
+            spec.update(rbound=rp.data_ptr(), rplanes=1)
+        elif out:
+            ra = amax_of(residual)
+            if ra is None:
+                out = False
+            else:
+                spec.update(rbound=ra.data_ptr())
+    om = omax_of(x) if out else None
+    if om is not None and _conv._F32_PLANES:
+        obound = torch.empty(_conv.BOUND_FLOATS, dtype=torch.float32, device=x.device)
+        spec.update(obound=obound.data_ptr(), xmax=om[0].data_ptr(), xep=om[1])
+    elif spec.get("rplanes") != 1:
+        return None, None
+    else:
+        spec.pop("obound", None)
+    return spec, obound
+
+
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, residual, momentum, eps, relu, res_slot=None,
-                tstats=None, link=None, amax=None):
+                tstats=None, link=None, amax=None, planes=None):
         x = _cl(x)
-        if residual is not None:
+        if residual is not None and planes_of(residual) is None:
             residual = _cl(residual).to(x.dtype)
         M, C = _rows(x)
         m = native()
@@ -199,8 +231,10 @@ class _BNActFn(torch.autograd.Function):
                      mask.data_ptr() if mask is not None else 0,
                      stats=ts[0].data_ptr() if ts is not None else 0, nstat=ts[1] if ts is not None else 0,
                      amax=amax.data_ptr() if amax is not None else 0,
-                     coef=fold.coef.data_ptr() if fold is not None else 0)
+                     coef=fold.coef.data_ptr() if fold is not None else 0, planes=planes)
         ctx.save_for_backward(x, mask, w, mean, rstd)
+        # fp16-planes backward (dx read only by GEMMs): max |x| of the forward for its bound
+        ctx.xmax = omax_of(x) if (planes is not None or getattr(link, "gbuf", None) is not None) else None
         ctx.link = link
         if link is not None:
             link.x, link.mask, link.mean = x, mask, mean
@@ -230,8 +264,17 @@ class _BNActFn(torch.autograd.Function):
         ws = torch.empty(m.bn_workspace_floats(C), dtype=torch.float32, device=x.device)
         # reductions folded into the consumer convolution's backward-data GEMM (BNLink); with
         # a folded finalize the GEMM also left the coefficients, dgamma and dbeta
+        gm = (ctx.link.gbuf, ctx.link.gep) if ctx.link is not None else (None, 0)
         part, npart = ctx.link.take(dy) if ctx.link is not None else (None, 0)
         fold = ctx.link.take_fold() if part is not None else None
+        # dx as fp16 planes: the consumer's GEMM wrote this very dy (linked) with its max, and the
+        # forward's input max is known; not with a residual gradient to write
+        pspec, pbound = None, None
+        if (part is not None and gm[0] is not None and gm[1] and getattr(ctx, "xmax", None) is not None
+                and dres is None and x.dtype == torch.float32):
+            pbound = torch.empty(_conv.BOUND_FLOATS, dtype=torch.float32, device=x.device)
+            pspec = dict(obound=pbound.data_ptr(), gmax=gm[0].data_ptr(), gep=gm[1], xmax=ctx.xmax[0].data_ptr(),
+                         xep=ctx.xmax[1])
         coef = 0
         if part is not None:
             COUNTERS["bwd_linked"] += 1
@@ -252,8 +295,11 @@ class _BNActFn(torch.autograd.Function):
                      mean.data_ptr(), rstd.data_ptr(), dgamma.data_ptr() if dgamma is not None else 0,
                      dbeta.data_ptr() if dbeta is not None else 0, ws.data_ptr(), bool(ctx.relu),
                      part=part.data_ptr() if part is not None else 0, npart=npart, coef=coef,
-                     amax=amax.data_ptr() if amax is not None else 0)
-        if amax is not None:
+                     amax=amax.data_ptr() if amax is not None else 0, planes=pspec)
+        if pbound is not None:
+            set_planes(dx, pbound)
+            COUNTERS["bwd_planes"] += 1
+        elif amax is not None:
             set_amax(dx, amax)
         if ctx.res_slot is not None:  # the shortcut's gradient is added by the block's first conv
             if park:
@@ -262,7 +308,7 @@ class _BNActFn(torch.autograd.Function):
             elif not ctx.res_slot.put(dres):
                 raise RuntimeError("GradSlot consumer ran before the BN backward")
             dres = None
-        return dx, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None
+        return dx, dgamma, dbeta, None, None, dres, None, None, None, None, None, None, None, None
 
 
 def bn_act_eval(x, weight, bias, running_mean, running_var, eps, residual=None, relu=True):
@@ -298,6 +344,11 @@ class BatchNormAct2d(nn.BatchNorm2d):
         # count is kept on the host and folded into the buffer when the state is read
         # (one tiny "+= 1" kernel per BN per step otherwise: 53 launches in ResNet-50)
         self._nbt_pending = 0
+        # fp32 steps: out_planes — the output is read only by fp16x3 GEMMs (and planes-aware
+        # residual adds): written as fp16 planes (ops/conv.py _F32_PLANES); grad_planes — the
+        # input gradient is read only by GEMMs: dx as planes. Set by the model that knows.
+        self.out_planes = False
+        self.grad_planes = False
 
     def sync_num_batches_tracked(self):
         if self._nbt_pending:
@@ -344,11 +395,20 @@ class BatchNormAct2d(nn.BatchNorm2d):
             fold = ts[2] if ts is not None else None
             # a folded finalize zeroed its own output bound (the apply pass raises it)
             amax = fold.amax if (fold is not None and _want_amax(x)) else _amax_buf(x)
+            spec, obound = _fwd_planes(self, x, residual, self.out_planes)
+            if obound is not None:
+                amax = None
+            if link is not None and self.grad_planes and _conv._F32_PLANES and x.dtype == torch.float32 \
+                    and self.running_mean is not None:
+                link.gbuf = omax_buf(self.running_mean, "g", x.device)
             y = _BNActFn.apply(x, self.weight, self.bias, rm, rv, residual, momentum, self.eps, self.act,
-                               res_slot, ts, link, amax)
+                               res_slot, ts, link, amax, spec)
             if link is not None:
                 y._mpit_bnlink = link
-            if amax is not None:
+            if obound is not None:
+                set_planes(y, obound)
+                COUNTERS["fwd_planes"] += 1
+            elif amax is not None:
                 set_amax(y, amax)
             return y
         return bn_act_eval(x, self.weight, self.bias, self.running_mean, self.running_var, self.eps, residual, self.act)
@@ -363,7 +423,8 @@ class _BNPairFn(torch.autograd.Function):
     residual-gradient tensor of the unpaired form."""
 
     @staticmethod
-    def forward(ctx, x1, w1, b1, rm1, rv1, x2, w2, b2, rm2, rv2, mom1, eps1, mom2, eps2, ts1, ts2, link, amax=None):
+    def forward(ctx, x1, w1, b1, rm1, rv1, x2, w2, b2, rm2, rv2, mom1, eps1, mom2, eps2, ts1, ts2, link, amax=None,
+                planes=None):
         x1, x2 = _cl(x1), _cl(x2).to(x1.dtype)
         M, C = _rows(x1)
         m = native()
@@ -402,13 +463,14 @@ class _BNPairFn(torch.autograd.Function):
         # (scratch of the output bound: bn1's workspace past its coefficients)
         m.bn_pair_apply(dev, stream, x1.data_ptr(), outs[0][3].data_ptr(), x2.data_ptr(), outs[1][3].data_ptr(),
                         y.data_ptr(), M, C, mask.data_ptr(), f32=not bf16,
-                        amax=amax.data_ptr() if amax is not None else 0)
+                        amax=amax.data_ptr() if amax is not None else 0, planes=planes)
         (wf1, mean1, rstd1, _), (wf2, mean2, rstd2, _) = outs
         ctx.save_for_backward(x1, x2, mask, wf1, mean1, rstd1, wf2, mean2, rstd2)
         ctx.has = (w1 is not None, b1 is not None, w2 is not None, b2 is not None)
         ctx.link = link
         if link is not None:
             link.x, link.mask, link.mean, link.x2, link.mean2 = x1, mask, mean1, x2, mean2
+        ctx.xmax = (omax_of(x1), omax_of(x2)) if getattr(link, "gbuf", None) is not None else None
         return y
 
     @staticmethod
@@ -418,7 +480,11 @@ class _BNPairFn(torch.autograd.Function):
         M, C = _rows(x1)
         m = native()
         dev, stream = x1.device.index, torch.cuda.current_stream(x1.device).cuda_stream
+        gm = (ctx.link.gbuf, ctx.link.gep) if ctx.link is not None else (None, 0)
         part, npart, part2 = ctx.link.take(dy, pair=True) if ctx.link is not None else (None, 0, None)
+        xm = getattr(ctx, "xmax", None)
+        planes = (part is not None and gm[0] is not None and gm[1] and xm is not None and xm[0] is not None
+                  and xm[1] is not None and x1.dtype == torch.float32)
         if part is not None:
             COUNTERS["bwd_linked"] += 2
         f32 = dict(dtype=torch.float32, device=x1.device)
@@ -438,15 +504,26 @@ class _BNPairFn(torch.autograd.Function):
             wss.append(ws)
         dx1 = torch.empty_like(x1, memory_format=torch.channels_last)
         dx2 = torch.empty_like(x2, memory_format=torch.channels_last)
+        p1 = p2 = None
+        if planes:
+            pb1 = torch.empty(_conv.BOUND_FLOATS, **f32)
+            pb2 = torch.empty(_conv.BOUND_FLOATS, **f32)
+            p1 = dict(obound=pb1.data_ptr(), gmax=gm[0].data_ptr(), gep=gm[1], xmax=xm[0][0].data_ptr(), xep=xm[0][1])
+            p2 = dict(obound=pb2.data_ptr(), gmax=gm[0].data_ptr(), gep=gm[1], xmax=xm[1][0].data_ptr(), xep=xm[1][1])
         m.bn_pair_bwd_apply(dev, stream, dy.data_ptr(), mask.data_ptr(), x1.data_ptr(), wss[0].data_ptr(),
                             dx1.data_ptr(), x2.data_ptr(), wss[1].data_ptr(), dx2.data_ptr(), M, C,
                             f32=x1.dtype == torch.float32, amax1=am1.data_ptr() if am1 is not None else 0,
-                            amax2=am2.data_ptr() if am2 is not None else 0)
-        if am1 is not None:
+                            amax2=am2.data_ptr() if am2 is not None else 0, planes1=p1, planes2=p2)
+        if planes:
+            set_planes(dx1, pb1)
+            set_planes(dx2, pb2)
+            COUNTERS["bwd_planes"] += 2
+        elif am1 is not None:
             set_amax(dx1, am1)
             set_amax(dx2, am2)
         (dg1, db1), (dg2, db2) = grads
-        return (dx1, dg1, db1, None, None, dx2, dg2, db2, None, None, None, None, None, None, None, None, None, None)
+        return (dx1, dg1, db1, None, None, dx2, dg2, db2, None, None, None, None, None, None, None, None, None, None,
+                None)
 
 
 def bn_pair(bn1: "BatchNormAct2d", x1: torch.Tensor, bn2: "BatchNormAct2d", x2: torch.Tensor) -> torch.Tensor:
@@ -461,10 +538,24 @@ def bn_pair(bn1: "BatchNormAct2d", x1: torch.Tensor, bn2: "BatchNormAct2d", x2: 
     mom2, rm2, rv2 = bn2._train_args()
     link = BNLink() if torch.is_grad_enabled() else None
     amax = _amax_buf(x1)
+    # fp16 planes: the output (both inputs' maxima known), the input gradients (bn1.grad_planes)
+    spec = obound = None
+    if bn1.out_planes and _conv._F32_PLANES and x1.dtype == torch.float32:
+        o1, o2 = omax_of(x1), omax_of(x2)
+        if o1 is not None and o2 is not None:
+            obound = torch.empty(_conv.BOUND_FLOATS, dtype=torch.float32, device=x1.device)
+            spec = dict(obound=obound.data_ptr(), xmax=o1[0].data_ptr(), xep=o1[1], xmax2=o2[0].data_ptr(), xep2=o2[1])
+            amax = None
+    if link is not None and bn1.grad_planes and _conv._F32_PLANES and x1.dtype == torch.float32 \
+            and bn1.running_mean is not None and omax_of(x1) is not None and omax_of(x2) is not None:
+        link.gbuf = omax_buf(bn1.running_mean, "g", x1.device)
     y = _BNPairFn.apply(x1, bn1.weight, bn1.bias, rm1, rv1, x2, bn2.weight, bn2.bias, rm2, rv2, mom1, bn1.eps, mom2,
-                        bn2.eps, tile_stats_of(x1), tile_stats_of(x2), link, amax)
+                        bn2.eps, tile_stats_of(x1), tile_stats_of(x2), link, amax, spec)
     if link is not None:
         y._mpit_bnlink = link
-    if amax is not None:
+    if obound is not None:
+        set_planes(y, obound)
+        COUNTERS["fwd_planes"] += 1
+    elif amax is not None:
         set_amax(y, amax)
     return y

@@ -290,11 +290,79 @@ def amax_of(t: torch.Tensor):
     return a[0]
 
 
+# fp32 steps (fp16x3): activations and gradients that only GEMMs read are written by their
+# producers (BN apply passes, the stem's max pool) as the two fp16 planes h, l of x * 2^e
+# (csrc/kernels/planes.h), with e from a bound known before the pass; the GEMMs then split
+# nothing (gemm.hip FM 13: A planes in gemm_nt, both operands in gemm_tn). Same 4 bytes per
+# element as fp32, so the tensor keeps its fp32 dtype and shape; the tag below says its memory
+# holds planes. MPIT_F32_PLANES=0: fp32 activations (the GEMMs split them, FM 11 / 12).
+_F32_PLANES = os.environ.get("MPIT_F32_PLANES", "1") != "0" and _F32_SPLIT == "f16x3"
+
+
+def set_planes(t: torch.Tensor, bound: torch.Tensor) -> torch.Tensor:
+    """Mark ``t``'s memory as fp16 planes scaled by the slotted ``bound`` (valid for this
+    storage and version only)."""
+    t._mpit_planes = (bound, t.data_ptr(), t._version)
+    return t
+
+
+def planes_of(t: torch.Tensor):
+    """The bound of ``t``'s fp16 planes when its memory holds planes, else None."""
+    a = getattr(t, "_mpit_planes", None)
+    if a is None or a[1] != t.data_ptr() or a[2] != t._version:
+        return None
+    return a[0]
+
+
+def unplanes(t: torch.Tensor) -> torch.Tensor:
+    """A planes tensor as plain fp32 values (PyTorch ops; for the rare consumer without a
+    planes path): (h + l / 2^11) / 2^e, exact."""
+    b = planes_of(t)
+    if b is None:
+        return t
+    if t.dim() == 4:
+        n, c, h, w = t.shape
+        flat = t.permute(0, 2, 3, 1).reshape(-1).view(torch.float16)
+    else:
+        flat = t.reshape(-1).view(torch.float16)
+    ne = t.numel()
+    v = (flat[:ne].float() + flat[ne:].float() / 2048.0) * _exp2i(-_f16_exp(bound_value(b)))
+    COUNTERS["unplanes"] += 1
+    if t.dim() == 4:
+        return v.view(n, h, w, c).permute(0, 3, 1, 2)
+    return v.view(t.shape)
+
+
+_OEPOCH = [0]
+
+
+def next_epoch() -> int:
+    """A fresh launch epoch for the (epoch, max) slots of gemm.hip EpiArgs::omax (never 0)."""
+    _OEPOCH[0] = _OEPOCH[0] % 0xFFFFFFF0 + 1
+    return _OEPOCH[0]
+
+
+def omax_buf(key: torch.Tensor, site: str, device) -> torch.Tensor:
+    """The persistent epoch-slot buffer of a (key, site) GEMM output maximum (zeroed once; its
+    slots only ever hold pairs of earlier launches, so a stale slot is never taken for ours)."""
+    return tagged_part(key, "omax_" + site, BOUND_FLOATS, device)
+
+
+def omax_of(t: torch.Tensor):
+    """(slot buffer, epoch) of max |t| left by the GEMM that wrote ``t``, or None."""
+    a = getattr(t, "_mpit_omax", None)
+    if a is None or a[2] != t.data_ptr():
+        return None
+    return a[0], a[1]
+
+
 def _amax_arg(t: torch.Tensor, keep: list) -> int:
     """Device pointer of a bound of |t| for an fp16x3 GEMM: the producer's, else one reduction
     (the tensor is kept alive in ``keep`` until the launch is queued)."""
     a = amax_of(t)
     if a is None:
+        if planes_of(t) is not None:
+            raise RuntimeError("an fp16-planes tensor reached an fp32 operand path")
         a = bound_of_value(torch.linalg.vector_norm(t, float("inf")))
         COUNTERS["amax_fallback"] += 1
     keep.append(a)
@@ -302,19 +370,47 @@ def _amax_arg(t: torch.Tensor, keep: list) -> int:
 
 
 def _split_kw(a: torch.Tensor, w: torch.Tensor, f32: bool, keep: list) -> dict:
-    """GEMM keyword arguments of the weight operand ``w`` (planes) and the operand ``a``."""
+    """GEMM keyword arguments of the weight operand ``w`` (planes) and the operand ``a`` (fp32,
+    or fp16 planes: FM 13)."""
     bps = _bps(w, f32)
     kw = dict(bps=bps)
     bam = _bamax(w) if bps else 0
-    if bam:
+    pb = planes_of(a) if f32 else None
+    if pb is not None:
+        if not bam:
+            raise RuntimeError("an fp16-planes operand needs the weight as fp16 planes (fp16x3)")
+        keep.append(pb)
+        COUNTERS["nt_planes"] += 1
+        kw.update(amax_a=pb.data_ptr(), amax_b=bam, aps=a.numel())
+    elif bam:
         kw.update(amax_a=_amax_arg(a, keep), amax_b=bam)
     return kw
 
 
-def _wgrad_kw(dy: torch.Tensor, xamax, f32: bool, side, keep: list) -> dict:
+def _as_operand(a: torch.Tensor, w: torch.Tensor, f32: bool) -> torch.Tensor:
+    """``a`` as the A operand of an fp32 GEMM against ``w``: fp16 planes need the weight as fp16
+    planes too (the step's weight plan, WeightCastPlan); a call without the plan decodes them
+    (counted in COUNTERS["unplanes"])."""
+    if f32 and w is not None and planes_of(a) is not None and not _bamax(w):
+        v = _cl(unplanes(a))
+        return set_amax(v, bound_of_value(torch.linalg.vector_norm(v, float("inf"))))
+    return a
+
+
+def _wgrad_kw(dy: torch.Tensor, xamax, f32: bool, side, keep: list, x: torch.Tensor = None, xplanes=False) -> dict:
     """fp16x3 operand bounds of a backward-weight GEMM (both producers' bounds, else the bf16x6
     path: a fallback reduction on the compute stream would not be ordered before the side
-    stream's GEMM); the bound tensors are kept alive for the side stream."""
+    stream's GEMM); the bound tensors are kept alive for the side stream. Operands given as
+    fp16 planes (both: FM 13; :func:`_wgrad_operands` settles a mixed pair first) add their
+    plane strides."""
+    ya = planes_of(dy) if f32 else None
+    if ya is not None or xplanes:
+        if ya is None or not xplanes or xamax is None:
+            raise RuntimeError("backward-weight GEMM: one operand is fp16 planes, the other fp32")
+        keep += [ya, xamax]
+        _used_on(side, ya, xamax)
+        COUNTERS["wgrad_planes"] += 1
+        return dict(amax_y=ya.data_ptr(), amax_x=xamax.data_ptr(), yps=dy.numel(), xps=x.numel())
     ya = amax_of(dy)
     if not f32 or _F32_SPLIT != "f16x3" or ya is None or xamax is None:
         return {}
@@ -324,7 +420,24 @@ def _wgrad_kw(dy: torch.Tensor, xamax, f32: bool, side, keep: list) -> dict:
     return dict(amax_y=ya.data_ptr(), amax_x=xamax.data_ptr())
 
 
-COUNTERS = {"amax_fallback": 0, "wgrad_f16x3": 0}
+def _wgrad_operands(dy: torch.Tensor, x: torch.Tensor, xamax, xplanes: bool):
+    """(dy, x, xamax, xplanes, mixed) for a backward-weight GEMM: when exactly one operand is
+    fp16 planes (a gradient that came through autograd's sum instead of a planes-writing BN),
+    the planes one is decoded to fp32 (on the compute stream: the caller then keeps the GEMM
+    there) — counted, never silent."""
+    yp = planes_of(dy) is not None
+    if yp == bool(xplanes):
+        return dy, x, xamax, xplanes, False
+    COUNTERS["wgrad_mixed"] += 1
+    if yp:
+        dyf = _cl(unplanes(dy))
+        return set_amax(dyf, bound_of_value(torch.linalg.vector_norm(dyf, float("inf")))), x, xamax, xplanes, True
+    xf = _cl(unplanes(x))
+    return dy, xf, bound_of_value(torch.linalg.vector_norm(xf, float("inf"))), False, True
+
+
+COUNTERS = {"amax_fallback": 0, "wgrad_f16x3": 0, "nt_planes": 0, "wgrad_planes": 0, "wgrad_mixed": 0,
+            "unplanes": 0}
 
 
 def _to(x: torch.Tensor, dt) -> torch.Tensor:
@@ -448,6 +561,9 @@ def _red_args(link, c: int, ntiles: int, device, fold: bool = False):
         part = torch.empty(ntiles * 2 * c, dtype=torch.float32, device=device)
     kw = dict(red_part=part.data_ptr(), red_x=link.x.data_ptr(),
               red_mask=link.mask.data_ptr() if link.mask is not None else 0, red_mean=link.mean.data_ptr())
+    if getattr(link, "gbuf", None) is not None:  # the BN backward writes fp16 planes: max |dy| first
+        link.gep = next_epoch()
+        kw.update(omax=link.gbuf.data_ptr(), oepoch=link.gep)
     part2 = fb = None
     if link.x2 is not None:
         part2 = torch.empty(ntiles * 2 * c, dtype=torch.float32, device=device)
@@ -478,11 +594,13 @@ def _link_of(x: torch.Tensor, dt, pair_ok: bool = True):
 class _Hold(list):
     """Receives (partials, tiles, fold) from a statistics GEMM. ``bn``: the BatchNormAct2d the
     output feeds, whose forward finalize the GEMM then runs in its last blocks (ops/bn.py
-    bn_fold_for, gemm.hip stats_fold) — the BN forward is left with its apply pass."""
+    bn_fold_for, gemm.hip stats_fold) — the BN forward is left with its apply pass. ``omax``:
+    (slot buffer, epoch) of the output's max |C| (a planes-writing BN's input bound)."""
 
     def __init__(self, bn=None):
         super().__init__()
         self.bn = bn
+        self.omax = None
 
 
 # conv -> weak reference of the BN its output feeds (kept outside the modules: no submodule,
@@ -523,10 +641,26 @@ def _fold_arg(fold):
     return fold.args if fold is not None else None
 
 
+def _omax_kw(hold, device, dt) -> dict:
+    """fp32 statistics GEMM feeding a BN that writes fp16 planes: the launch's max |C| in epoch
+    slots (the BN's output bound needs it before its pass), recorded on the hold."""
+    bn = getattr(hold, "bn", None) if hold is not None else None
+    if not (_F32_PLANES and dt == torch.float32 and bn is not None
+            and (getattr(bn, "out_planes", False) or getattr(bn, "grad_planes", False))
+            and getattr(bn, "running_mean", None) is not None):
+        return {}
+    buf, ep = omax_buf(bn.running_mean, "x", device), next_epoch()
+    hold.omax = (buf, ep)
+    return dict(omax=buf.data_ptr(), oepoch=ep)
+
+
 def _attach_stats(y: torch.Tensor, hold: list) -> torch.Tensor:
     if hold:
         part, nt, fold = hold[0]
         y._mpit_tstats = (part, nt, y.data_ptr(), fold)
+        om = getattr(hold, "omax", None)
+        if om is not None:
+            y._mpit_omax = (om[0], om[1], y.data_ptr())
     return y
 
 
@@ -587,6 +721,9 @@ def park_grad(x: torch.Tensor, slot: GradSlot) -> torch.Tensor:
     a = amax_of(x)
     if a is not None:
         set_amax(v, a)
+    p = planes_of(x)
+    if p is not None:
+        set_planes(v, p)
     return v
 
 
@@ -662,6 +799,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         co = weight.shape[0]
         M = n * h * w
         wb, wt = wcast if wcast is not None else cast_transpose(weight, dt)
+        x = _as_operand(x, wb, f32)
         y = torch.empty((n, co, h, w), dtype=dt, device=x.device, memory_format=torch.channels_last)
         m = native()
         st = None
@@ -672,9 +810,11 @@ class _Conv1x1Fn(torch.autograd.Function):
         keep = []
         m.gemm_nt(x.device.index, _stream(x), M, co, ci, x.data_ptr(), ci, wb.data_ptr(), ci, y.data_ptr(), co,
                   st.data_ptr() if st is not None else 0, f32=f32, bn_fold=_fold_arg(fold),
-                  **_split_kw(x, wb, f32, keep))
+                  **_split_kw(x, wb, f32, keep), **(_omax_kw(hold, x.device, dt) if st is not None else {}))
         ctx.save_for_backward(x, wt)
-        ctx.xamax = amax_of(x) if f32 else None
+        xp = planes_of(x) if f32 else None
+        ctx.xplanes = xp is not None
+        ctx.xamax = xp if xp is not None else (amax_of(x) if f32 else None)
         ctx.wshape = weight.shape
         ctx.wparam = weight
         ctx.slot = slot
@@ -697,6 +837,7 @@ class _Conv1x1Fn(torch.autograd.Function):
         side = WgradStream.begin(x.device) if use_side and not WgradStream.after else None
         extra, emask = ctx.slot.take() if ctx.slot is not None else (None, None)
         if ctx.needs_input_grad[0]:
+            dy = _as_operand(dy, wt, f32)
             dx = torch.empty_like(x, memory_format=torch.channels_last)
             kw, part, part2 = {}, None, None
             if ctx.link is not None:  # the producing BN's backward reduction, in the epilogue
@@ -721,13 +862,16 @@ class _Conv1x1Fn(torch.autograd.Function):
             dw = grad_out(ctx.wparam, ctx.wshape, x.device)
             if getattr(dw, "_mpit_repeat", False):
                 side = None  # a weight used twice: autograd sums the gradients on this stream
+            wy, wx, xam, xpl, mixed = _wgrad_operands(dy, x, ctx.xamax, ctx.xplanes)
+            if mixed:
+                side = None  # the decoded operand was made on this stream
             nws = m.gemm_tn_ws_floats(dev, M, co, ci)
             ws = torch.empty(nws, dtype=torch.float32, device=x.device) if nws else None
             keep = []
-            m.gemm_tn(dev, side.cuda_stream if side is not None else s, M, co, ci, dy.data_ptr(), co, x.data_ptr(),
+            m.gemm_tn(dev, side.cuda_stream if side is not None else s, M, co, ci, wy.data_ptr(), co, wx.data_ptr(),
                       ci, dw.data_ptr(), ws.data_ptr() if ws is not None else 0, 0.0, f32=f32,
-                      **_wgrad_kw(dy, ctx.xamax, f32, side, keep))
-            _used_on(side, dy, x, ws, out=dw)
+                      **_wgrad_kw(wy, xam, f32, side, keep, wx, xpl))
+            _used_on(side, wy, wx, ws, out=dw)
         return dx, dw, None, None, None, None, None
 
 
@@ -840,6 +984,7 @@ def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None, up=None
     use_side = ctx.needs_input_grad[1] and WgradStream.wants(f32, r * s > 1)
     side = WgradStream.begin(x.device) if use_side and not WgradStream.after else None
     if ctx.needs_input_grad[0]:
+        dz = _as_operand(dz, wt, f32)
         if stride == 1 and wt is not None:
             # backward-data = forward conv of dz with the flipped, transposed weight
             dx = torch.empty_like(x, memory_format=torch.channels_last)
@@ -871,6 +1016,7 @@ def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None, up=None
             if part is not None:
                 link.publish(part, nt, dx)
         else:  # MIOpen's NHWC backward-data
+            dz, x = unplanes(dz), unplanes(x)
             wf = _unsplit(wb) if _bps(wb, f32) else wb
             wv = wf.permute(0, 3, 1, 2).to(x.dtype)  # [Co, C, R, S] view with channels_last strides
             dx = torch.ops.aten.convolution_backward(dz, x, wv, None, [stride, stride], [pad, pad], [1, 1], False,
@@ -881,13 +1027,16 @@ def _conv_backward(ctx, x, wb, wt, dz, stride: int, pad: int, link=None, up=None
         dw = grad_out(getattr(ctx, "wparam", None), (co, c, r, s), x.device, torch.channels_last)
         if getattr(dw, "_mpit_repeat", False):
             side = None  # a weight used twice: autograd sums the gradients on this stream
+        wy, wx, xam, xpl, mixed = _wgrad_operands(dz, x, getattr(ctx, "xamax", None), getattr(ctx, "xplanes", False))
+        if mixed:
+            side = None  # the decoded operand was made on this stream
         nws = m.conv_wgrad_ws_floats(dev, nb, h, w, c, co, r, s, stride, pad)
         ws = torch.empty(nws, dtype=torch.float32, device=x.device) if nws else None
         keep = []
         m.conv_wgrad(dev, side.cuda_stream if side is not None else st, nb, h, w, c, co, r, s, stride, pad,
-                     dz.data_ptr(), x.data_ptr(), dw.data_ptr(), ws.data_ptr() if ws is not None else 0, 0.0, f32=f32,
-                     **_wgrad_kw(dz, getattr(ctx, "xamax", None), f32, side, keep))
-        _used_on(side, dz, x, ws, out=dw)
+                     wy.data_ptr(), wx.data_ptr(), dw.data_ptr(), ws.data_ptr() if ws is not None else 0, 0.0, f32=f32,
+                     **_wgrad_kw(wy, xam, f32, side, keep, wx, xpl))
+        _used_on(side, wy, wx, ws, out=dw)
     return dx, dw
 
 
@@ -933,6 +1082,7 @@ class _ConvFn(torch.autograd.Function):
             wb, wt = strided_dgrad_weights(weight, stride, pad, dt)
         else:
             wb, wt = conv_weights(weight, need_dx and stride == 1, dt)
+        x = _as_operand(x, wb, f32)
         y = torch.empty((nb, co, ho, wo), dtype=dt, device=x.device, memory_format=torch.channels_last)
         b = None
         if bias is not None:
@@ -946,9 +1096,12 @@ class _ConvFn(torch.autograd.Function):
         native().conv_fwd(x.device.index, _stream(x), nb, h, w, c, co, r, s, stride, pad, x.data_ptr(), wb.data_ptr(),
                           y.data_ptr(), stats=st.data_ptr() if st is not None else 0,
                           bias=b.data_ptr() if b is not None else 0, relu=bool(relu), f32=f32,
-                          bn_fold=_fold_arg(fold), **_split_kw(x, wb, f32, keep))
+                          bn_fold=_fold_arg(fold), **_split_kw(x, wb, f32, keep),
+                          **(_omax_kw(hold, x.device, dt) if st is not None else {}))
         ctx.save_for_backward(x, wb, wt, y if relu else None)
-        ctx.xamax = amax_of(x) if f32 else None
+        xp = planes_of(x) if f32 else None
+        ctx.xplanes = xp is not None
+        ctx.xamax = xp if xp is not None else (amax_of(x) if f32 else None)
         ctx.geo = (stride, pad, bias is not None, bool(relu))
         ctx.wparam = weight
         ctx.link = link

@@ -14,7 +14,8 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .._ext import native
-from .conv import ReluLink, amax_of, set_amax
+from . import conv as _conv
+from .conv import ReluLink, amax_of, set_amax, set_planes
 
 
 def _stream(t: torch.Tensor) -> int:
@@ -23,7 +24,7 @@ def _stream(t: torch.Tensor) -> int:
 
 class _MaxPoolFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, k: int, stride: int, pad: int):
+    def forward(ctx, x, k: int, stride: int, pad: int, obound=None):
         up = ReluLink.of(x)
         if up is not None and 256 % (x.shape[1] // 8):
             up = None
@@ -33,8 +34,12 @@ class _MaxPoolFn(torch.autograd.Function):
         ho, wo = (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
         y = torch.empty((n, c, ho, wo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
         idx = torch.empty((n, ho, wo, c), dtype=torch.uint8, device=x.device)
+        ib = amax_of(x) if obound is not None else None
+        if obound is not None and (ib is None or up is not None or x.dtype != torch.float32):
+            raise RuntimeError("max pool planes output needs an fp32 input with its bound and no ReLU link")
         native().maxpool_fwd(x.device.index, _stream(x), n, h, w, c, k, stride, pad, x.data_ptr(), y.data_ptr(),
-                             idx.data_ptr(), f32=x.dtype == torch.float32)
+                             idx.data_ptr(), f32=x.dtype == torch.float32, ibound=ib.data_ptr() if ib is not None else 0,
+                             obound=obound.data_ptr() if obound is not None else 0)
         ctx.dt = x.dtype
         ctx.up = up
         ctx.save_for_backward(idx, y if up is not None else None)
@@ -60,7 +65,7 @@ class _MaxPoolFn(torch.autograd.Function):
                       dx.data_ptr(), f32=ctx.dt == torch.float32, **kw)
         if up is not None:
             up.give(dx, db)
-        return dx, None, None, None
+        return dx, None, None, None, None
 
 
 def _int(v):
@@ -77,11 +82,21 @@ class MaxPool2dNHWC(nn.MaxPool2d):
                 and 2 * p <= k <= 15 and self.kernel_size in (k, (k, k)) and self.stride in (s, (s, s))
                 and self.padding in (p, (p, p)))
 
+    # out_planes (fp32 steps): the output is read only by fp16x3 GEMMs (a ResNet stem pool feeds
+    # the first block's convolutions and its residual add): written as fp16 planes scaled by the
+    # input's bound (ops/conv.py _F32_PLANES). Set by the model.
+    out_planes = False
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if self.fused(x):
-            y = _MaxPoolFn.apply(x, _int(self.kernel_size), _int(self.stride), _int(self.padding))
             a = amax_of(x)
-            if a is not None:  # every output is one of the inputs: the input's bound holds
+            pl = (self.out_planes and _conv._F32_PLANES and x.dtype == torch.float32 and a is not None
+                  and ReluLink.of(x) is None and self.training)
+            ob = torch.empty(_conv.BOUND_FLOATS, dtype=torch.float32, device=x.device) if pl else None
+            y = _MaxPoolFn.apply(x, _int(self.kernel_size), _int(self.stride), _int(self.padding), ob)
+            if ob is not None:
+                set_planes(y, ob)
+            elif a is not None:  # every output is one of the inputs: the input's bound holds
                 set_amax(y, a)
             return y
         return super().forward(x)

@@ -245,14 +245,28 @@ def _ref_block(blk, x):
     return F.relu(out + idt)
 
 
+def planes_input(x):
+    """x (fp32, channels_last) as an fp16-planes tensor (ops/conv.py set_planes), and the
+    values those planes carry (exact decode)."""
+    b = C.bound_of_value(torch.linalg.vector_norm(x, float("inf")))
+    n, c, h, w = x.shape
+    p = C.f16_planes(x.permute(0, 2, 3, 1).reshape(-1).contiguous(), b)
+    xp = p.reshape(-1).view(torch.float32).view(n, h, w, c).permute(0, 3, 1, 2)
+    C.set_planes(xp, b)
+    return xp, C.unplanes(xp).contiguous(memory_format=torch.channels_last)
+
+
 @gpu
-@pytest.mark.parametrize("plan", [False, True])
+@pytest.mark.parametrize("plan,pl", [(False, False), (True, False), (True, True)])
 @pytest.mark.parametrize("inp,planes,stride", [(256, 64, 1), (256, 128, 2)])
-def test_bottleneck_fp32_vs_fp64(inp, planes, stride, plan):
+def test_bottleneck_fp32_vs_fp64(inp, planes, stride, plan, pl):
     """A whole fused bottleneck block in fp32 (GEMM-epilogue BN statistics and backward
     reductions, parked shortcut gradients, bn_pair) against fp64 on the CPU: within 2x of
     the same block on PyTorch's fp32 ops. With the weight plan (the trainer's setting) every
-    GEMM runs the fp16x3 split products on the bounds the BN passes wrote."""
+    GEMM runs the fp16x3 split products on the bounds the BN passes wrote. ``pl``: as inside
+    ResNet-50's fp32 step — the block input, its BN outputs and their input gradients as fp16
+    planes (gemm.hip FM 13; the residual add decodes its planes), the reference on the values
+    the input planes carry."""
     from mpit_amd.models.resnet import Bottleneck, conv1x1
     from mpit_amd.ops.bn import BatchNormAct2d
 
@@ -265,10 +279,19 @@ def test_bottleneck_fp32_vs_fp64(inp, planes, stride, plan):
         if isinstance(m, BatchNormAct2d):
             m.weight.data.uniform_(0.5, 1.5)
             m.bias.data.uniform_(-0.2, 0.2)
+            # (the block output stays fp32: the test reads it; its gradient comes from the test)
+            m.out_planes = m.grad_planes = pl and m is not blk.bn3
+    blk.bn3.grad_planes = pl
     x = _cl(torch.randn(4, inp, 14, 14, device="cuda"))
-    x1 = x.clone().requires_grad_(True)
+    if pl:
+        xp, x = planes_input(x)
+        x1 = xp.detach().requires_grad_(True)
+        C.set_planes(x1, C.planes_of(xp))
+    else:
+        x1 = x.clone().requires_grad_(True)
     wp = C.WeightCastPlan(blk, torch.float32) if plan else None
-    n16 = C.COUNTERS["wgrad_f16x3"]
+    n16 = C.COUNTERS["wgrad_f16x3"] + C.COUNTERS["wgrad_planes"]
+    npl, nmix = C.COUNTERS["wgrad_planes"], C.COUNTERS["wgrad_mixed"]
     if wp is not None:
         wp.run()
     y1 = blk(x1)
@@ -278,7 +301,12 @@ def test_bottleneck_fp32_vs_fp64(inp, planes, stride, plan):
     if wp is not None:
         wp.invalidate()
         if C._F32_SPLIT == "f16x3":
-            assert C.COUNTERS["wgrad_f16x3"] > n16  # bounds reached the backward-weight GEMMs
+            # bounds reached the backward-weight GEMMs
+            assert C.COUNTERS["wgrad_f16x3"] + C.COUNTERS["wgrad_planes"] > n16
+    if pl and C._F32_PLANES:
+        # conv1, conv2 (and the shortcut conv) take both operands as planes; conv3's gradient
+        # comes from the test's fp32 g through bn3 (not linked): decoded, counted
+        assert C.COUNTERS["wgrad_planes"] - npl >= 2, C.COUNTERS
     ours = {n: p.grad.detach().clone() for n, p in blk.named_parameters()}
     ours.update(y=y1.detach(), dx=x1.grad)
     blk.zero_grad(set_to_none=True)
@@ -348,13 +376,21 @@ def test_resnet50_fp32_step_runs_native():
     convs = [m for m in net.modules() if isinstance(m, torch.nn.Conv2d)]
     x = _cl(torch.randn(4, 3, 64, 64, device="cuda"))
     assert net.conv1.fused(x)
+    plan = C.WeightCastPlan(net, torch.float32)  # the trainer's per-step weight planes
+    plan.run()
     out = net(x)
     assert out.dtype == torch.float32
+    n0 = dict(C.COUNTERS)
     loss = F.cross_entropy(out, torch.randint(0, 10, (4,), device="cuda"))
     loss.backward()
     assert torch.isfinite(loss)
     for m in convs:
         assert m.weight.grad is not None and torch.isfinite(m.weight.grad).all()
+    plan.invalidate()
+    if C._F32_PLANES:  # activations / gradients as fp16 planes wherever only GEMMs read them
+        assert C.COUNTERS["wgrad_planes"] - n0["wgrad_planes"] >= 45, C.COUNTERS
+        assert C.COUNTERS["wgrad_mixed"] == n0["wgrad_mixed"], C.COUNTERS
+        assert C.COUNTERS["unplanes"] == n0["unplanes"], C.COUNTERS
 
 
 @pytest.mark.gpu

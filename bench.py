@@ -93,6 +93,12 @@ def _fp32_gemm() -> str:
     return conv._F32_SPLIT + ("+planes" if conv._F32_PLANES else "")
 
 
+def _gemm_counters() -> dict:
+    from mpit_amd.ops import conv
+
+    return dict(conv.COUNTERS)
+
+
 def _devices(W, tr) -> list:
     """[(rank, device index, PCI bus id)] of every rank: the record itself shows which GPUs ran."""
     import torch
@@ -290,6 +296,9 @@ def main(argv=None) -> int:
                        "master_weights": "fp32", "loss_last": lossv, "defer_ps_wait": a.defer_ps_wait,
                        "datapath": a.datapath},
             "fp32_gemm": _fp32_gemm() if not (tr.on_gpu and amp) else None,
+            # operand-path counters over the whole run (ops/conv.py COUNTERS): planes GEMMs, and the
+            # fallbacks that must stay 0 on the flagship (decoded planes, mixed pairs, amax passes)
+            "gemm_counters": _gemm_counters(),
             "world": st.world, "shared_devices": st.shared_devices, "devices": devices, "rccl": rccl,
             "ps_check": check, "preflight": preflight, "peak_mem_gib": peak_gib,
             **({"emulate_shards": a.emulate_shards} if a.emulate_shards > 1 else {}),

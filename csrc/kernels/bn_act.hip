@@ -680,8 +680,10 @@ __global__ __launch_bounds__(1024) void bn_apply_kernel(const T* __restrict__ x,
   if constexpr (sizeof(T) == 4) {
     const float rb = RES && am.rbound ? slots_max_wave(am.rbound) : 0.f;
     if (RES && am.rplanes) rinv = pexp2(-plane_exp(rb));
-    if (am.obound) {  // (per wave, from the coefficient arrays: no block barrier)
-      float bound = fmaf(coef_max_wave(coef, C, 0), epoch_max_wave(am.xmax, am.xep), coef_max_wave(coef, C, 1));
+    if (am.obound) {  // (from the coefficients in registers)
+      float m[2] = {abs_max8(sc), abs_max8(sh)};
+      coef_max_block(m, C);
+      float bound = fmaf(m[0], epoch_max_wave(am.xmax, am.xep), m[1]);
       if constexpr (RES) bound += rb;
       ps = plane_scale(bound, am.obound);
     }
@@ -835,9 +837,10 @@ __global__ __launch_bounds__(1024) void bn_bwd_apply_kernel(const T* __restrict_
   [[maybe_unused]] PlaneScale ps{1.f, 2048.f};
   const int64_t nel = nvec * 8;
   if constexpr (sizeof(T) == 4) {
-    if (am.obound) {  // (per wave, from the coefficient arrays: no block barrier)
-      const float ma = coef_max_wave(coef, C, 0), mc = coef_max_wave(coef, C, 1), mbb = coef_max_wave(coef, C, 2);
-      ps = plane_scale(fmaf(ma, epoch_max_wave(am.gmax, am.gep), fmaf(mc, epoch_max_wave(am.xmax, am.xep), mbb)),
+    if (am.obound) {  // (from the coefficients in registers)
+      float m[3] = {abs_max8(A), abs_max8(Cc), abs_max8(B)};
+      coef_max_block(m, C);
+      ps = plane_scale(fmaf(m[0], epoch_max_wave(am.gmax, am.gep), fmaf(m[1], epoch_max_wave(am.xmax, am.xep), m[2])),
                        am.obound);
     }
   }
@@ -891,9 +894,11 @@ __global__ __launch_bounds__(1024) void bn_pair_apply_kernel(const T* __restrict
   [[maybe_unused]] PlaneScale ps{1.f, 2048.f};
   const int64_t nel = nvec * 8;
   if constexpr (sizeof(T) == 4) {
-    if (am.obound) {  // |y| <= max|a1| max|x1| + max|b1| + max|a2| max|x2| + max|b2| (per wave)
-      ps = plane_scale(fmaf(coef_max_wave(coef1, C, 0), epoch_max_wave(am.xmax, am.xep), coef_max_wave(coef1, C, 1)) +
-                           fmaf(coef_max_wave(coef2, C, 0), epoch_max_wave(am.xmax2, am.xep2), coef_max_wave(coef2, C, 1)),
+    if (am.obound) {  // |y| <= max|a1| max|x1| + max|b1| + max|a2| max|x2| + max|b2|
+      float m[4] = {abs_max8(a1), abs_max8(b1), abs_max8(a2), abs_max8(b2)};
+      coef_max_block(m, C);
+      ps = plane_scale(fmaf(m[0], epoch_max_wave(am.xmax, am.xep), m[1]) +
+                           fmaf(m[2], epoch_max_wave(am.xmax2, am.xep2), m[3]),
                        am.obound);
     }
   }
@@ -944,15 +949,17 @@ __global__ __launch_bounds__(1024) void bn_pair_bwd_apply_kernel(
   [[maybe_unused]] PlaneScale ps1{1.f, 2048.f}, ps2{1.f, 2048.f};
   const int64_t nel = nvec * 8;
   if constexpr (sizeof(T) == 4) {
-    // |dx_k| <= max|A_k| max|dy| + max|C_k| max|x_k| + max|B_k| (per wave, no block barrier)
-    if (am1.obound)
-      ps1 = plane_scale(fmaf(coef_max_wave(coef1, C, 0), epoch_max_wave(am1.gmax, am1.gep),
-                             fmaf(coef_max_wave(coef1, C, 1), epoch_max_wave(am1.xmax, am1.xep), coef_max_wave(coef1, C, 2))),
-                        am1.obound);
-    if (am2.obound)
-      ps2 = plane_scale(fmaf(coef_max_wave(coef2, C, 0), epoch_max_wave(am2.gmax, am2.gep),
-                             fmaf(coef_max_wave(coef2, C, 1), epoch_max_wave(am2.xmax, am2.xep), coef_max_wave(coef2, C, 2))),
-                        am2.obound);
+    // |dx_k| <= max|A_k| max|dy| + max|C_k| max|x_k| + max|B_k| (coefficients in registers)
+    if (am1.obound || am2.obound) {
+      float m[6] = {abs_max8(A1), abs_max8(C1), abs_max8(B1), abs_max8(A2), abs_max8(C2), abs_max8(B2)};
+      coef_max_block(m, C);
+      if (am1.obound)
+        ps1 = plane_scale(fmaf(m[0], epoch_max_wave(am1.gmax, am1.gep), fmaf(m[1], epoch_max_wave(am1.xmax, am1.xep), m[2])),
+                          am1.obound);
+      if (am2.obound)
+        ps2 = plane_scale(fmaf(m[3], epoch_max_wave(am2.gmax, am2.gep), fmaf(m[4], epoch_max_wave(am2.xmax, am2.xep), m[5])),
+                          am2.obound);
+    }
   }
   for_slots<SPLIT, U>(i, stride, nvec, [&](const auto& s) {
     float d[V], p[V], q[V];

@@ -38,13 +38,39 @@ __device__ __forceinline__ float epoch_max_wave(const unsigned long long* p, uin
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
   return m;
 }
-// max |coef[row * C + c]| over the C channels, per wave (lanes stride the channels; every lane
-// of the wave must call it): a pass's per-channel coefficients without a block barrier
-__device__ __forceinline__ float coef_max_wave(const float* coef, int C, int row) {
-  float m = 0.f;
-  for (int c = threadIdx.x & 63; c < C; c += 64) m = fmaxf(m, fabsf(coef[int64_t(row) * C + c]));
+// max |coefficient| over the C channels from the coefficients the apply threads already hold
+// in registers (m[n] = the thread's max of row n): a wave's 64 lanes x 8 elements are 512
+// consecutive elements and a block's 8 * blockDim >= C (bn_act.hip block_for), so a wave
+// reduction covers every channel when C <= 512 and a block one otherwise. Replaces a loop of
+// C / 64 coefficient loads per row and wave (the fp32 apply passes run one 512-element slot
+// per wave: those loads outnumbered the pass's own). Every thread of the block must call it
+// (C is block-uniform, so is the barrier).
+template <int N>
+__device__ __forceinline__ void coef_max_block(float (&m)[N], int C) {
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int n = 0; n < N; ++n) m[n] = fmaxf(m[n], __shfl_xor(m[n], o));
+  if (C > 512) {
+    __shared__ float sm[N][16];
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+      for (int n = 0; n < N; ++n) sm[n][w] = m[n];
+    __syncthreads();
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      float r = 0.f;
+      for (int k = 0; k < nw; ++k) r = fmaxf(r, sm[n][k]);
+      m[n] = r;
+    }
+  }
+}
+// a thread's max |v| over its 8 per-element coefficients
+__device__ __forceinline__ float abs_max8(const float (&v)[8]) {
+  float m = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) m = fmaxf(m, fabsf(v[k]));
   return m;
 }
 // slots_max with one slot per lane and a wave reduction (every lane of the wave calls it)

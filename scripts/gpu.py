@@ -19,6 +19,7 @@ Steps:
   gemmcalls:<name>:<args> per-call GEMM shapes + times of one steady step     -> gemm_calls_<name>.md
   mp:<script>:<n>[:K=V;K=V] tests/mp/<script> on n ranks with extra env   -> mp_<script>_<n>.log
   py:<file>[:args[:K=V;K=V]] python3 <file> <args> with extra env (benchmarks/ probes) -> py_<n>.log
+  profpy:<name>:<file>[:args[:K=V;K=V]] rocprofv3 --kernel-trace --stats of python3 <file> -> pp_<name>/
 """
 from __future__ import annotations
 
@@ -155,6 +156,20 @@ def main(argv) -> int:
                        "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join("tests", "mp", script)],
                       500, env=env)
             print(_tail(os.path.join(out, f"mp_{script}_{n}_{i}.log"), 6))
+        elif kind == "profpy":  # rocprofv3 kernel trace + stats of python3 <file> (names and times per kernel)
+            parts = rest.split(":")
+            name, f = parts[0], parts[1]
+            args = parts[2] if len(parts) > 2 else ""
+            env = dict(kv.split("=", 1) for kv in parts[3].split(";")) if len(parts) > 3 and parts[3] else {}
+            d = os.path.join(out, f"pp_{name}")
+            rc = _run(out, f"pp_{name}.log", ["rocprofv3", "--kernel-trace", "--stats", "-d", d, "-o", "t",
+                                             "--output-format", "csv", "--", PY, "-u", f]
+                      + (args.split(",") if args else []), 600, env=env)
+            for root, _, files in os.walk(d):
+                for fn in files:
+                    if fn.endswith("kernel_trace.csv") and os.path.getsize(os.path.join(root, fn)) > 40 << 20:
+                        os.remove(os.path.join(root, fn))
+            print(_tail(os.path.join(out, f"pp_{name}.log"), 4))
         elif kind == "py":
             parts = rest.split(":")
             f, args = parts[0], parts[1] if len(parts) > 1 else ""

@@ -6,6 +6,8 @@ SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024) (the round-3 recipe,
 profiles/gemm_fp16x3_cycles_r03.md).
 
     gpurun -- python3 scripts/pmc_gemm.py <outdir> ["conv 256 14 14 256 256 3 1" ...]
+
+PMC_PROBE_FLAGS="--planes": the operands as fp16 planes (gemm.hip FM 13).
 """
 import collections
 import csv
@@ -37,7 +39,8 @@ def main():
             d = os.path.join(out, f"{ps}{i}")
             cmd = (["timeout", "-s", "KILL", "90", "rocprofv3", "--pmc"] + ctrs.split() +
                    ["--kernel-trace", "-d", d, "-o", ps, "--output-format", "csv", "--", sys.executable,
-                    "benchmarks/gemm_probe.py", "--f32", "--f16x3"] + shape.split() + ["5"])
+                    "benchmarks/gemm_probe.py", "--f32", "--f16x3"] + os.environ.get("PMC_PROBE_FLAGS", "").split()
+                   + shape.split() + ["5"])
             with open(os.path.join(out, f"{ps}{i}.log"), "w") as f:
                 rc = subprocess.call(cmd, stdout=f, stderr=subprocess.STDOUT, cwd=ROOT, env=env)
             if rc != 0:

@@ -2524,7 +2524,7 @@ __device__ __forceinline__ O cvt_out(float v) {
 }
 template <typename O>
 __device__ __forceinline__ void cast_tile(const float* __restrict__ w, int R, int Cc, int T, O* __restrict__ wb,
-                                          O* __restrict__ wt, const TapMap& map, int cx, int ry, int tap) {
+                                          O* __restrict__ wt, const TapMap& map, int cx, int ry, int tap, int ldt) {
   __shared__ O tile[32][33];
   const int c0 = cx * 32, r0 = ry * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 8 rows per pass
@@ -2543,7 +2543,7 @@ __device__ __forceinline__ void cast_tile(const float* __restrict__ w, int R, in
   const int tc = map.tc[tap], dt = map.dt[tap];
   for (int y = ty; y < 32; y += 8) {
     const int c = c0 + y, r = r0 + tx;
-    if (r < R && c < Cc) wt[base + (int64_t(c) * tc + dt) * R + r] = tile[tx][y];
+    if (r < R && c < Cc) wt[base + (int64_t(c) * tc + dt) * ldt + r] = tile[tx][y];
   }
 }
 
@@ -2656,7 +2656,7 @@ __device__ __forceinline__ void cast_tile_planes(const float* __restrict__ w, in
 template <typename O>
 __global__ __launch_bounds__(256) void cast_transpose_kernel(const float* __restrict__ w, int R, int Cc, int T,
                                                              O* __restrict__ wb, O* __restrict__ wt, TapMap map) {
-  cast_tile<O>(w, R, Cc, T, wb, wt, map, blockIdx.x, blockIdx.y, blockIdx.z);
+  cast_tile<O>(w, R, Cc, T, wb, wt, map, blockIdx.x, blockIdx.y, blockIdx.z, R);
 }
 
 // Every convolution weight of a model in one launch (the per-step bf16 casts of the fp32
@@ -2673,6 +2673,7 @@ struct CastJob {
   const float* amax;       // (f16) device upper bound of |w| over the plan
   int64_t block0;
   int64_t pb, pt;          // plane strides (elements) of wb / wt when f32 == 2
+  int ldt;                 // row length of a plain transpose wt (R, or a padded classifier's Np)
   TapMap map;
 };
 
@@ -2746,10 +2747,10 @@ __global__ __launch_bounds__(256) void cast_batch_kernel(const CastJob* __restri
   }
   else if (J.f32)
     cast_tile<float>(J.w, J.R, J.Cc, J.T, static_cast<float*>(J.wb), static_cast<float*>(J.wt), J.map, rem % J.tcx,
-                     rem / J.tcx, tap);
+                     rem / J.tcx, tap, J.ldt);
   else
     cast_tile<uint16_t>(J.w, J.R, J.Cc, J.T, static_cast<uint16_t*>(J.wb), static_cast<uint16_t*>(J.wt), J.map,
-                        rem % J.tcx, rem / J.tcx, tap);
+                        rem % J.tcx, rem / J.tcx, tap, J.ldt);
 }
 
 void check_ptr(uintptr_t p, const char* what) {
@@ -3799,7 +3800,9 @@ int64_t cast_jobs_build(uintptr_t host_table, const std::vector<std::array<int64
     //        | 512: wb as three pre-split bf16 planes (else none: the forward reads the master)
     //        | 1024: wt as three pre-split bf16 planes (else fp32)
     //        | 2048: the planes are fp16x3's two fp16 planes, scaled by the bound at q[10]
-    //        | 4096: a classifier weight: its bf16 transpose only (64 x 64 tiles when they fit)
+    //        | 4096: a classifier weight: its transpose only (bf16, or fp32 with f32; 64 x 64 tiles
+    //          when they fit), rows of q[9] elements when q[9] > 0 (a padded output layer's
+    //          wt[K][Np]: the Np - Co pad columns are never written, the caller zeroes them once)
     const int kind = int(q[0] & 0xff), Co = int(q[4]), C = int(q[5]), R = int(q[6]), S = int(q[7]);
     const int stride = int(q[8]), pad = int(q[9]);
     CastJob J{};
@@ -3818,6 +3821,8 @@ int64_t cast_jobs_build(uintptr_t host_table, const std::vector<std::array<int64
     J.R = Co;
     J.Cc = C;
     J.T = R * S;
+    J.ldt = ((q[0] >> 12) & 1) && pad > 0 ? pad : Co;
+    if (J.ldt < Co) throw std::invalid_argument("cast_jobs_build: transpose rows shorter than the weight's");
     if (J.T < 1 || J.T > kMaxTaps) throw std::invalid_argument("cast_jobs_build: 1 <= taps <= 49");
     if (kind == 1) {  // strided backward-data: parity-class packed weights
       J.map = strided_plan(2 * stride, 2 * stride, C, Co, R, S, stride, pad).map;
@@ -3830,7 +3835,7 @@ int64_t cast_jobs_build(uintptr_t host_table, const std::vector<std::array<int64
       if (kind == 2) J.wt = nullptr;
     }
     J.big = ((q[0] >> 12) & 1) && J.f32 == 0 && kind == 0 && J.T == 1 && C % 64 == 0 && Co % 128 == 0 && !J.wb &&
-            J.wt && q[1] % 16 == 0 && q[3] % 8 == 0;
+            J.wt && q[1] % 16 == 0 && q[3] % 8 == 0 && J.ldt == Co;
     J.tcx = J.big ? C / 64 : (C + 31) / 32;
     J.tcy = J.big ? Co / 128 : (Co + 31) / 32;
     J.block0 = blocks;

@@ -54,8 +54,11 @@ def _feeds_bn(*pairs):
 # measurements), MPIT_MFMA_CONV3=0 only the 3x3s.
 MFMA_CONV = os.environ.get("MPIT_MFMA_CONV", "1") != "0"
 MFMA_CONV3 = MFMA_CONV and os.environ.get("MPIT_MFMA_CONV3", "1") != "0"
-# MPIT_FC_FP32=0: the classifier follows autocast (bf16) instead of running in fp32
-_FC_FP32 = os.environ.get("MPIT_FC_FP32", "1") != "0"
+# MPIT_FC_FP32=1: the classifier runs in fp32 under bf16 autocast (round 4 default, when it was a
+# hipBLASLt GEMM whose backward call left a host gap). Default: it follows autocast on LinearAct's
+# bf16 MFMA path (fp32 accumulation, fp32 logits into the loss; its transpose is made by the
+# step's weight cast launch) — no library GEMM in the step (tests/test_linear_act.py)
+_FC_FP32 = os.environ.get("MPIT_FC_FP32", "0") != "0"
 
 
 def conv3x3(i, o, stride=1):
@@ -225,9 +228,8 @@ class ResNet(nn.Module):
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(self.avgpool(x), 1)
         if _FC_FP32 and x.is_cuda and torch.is_autocast_enabled("cuda"):
-            # the classifier in fp32 under bf16 autocast: more accurate logits, and the bf16
-            # library GEMM's backward call left a ~100 us host gap at the start of the
-            # backward (profiles/boundary_r04/README.md); MPIT_FC_FP32=0 keeps it in bf16
+            # (MPIT_FC_FP32=1) the classifier in fp32 under bf16 autocast, on LinearAct's fp32
+            # path (its own transpose per call: the step's cast launch is bf16)
             with torch.autocast("cuda", enabled=False):
                 return self.fc(x.float())
         return self.fc(x)

@@ -1234,15 +1234,17 @@ class WeightCastPlan:
         self.amax = None
         for mod in self.model.modules():
             kind = None
-            if getattr(mod, "_mpit_linear", False):  # ops/linear.py LinearAct: wt[K, N] only, bf16 steps
+            if getattr(mod, "_mpit_linear", False):  # ops/linear.py LinearAct: its transpose wt[K, Np] only
                 w = mod.weight
-                if f32 or not w.is_cuda or w.dtype != torch.float32 or not w.is_contiguous():
+                if not w.is_cuda or w.dtype != torch.float32 or not w.is_contiguous():
                     continue
                 co, c = w.shape
-                if co % 64:  # (a padded output layer casts its own transpose: ops/linear.py _wt_of)
-                    continue
-                wt = torch.empty((c, co), dtype=torch.bfloat16, device=w.device)
-                specs.append([4096, w.data_ptr(), 0, wt.data_ptr(), co, c, 1, 1, 1, 0, 0])
+                # out_features not a multiple of 64 (a 1000-class output layer): rows of Np, the
+                # pad columns zeroed here once and never written by the cast (bf16 or fp32)
+                np_ = (co + 63) // 64 * 64
+                wt = (torch.zeros if np_ != co else torch.empty)((c, np_), dtype=self.dtype, device=w.device)
+                specs.append([4096 | (256 if f32 else 0), w.data_ptr(), 0, wt.data_ptr(), co, c, 1, 1, 1,
+                              np_ if np_ != co else 0, 0])
                 self.mods.append((mod, w.data_ptr(), (None, wt)))
                 continue
             if isinstance(mod, Conv1x1) and mod.stride == (1, 1):

@@ -1,4 +1,4 @@
-"""LinearAct (ops/linear.py): the classifier's Linear(+ReLU) on the MFMA kernels in bf16
+"""LinearAct (ops/linear.py): the classifier's Linear(+ReLU) on the MFMA kernels in bf16 and fp32
 steps, against fp32 PyTorch on the same bf16-rounded operands; CPU fallback == F.linear."""
 import pytest
 import torch
@@ -46,3 +46,34 @@ def test_linear_act_bf16(act, M, K, N):
     for a, r, name in ((x.grad, xq.grad, "x"), (lin.weight.grad, wq.grad, "w"), (lin.bias.grad, bq.grad, "b")):
         assert a.dtype == torch.float32 and a.shape == r.shape, name
         assert (a - r).abs().max().item() <= 2e-2 * r.abs().max().item() + 1e-4, name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("act", [True, False])
+@pytest.mark.parametrize("M,K,N", [(64, 4096, 4096), (256, 2048, 1000)])
+def test_linear_act_fp32(act, M, K, N):
+    """fp32 steps (and ResNet's fp32 classifier): the same GEMMs on fp32 operands (bf16x6
+    split products), against fp64 — fp32-class error, and no library GEMM."""
+    from mpit_amd.ops.linear import LinearAct
+
+    torch.manual_seed(1)
+    lin = LinearAct(K, N, act=act, pad_out=N % 64 != 0).cuda()
+    with torch.no_grad():
+        lin.bias.uniform_(-0.1, 0.1)
+    x = torch.randn(M, K, device="cuda").requires_grad_(True)
+    assert lin.fused(x)
+    y = lin(x)
+    assert y.dtype == torch.float32 and y.shape == (M, N)
+    xd = x.detach().double().requires_grad_(True)
+    wd = lin.weight.detach().double().requires_grad_(True)
+    bd = lin.bias.detach().double().requires_grad_(True)
+    ref = F.linear(xd, wd, bd)
+    if act:
+        ref = F.relu(ref)
+    assert (y.double() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+    g = torch.randn(M, N, device="cuda")
+    y.backward(g)
+    ref.backward(g.double() * ((y > 0).double() if act else 1.0))
+    for a, r, name in ((x.grad, xd.grad, "x"), (lin.weight.grad, wd.grad, "w"), (lin.bias.grad, bd.grad, "b")):
+        assert a.dtype == torch.float32 and a.shape == r.shape, name
+        assert (a.double() - r).abs().max().item() <= 1e-5 * r.abs().max().item() + 1e-7, name

@@ -16,7 +16,9 @@ import mpit_amd as mp
 from mpit_amd.train import TrainConfig, Trainer
 
 mp.Init()
-tr = Trainer(TrainConfig(model=sys.argv[1] if len(sys.argv) > 1 else "resnet50", batch=256))
+# T_AMP=1: the bf16 autocast step (the one whose host can fall behind the GPU)
+tr = Trainer(TrainConfig(model=sys.argv[1] if len(sys.argv) > 1 else "resnet50", batch=256,
+                         amp=os.environ.get("T_AMP") == "1"))
 marks = {}
 orig_forward = tr.model.forward
 

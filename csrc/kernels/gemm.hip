@@ -3306,7 +3306,13 @@ static int tn_plan(int dev, int64_t M, int N, int K, int64_t* rows_per_split, in
   const int64_t target = std::max<int64_t>(1, int64_t(per_cu) * cu_count(dev) * split_mul / split_div);
   // floor: one more block than there are slots would run as a whole second round
   int64_t ns = std::max<int64_t>(1, target / ntiles);
-  const int64_t min_rows = 8 * kRows;  // keep >= 8 staged steps per block
+  // keep >= 8 staged steps per block; MPIT_TN_MIN_ROWS=r raises the floor (fewer, longer splits
+  // where M is deep and the output small — less partial-sum traffic; A/B knob)
+  static const int64_t min_rows_env = [] {
+    const char* e = std::getenv("MPIT_TN_MIN_ROWS");
+    return e ? std::max<int64_t>(8 * kRows, std::atoll(e)) : int64_t(8 * kRows);
+  }();
+  const int64_t min_rows = min_rows_env;
   ns = std::min<int64_t>(ns, std::max<int64_t>(1, M / min_rows));
   ns = std::min<int64_t>(ns, int64_t(kReduceGroup) * kReduceGroup);  // two reduce levels at most
   int64_t rps = (M + ns - 1) / ns;

@@ -391,6 +391,19 @@ __device__ __forceinline__ void blds16u(i32x4 rsrc, uint32_t voff, uint32_t lds)
                "s"(r), "s"(l)
                : "memory", "m0");
 }
+// FM 13 wave grid: 4 x 1 (FM 11's, where it made one wave split each A row) or, built with
+// -DMPIT_FM13_W22 (A/B variant), 2 x 2: with both operands ready-made a 64 x 64 wave reads 8
+// fragments per 12 MFMAs instead of 10
+#ifdef MPIT_FM13_W22
+constexpr bool kFm13W22 = true;
+#else
+constexpr bool kFm13W22 = false;
+#endif
+#ifdef MPIT_FM13_PF
+constexpr bool kFm13Pf = true;
+#else
+constexpr bool kFm13Pf = false;
+#endif
 // MPIT_GLOBAL_DMA (build define, A/B only): gemm_nt's bf16 and fp16x3 kernels and gemm_tn
 // stage through per-lane 64-bit global addresses as before round 5 instead of the buffer
 // descriptors; MPIT_F11_GLOBAL_DMA only the fp16x3 gemm_nt ones
@@ -767,7 +780,8 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
   // wave grid over the tile: 2 x 2 (each wave 64 x 64 of a 128 x 128 tile), or for FM 9
   // (pre-split B) 4 x 1: each wave owns 32 rows x all 128 columns, so every A row is split in
   // registers by exactly one wave (the ready-made B planes are the shared operand)
-  constexpr int WGM = (sizeof(T) == 4 && (FM == 9 || FM == 10 || FM == 11 || FM == 13)) ? 4 : 2, WGN = NW / WGM;
+  constexpr int WGM = (sizeof(T) == 4 && (FM == 9 || FM == 10 || FM == 11 || (FM == 13 && !kFm13W22))) ? 4 : 2,
+                WGN = NW / WGM;
   constexpr int WM = BM / WGM, WN = BN / WGN;
   constexpr int TM = WM / 32, TN = WN / 32;
   constexpr int EPC = epc<T>();                          // elements per 16-B chunk
@@ -1090,30 +1104,41 @@ __global__ __launch_bounds__(256, sizeof(T) == 4 ? (BM == 256 ? (BN == 64 ? 2 : 
       // row); hh -> acc, hl + lh -> tacc — FM 11's products on the same planes, no split
       const uint16_t* Bp = reinterpret_cast<const uint16_t*>(Bs);
       const uint16_t* Ap = reinterpret_cast<const uint16_t*>(As);
-#pragma unroll
-      for (int kk = 0; kk < BK / 16; ++kk) {
-        f16x8 ah[TM], al[TM], bh[TN], bl[TN];
+      // MPIT_FM13_PF (A/B build define): every fragment of the stage read before its first
+      // MFMA (KK sets of fragment registers), instead of per k16 step
+      constexpr int KK = BK / 16, KS = kFm13Pf ? KK : 1;
+      f16x8 ah[KS][TM], al[KS][TM], bh[KS][TN], bl[KS][TN];
+      auto rd = [&](int kk, int sl) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int r = wn * WN + j * 32 + fr;
           const int o = r * 32 + swz(r, 2 * kk + fh) * 8;
-          bh[j] = *reinterpret_cast<const f16x8*>(Bp + o);
-          bl[j] = *reinterpret_cast<const f16x8*>(Bp + BN * 32 + o);
+          bh[sl][j] = *reinterpret_cast<const f16x8*>(Bp + o);
+          bl[sl][j] = *reinterpret_cast<const f16x8*>(Bp + BN * 32 + o);
         }
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           const int r = wm * WM + i * 32 + fr;
           const int o = r * 32 + swz(r, 2 * kk + fh) * 8;
-          ah[i] = *reinterpret_cast<const f16x8*>(Ap + o);
-          al[i] = *reinterpret_cast<const f16x8*>(Ap + BM * 32 + o);
+          ah[sl][i] = *reinterpret_cast<const f16x8*>(Ap + o);
+          al[sl][i] = *reinterpret_cast<const f16x8*>(Ap + BM * 32 + o);
         }
+      };
+      if constexpr (kFm13Pf) {
+#pragma unroll
+        for (int kk = 0; kk < KK; ++kk) rd(kk, kk);
+      }
+#pragma unroll
+      for (int kk = 0; kk < KK; ++kk) {
+        const int sl = kFm13Pf ? kk : 0;
+        if constexpr (!kFm13Pf) rd(kk, 0);
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bh[j], ah[i], acc[i][j], 0, 0, 0);
-            tacc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bl[j], ah[i], tacc[i][j], 0, 0, 0);
-            tacc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bh[j], al[i], tacc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bh[sl][j], ah[sl][i], acc[i][j], 0, 0, 0);
+            tacc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bl[sl][j], ah[sl][i], tacc[i][j], 0, 0, 0);
+            tacc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bh[sl][j], al[sl][i], tacc[i][j], 0, 0, 0);
           }
       }
       continue;

@@ -649,6 +649,66 @@ def test_gemm_tn_hostile_rows(dist, M, N, K, mode):
     _check_rows(f"tn {dist} {M}x{N}x{K}", _row_rel(out, ref), _row_rel(y.t() @ x, ref), mode, cond)
 
 
+def _loose_planes(t, factor):
+    """fp16 planes of ``t`` (its memory order) scaled by a bound ``factor`` x max |t| — a producer
+    bound that overshoots (the BN apply passes bound their output from coefficient and input
+    maxima, never below the true maximum, up to a few times above it)."""
+    bnd = C.bound_of_value(torch.linalg.vector_norm(t.float(), float("inf")) * factor)
+    return C.f16_planes(t.reshape(-1).contiguous(), bnd), bnd
+
+
+@gpu
+@pytest.mark.parametrize("factor", [1.0, 4.0, 16.0])
+@pytest.mark.parametrize("dist", ["student_t2", "outlier_row"])
+@pytest.mark.parametrize("M,N,K", [(4096, 256, 512), (12544, 512, 2048)])
+def test_gemm_nt_hostile_rows_planes(dist, M, N, K, factor):
+    """FM 13: the activation operand arrives as fp16 planes whose bound overshoots max |A| by
+    ``factor`` (the precision floor moves up by log2(factor) bits: 22 bits down to 2^-27 of the
+    bound) — same per-row acceptance as the in-kernel split."""
+    from mpit_amd._ext import native
+
+    a = _hostile(dist, (M, K), M + K)
+    b = _hostile("student_t2", (N, K), N + K, 0.05)
+    ref = a.double().cpu() @ b.double().cpu().t()
+    ap, abnd = _loose_planes(a, factor)
+    bp = C.f16_planes(b.contiguous(), C.bound_of_value(torch.linalg.vector_norm(b, float("inf"))))
+    c = torch.empty(M, N, device="cuda")
+    native().gemm_nt(0, torch.cuda.current_stream().cuda_stream, M, N, K, ap.data_ptr(), K, bp.data_ptr(), K,
+                     c.data_ptr(), N, 0, f32=True, bps=bp[0].numel(), amax_a=abnd.data_ptr(),
+                     amax_b=bp._mpit_wamax.data_ptr(), aps=ap[0].numel())
+    torch.cuda.synchronize()
+    assert torch.isfinite(c).all()
+    cond = _row_cond(a.abs().double().cpu() @ b.abs().double().cpu().t(), ref)
+    _check_rows(f"nt planes x{factor} {dist} {M}x{N}x{K}", _row_rel(c, ref), _row_rel(a @ b.t(), ref), "planes",
+                cond)
+
+
+@gpu
+@pytest.mark.parametrize("factor", [1.0, 4.0, 16.0])
+@pytest.mark.parametrize("dist", ["student_t2", "outlier_row"])
+@pytest.mark.parametrize("M,N,K", [(5000, 192, 320), (12544, 512, 256)])
+def test_gemm_tn_hostile_rows_planes(dist, M, N, K, factor):
+    """FM 13 backward-weight: dY and X both as fp16 planes with overshooting bounds."""
+    from mpit_amd._ext import native
+
+    y = _hostile("student_t2", (M, N), M + N, 1e-6)
+    x = _hostile(dist, (K, M), K + M).t().contiguous()
+    ref = y.double().cpu().t() @ x.double().cpu()
+    yp, yb = _loose_planes(y, factor)
+    xp, xb = _loose_planes(x, factor)
+    m = native()
+    out = torch.empty(N, K, device="cuda")
+    ws = torch.empty(max(1, m.gemm_tn_ws_floats(0, M, N, K)), device="cuda")
+    m.gemm_tn(0, torch.cuda.current_stream().cuda_stream, M, N, K, yp.data_ptr(), N, xp.data_ptr(), K,
+              out.data_ptr(), ws.data_ptr(), 0.0, f32=True, amax_y=yb.data_ptr(), amax_x=xb.data_ptr(),
+              yps=yp[0].numel(), xps=xp[0].numel())
+    torch.cuda.synchronize()
+    assert torch.isfinite(out).all()
+    cond = _row_cond(y.abs().double().cpu().t() @ x.abs().double().cpu(), ref)
+    _check_rows(f"tn planes x{factor} {dist} {M}x{N}x{K}", _row_rel(out, ref), _row_rel(y.t() @ x, ref), "planes",
+                cond)
+
+
 @gpu
 def test_conv_f16x3_hostile_input_rows():
     """A 3x3 convolution through the fp32 weight plan (fp16x3 planes) on a heavy-tailed input

@@ -527,6 +527,7 @@ PYBIND11_MODULE(_mpit, m) {
       .def("stop", &PSClient::stop, py::call_guard<py::gil_scoped_release>())
       .def("wait", &PSClient::wait, py::call_guard<py::gil_scoped_release>())
       .def("test", &PSClient::test)
+      .def("take_deps", [](PSClient& c, uintptr_t s) { c.take_deps(S(s)); })
       .def("pending", &PSClient::pending)
       .def("replies", &PSClient::replies)
       .def("set_link", &PSClient::set_link, py::keep_alive<1, 2>());

@@ -9,11 +9,41 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <stdexcept>
 
 #include "../kernels/kernels.h"
 
 namespace mpit {
+
+// Co-located device clients (PSClient::local): a server on the same rank hands its update's
+// GPU event to the client and replies at once. MPIT_PS_LOCAL_EVENTS=0: reply after a host
+// poll of that event (the step boundary then pays the poll and the reply's wake-up while the
+// GPU idles: the update kernel -> next step's weight cast gap, profiles/step_idle_r06.md).
+namespace {
+std::mutex g_local_mu;
+std::map<std::pair<int, int>, PSClient*> g_local_clients;
+std::map<std::pair<int, int>, PSServer*> g_local_servers;
+bool local_events() {
+  static const bool on = [] {
+    const char* e = std::getenv("MPIT_PS_LOCAL_EVENTS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+// MPIT_PS_LOCAL_GATE=1 (A/B, off): the co-located client's messages also skip the host gate
+// (PSClient::send_local). The step boundary's idle goes (0.6 -> 0.2 ms traced), but the host
+// then queues a whole backward ahead of the GPU and the backward-weight side stream's small
+// kernels end up behind the critical stream's (split_reduce 1.3 -> 3.9 ms per fp32 step):
+// fp32 neutral, bf16 -6 % (gpurun_out/r06n, profiles/ps_local_events_r06.md)
+bool local_gate() {
+  static const bool on = [] {
+    const char* e = std::getenv("MPIT_PS_LOCAL_GATE");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+}  // namespace
 
 namespace {
 void hipp(hipError_t e, const char* what) {
@@ -105,6 +135,11 @@ PSServer::PSServer(Engine& eng, int ps_id, Window& rx, Window& tx, std::vector<i
 }
 
 PSServer::~PSServer() {
+  {
+    std::lock_guard<std::mutex> g(g_local_mu);
+    auto it = g_local_servers.find({ps_id_, eng_.rank()});
+    if (it != g_local_servers.end() && it->second == this) g_local_servers.erase(it);
+  }
   for (int t = 1; t <= 8; ++t) eng_.register_am(ps_am_id(ps_id_, t), [](const Msg&) {});
   if (fg_) {
     {
@@ -127,6 +162,77 @@ PSServer::~PSServer() {
   }
 }
 
+
+PSServer* PSServer::local(int ps_id, int rank) {
+  std::lock_guard<std::mutex> g(g_local_mu);
+  auto it = g_local_servers.find({ps_id, rank});
+  return it == g_local_servers.end() ? nullptr : it->second;
+}
+
+hipEvent_t PSClient::pop_gate() {
+  std::lock_guard<std::mutex> g(dep_mu_);
+  if (gates_.empty()) throw std::logic_error("mpit: a kPsGpuGate message without its gate event");
+  hipEvent_t e = gates_.front();
+  gates_.pop_front();
+  return e;
+}
+
+
+// the co-located server's message, sent now: its stream waits on the gate event instead of
+// this client's progress thread polling it (the push of the step's last shard is then queued
+// while the backward still runs, and the replies come back without waiting for the GPU)
+void PSClient::send_local(hipStream_t s, int k, int tag, int64_t flags) {
+  hipp(hipSetDevice(eng_.device()), "hipSetDevice");
+  hipEvent_t e = eng_.get_event();
+  Engine::record_event(e, s);
+  {
+    std::lock_guard<std::mutex> g(dep_mu_);
+    gates_.push_back(e);
+  }
+  send_entry(k, tag, flags | kPsGpuGate);
+}
+
+PSClient* PSClient::local(int ps_id, int rank) {
+  std::lock_guard<std::mutex> g(g_local_mu);
+  auto it = g_local_clients.find({ps_id, rank});
+  return it == g_local_clients.end() ? nullptr : it->second;
+}
+
+void PSClient::add_gpu_dep(hipEvent_t e) {
+  std::lock_guard<std::mutex> g(dep_mu_);
+  deps_.push_back(e);
+}
+
+void PSClient::take_deps(hipStream_t s) {
+  std::vector<hipEvent_t> d;
+  {
+    std::lock_guard<std::mutex> g(dep_mu_);
+    d.swap(deps_);
+  }
+  if (d.empty()) return;
+  hipp(hipSetDevice(eng_.device()), "hipSetDevice");
+  for (auto e : d) {
+    hipp(hipStreamWaitEvent(s, e, 0), "wait co-located update");
+    eng_.put_event(e);  // (the wait is queued: re-recording the event later does not affect it)
+  }
+}
+
+PSClient* PSServer::early_client(int c) const {
+  if (!device_ || c != eng_.rank() || !local_events()) return nullptr;
+  return PSClient::local(ps_id_, c);
+}
+
+void PSServer::finish_for(int c, std::function<void()> replies) {
+  if (PSClient* l = early_client(c)) {
+    hipEvent_t e = eng_.get_event();
+    Engine::record_event(e, stream_);
+    l->add_gpu_dep(e);  // (before the replies: the client's wait sees it once they are in)
+    replies();
+    return;
+  }
+  finish(std::move(replies));
+}
+
 void PSServer::finish_on(hipStream_t s, std::function<void()> then) {
   hipEvent_t ev = eng_.get_event();
   Engine::record_event(ev, s);
@@ -146,6 +252,10 @@ void PSServer::start() {
   }
   for (int t : {kTagInit, kTagGrad, kTagParam, kTagHeader, kTagStop})
     eng_.register_am(ps_am_id(ps_id_, t), [this](const Msg& m) { on_msg(m); });
+  if (device_ && stream_) {
+    std::lock_guard<std::mutex> g(g_local_mu);
+    g_local_servers[{ps_id_, eng_.rank()}] = this;
+  }
 }
 
 bool PSServer::batchable(int c) const {
@@ -216,12 +326,29 @@ bool PSServer::flush_grads() {
     ++stats_.batches;
     if (batch.size() >= 2) ++stats_.multi;
   }
-  finish([this, batch] {
-    for (const auto& q : batch) {
-      reply(q.c, kTagGradTail);
-      if (q.pull && !q.defer) reply(q.c, kTagSendParam);
-    }
-  });
+  std::vector<PendingGrad> remote;
+  PSClient* lc = nullptr;
+  for (const auto& q : batch) {
+    if (PSClient* l = early_client(q.c)) lc = l;
+    else remote.push_back(q);
+  }
+  if (lc) {  // the co-located client: its GPU waits on this event, its host need not
+    hipEvent_t e = eng_.get_event();
+    Engine::record_event(e, stream_);
+    lc->add_gpu_dep(e);
+    for (const auto& q : batch)
+      if (early_client(q.c)) {
+        reply(q.c, kTagGradTail);
+        if (q.pull && !q.defer) reply(q.c, kTagSendParam);
+      }
+  }
+  if (!remote.empty())
+    finish([this, remote] {
+      for (const auto& q : remote) {
+        reply(q.c, kTagGradTail);
+        if (q.pull && !q.defer) reply(q.c, kTagSendParam);
+      }
+    });
   release_deferred();
   return true;
 }
@@ -258,6 +385,17 @@ bool PSServer::maybe_fault(int kind) {
 
 void PSServer::on_msg(const Msg& m) {
   const int tag = (m.tag - 4096) % 16;
+  if ((tag == kTagGrad || tag == kTagHeader || tag == kTagParam) && (m.aux0 & kPsGpuGate)) {
+    // sent before the co-located client's GPU work behind it finished: everything this
+    // message makes stream_ do waits for that work (queued now, so a backlogged message
+    // served later is ordered too)
+    PSClient* l = PSClient::local(ps_id_, m.src);
+    if (!l || !device_) throw std::logic_error("mpit: kPsGpuGate from a client that is not the co-located one");
+    hipEvent_t e = l->pop_gate();
+    hipp(hipSetDevice(eng_.device()), "hipSetDevice");
+    hipp(hipStreamWaitEvent(stream_, e, 0), "server waits client gate");
+    eng_.put_event(e);
+  }
   // asyncsgd/pserver.lua:152-158: the shard is initialised from the first client's
   // parameter push before any gradient or pull is served
   if (init_rank_ >= 0 && (tag == kTagGrad || tag == kTagHeader)) {
@@ -423,7 +561,7 @@ void PSServer::do_param(int c, bool from_rx, Sub sb) {
     std::lock_guard<std::mutex> g(mu_);
     ++stats_.param_pushes;
   }
-  finish([this, c] { reply(c, kTagParamTail); });
+  finish_for(c, [this, c] { reply(c, kTagParamTail); });
 }
 
 void PSServer::copy_out(int c, Sub sb) {
@@ -483,7 +621,7 @@ void PSServer::do_pull(int c, Sub sb) {
     std::lock_guard<std::mutex> g(mu_);
     ++stats_.pulls;
   }
-  finish([this, c] { reply(c, kTagSendParam); });
+  finish_for(c, [this, c] { reply(c, kTagSendParam); });
 }
 
 void PSServer::do_grad(int c, bool pull, Sub sb) {
@@ -567,7 +705,7 @@ void PSServer::do_grad(int c, bool pull, Sub sb) {
       ++stats_.deferred;
     }
   }
-  finish([this, c, pull, defer_pull] {
+  finish_for(c, [this, c, pull, defer_pull] {
     reply(c, kTagGradTail);
     if (pull && !defer_pull) reply(c, kTagSendParam);
   });
@@ -762,6 +900,15 @@ struct PSClient::GateQueue {
   std::deque<Gate> q;
 };
 
+bool PSClient::gpu_gate(int k) const {
+  if (eng_.device() < 0 || link_ || servers_[size_t(k)] != eng_.rank() || !local_events() || !local_gate() ||
+      PSServer::local(ps_id_, eng_.rank()) == nullptr)
+    return false;
+  // an entry still waiting in the gate queue may be for this server: keep the call order
+  std::lock_guard<std::mutex> l(gq_->mu);
+  return gq_->q.empty();
+}
+
 PSClient::PSClient(Engine& eng, int ps_id, std::vector<int> servers, std::vector<int64_t> offs,
                    std::vector<int64_t> lens)
     : eng_(eng), ps_id_(ps_id), servers_(std::move(servers)), offs_(std::move(offs)), lens_(std::move(lens)) {
@@ -800,6 +947,18 @@ PSClient::PSClient(Engine& eng, int ps_id, std::vector<int> servers, std::vector
 }
 
 PSClient::~PSClient() {
+  {
+    std::lock_guard<std::mutex> g(g_local_mu);
+    auto it = g_local_clients.find({ps_id_, eng_.rank()});
+    if (it != g_local_clients.end() && it->second == this) g_local_clients.erase(it);
+  }
+  {
+    std::lock_guard<std::mutex> g(dep_mu_);
+    for (auto e : deps_) eng_.put_event(e);
+    deps_.clear();
+    for (auto e : gates_) eng_.put_event(e);
+    gates_.clear();
+  }
   if (hook_ >= 0) eng_.remove_hook(hook_);
   if (link_) link_->set_client(nullptr);
   // gates never retired (the client went away with pushes queued): release their events
@@ -818,6 +977,10 @@ PSClient::~PSClient() {
 }
 
 void PSClient::start() {
+  if (eng_.device() >= 0) {
+    std::lock_guard<std::mutex> g(g_local_mu);
+    g_local_clients[{ps_id_, eng_.rank()}] = this;
+  }
   for (int t : {kTagSendParam, kTagParamTail, kTagGradTail})
     eng_.register_am(ps_am_id(ps_id_, t), [this](const Msg& m) { on_reply(m); });
   for (size_t i = 0; i < servers_.size(); ++i)
@@ -893,19 +1056,33 @@ void PSClient::send_entry(int k, int tag, int64_t flags) {
   }
 }
 
+// Entries of the co-located device server go out at once with a gate event (send_local);
+// the others wait in the gate queue for the GPU work queued so far on s. (Per server the
+// call order is kept either way: a server's entries all take the same route.)
 void PSClient::send_grad(hipStream_t s, bool with_pull) {
   const int64_t n = int64_t(servers_.size());
   int64_t extra = 0;
   for (int k = 0; k < int(n); ++k) extra += link_recvs(k, kTagGrad, with_pull ? kPsWithPull : 0);
   pending_.fetch_add((with_pull ? 2 * n : n) + extra);
-  gate(s, [this, with_pull, n] {
-    for (int k = 0; k < int(n); ++k) send_entry(k, kTagGrad, with_pull ? kPsWithPull : 0);
-  });
+  const int64_t fl = with_pull ? kPsWithPull : 0;
+  std::vector<int> gated;
+  for (int k = 0; k < int(n); ++k) {
+    if (gpu_gate(k)) send_local(s, k, kTagGrad, fl);
+    else gated.push_back(k);
+  }
+  if (!gated.empty())
+    gate(s, [this, gated, fl] {
+      for (int k : gated) send_entry(k, kTagGrad, fl);
+    });
 }
 
 void PSClient::send_grad_to(hipStream_t s, int k, bool with_pull) {
   if (k < 0 || k >= int(servers_.size())) throw std::out_of_range("PSClient::send_grad_to: bad shard");
   pending_.fetch_add((with_pull ? 2 : 1) + link_recvs(k, kTagGrad, with_pull ? kPsWithPull : 0));
+  if (gpu_gate(k)) {
+    send_local(s, k, kTagGrad, with_pull ? kPsWithPull : 0);
+    return;
+  }
   gate(s, [this, k, with_pull] { send_entry(k, kTagGrad, with_pull ? kPsWithPull : 0); });
 }
 
@@ -915,17 +1092,30 @@ void PSClient::recv_param(hipStream_t s) {
   for (int k = 0; k < n; ++k) extra += link_recvs(k, kTagHeader, 0);
   pending_.fetch_add(n + extra);
   // ordered behind any gated push of this client
-  gate(s, [this, n] {
-    for (int k = 0; k < n; ++k) send_entry(k, kTagHeader, 0);
-  });
+  std::vector<int> gated;
+  for (int k = 0; k < n; ++k) {
+    if (gpu_gate(k)) send_local(s, k, kTagHeader, 0);
+    else gated.push_back(k);
+  }
+  if (!gated.empty())
+    gate(s, [this, gated] {
+      for (int k : gated) send_entry(k, kTagHeader, 0);
+    });
 }
 
 void PSClient::send_param(hipStream_t s, bool from_rx) {
   const int n = int(servers_.size());
   pending_.fetch_add(n);
-  gate(s, [this, from_rx, n] {
-    for (int k = 0; k < n; ++k) send_entry(k, kTagParam, from_rx ? kPsFromRx : 0);
-  });
+  const int64_t fl = from_rx ? kPsFromRx : 0;
+  std::vector<int> gated;
+  for (int k = 0; k < n; ++k) {
+    if (gpu_gate(k)) send_local(s, k, kTagParam, fl);
+    else gated.push_back(k);
+  }
+  if (!gated.empty())
+    gate(s, [this, gated, fl] {
+      for (int k : gated) send_entry(k, kTagParam, fl);
+    });
 }
 
 void PSClient::stop() {

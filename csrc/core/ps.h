@@ -57,7 +57,10 @@ enum PsTag : int {
 // kPsWithPull (tag 2): reply with the refreshed shard; kPsFromRx (tag 4): the pushed
 // parameters are in the client's fp32 rx window, not its tx window (an EASGD client whose
 // wire is bf16 initialises the shards with exact fp32 weights).
-enum PsFlags : int64_t { kPsWithPull = 1, kPsFromRx = 2 };
+// kPsGpuGate: from the co-located device client — the message was sent when issued, not when
+// the client's GPU work before it finished; the server's stream waits on the client's gate
+// event (PSClient::pop_gate) before serving it
+enum PsFlags : int64_t { kPsWithPull = 1, kPsFromRx = 2, kPsGpuGate = 4 };
 
 inline int ps_am_id(int ps_id, int tag) { return 4096 + ps_id * 16 + tag; }
 
@@ -85,6 +88,8 @@ struct Sub {
   int64_t o = 0, n = 0;
 };
 
+class PSClient;
+
 class PSServer {
  public:
   // members: world ranks of the window members, in window member order; clients: the
@@ -94,6 +99,8 @@ class PSServer {
            int64_t shard_off, int64_t shard_len, bool device, uintptr_t p, std::vector<uintptr_t> state,
            uintptr_t inbox, ServerRule rule, int datapath, int64_t staleness, bool grad_bf16, int init_rank);
   ~PSServer();
+  // the started device server of (ps_id, rank) in this process (the co-located one)
+  static PSServer* local(int ps_id, int rank);
   void start();
   bool done() const { return stopped_.load() >= int(clients_.size()); }
   void wait_done();
@@ -152,6 +159,11 @@ class PSServer {
   void pull_msg(int c, int ci, Sub sb);
   void param_msg(int c, int ci, bool from_rx, Sub sb, std::function<void()> after = nullptr);
   void reply(int c, int tag);
+  // the co-located device client of rank c that takes GPU events instead of finished replies
+  PSClient* early_client(int c) const;
+  // replies to client c: at once with the update's event for the co-located device client,
+  // else once the work queued so far on stream_ finished
+  void finish_for(int c, std::function<void()> replies);
   void finish(std::function<void()> then);
   void release_deferred();
   int member_of(int world_rank) const;
@@ -234,6 +246,17 @@ class PSClient {
   bool test() const { return pending_.load() == 0; }
   int64_t pending() const { return pending_.load(); }
   int64_t replies() const { return replies_.load(); }
+  // Co-located server (the same rank, a device shard on the local fused path): it replies as
+  // soon as its update is QUEUED and hands over the GPU event that completes it, instead of
+  // replying after a host poll of that event (MPIT_PS_LOCAL_EVENTS=0: the poll). The client's
+  // next GPU work must wait on those events: take_deps(s) makes stream s wait on every event
+  // handed over so far (called by the Python wait / test before anything reads the shard).
+  void add_gpu_dep(hipEvent_t e);
+  void take_deps(hipStream_t s);
+  // the gate event of the oldest kPsGpuGate message not yet served (server side)
+  hipEvent_t pop_gate();
+  // the client of (ps_id, rank) in this process, if it runs as a device client
+  static PSClient* local(int ps_id, int rank);
 
  private:
   struct GateQueue;
@@ -256,6 +279,11 @@ class PSClient {
   std::atomic<int64_t> pending_{0};
   std::atomic<int64_t> replies_{0};
   std::atomic<uint32_t> reply_seq_{0};  // futex word bumped by every reply
+  std::mutex dep_mu_;
+  std::vector<hipEvent_t> deps_;  // update events of the co-located server not yet waited on
+  std::deque<hipEvent_t> gates_;  // gate events of kPsGpuGate messages, in send order
+  bool gpu_gate(int k) const;     // entry k's server is the co-located device server
+  void send_local(hipStream_t s, int k, int tag, int64_t flags);
 };
 
 }  // namespace mpit

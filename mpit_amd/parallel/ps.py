@@ -449,13 +449,24 @@ class PClient:
             gc.collect(0)
         with _trace.range("ps_wait"):
             self.native.wait()
+        self._take_deps()
         if self._pull_pending:
             self._pull_pending = False
             if self._user_p is not None and self._user_p.data_ptr() != self.rx.data_ptr():
                 self._user_p.reshape(-1).copy_(self.rx)
 
+    def _take_deps(self):
+        """A co-located server replies once its update is QUEUED (csrc/core/ps.h
+        PSClient::take_deps): the current stream waits on those updates before anything that
+        follows reads the shard or rewrites the push window."""
+        if self.rx is not None and self.rx.is_cuda:
+            self.native.take_deps(torch.cuda.current_stream(self.rx.device).cuda_stream)
+
     def test(self) -> bool:
-        return self.native.test()
+        done = self.native.test()
+        if done:
+            self._take_deps()
+        return done
 
     def reset(self, p: Optional[torch.Tensor] = None, g: Optional[torch.Tensor] = None):
         """Rebind the client's parameter / gradient tensors (asyncsgd/pclient.lua:146-155)."""
@@ -471,6 +482,7 @@ class PClient:
     def stop(self):
         if self.native is not None and self.on:
             self.native.stop()
+            self._take_deps()
             self.on = False
 
     def replies(self) -> int:

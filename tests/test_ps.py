@@ -153,8 +153,10 @@ def test_datapath3_pre_sequencer_layout_deadlocks():
     """The layout before the sequencer (each client queues its ops when it sends its control
     message, each server when the message arrives; all on one FIFO per rank) deadlocks under
     the same blocking semantics: the clients' finite wait reports it."""
-    out = run_ranks("ps_link_rdv.py", 8, dict(_RDV, T_TOPO="colocated", MPIT_LINK_LEGACY="1", MPIT_PS_TIMEOUT_S="6"),
-                    timeout=300)
+    # (the deadlock needs an unlucky arrival order; 1,000 random steps make one all but certain,
+    # and the run ends at the first one)
+    out = run_ranks("ps_link_rdv.py", 8, dict(_RDV, T_TOPO="colocated", MPIT_LINK_LEGACY="1", MPIT_PS_TIMEOUT_S="6",
+                                              T_STEPS="1000"), timeout=300)
     assert "RESULT RDV_TIMEOUT" in out and "RESULT RDV_OK" not in out, out
 
 

@@ -325,6 +325,12 @@ PYBIND11_MODULE(_mpit, m) {
       py::arg("red_part2") = 0, py::arg("red_x2") = 0, py::arg("red_mean2") = 0, py::arg("f32") = false,
       py::arg("bps") = 0, py::arg("amax_a") = 0, py::arg("amax_b") = 0, py::arg("aps") = 0, py::arg("omax") = 0,
       py::arg("oepoch") = 0);
+  m.def(
+      "softmax_xent",
+      [](int dev, uintptr_t s, int64_t rows, int C, uintptr_t x, int64_t ldx, bool bf16, uintptr_t tgt, float scale,
+         uintptr_t loss, uintptr_t d) { softmax_xent(dev, S(s), rows, C, x, ldx, bf16, tgt, scale, loss, d); },
+      py::arg("dev"), py::arg("stream"), py::arg("rows"), py::arg("C"), py::arg("x"), py::arg("ldx"),
+      py::arg("bf16"), py::arg("tgt"), py::arg("scale"), py::arg("loss"), py::arg("d"));
   m.def("relu_bias_bwd_ws_floats", &relu_bias_bwd_ws_floats);
   m.def(
       "relu_bias_bwd",

@@ -240,6 +240,10 @@ int64_t conv_dgrad_strided_tiles(int Nb, int H, int W, int C, int Co, int R, int
 void conv_dgrad_strided(int dev, hipStream_t s, int Nb, int H, int W, int C, int Co, int R, int S, int stride, int pad,
                         uintptr_t dy, uintptr_t wcls, uintptr_t dx, const BnRed* red = nullptr, bool f32 = false,
                         int64_t bps = 0);
+// softmax cross-entropy over rows of logits x [rows][ldx] (bf16 or fp32; loss.hip): per-row
+// loss (fp32 [rows]) and the logits' gradient d = (softmax - onehot) * scale (fp32 [rows][C])
+void softmax_xent(int dev, hipStream_t s, int64_t rows, int C, uintptr_t x, int64_t ldx, bool bf16, uintptr_t tgt,
+                  float scale, uintptr_t loss, uintptr_t d);
 int64_t relu_bias_bwd_ws_floats(int C);
 // out[c] = sum over rows k < nb of part[k * ld + c] (fp32, fixed order: deterministic); mid:
 // col_sums_ws_floats(C) floats of workspace (needed when nb > 64)

@@ -29,6 +29,7 @@ from . import runtime as _rt
 from .comm import COMM_WORLD, MAX
 from .models import get_model
 from .models.cnn import INPUT_SHAPES
+from .ops.loss import cross_entropy as xent
 from .optim import distributed as dopt
 from .parallel.ps import PClient, PServer, ServerOpt
 from .utils import trace as _trace
@@ -252,11 +253,11 @@ class Trainer:
                 if self.on_gpu and self.cfg.amp:
                     with torch.autocast("cuda", dtype=torch.bfloat16):
                         out = self.model(self.x)
-                    loss = F.cross_entropy(out.float(), self.y)
+                    loss = xent(out, self.y)  # (fp32 math on the bf16 logits)
                 else:
                     out = self.model(self.x)
                     loss = (F.nll_loss(out, self.y) if self.cfg.model in ("cnn7", "lenet")
-                            else F.cross_entropy(out, self.y))
+                            else xent(out, self.y))
             with _trace.range("bwd"):
                 loss.backward()
         finally:

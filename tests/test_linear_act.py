@@ -77,3 +77,35 @@ def test_linear_act_fp32(act, M, K, N):
     for a, r, name in ((x.grad, xd.grad, "x"), (lin.weight.grad, wd.grad, "w"), (lin.bias.grad, bd.grad, "b")):
         assert a.dtype == torch.float32 and a.shape == r.shape, name
         assert (a.double() - r).abs().max().item() <= 1e-5 * r.abs().max().item() + 1e-7, name
+
+
+def test_fused_xent_cpu_fallback():
+    from mpit_amd.ops.loss import cross_entropy
+
+    torch.manual_seed(0)
+    x = torch.randn(8, 10, requires_grad=True)
+    t = torch.randint(0, 10, (8,))
+    assert torch.equal(cross_entropy(x, t), F.cross_entropy(x, t))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,C", [(256, 1000), (64, 10), (3, 4097)])
+def test_fused_xent_vs_pytorch(dt, B, C):
+    """ops/loss.py: the one-launch softmax cross-entropy (loss and logits' gradient) against
+    PyTorch's F.cross_entropy on the same (fp32-promoted) logits."""
+    from mpit_amd.ops.loss import cross_entropy
+
+    torch.manual_seed(3)
+    x = (torch.randn(B, C, device="cuda") * 4).to(dt).requires_grad_(True)
+    t = torch.randint(0, C, (B,), device="cuda")
+    loss = cross_entropy(x, t)
+    loss.backward(torch.tensor(0.5, device="cuda"))
+    xr = x.detach().float().requires_grad_(True)
+    ref = F.cross_entropy(xr, t)
+    ref.backward(torch.tensor(0.5, device="cuda"))
+    assert loss.dtype == torch.float32
+    assert abs(loss.item() - ref.item()) <= 1e-5 * max(1.0, abs(ref.item()))
+    assert x.grad.dtype == dt and x.grad.shape == x.shape
+    tol = 1e-6 if dt == torch.float32 else 1e-2 * xr.grad.abs().max().item()
+    assert (x.grad.float() - xr.grad).abs().max().item() <= tol

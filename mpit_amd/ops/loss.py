@@ -8,8 +8,10 @@ by the incoming scalar gradient. PyTorch's path is log_softmax + nll_loss forwar
 backward kernels and their fills (plus a cast for bf16 logits) — small launches at the turn
 from forward to backward, where the host issues them one by one.
 
-Falls back to ``F.cross_entropy`` on the CPU, for other dtypes, class weights, ignore_index,
-label smoothing or a non-mean reduction. MPIT_FUSED_XENT=0: always the fallback."""
+Falls back to ``F.cross_entropy`` on the CPU, for other dtypes, targets on another device or
+given as probabilities. Class weights, ignore_index, label smoothing and other reductions are
+not part of this API (call ``F.cross_entropy``). A target outside [0, C) gives a NaN loss (PyTorch
+raises a device-side assert). MPIT_FUSED_XENT=0: always the fallback."""
 from __future__ import annotations
 
 import os
@@ -43,8 +45,11 @@ class _SoftmaxXentFn(torch.autograd.Function):
 
 
 def fused_ok(logits: torch.Tensor, target: torch.Tensor) -> bool:
+    # (the kernel reads the targets on the logits' device: anything else takes PyTorch's path,
+    # which also raises the usual errors for it)
     return (_ENABLED and logits.is_cuda and logits.dim() == 2 and logits.dtype in (torch.float32, torch.bfloat16)
-            and target.dim() == 1 and target.shape[0] == logits.shape[0] and logits.shape[0] > 0)
+            and target.dim() == 1 and target.shape[0] == logits.shape[0] and logits.shape[0] > 0
+            and target.device == logits.device and not target.dtype.is_floating_point)
 
 
 def cross_entropy(logits: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
